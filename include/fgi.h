@@ -1,0 +1,225 @@
+/*
+ * fgi.h — C-ABI of the MI355X cascading-invalidation engine ("fgi": Fusion Graph Invalidation).
+ *
+ * The engine keeps Stl.Fusion's reverse dependency graph (every Computed's `_usedBy` set) in HBM
+ * and runs `Computed.Invalidate()` cascades as batched frontier BFS waves in gfx950 HIP kernels.
+ * The reference exposes no FFI seam for the cascade (Computed<T>.Invalidate is non-virtual,
+ * `_usedBy` private: src/Stl.Fusion/Computed.cs:36-37, 162); the boundary is a host layer that
+ * mirrors ComputedRegistry / `using (Computed.Invalidate())` / IComputed.Invalidated and calls
+ * this library (C# `[LibraryImport("fgi")]` stubs in INTEGRATION.md; the C++ mirror is
+ * stl.fusion_amd/host/fusion.hpp). Every entry point below names the reference member it
+ * replaces.
+ *
+ * Conventions
+ *   - Plain C types only; all arrays are HOST pointers unless the name ends in `_dev`.
+ *   - Every function returns an fgi_status; nothing throws or aborts, mirroring
+ *     "Invalidate doesn't throw - ever" (Computed.cs:200-229). fgi_last_error() describes the
+ *     last failure on a graph.
+ *   - A graph is externally synchronised: one caller thread at a time (the host layer funnels
+ *     all calls through one dispatcher, which replaces the per-node `lock(this)` of
+ *     Computed.cs:42). Calls are synchronous: they return after the device work completed.
+ *
+ * Node model ("handles")
+ *   - A slot is a ComputedInput (ComputedInput.cs / ComputeMethodInput.cs); the host maps each
+ *     input to a dense slot id in [0, n_slots). Handle h < n_slots addresses the slot's current
+ *     node (the registry entry, ComputedRegistry.cs:22).
+ *   - Handles >= n_slots are "detached" nodes: nodes displaced from the registry by a newer
+ *     computation while still Computing or while a delayed invalidation is pending
+ *     (ComputedRegistry.cs:91-96 leaves such an object alive and unregistered). They keep their
+ *     own `_usedBy` row and state; fgi_begin_compute hands them out.
+ *   - state_flags word: bits 0-1 ConsistencyState (Computing 0, Consistent 1, Invalidated 2 —
+ *     ConsistencyState.cs:5-10), bit 2 InvalidateOnSetOutput, bit 3 InvalidationDelayStarted
+ *     (ComputedFlags.cs:4-8), bit 4 hasDelay (ComputedOptions.InvalidationDelay != 0).
+ *     Reported flags are canonical: an Invalidated node reports no IOSO/DelayStarted bits and a
+ *     non-Computing node no IOSO bit (the reference never reads them again, Computed.cs:145,
+ *     164-172), so results are independent of the order in which a batch is applied.
+ *   - version: the node's LTag (LTag.cs:13-22), 1 <= version < 2^56 (ConcurrentLTagGenerator
+ *     yields values in [1, 2^55]). Edge tags are full 64-bit LTags.
+ */
+#ifndef FGI_H
+#define FGI_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int fgi_status;
+#define FGI_OK 0
+#define FGI_EINVAL 1     /* bad argument */
+#define FGI_ENOMEM 2     /* device allocation failed */
+#define FGI_ECAPACITY 3  /* output buffer too small: *out_n holds the required size */
+#define FGI_EDEVICE 4    /* HIP / RCCL runtime error */
+#define FGI_ESTATE 5     /* operation invalid in the node's state */
+#define FGI_ENOTSUP 6    /* not supported in this configuration */
+
+#define FGI_NONE 0xFFFFFFFFu
+
+#define FGI_COMPUTING 0u
+#define FGI_CONSISTENT 1u
+#define FGI_INVALIDATED 2u
+#define FGI_STATE_MASK 3u
+#define FGI_F_INVALIDATE_ON_SET_OUTPUT 4u
+#define FGI_F_INVALIDATION_DELAY_STARTED 8u
+#define FGI_F_HAS_DELAY 16u
+
+/* fgi_add_used per-item outcome (Computed.cs:347-385) */
+#define FGI_USED_ADDED 0u        /* (dependant.input, dependant.version) added to used._usedBy */
+#define FGI_USED_DROPPED 1u      /* dependant not Computing: no-op (Computed.cs:351-364) */
+#define FGI_USED_INVALIDATED 2u  /* used already Invalidated: dependant gets InvalidateOnSetOutput (376-378) */
+#define FGI_USED_ESTATE 3u       /* used is Computing: the reference throws WrongComputedState (374-375) */
+
+typedef struct fgi_graph fgi_graph;
+
+typedef struct fgi_config {
+    uint32_t struct_size;      /* sizeof(fgi_config) */
+    int32_t device;            /* HIP device ordinal */
+    uint32_t n_slots;          /* slot capacity (registry keys) */
+    uint32_t n_detached;       /* capacity for detached nodes (handles n_slots .. n_slots+n_detached) */
+    uint64_t edge_capacity;    /* initial edge-pool capacity (grows on demand) */
+    /* multi-GPU 1-D vertex partition (fgi_part_*); 0/1 for a single device */
+    int32_t rank;
+    int32_t world;
+} fgi_config;
+
+typedef struct fgi_wave_stats {
+    uint64_t roots;            /* root entries submitted */
+    uint64_t levels;           /* BFS levels with a non-empty frontier */
+    uint64_t v_inv;            /* Consistent -> Invalidated transitions (= expanded nodes) */
+    uint64_t e_trav;           /* sum of |_usedBy| over invalidated nodes (TEPS numerator) */
+    uint64_t e_match;          /* traversed edges whose tag == version of the dst slot's node */
+    uint64_t n_flagged;        /* visits that only set InvalidateOnSetOutput / DelayStarted */
+    uint64_t alg_bytes;        /* algorithmic HBM bytes of the wave */
+    double kernel_ms;          /* device time of the wave's kernels (HIP events) */
+    double total_ms;           /* wall time of the call */
+    uint64_t remote_msgs;      /* multi-GPU: frontier messages sent to other partitions */
+    uint64_t f_total;          /* frontier entries expanded (invalidated nodes with |_usedBy| > 0) */
+    uint64_t expand_launches;  /* expand kernel launches that had work */
+    double expand_ms;          /* summed device time of those launches (HIP events) */
+    uint64_t expand_bytes;     /* algorithmic bytes of those launches */
+} fgi_wave_stats;
+
+typedef struct fgi_prune_stats {
+    uint64_t old_edges;        /* sum of |_usedBy| over pruned (Consistent, registered) nodes before */
+    uint64_t new_edges;        /* ... and after (ComputedGraphPruner.cs:91-93) */
+    uint64_t pool_before;      /* edge-pool slots in use before compaction */
+    uint64_t pool_after;
+    double kernel_ms;
+} fgi_prune_stats;
+
+/* ---- lifetime ------------------------------------------------------------------------------ */
+fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out);      /* new ComputedRegistry (ComputedRegistry.cs:38-52) */
+fgi_status fgi_destroy(fgi_graph* g);                                /* ComputedRegistry.Dispose (54-55) */
+const char* fgi_last_error(const fgi_graph* g);
+fgi_status fgi_version(uint32_t* major, uint32_t* minor);
+
+/* ---- registry / node state ---------------------------------------------------------------- */
+/* Bulk import of current nodes (ComputedRegistry.Register, ComputedRegistry.cs:72-105, without
+ * displacement: the slots must be empty). version[i] == 0 leaves the slot empty. */
+fgi_status fgi_register_nodes(fgi_graph* g, uint32_t n, const uint32_t* slot, const uint64_t* version,
+                              const uint32_t* state_flags);
+/* Bulk import of `_usedBy` entries: used[i]._usedBy += (dependant_slot[i], tag[i])
+ * (IComputedImpl.AddUsedBy body, Computed.cs:381-382, no state checks). Set semantics
+ * (HashSetSlim3.Add, HashSetSlim3.cs:31-64): duplicate entries collapse. */
+fgi_status fgi_load_edges(fgi_graph* g, uint64_t m, const uint32_t* used, const uint32_t* dependant_slot,
+                          const uint64_t* tag);
+/* IComputed.Version / ConsistencyState / flags for handles (Computed.cs:46-48). */
+fgi_status fgi_get_state(fgi_graph* g, uint32_t n, const uint32_t* handle, uint64_t* version,
+                         uint32_t* state_flags);
+/* Whole-table dump (n_slots + n_detached entries) — for parity checks. */
+fgi_status fgi_dump_states(fgi_graph* g, uint64_t* version, uint32_t* state_flags);
+/* IComputedImpl.UsedBy (Computed.cs:337-345): the live `_usedBy` entries of one node. An
+ * Invalidated node reports none (its set was cleared, Computed.cs:217). */
+fgi_status fgi_get_used_by(fgi_graph* g, uint32_t handle, uint32_t* dependant_slot, uint64_t* tag,
+                           uint64_t cap, uint64_t* out_n);
+/* IComputedImpl.Used.Length for a node (Computed.cs:327-335). */
+fgi_status fgi_get_used_count(fgi_graph* g, uint32_t handle, uint32_t* out);
+/* Out-degree (|_usedBy|) of every handle, and the total. */
+fgi_status fgi_get_degrees(fgi_graph* g, uint32_t* degree /*n_slots+n_detached, nullable*/, uint64_t* total);
+
+/* ---- dependency capture (compute-method call path) ----------------------------------------- */
+/* ComputeMethodFunctionBase.Compute (ComputeMethodFunctionBase.cs:19-27): a new Computing node of
+ * version[i] becomes the current node of slot[i] (registered in its ctor,
+ * ComputeMethodComputed.cs:9-11). A current node is displaced as ComputedRegistry.Register does
+ * (ComputedRegistry.cs:83-97): it is invalidated (immediately=false) — a cascade root — and, if it
+ * survives that (Computing, or Consistent with an invalidation delay), it is detached and its
+ * handle returned in out_detached[i] (FGI_NONE otherwise). Slots must be distinct in one call. */
+fgi_status fgi_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, const uint64_t* version,
+                             const uint8_t* has_delay /*nullable*/, uint32_t* out_detached /*nullable*/,
+                             fgi_wave_stats* stats /*nullable*/);
+/* dependant.AddUsed(used) for each pair (IComputedImpl.AddUsed/AddUsedBy, Computed.cs:347-385,
+ * reached from ComputedExt.UseNew / TryUseExisting, Internal/ComputedExt.cs:13-22, 70-76).
+ * out_result[i] gets an FGI_USED_* code. Pairs in one call are applied as one batch. */
+fgi_status fgi_add_used(fgi_graph* g, uint32_t n, const uint32_t* dependant, const uint32_t* used,
+                        uint32_t* out_result /*nullable*/);
+/* Computed<T>.TrySetOutput (Computed.cs:141-160) for each handle: Computing -> Consistent;
+ * nodes flagged InvalidateOnSetOutput are invalidated at once in one cascade wave.
+ * out_set[i] = 1 if the node was Computing. */
+fgi_status fgi_set_output(fgi_graph* g, uint32_t n, const uint32_t* handle, uint8_t* out_set /*nullable*/,
+                          uint32_t* out_ids /*nullable*/, uint64_t cap, uint64_t* out_n /*nullable*/,
+                          fgi_wave_stats* stats /*nullable*/);
+
+/* ---- invalidation (the hot path) ----------------------------------------------------------- */
+/* One batched cascade: for each root handle, `existing.Invalidate(immediately[i])`
+ * (Computed.Invalidate() scope -> ComputedExt.TryUseExisting -> Computed.cs:162-230, recursing
+ * through every `_usedBy` entry whose version still matches, 212-216). immediately may be NULL
+ * (all false — what the scope does). The invalidated set is written to out_ids (slots, in BFS
+ * level order); if cap is too small, FGI_ECAPACITY is returned with *out_n = required size (the
+ * wave itself has completed). out_ids may be NULL to skip the copy. */
+fgi_status fgi_invalidate(fgi_graph* g, uint32_t n_roots, const uint32_t* roots, const uint8_t* immediately,
+                          uint32_t* out_ids, uint64_t cap, uint64_t* out_n, fgi_wave_stats* stats);
+/* Same with device-resident roots / flags / output (bench and pipelined host layers). out_ids_dev
+ * may be NULL (the ids stay in the engine's own buffer, see fgi_wave_ids_dev). */
+fgi_status fgi_invalidate_dev(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev,
+                              const uint8_t* immediately_dev, uint32_t* out_ids_dev, uint64_t* out_n,
+                              fgi_wave_stats* stats);
+/* Device pointer to the last wave's invalidated-slot list (valid until the next call). */
+fgi_status fgi_wave_ids_dev(fgi_graph* g, const uint32_t** ids_dev, uint64_t* n);
+/* ComputedRegistry.InvalidateEverything (ComputedRegistry.cs:142-147). */
+fgi_status fgi_invalidate_all(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n,
+                              fgi_wave_stats* stats);
+
+/* ---- graph maintenance ---------------------------------------------------------------------- */
+/* One ComputedGraphPruner pass (Internal/ComputedGraphPruner.cs:79-94): PruneUsedBy on every
+ * registered Consistent node (Computed.cs:400-419) — keep (slot, tag) iff the slot's current node
+ * exists with version == tag — then compact the edge pool. */
+fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats);
+/* Release a detached handle once the host no longer references the node. */
+fgi_status fgi_release(fgi_graph* g, uint32_t n, const uint32_t* handle);
+
+/* ---- bench / test support ------------------------------------------------------------------- */
+/* Save / restore node states and row lengths on the device (reset from a pristine copy). */
+fgi_status fgi_snapshot(fgi_graph* g);
+fgi_status fgi_restore(fgi_graph* g);
+/* Device-side synthetic workloads. All nodes Consistent with
+ * version (splitmix64(seed ^ slot) & (2^55-1)) | 1. stale_pct% of edges (by hash with
+ * stale_seed) carry tag = version + 1. The graph must be empty. */
+fgi_status fgi_synth_layered(fgi_graph* g, uint32_t levels, uint32_t width, uint32_t fanout, uint64_t seed);
+fgi_status fgi_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_factor, uint64_t seed,
+                          uint32_t stale_pct, uint64_t stale_seed);
+/* Copy the full edge set (sorted by (used, dependant, tag)) to the host: parity tests. */
+fgi_status fgi_export_edges(fgi_graph* g, uint32_t* used, uint32_t* dependant_slot, uint64_t* tag,
+                            uint64_t cap, uint64_t* out_n);
+/* HIP stream the graph's kernels run on (as void* = hipStream_t) — for event timing in bench. */
+fgi_status fgi_stream(fgi_graph* g, void** stream);
+
+/* ---- multi-GPU (1-D vertex-range partition, RCCL all-to-all frontier exchange) --------------- */
+/* RCCL unique id (128 bytes) made by rank 0 and broadcast by the caller (e.g. torch.distributed). */
+fgi_status fgi_part_unique_id(uint8_t* id128);
+/* Join the partitioned engine: this graph owns slots [rank*ceil(N/world), ...) of a global
+ * N = n_global slots; cfg->rank/world must be set. */
+fgi_status fgi_part_init(fgi_graph* g, uint32_t n_global, const uint8_t* id128);
+/* Partitioned R-MAT: every rank generates the same global edge set and keeps the rows it owns. */
+fgi_status fgi_part_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_factor, uint64_t seed,
+                               uint32_t stale_pct, uint64_t stale_seed);
+/* Collective wave: every rank passes the same global root list; each rank reports the
+ * invalidated slots it owns (global ids) and its own share of the statistics. */
+fgi_status fgi_part_invalidate(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev,
+                               const uint8_t* immediately_dev, uint64_t* out_n, fgi_wave_stats* stats);
+fgi_status fgi_part_export_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FGI_H */

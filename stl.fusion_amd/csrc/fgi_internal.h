@@ -1,0 +1,197 @@
+// fgi_internal.h — device data layout and shared helpers of the fgi engine (gfx950 only).
+//
+// HBM layout, one entry per handle h in [0, n_slots + n_detached):
+//   node[h]    u64  packed node word: bits 0-55 version (LTag; 0 = no node), bits 56-57
+//                   ConsistencyState, bit 58 InvalidateOnSetOutput, bit 59 InvalidationDelayStarted,
+//                   bit 60 hasDelay. One 64-bit CAS checks the version and moves the state.
+//   row_off[h] u64  start of h's `_usedBy` row in the edge pool
+//   row_len[h] u32  entries in the row (logical length is 0 once the node is Invalidated)
+//   row_cap[h] u32  reserved entries (appends go in place while len < cap)
+//   used_cnt[h]u32  |_used| of the node (forward links created while it was Computing)
+// Edge pool (structure of arrays, rows are contiguous runs):
+//   pool_col[p] u32 dependant slot (ComputedInput of the `_usedBy` entry)
+//   pool_tag[p] u64 dependant version at capture time (LTag of the `_usedBy` entry)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+#include <vector>
+
+#include "../../include/fgi.h"
+
+namespace fgi {
+
+constexpr uint64_t kVMask = (1ull << 56) - 1;
+constexpr int kStateShift = 56;
+constexpr uint64_t kStateBits = 3ull << kStateShift;
+constexpr uint64_t kW_IOSO = 1ull << 58;
+constexpr uint64_t kW_DS = 1ull << 59;
+constexpr uint64_t kW_HasDelay = 1ull << 60;
+constexpr uint64_t kW_Computing = 0ull;
+constexpr uint64_t kW_Consistent = 1ull << kStateShift;
+constexpr uint64_t kW_Invalidated = 2ull << kStateShift;
+
+__host__ __device__ inline uint32_t word_state(uint64_t w) { return (uint32_t)((w >> kStateShift) & 3u); }
+__host__ __device__ inline bool word_is_current(uint64_t w) {
+    return (w & kVMask) != 0 && word_state(w) != FGI_INVALIDATED;
+}
+
+// Host-visible state_flags <-> node word (canonical flags, fgi.h)
+__host__ __device__ inline uint32_t word_to_flags(uint64_t w) {
+    if ((w & kVMask) == 0) return 0;
+    uint32_t st = word_state(w);
+    uint32_t f = st;
+    if (st == FGI_COMPUTING) {
+        if (w & kW_IOSO) f |= FGI_F_INVALIDATE_ON_SET_OUTPUT;
+        if (w & kW_DS) f |= FGI_F_INVALIDATION_DELAY_STARTED;
+    } else if (st == FGI_CONSISTENT) {
+        if (w & kW_DS) f |= FGI_F_INVALIDATION_DELAY_STARTED;
+    }
+    if (w & kW_HasDelay) f |= FGI_F_HAS_DELAY;
+    return f;
+}
+__host__ __device__ inline uint64_t flags_to_word(uint64_t version, uint32_t f) {
+    uint64_t w = (version & kVMask) | ((uint64_t)(f & 3u) << kStateShift);
+    if (f & FGI_F_INVALIDATE_ON_SET_OUTPUT) w |= kW_IOSO;
+    if (f & FGI_F_INVALIDATION_DELAY_STARTED) w |= kW_DS;
+    if (f & FGI_F_HAS_DELAY) w |= kW_HasDelay;
+    return w;
+}
+
+// splitmix64 finaliser
+__host__ __device__ inline uint64_t sm64(uint64_t x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+__host__ __device__ inline uint64_t synth_version(uint64_t seed, uint32_t slot) {
+    return (sm64(seed ^ (uint64_t)slot) & ((1ull << 55) - 1)) | 1ull;
+}
+
+// ---- wave bookkeeping -------------------------------------------------------------------------
+constexpr int kRing = 64;               // per-level counters live in a ring (deep waves roll over)
+constexpr int kScanBlocks = 1024;       // fixed grid of the two-pass frontier scan
+constexpr int kBlock = 256;             // threads per block for the traversal kernels
+constexpr int kEPT = 8;                 // edges per thread per chunk
+constexpr int kChunk = kBlock * kEPT;   // edges per expand chunk
+
+struct LevelCtr {
+    unsigned long long F;       // frontier entries (expandable = invalidated with |row| > 0)
+    unsigned long long T;       // edges of the frontier (sum of row lengths)
+    unsigned long long nchunks; // ceil(T / kChunk)
+    unsigned long long pad[5];
+};
+
+struct WaveCtr {
+    unsigned long long inv;         // invalidated nodes appended so far (V_inv)
+    unsigned long long e_match;
+    unsigned long long n_flagged;
+    unsigned long long root_inv;    // winners of the roots kernel
+    unsigned long long pad[4];
+    LevelCtr lvl[kRing];
+};
+
+// ---- host-side graph object -------------------------------------------------------------------
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace fgi
+
+struct fgi_graph {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    uint32_t n_slots = 0, n_detached = 0, n_handles = 0;
+    int rank = 0, world = 1;
+
+    // node table
+    uint64_t* node = nullptr;
+    uint64_t* row_off = nullptr;
+    uint32_t* row_len = nullptr;
+    uint32_t* row_cap = nullptr;
+    uint32_t* used_cnt = nullptr;
+    uint32_t* home = nullptr;          // [n_detached]: home slot of a detached handle
+    std::vector<uint32_t> free_detached;  // host free list of detached handles
+
+    // edge pool
+    uint32_t* pool_col = nullptr;
+    uint64_t* pool_tag = nullptr;
+    uint64_t pool_cap = 0;             // entries
+    uint64_t pool_top = 0;             // bump pointer (host mirror of device counter)
+    unsigned long long* pool_top_dev = nullptr;
+    uint64_t pool_epoch = 0;           // bumped on compaction (invalidates snapshots)
+
+    // wave workspace
+    uint32_t* inv = nullptr;           // [n_handles] invalidated handles of the last wave
+    uint64_t* fr_off[2] = {nullptr, nullptr};
+    uint32_t* fr_len[2] = {nullptr, nullptr};
+    uint64_t* escan = nullptr;         // [n_handles]
+    uint32_t* cstart = nullptr;        // [cstart_cap]
+    uint64_t cstart_cap = 0;
+    unsigned long long* partials = nullptr;  // [kScanBlocks]
+    fgi::WaveCtr* ctr = nullptr;
+    fgi::WaveCtr* ctr_host = nullptr;  // pinned
+    uint32_t* roots_buf = nullptr;     // staging for host roots
+    uint8_t* imm_buf = nullptr;
+    uint64_t roots_cap = 0;
+    uint64_t last_wave_n = 0;
+
+    // generic scratch (sorts, batches)
+    void* scratch = nullptr;
+    size_t scratch_bytes = 0;
+    unsigned long long* misc_dev = nullptr;   // small device counters [16]
+    unsigned long long* misc_host = nullptr;  // pinned [16]
+
+    // snapshot
+    uint64_t* snap_node = nullptr;
+    uint64_t* snap_row_off = nullptr;
+    uint32_t* snap_row_len = nullptr;
+    uint32_t* snap_row_cap = nullptr;
+    uint32_t* snap_used = nullptr;
+    uint64_t snap_epoch = ~0ull;
+
+    // timing
+    std::vector<hipEvent_t> ev;        // pairs around expand launches
+    hipEvent_t ev_w0 = nullptr, ev_w1 = nullptr;
+
+    // multi-GPU
+    void* part = nullptr;
+
+    std::string err;
+};
+
+// ---- internal entry points shared between translation units ----------------------------------
+namespace fgi {
+fgi_status set_err(fgi_graph* g, fgi_status st, const char* fmt, ...);
+fgi_status hip_check(fgi_graph* g, hipError_t e, const char* what);
+fgi_status ensure_scratch(fgi_graph* g, size_t bytes);
+fgi_status ensure_pool(fgi_graph* g, uint64_t entries);
+fgi_status ensure_cstart(fgi_graph* g, uint64_t total_edges);
+// Run one cascade wave from `n_roots` device-resident roots. Fills stats (nullable).
+fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
+                    fgi_wave_stats* stats);
+// Build rows from device edge keys (src << 32 | dst) + optional tags; pool must be empty.
+// Consumes `keys`/`tags` buffers (they may be overwritten). If tags == nullptr the tag of each
+// edge is synth_version(ver_seed, dst) (+1 if stale by hash).
+fgi_status build_rows_from_keys(fgi_graph* g, uint64_t m, uint64_t* keys, uint64_t* tags,
+                                uint64_t ver_seed, uint32_t stale_pct, uint64_t stale_seed);
+// Release multi-GPU resources (part.hip).
+fgi_status part_destroy(fgi_graph* g);
+// Append (used, dependant slot, tag) entries to rows (set semantics, no state checks).
+fgi_status append_edges(fgi_graph* g, uint64_t m, const uint32_t* used_dev, const uint32_t* dep_dev,
+                        const uint64_t* tag_dev, const uint32_t* dep_handle_dev);
+}  // namespace fgi
+
+#define FGI_HIP(g, call)                                                   \
+    do {                                                                   \
+        hipError_t _e = (call);                                            \
+        if (_e != hipSuccess) return fgi::hip_check((g), _e, #call);       \
+    } while (0)
+#define FGI_TRY(call)                          \
+    do {                                       \
+        fgi_status _s = (call);                \
+        if (_s != FGI_OK) return _s;           \
+    } while (0)

@@ -1,0 +1,1189 @@
+// graph.hip — node table, edge pool and the graph-mutation entry points of the fgi C-ABI.
+//
+// Reference members restated here (paths relative to the Stl.Fusion tree):
+//   ComputedRegistry.Register / Get / InvalidateEverything   ComputedRegistry.cs:57-147
+//   ComputeMethodFunctionBase.Compute (new Computing node)   Interception/ComputeMethodFunctionBase.cs:19-27
+//   IComputedImpl.AddUsed / AddUsedBy                        Computed.cs:347-385
+//   Computed<T>.TrySetOutput                                 Computed.cs:141-160
+//   IComputedImpl.PruneUsedBy + ComputedGraphPruner          Computed.cs:400-419, Internal/ComputedGraphPruner.cs:79-94
+#include <hip/hip_runtime.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+
+#include "fgi_internal.h"
+
+namespace fgi {
+
+fgi_status set_err(fgi_graph* g, fgi_status st, const char* fmt, ...) {
+    if (g) {
+        char buf[512];
+        va_list ap;
+        va_start(ap, fmt);
+        vsnprintf(buf, sizeof(buf), fmt, ap);
+        va_end(ap);
+        g->err = buf;
+    }
+    return st;
+}
+
+fgi_status hip_check(fgi_graph* g, hipError_t e, const char* what) {
+    if (e == hipSuccess) return FGI_OK;
+    return set_err(g, e == hipErrorOutOfMemory ? FGI_ENOMEM : FGI_EDEVICE, "%s: %s", what, hipGetErrorString(e));
+}
+
+namespace {
+
+template <class T>
+fgi_status dmalloc(fgi_graph* g, T** p, size_t count) {
+    *p = nullptr;
+    if (count == 0) count = 1;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T));
+    if (e != hipSuccess) return hip_check(g, e, "hipMalloc");
+    return FGI_OK;
+}
+
+template <class T>
+void dfree(T*& p) {
+    if (p) hipFree(p);
+    p = nullptr;
+}
+
+// RAII device temporaries for non-hot-path operations
+struct Tmp {
+    void* p = nullptr;
+    ~Tmp() {
+        if (p) hipFree(p);
+    }
+};
+template <class T>
+fgi_status tmalloc(fgi_graph* g, Tmp& t, T** p, size_t count) {
+    hipError_t e = hipMalloc(&t.p, (count ? count : 1) * sizeof(T));
+    if (e != hipSuccess) return hip_check(g, e, "hipMalloc(tmp)");
+    *p = reinterpret_cast<T*>(t.p);
+    return FGI_OK;
+}
+
+__device__ __forceinline__ uint32_t home_of(uint32_t h, uint32_t n_slots, const uint32_t* home) {
+    return h < n_slots ? h : home[h - n_slots];
+}
+
+// ---- bulk row build -------------------------------------------------------------------------
+__global__ void k_mark_unique(uint64_t m, const uint64_t* __restrict__ keys, const uint64_t* __restrict__ tags,
+                              uint32_t* __restrict__ keep) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    const uint64_t k = keys[e];
+    uint32_t kp = 1;
+    if (e > 0 && keys[e - 1] == k) {
+        if (!tags) {
+            kp = 0;
+        } else {
+            // run of equal (used, dependant): a tag already seen earlier in the run is a duplicate
+            const uint64_t t = tags[e];
+            for (uint64_t q = e; q > 0 && keys[q - 1] == k; --q)
+                if (tags[q - 1] == t) {
+                    kp = 0;
+                    break;
+                }
+        }
+    }
+    keep[e] = kp;
+}
+
+__device__ __forceinline__ uint64_t edge_tag(uint64_t ver_seed, uint32_t stale_pct, uint64_t stale_seed,
+                                             uint32_t src, uint32_t dst) {
+    uint64_t v = synth_version(ver_seed, dst);
+    if (stale_pct) {
+        const uint64_t h = sm64(stale_seed ^ sm64(((uint64_t)src << 32) | dst));
+        if (h % 100 < stale_pct) v += 1;
+    }
+    return v;
+}
+
+__global__ void k_scatter_rows(uint64_t m, const uint64_t* __restrict__ keys, const uint64_t* __restrict__ tags,
+                               const uint32_t* __restrict__ keep, const uint32_t* __restrict__ pos,
+                               uint64_t ver_seed, uint32_t stale_pct, uint64_t stale_seed, uint32_t* pool_col,
+                               uint64_t* pool_tag, uint64_t* row_off, uint32_t* row_len, uint32_t* used_cnt,
+                               const unsigned long long* node, uint32_t n_slots) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    const uint64_t k = keys[e];
+    const uint32_t src = (uint32_t)(k >> 32), dst = (uint32_t)k;
+    const uint32_t p = pos[e];
+    if (keep[e]) {
+        const uint64_t t = tags ? tags[e] : edge_tag(ver_seed, stale_pct, stale_seed, src, dst);
+        pool_col[p] = dst;
+        pool_tag[p] = t;
+        // the forward link dependant._used += used exists iff the tag is the dependant's version
+        if (dst < n_slots && (node[dst] & kVMask) == t && t != 0) atomicAdd(&used_cnt[dst], 1u);
+    }
+    const bool first = (e == 0) || (uint32_t)(keys[e - 1] >> 32) != src;
+    const bool last = (e + 1 == m) || (uint32_t)(keys[e + 1] >> 32) != src;
+    if (first) row_off[src] = p;
+    if (last) row_len[src] = p + keep[e];   // temporarily the row end
+}
+
+__global__ void k_fix_rows(uint32_t n, const uint64_t* __restrict__ row_off, uint32_t* row_len, uint32_t* row_cap) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= n) return;
+    const uint32_t end = row_len[h];
+    const uint32_t len = end ? (uint32_t)(end - row_off[h]) : 0u;
+    row_len[h] = len;
+    row_cap[h] = len;
+}
+
+// Live edges of every row (rows of Invalidated / empty nodes are logically empty) as keys+tags.
+__global__ void k_live_len(uint32_t n, const unsigned long long* node, const uint32_t* row_len, uint32_t* out) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= n) return;
+    const unsigned long long w = node[h];
+    out[h] = word_is_current(w) ? row_len[h] : 0u;
+}
+
+__global__ void k_gather_live(uint32_t n, const uint32_t* __restrict__ live_len, const uint64_t* __restrict__ dst_off,
+                              const uint64_t* __restrict__ row_off, const uint32_t* __restrict__ pool_col,
+                              const uint64_t* __restrict__ pool_tag, uint64_t* keys, uint64_t* tags) {
+    // one wave per row
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t h = wave; h < n; h += nw) {
+        const uint32_t len = live_len[h];
+        const uint64_t o = row_off[h], d = dst_off[h];
+        for (uint32_t i = lane; i < len; i += 64) {
+            keys[d + i] = ((uint64_t)h << 32) | pool_col[o + i];
+            tags[d + i] = pool_tag[o + i];
+        }
+    }
+}
+
+// ---- node import / query ---------------------------------------------------------------------
+__global__ void k_register(uint32_t n, const uint32_t* slot, const uint64_t* version, const uint32_t* flags,
+                           unsigned long long* node, uint32_t* row_len, unsigned long long* err) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = slot[i];
+    if (word_is_current(node[s])) {
+        atomicAdd(err, 1ull);
+        return;
+    }
+    node[s] = version[i] ? flags_to_word(version[i], flags ? flags[i] : FGI_CONSISTENT) : 0ull;
+    row_len[s] = 0;
+}
+
+__global__ void k_gather_words(uint32_t n, const uint32_t* __restrict__ h, const unsigned long long* node,
+                               unsigned long long* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = node[h[i]];
+}
+
+// ---- begin_compute ---------------------------------------------------------------------------
+// class: 0 nothing current, 1 displacement root (Consistent, no delay), 2 detach (Computing, or
+// Consistent with a delay: ComputedRegistry.cs:91-96 invalidates it, which only flags it).
+__global__ void k_bc_classify(uint32_t n, const uint32_t* __restrict__ slot, const unsigned long long* node,
+                              uint8_t* cls, uint32_t* roots, unsigned long long* cnt /*[0]=roots,[1]=detach*/) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long w = node[slot[i]];
+    uint8_t c = 0;
+    if (word_is_current(w)) {
+        if (word_state(w) == FGI_CONSISTENT && !(w & kW_HasDelay)) c = 1;
+        else c = 2;
+    }
+    cls[i] = c;
+    if (c == 1) roots[atomicAdd(&cnt[0], 1ull)] = slot[i];
+    if (c == 2) atomicAdd(&cnt[1], 1ull);
+}
+
+__global__ void k_bc_install(uint32_t n, const uint32_t* __restrict__ slot, const uint64_t* __restrict__ version,
+                             const uint8_t* __restrict__ has_delay, const uint8_t* __restrict__ cls,
+                             const uint32_t* __restrict__ free_h, unsigned long long* cursor, uint32_t n_slots,
+                             unsigned long long* node, uint64_t* row_off, uint32_t* row_len, uint32_t* row_cap,
+                             uint32_t* used_cnt, uint32_t* home, uint32_t* out_det) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = slot[i];
+    uint32_t det = FGI_NONE;
+    if (cls[i] == 2) {
+        const uint32_t h = free_h[atomicAdd(cursor, 1ull)];
+        unsigned long long w = node[s];
+        // Register's displacement Invalidate() (ComputedRegistry.cs:91-94, Computed.cs:173-191)
+        if (word_state(w) == FGI_COMPUTING) w |= kW_IOSO;
+        else if (word_state(w) == FGI_CONSISTENT) w |= kW_DS;
+        node[h] = w;
+        row_off[h] = row_off[s];
+        row_len[h] = row_len[s];
+        row_cap[h] = row_cap[s];
+        used_cnt[h] = used_cnt[s];
+        home[h - n_slots] = s;
+        row_off[s] = 0;
+        row_cap[s] = 0;
+        det = h;
+    }
+    row_len[s] = 0;   // the new node starts with an empty `_usedBy`; an invalidated row is reused
+    used_cnt[s] = 0;
+    node[s] = (version[i] & kVMask) | kW_Computing | ((has_delay && has_delay[i]) ? kW_HasDelay : 0ull);
+    out_det[i] = det;
+}
+
+// ---- add_used --------------------------------------------------------------------------------
+struct Cand {
+    uint32_t used, dep_handle, dep_slot, pad;
+    uint64_t tag;
+};
+
+__global__ void k_au_classify(uint32_t n, const uint32_t* __restrict__ dep, const uint32_t* __restrict__ used,
+                              uint32_t n_slots, const uint32_t* __restrict__ home, unsigned long long* node,
+                              const uint64_t* __restrict__ row_off, const uint32_t* __restrict__ row_len,
+                              const uint32_t* __restrict__ used_cnt, const uint32_t* __restrict__ pool_col,
+                              const uint64_t* __restrict__ pool_tag, unsigned long long* hset, uint64_t hmask,
+                              uint32_t* result, Cand* cand, unsigned long long* ncand) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t d = dep[i], u = used[i];
+    const unsigned long long wd = node[d];
+    if ((wd & kVMask) == 0 || word_state(wd) != FGI_COMPUTING) {   // Computed.cs:351-364
+        result[i] = FGI_USED_DROPPED;
+        return;
+    }
+    const unsigned long long wu = node[u];
+    if ((wu & kVMask) == 0 || word_state(wu) == FGI_INVALIDATED) {  // Computed.cs:376-378
+        atomicOr(node + d, kW_IOSO);
+        result[i] = FGI_USED_INVALIDATED;
+        return;
+    }
+    if (word_state(wu) == FGI_COMPUTING) {                           // Computed.cs:374-375
+        result[i] = FGI_USED_ESTATE;
+        return;
+    }
+    result[i] = FGI_USED_ADDED;                                      // Computed.cs:381-383
+    // set semantics: (u, d) within this batch ...
+    const unsigned long long key = ((unsigned long long)u << 32) | d;
+    uint64_t p = sm64(key) & hmask;
+    while (true) {
+        const unsigned long long prev = atomicCAS(hset + p, ~0ull, key);
+        if (prev == ~0ull) break;
+        if (prev == key) return;
+        p = (p + 1) & hmask;
+    }
+    const uint32_t ds = home_of(d, n_slots, home);
+    const uint64_t tag = wd & kVMask;
+    // ... and across batches: only a dependant that already captured deps can repeat one
+    if (used_cnt[d]) {
+        const uint64_t o = row_off[u];
+        const uint32_t len = row_len[u];
+        for (uint32_t k = 0; k < len; ++k)
+            if (pool_col[o + k] == ds && pool_tag[o + k] == tag) return;
+    }
+    const unsigned long long c = atomicAdd(ncand, 1ull);
+    cand[c] = Cand{u, d, ds, 0, tag};
+}
+
+__global__ void k_au_reserve(uint64_t nc, const Cand* __restrict__ cand, const uint64_t* __restrict__ row_off,
+                             uint32_t* row_len, const uint32_t* __restrict__ row_cap, uint32_t* used_cnt,
+                             uint32_t* pool_col, uint64_t* pool_tag, uint32_t* pend_pos, uint32_t* ovf_rows,
+                             unsigned long long* cnt /*[0] pending, [1] overflow rows*/) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nc) return;
+    const Cand c = cand[i];
+    const uint32_t pos = atomicAdd(&row_len[c.used], 1u);
+    const uint32_t cap = row_cap[c.used];
+    atomicAdd(&used_cnt[c.dep_handle], 1u);                          // dependant._used.Add (365-366)
+    if (pos < cap) {
+        pool_col[row_off[c.used] + pos] = c.dep_slot;
+        pool_tag[row_off[c.used] + pos] = c.tag;
+        pend_pos[i] = FGI_NONE;
+    } else {
+        pend_pos[i] = pos;
+        atomicAdd(&cnt[0], 1ull);
+        if (pos == cap) ovf_rows[atomicAdd(&cnt[1], 1ull)] = c.used;
+    }
+}
+
+__device__ __forceinline__ uint32_t grow_cap(uint32_t need) {
+    const uint64_t c = (uint64_t)need + (need >> 1);
+    return (uint32_t)(c < 4 ? 4 : (c > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : c));
+}
+
+__global__ void k_au_size(uint64_t no, const uint32_t* __restrict__ ovf_rows, const uint32_t* __restrict__ row_len,
+                          unsigned long long* sum) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < no) atomicAdd(sum, (unsigned long long)grow_cap(row_len[ovf_rows[i]]));
+}
+
+// one wave per overflowing row: allocate a larger run at the pool top and move the old entries
+__global__ void k_au_relocate(uint64_t no, const uint32_t* __restrict__ ovf_rows, uint64_t* row_off,
+                              const uint32_t* __restrict__ row_len, uint32_t* row_cap, uint32_t* pool_col,
+                              uint64_t* pool_tag, unsigned long long* top) {
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    if (wave >= no) return;
+    const uint32_t u = ovf_rows[wave];
+    const uint32_t ncap = grow_cap(row_len[u]);
+    unsigned long long base = 0;
+    if (lane == 0) base = atomicAdd(top, (unsigned long long)ncap);
+    base = __shfl(base, 0, 64);
+    const uint64_t o = row_off[u];
+    const uint32_t old_cap = row_cap[u];
+    for (uint32_t k = lane; k < old_cap; k += 64) {
+        pool_col[base + k] = pool_col[o + k];
+        pool_tag[base + k] = pool_tag[o + k];
+    }
+    if (lane == 0) {
+        row_off[u] = base;
+        row_cap[u] = ncap;
+    }
+}
+
+__global__ void k_au_pending(uint64_t nc, const Cand* __restrict__ cand, const uint32_t* __restrict__ pend_pos,
+                             const uint64_t* __restrict__ row_off, uint32_t* pool_col, uint64_t* pool_tag) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nc || pend_pos[i] == FGI_NONE) return;
+    const Cand c = cand[i];
+    pool_col[row_off[c.used] + pend_pos[i]] = c.dep_slot;
+    pool_tag[row_off[c.used] + pend_pos[i]] = c.tag;
+}
+
+// ---- set_output ------------------------------------------------------------------------------
+__global__ void k_set_output(uint32_t n, const uint32_t* __restrict__ h, uint32_t n_handles, unsigned long long* node,
+                             uint8_t* out_set, uint32_t* roots, unsigned long long* nroots) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    uint8_t set = 0;
+    const uint32_t x = h[i];
+    if (x < n_handles) {
+        unsigned long long w = node[x];
+        while ((w & kVMask) != 0 && word_state(w) == FGI_COMPUTING) {      // Computed.cs:145-146
+            const unsigned long long nw = (w & ~(kStateBits | kW_IOSO)) | kW_Consistent;   // 148
+            const unsigned long long prev = atomicCAS(node + x, w, nw);
+            if (prev == w) {
+                set = 1;
+                if (w & kW_IOSO) roots[atomicAdd(nroots, 1ull)] = x;     // 150-156
+                break;
+            }
+            w = prev;
+        }
+    }
+    out_set[i] = set;
+}
+
+// ---- prune -----------------------------------------------------------------------------------
+// keep(h): 0 = drop the whole row, 1 = PruneUsedBy filter, 2 = keep all
+__device__ __forceinline__ int prune_mode(uint32_t h, uint32_t n_slots, unsigned long long w) {
+    if (!word_is_current(w)) return 0;                 // Invalidated / empty: `_usedBy` cleared (217)
+    if (h < n_slots && word_state(w) == FGI_CONSISTENT) return 1;   // registered Consistent (ComputedGraphPruner.cs:87-90)
+    return 2;                                          // Computing, or detached (not in the registry)
+}
+
+__device__ __forceinline__ bool edge_live(const unsigned long long* node, uint32_t dst, uint64_t tag) {
+    const unsigned long long w = node[dst];              // Computed.cs:412-413
+    return word_is_current(w) && (w & kVMask) == tag;
+}
+
+__global__ void k_prune_count(uint32_t n, uint32_t n_slots, const unsigned long long* node,
+                              const uint64_t* __restrict__ row_off, const uint32_t* __restrict__ row_len,
+                              const uint32_t* __restrict__ pool_col, const uint64_t* __restrict__ pool_tag,
+                              uint32_t* newlen, unsigned long long* st /*[0] old,[1] new*/) {
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    unsigned long long old_e = 0, new_e = 0;
+    for (uint64_t h = wave; h < n; h += nw) {
+        const unsigned long long w = node[h];
+        const int mode = prune_mode((uint32_t)h, n_slots, w);
+        const uint32_t len = row_len[h];
+        uint32_t kept = 0;
+        if (mode == 2) {
+            kept = len;
+        } else if (mode == 1) {
+            const uint64_t o = row_off[h];
+            for (uint32_t k = lane; k < len; k += 64)
+                if (edge_live(node, pool_col[o + k], pool_tag[o + k])) ++kept;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) kept += __shfl_xor(kept, d, 64);
+            old_e += len;
+            new_e += kept;
+        }
+        if (lane == 0) newlen[h] = kept;
+    }
+    if (lane == 0) {
+        if (old_e) atomicAdd(&st[0], old_e);
+        if (new_e) atomicAdd(&st[1], new_e);
+    }
+}
+
+__global__ void k_prune_scatter(uint32_t n, uint32_t n_slots, const unsigned long long* node,
+                                const uint64_t* __restrict__ row_off, const uint32_t* __restrict__ row_len,
+                                const uint32_t* __restrict__ pool_col, const uint64_t* __restrict__ pool_tag,
+                                const uint64_t* __restrict__ new_off, uint32_t* ncol, uint64_t* ntag) {
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t h = wave; h < n; h += nw) {
+        const int mode = prune_mode((uint32_t)h, n_slots, node[h]);
+        if (mode == 0) continue;
+        const uint32_t len = row_len[h];
+        const uint64_t o = row_off[h];
+        uint64_t dst = new_off[h];
+        for (uint32_t base = 0; base < len; base += 64) {
+            const uint32_t k = base + lane;
+            uint32_t col = 0;
+            uint64_t tag = 0;
+            bool keep = false;
+            if (k < len) {
+                col = pool_col[o + k];
+                tag = pool_tag[o + k];
+                keep = (mode == 2) || edge_live(node, col, tag);
+            }
+            const unsigned long long mask = __ballot(keep);
+            const uint32_t before = __popcll(mask & ((1ull << lane) - 1ull));
+            if (keep) {
+                ncol[dst + before] = col;
+                ntag[dst + before] = tag;
+            }
+            dst += __popcll(mask);
+        }
+    }
+}
+
+__global__ void k_prune_rows(uint32_t n, const uint64_t* __restrict__ new_off, const uint32_t* __restrict__ newlen,
+                             uint64_t* row_off, uint32_t* row_len, uint32_t* row_cap) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= n) return;
+    row_off[h] = new_off[h];
+    row_len[h] = newlen[h];
+    row_cap[h] = newlen[h];
+}
+
+__global__ void k_invalidate_all_roots(uint32_t n_slots, const unsigned long long* node, uint32_t* roots,
+                                       unsigned long long* cnt) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < n_slots && word_is_current(node[s])) roots[atomicAdd(cnt, 1ull)] = s;
+}
+
+inline uint32_t nblk(uint64_t n, uint32_t b = 256) { return (uint32_t)((n + b - 1) / b); }
+
+template <class T>
+fgi_status h2d(fgi_graph* g, T* dst, const T* src, size_t count) {
+    if (count == 0) return FGI_OK;
+    FGI_HIP(g, hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyHostToDevice, g->stream));
+    return FGI_OK;
+}
+template <class T>
+fgi_status d2h(fgi_graph* g, T* dst, const T* src, size_t count) {
+    if (count == 0) return FGI_OK;
+    FGI_HIP(g, hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyDeviceToHost, g->stream));
+    FGI_HIP(g, hipStreamSynchronize(g->stream));
+    return FGI_OK;
+}
+
+// gather all live edges (rows of current nodes) into fresh device arrays keys/tags
+fgi_status gather_live(fgi_graph* g, Tmp& tk, Tmp& tt, uint64_t** keys, uint64_t** tags, uint64_t extra,
+                       uint64_t* out_m) {
+    const uint32_t H = g->n_handles;
+    Tmp tl, to, ts;
+    uint32_t* live;
+    uint64_t* off;
+    FGI_TRY(tmalloc(g, tl, &live, H));
+    FGI_TRY(tmalloc(g, to, &off, (size_t)H + 1));
+    hipLaunchKernelGGL(k_live_len, dim3(nblk(H)), dim3(256), 0, g->stream, H,
+                       reinterpret_cast<const unsigned long long*>(g->node), g->row_len, live);
+    size_t tb = 0;
+    FGI_HIP(g, rocprim::exclusive_scan(nullptr, tb, live, off, (uint64_t)0, (size_t)H + 0, rocprim::plus<uint64_t>(),
+                                       g->stream));
+    void* tmp;
+    FGI_TRY(tmalloc(g, ts, reinterpret_cast<char**>(&tmp), tb));
+    FGI_HIP(g, rocprim::exclusive_scan(tmp, tb, live, off, (uint64_t)0, (size_t)H, rocprim::plus<uint64_t>(), g->stream));
+    uint64_t last_off = 0;
+    uint32_t last_len = 0;
+    FGI_TRY(d2h(g, &last_off, off + H - 1, 1));
+    FGI_TRY(d2h(g, &last_len, live + H - 1, 1));
+    const uint64_t m = last_off + last_len;
+    FGI_TRY(tmalloc(g, tk, keys, m + extra));
+    FGI_TRY(tmalloc(g, tt, tags, m + extra));
+    if (m)
+        hipLaunchKernelGGL(k_gather_live, dim3(std::min<uint64_t>(nblk((uint64_t)H * 64), 65536)), dim3(256), 0,
+                           g->stream, H, live, off, g->row_off, g->pool_col, g->pool_tag, *keys, *tags);
+    FGI_HIP(g, hipGetLastError());
+    *out_m = m;
+    return FGI_OK;
+}
+
+}  // namespace
+
+fgi_status ensure_cstart(fgi_graph* g, uint64_t total_edges) {
+    const uint64_t need = total_edges / kChunk + 4;
+    if (g->cstart_cap >= need) return FGI_OK;
+    dfree(g->cstart);
+    const uint64_t cap = std::max<uint64_t>(need, g->cstart_cap * 3 / 2);
+    FGI_TRY(dmalloc(g, &g->cstart, cap));
+    g->cstart_cap = cap;
+    return FGI_OK;
+}
+
+fgi_status ensure_pool(fgi_graph* g, uint64_t entries) {
+    if (g->pool_cap >= entries && g->pool_col) return FGI_OK;
+    const uint64_t cap = std::max<uint64_t>({entries, g->pool_cap + g->pool_cap / 2, (uint64_t)1024});
+    uint32_t* col = nullptr;
+    uint64_t* tag = nullptr;
+    FGI_TRY(dmalloc(g, &col, cap));
+    fgi_status st = dmalloc(g, &tag, cap);
+    if (st != FGI_OK) {
+        hipFree(col);
+        return st;
+    }
+    if (g->pool_top) {
+        FGI_HIP(g, hipMemcpyAsync(col, g->pool_col, g->pool_top * sizeof(uint32_t), hipMemcpyDeviceToDevice, g->stream));
+        FGI_HIP(g, hipMemcpyAsync(tag, g->pool_tag, g->pool_top * sizeof(uint64_t), hipMemcpyDeviceToDevice, g->stream));
+        FGI_HIP(g, hipStreamSynchronize(g->stream));
+    }
+    dfree(g->pool_col);
+    dfree(g->pool_tag);
+    g->pool_col = col;
+    g->pool_tag = tag;
+    g->pool_cap = cap;
+    return ensure_cstart(g, cap);
+}
+
+fgi_status build_rows_from_keys(fgi_graph* g, uint64_t m, uint64_t* keys, uint64_t* tags, uint64_t ver_seed,
+                                uint32_t stale_pct, uint64_t stale_seed) {
+    hipStream_t s = g->stream;
+    const uint32_t H = g->n_handles;
+    // reset all rows (the pool is rebuilt from scratch)
+    FGI_HIP(g, hipMemsetAsync(g->row_off, 0, (size_t)H * sizeof(uint64_t), s));
+    FGI_HIP(g, hipMemsetAsync(g->row_len, 0, (size_t)H * sizeof(uint32_t), s));
+    FGI_HIP(g, hipMemsetAsync(g->row_cap, 0, (size_t)H * sizeof(uint32_t), s));
+    FGI_HIP(g, hipMemsetAsync(g->used_cnt, 0, (size_t)H * sizeof(uint32_t), s));
+    g->pool_top = 0;
+    g->pool_epoch++;
+    if (m == 0) return FGI_OK;
+    if (m >= 0xFFFFFFF0ull) return set_err(g, FGI_ENOTSUP, "more than 2^32 edges on one device");
+    // 1. sort by (used, dependant) [, tag as payload]
+    Tmp tk2, tt2, ttmp;
+    uint64_t *k2 = nullptr, *t2 = nullptr;
+    FGI_TRY(tmalloc(g, tk2, &k2, m));
+    if (tags) FGI_TRY(tmalloc(g, tt2, &t2, m));
+    size_t tb = 0;
+    if (tags)
+        FGI_HIP(g, rocprim::radix_sort_pairs(nullptr, tb, keys, k2, tags, t2, (size_t)m, 0, 64, s));
+    else
+        FGI_HIP(g, rocprim::radix_sort_keys(nullptr, tb, keys, k2, (size_t)m, 0, 64, s));
+    char* tmp;
+    FGI_TRY(tmalloc(g, ttmp, &tmp, tb));
+    if (tags)
+        FGI_HIP(g, rocprim::radix_sort_pairs(tmp, tb, keys, k2, tags, t2, (size_t)m, 0, 64, s));
+    else
+        FGI_HIP(g, rocprim::radix_sort_keys(tmp, tb, keys, k2, (size_t)m, 0, 64, s));
+    // 2. set semantics: mark the first of each (used, dependant, tag)
+    Tmp tkeep, tpos, tsc;
+    uint32_t *keep, *pos;
+    FGI_TRY(tmalloc(g, tkeep, &keep, m));
+    FGI_TRY(tmalloc(g, tpos, &pos, m));
+    hipLaunchKernelGGL(k_mark_unique, dim3(nblk(m)), dim3(256), 0, s, m, k2, t2, keep);
+    size_t sb = 0;
+    FGI_HIP(g, rocprim::exclusive_scan(nullptr, sb, keep, pos, 0u, (size_t)m, rocprim::plus<uint32_t>(), s));
+    char* stmp;
+    FGI_TRY(tmalloc(g, tsc, &stmp, sb));
+    FGI_HIP(g, rocprim::exclusive_scan(stmp, sb, keep, pos, 0u, (size_t)m, rocprim::plus<uint32_t>(), s));
+    uint32_t lastp = 0, lastk = 0;
+    FGI_TRY(d2h(g, &lastp, pos + m - 1, 1));
+    FGI_TRY(d2h(g, &lastk, keep + m - 1, 1));
+    const uint64_t total = (uint64_t)lastp + lastk;
+    // validate handles of the sorted keys: largest used handle is in the last key
+    uint64_t maxkey = 0;
+    FGI_TRY(d2h(g, &maxkey, k2 + m - 1, 1));
+    if ((maxkey >> 32) >= H) return set_err(g, FGI_EINVAL, "used handle %u out of range", (unsigned)(maxkey >> 32));
+    FGI_TRY(ensure_pool(g, total));
+    hipLaunchKernelGGL(k_scatter_rows, dim3(nblk(m)), dim3(256), 0, s, m, k2, t2, keep, pos, ver_seed, stale_pct,
+                       stale_seed, g->pool_col, g->pool_tag, g->row_off, g->row_len, g->used_cnt,
+                       reinterpret_cast<const unsigned long long*>(g->node), g->n_slots);
+    hipLaunchKernelGGL(k_fix_rows, dim3(nblk(H)), dim3(256), 0, s, H, g->row_off, g->row_len, g->row_cap);
+    FGI_HIP(g, hipGetLastError());
+    FGI_HIP(g, hipStreamSynchronize(s));
+    g->pool_top = total;
+    FGI_HIP(g, hipMemcpy(g->pool_top_dev, &g->pool_top, sizeof(uint64_t), hipMemcpyHostToDevice));
+    return FGI_OK;
+}
+
+}  // namespace fgi
+
+using namespace fgi;
+
+extern "C" {
+
+fgi_status fgi_version(uint32_t* major, uint32_t* minor) {
+    if (major) *major = 0;
+    if (minor) *minor = 1;
+    return FGI_OK;
+}
+
+const char* fgi_last_error(const fgi_graph* g) { return g ? g->err.c_str() : "null graph"; }
+
+fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
+    if (!cfg || !out || cfg->struct_size < sizeof(fgi_config) || cfg->n_slots == 0) return FGI_EINVAL;
+    if ((uint64_t)cfg->n_slots + cfg->n_detached >= 0xFFFFFFF0ull) return FGI_EINVAL;
+    *out = nullptr;
+    fgi_graph* g = new fgi_graph();
+    g->device = cfg->device;
+    g->n_slots = cfg->n_slots;
+    g->n_detached = cfg->n_detached;
+    g->n_handles = cfg->n_slots + cfg->n_detached;
+    g->rank = cfg->rank;
+    g->world = cfg->world > 0 ? cfg->world : 1;
+    auto fail = [&](fgi_status st) {
+        fgi_destroy(g);
+        return st;
+    };
+    if (hipSetDevice(g->device) != hipSuccess) return fail(FGI_EDEVICE);
+    if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) return fail(FGI_EDEVICE);
+    const size_t H = g->n_handles;
+    if (dmalloc(g, &g->node, H) || dmalloc(g, &g->row_off, H) || dmalloc(g, &g->row_len, H) ||
+        dmalloc(g, &g->row_cap, H) || dmalloc(g, &g->used_cnt, H) || dmalloc(g, &g->home, g->n_detached + 1) ||
+        dmalloc(g, &g->inv, H) || dmalloc(g, &g->fr_off[0], H) || dmalloc(g, &g->fr_off[1], H) ||
+        dmalloc(g, &g->fr_len[0], H) || dmalloc(g, &g->fr_len[1], H) || dmalloc(g, &g->escan, H) ||
+        dmalloc(g, &g->partials, kScanBlocks) || dmalloc(g, &g->ctr, 1) || dmalloc(g, &g->misc_dev, 16) ||
+        dmalloc(g, &g->pool_top_dev, 1))
+        return fail(FGI_ENOMEM);
+    if (hipHostMalloc(reinterpret_cast<void**>(&g->ctr_host), sizeof(WaveCtr)) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&g->misc_host), 16 * sizeof(unsigned long long)) != hipSuccess)
+        return fail(FGI_ENOMEM);
+    hipMemset(g->node, 0, H * sizeof(uint64_t));
+    hipMemset(g->row_off, 0, H * sizeof(uint64_t));
+    hipMemset(g->row_len, 0, H * sizeof(uint32_t));
+    hipMemset(g->row_cap, 0, H * sizeof(uint32_t));
+    hipMemset(g->used_cnt, 0, H * sizeof(uint32_t));
+    hipMemset(g->pool_top_dev, 0, sizeof(unsigned long long));
+    if (hipEventCreate(&g->ev_w0) != hipSuccess || hipEventCreate(&g->ev_w1) != hipSuccess) return fail(FGI_EDEVICE);
+    g->free_detached.reserve(g->n_detached);
+    for (uint32_t i = g->n_detached; i > 0; --i) g->free_detached.push_back(g->n_slots + i - 1);
+    if (ensure_pool(g, std::max<uint64_t>(cfg->edge_capacity, 1024)) != FGI_OK) return fail(FGI_ENOMEM);
+    if (hipDeviceSynchronize() != hipSuccess) return fail(FGI_EDEVICE);
+    *out = g;
+    return FGI_OK;
+}
+
+fgi_status fgi_destroy(fgi_graph* g) {
+    if (!g) return FGI_OK;
+    hipSetDevice(g->device);
+    if (g->stream) hipStreamSynchronize(g->stream);
+    fgi::part_destroy(g);
+    dfree(g->node);
+    dfree(g->row_off);
+    dfree(g->row_len);
+    dfree(g->row_cap);
+    dfree(g->used_cnt);
+    dfree(g->home);
+    dfree(g->pool_col);
+    dfree(g->pool_tag);
+    dfree(g->pool_top_dev);
+    dfree(g->inv);
+    for (int i = 0; i < 2; ++i) {
+        dfree(g->fr_off[i]);
+        dfree(g->fr_len[i]);
+    }
+    dfree(g->escan);
+    dfree(g->cstart);
+    dfree(g->partials);
+    dfree(g->ctr);
+    dfree(g->roots_buf);
+    dfree(g->imm_buf);
+    dfree(g->misc_dev);
+    dfree(g->snap_node);
+    dfree(g->snap_row_off);
+    dfree(g->snap_row_len);
+    dfree(g->snap_row_cap);
+    dfree(g->snap_used);
+    if (g->scratch) hipFree(g->scratch);
+    if (g->ctr_host) hipHostFree(g->ctr_host);
+    if (g->misc_host) hipHostFree(g->misc_host);
+    for (hipEvent_t e : g->ev) hipEventDestroy(e);
+    if (g->ev_w0) hipEventDestroy(g->ev_w0);
+    if (g->ev_w1) hipEventDestroy(g->ev_w1);
+    if (g->stream) hipStreamDestroy(g->stream);
+    delete g;
+    return FGI_OK;
+}
+
+fgi_status fgi_stream(fgi_graph* g, void** stream) {
+    if (!g || !stream) return FGI_EINVAL;
+    *stream = g->stream;
+    return FGI_OK;
+}
+
+fgi_status fgi_register_nodes(fgi_graph* g, uint32_t n, const uint32_t* slot, const uint64_t* version,
+                              const uint32_t* state_flags) {
+    if (!g || (n && (!slot || !version))) return FGI_EINVAL;
+    for (uint32_t i = 0; i < n; ++i) {
+        if (slot[i] >= g->n_slots) return set_err(g, FGI_EINVAL, "slot %u out of range", slot[i]);
+        if (version[i] > kVMask) return set_err(g, FGI_EINVAL, "version of slot %u exceeds 2^56-1", slot[i]);
+        if (state_flags && (state_flags[i] & 3u) == 3u) return set_err(g, FGI_EINVAL, "bad state for slot %u", slot[i]);
+    }
+    if (n == 0) return FGI_OK;
+    hipSetDevice(g->device);
+    Tmp ts, tv, tf;
+    uint32_t *ds, *df = nullptr;
+    uint64_t* dv;
+    FGI_TRY(tmalloc(g, ts, &ds, n));
+    FGI_TRY(tmalloc(g, tv, &dv, n));
+    if (state_flags) FGI_TRY(tmalloc(g, tf, &df, n));
+    FGI_TRY(h2d(g, ds, slot, n));
+    FGI_TRY(h2d(g, dv, version, n));
+    if (state_flags) FGI_TRY(h2d(g, df, state_flags, n));
+    FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, sizeof(unsigned long long), g->stream));
+    hipLaunchKernelGGL(k_register, dim3(nblk(n)), dim3(256), 0, g->stream, n, ds, dv, df,
+                       reinterpret_cast<unsigned long long*>(g->node), g->row_len, g->misc_dev);
+    FGI_HIP(g, hipGetLastError());
+    unsigned long long bad = 0;
+    FGI_TRY(d2h(g, &bad, g->misc_dev, 1));
+    if (bad) return set_err(g, FGI_ESTATE, "%llu slots already had a current node", bad);
+    return FGI_OK;
+}
+
+fgi_status fgi_load_edges(fgi_graph* g, uint64_t m, const uint32_t* used, const uint32_t* dependant_slot,
+                          const uint64_t* tag) {
+    if (!g || (m && (!used || !dependant_slot || !tag))) return FGI_EINVAL;
+    for (uint64_t e = 0; e < m; ++e) {
+        if (used[e] >= g->n_handles || dependant_slot[e] >= g->n_slots)
+            return set_err(g, FGI_EINVAL, "edge %llu out of range", (unsigned long long)e);
+        if (tag[e] == 0) return set_err(g, FGI_EINVAL, "edge %llu has tag 0 (LTags are positive)", (unsigned long long)e);
+    }
+    hipSetDevice(g->device);
+    // existing live rows + the new entries, rebuilt in one sort (set semantics across both)
+    Tmp tk, tt;
+    uint64_t *keys, *tags, m0 = 0;
+    FGI_TRY(gather_live(g, tk, tt, &keys, &tags, m, &m0));
+    if (m) {
+        std::vector<uint64_t> hk(m);
+        for (uint64_t e = 0; e < m; ++e) hk[e] = ((uint64_t)used[e] << 32) | dependant_slot[e];
+        FGI_TRY(h2d(g, keys + m0, hk.data(), m));
+        FGI_TRY(h2d(g, tags + m0, tag, m));
+    }
+    return build_rows_from_keys(g, m0 + m, keys, tags, 0, 0, 0);
+}
+
+fgi_status fgi_get_state(fgi_graph* g, uint32_t n, const uint32_t* handle, uint64_t* version, uint32_t* state_flags) {
+    if (!g || (n && !handle)) return FGI_EINVAL;
+    for (uint32_t i = 0; i < n; ++i)
+        if (handle[i] >= g->n_handles) return set_err(g, FGI_EINVAL, "handle %u out of range", handle[i]);
+    if (n == 0) return FGI_OK;
+    hipSetDevice(g->device);
+    Tmp th, tw;
+    uint32_t* dh;
+    unsigned long long* dw;
+    FGI_TRY(tmalloc(g, th, &dh, n));
+    FGI_TRY(tmalloc(g, tw, &dw, n));
+    FGI_TRY(h2d(g, dh, handle, n));
+    hipLaunchKernelGGL(k_gather_words, dim3(nblk(n)), dim3(256), 0, g->stream, n, dh,
+                       reinterpret_cast<const unsigned long long*>(g->node), dw);
+    std::vector<unsigned long long> w(n);
+    FGI_TRY(d2h(g, w.data(), dw, n));
+    for (uint32_t i = 0; i < n; ++i) {
+        if (version) version[i] = w[i] & kVMask;
+        if (state_flags) state_flags[i] = word_to_flags(w[i]);
+    }
+    return FGI_OK;
+}
+
+fgi_status fgi_dump_states(fgi_graph* g, uint64_t* version, uint32_t* state_flags) {
+    if (!g) return FGI_EINVAL;
+    hipSetDevice(g->device);
+    std::vector<uint64_t> w(g->n_handles);
+    FGI_TRY(d2h(g, w.data(), g->node, g->n_handles));
+    for (uint32_t h = 0; h < g->n_handles; ++h) {
+        if (version) version[h] = w[h] & kVMask;
+        if (state_flags) state_flags[h] = word_to_flags(w[h]);
+    }
+    return FGI_OK;
+}
+
+fgi_status fgi_get_used_by(fgi_graph* g, uint32_t handle, uint32_t* dep, uint64_t* tag, uint64_t cap, uint64_t* out_n) {
+    if (!g || handle >= g->n_handles) return FGI_EINVAL;
+    hipSetDevice(g->device);
+    uint64_t w = 0, off = 0;
+    uint32_t len = 0;
+    FGI_TRY(d2h(g, &w, g->node + handle, 1));
+    FGI_TRY(d2h(g, &off, g->row_off + handle, 1));
+    FGI_TRY(d2h(g, &len, g->row_len + handle, 1));
+    if (!word_is_current(w)) len = 0;   // `_usedBy` of an Invalidated node is cleared (Computed.cs:217)
+    if (out_n) *out_n = len;
+    if (len > cap) return FGI_ECAPACITY;
+    if (dep) FGI_TRY(d2h(g, dep, g->pool_col + off, len));
+    if (tag) FGI_TRY(d2h(g, tag, g->pool_tag + off, len));
+    return FGI_OK;
+}
+
+fgi_status fgi_get_used_count(fgi_graph* g, uint32_t handle, uint32_t* out) {
+    if (!g || !out || handle >= g->n_handles) return FGI_EINVAL;
+    hipSetDevice(g->device);
+    uint64_t w = 0;
+    uint32_t c = 0;
+    FGI_TRY(d2h(g, &w, g->node + handle, 1));
+    FGI_TRY(d2h(g, &c, g->used_cnt + handle, 1));
+    *out = word_is_current(w) ? c : 0;   // `_used` is cleared on invalidation (Computed.cs:210-211)
+    return FGI_OK;
+}
+
+fgi_status fgi_get_degrees(fgi_graph* g, uint32_t* degree, uint64_t* total) {
+    if (!g) return FGI_EINVAL;
+    hipSetDevice(g->device);
+    const uint32_t H = g->n_handles;
+    std::vector<uint64_t> w(H);
+    std::vector<uint32_t> len(H);
+    FGI_TRY(d2h(g, w.data(), g->node, H));
+    FGI_TRY(d2h(g, len.data(), g->row_len, H));
+    uint64_t t = 0;
+    for (uint32_t h = 0; h < H; ++h) {
+        const uint32_t d = word_is_current(w[h]) ? len[h] : 0;
+        if (degree) degree[h] = d;
+        t += d;
+    }
+    if (total) *total = t;
+    return FGI_OK;
+}
+
+fgi_status fgi_export_edges(fgi_graph* g, uint32_t* used, uint32_t* dep, uint64_t* tag, uint64_t cap, uint64_t* out_n) {
+    if (!g) return FGI_EINVAL;
+    hipSetDevice(g->device);
+    Tmp tk, tt;
+    uint64_t *keys, *tags, m = 0;
+    FGI_TRY(gather_live(g, tk, tt, &keys, &tags, 0, &m));
+    if (out_n) *out_n = m;
+    if (m > cap) return FGI_ECAPACITY;
+    std::vector<uint64_t> hk(m);
+    FGI_TRY(d2h(g, hk.data(), keys, m));
+    if (tag) FGI_TRY(d2h(g, tag, tags, m));
+    for (uint64_t e = 0; e < m; ++e) {
+        if (used) used[e] = (uint32_t)(hk[e] >> 32);
+        if (dep) dep[e] = (uint32_t)hk[e];
+    }
+    return FGI_OK;
+}
+
+fgi_status fgi_snapshot(fgi_graph* g) {
+    if (!g) return FGI_EINVAL;
+    hipSetDevice(g->device);
+    const size_t H = g->n_handles;
+    if (!g->snap_node) {
+        if (dmalloc(g, &g->snap_node, H) || dmalloc(g, &g->snap_row_off, H) || dmalloc(g, &g->snap_row_len, H) ||
+            dmalloc(g, &g->snap_row_cap, H) || dmalloc(g, &g->snap_used, H))
+            return FGI_ENOMEM;
+    }
+    hipStream_t s = g->stream;
+    FGI_HIP(g, hipMemcpyAsync(g->snap_node, g->node, H * 8, hipMemcpyDeviceToDevice, s));
+    FGI_HIP(g, hipMemcpyAsync(g->snap_row_off, g->row_off, H * 8, hipMemcpyDeviceToDevice, s));
+    FGI_HIP(g, hipMemcpyAsync(g->snap_row_len, g->row_len, H * 4, hipMemcpyDeviceToDevice, s));
+    FGI_HIP(g, hipMemcpyAsync(g->snap_row_cap, g->row_cap, H * 4, hipMemcpyDeviceToDevice, s));
+    FGI_HIP(g, hipMemcpyAsync(g->snap_used, g->used_cnt, H * 4, hipMemcpyDeviceToDevice, s));
+    FGI_HIP(g, hipStreamSynchronize(s));
+    g->snap_epoch = g->pool_epoch;
+    return FGI_OK;
+}
+
+// Restores the node table; the edge pool is append-only between compactions, so the saved row
+// descriptors still address the saved rows unless fgi_prune / a bulk load ran in between.
+fgi_status fgi_restore(fgi_graph* g) {
+    if (!g || !g->snap_node) return FGI_EINVAL;
+    if (g->snap_epoch != g->pool_epoch) return set_err(g, FGI_ESTATE, "edge pool was rebuilt since the snapshot");
+    hipSetDevice(g->device);
+    const size_t H = g->n_handles;
+    hipStream_t s = g->stream;
+    FGI_HIP(g, hipMemcpyAsync(g->node, g->snap_node, H * 8, hipMemcpyDeviceToDevice, s));
+    FGI_HIP(g, hipMemcpyAsync(g->row_off, g->snap_row_off, H * 8, hipMemcpyDeviceToDevice, s));
+    FGI_HIP(g, hipMemcpyAsync(g->row_len, g->snap_row_len, H * 4, hipMemcpyDeviceToDevice, s));
+    FGI_HIP(g, hipMemcpyAsync(g->row_cap, g->snap_row_cap, H * 4, hipMemcpyDeviceToDevice, s));
+    FGI_HIP(g, hipMemcpyAsync(g->used_cnt, g->snap_used, H * 4, hipMemcpyDeviceToDevice, s));
+    FGI_HIP(g, hipStreamSynchronize(s));
+    return FGI_OK;
+}
+
+// ---- invalidation entry points ----------------------------------------------------------------
+static fgi_status stage_roots(fgi_graph* g, uint64_t n) {
+    if (g->roots_cap >= n && g->roots_buf) return FGI_OK;
+    dfree(g->roots_buf);
+    dfree(g->imm_buf);
+    const uint64_t cap = std::max<uint64_t>(n, 4096);
+    FGI_TRY(dmalloc(g, &g->roots_buf, cap));
+    FGI_TRY(dmalloc(g, &g->imm_buf, cap));
+    g->roots_cap = cap;
+    return FGI_OK;
+}
+
+static fgi_status copy_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n) {
+    const uint64_t n = g->last_wave_n;
+    if (out_n) *out_n = n;
+    if (!out_ids) return FGI_OK;
+    if (n > cap) return FGI_ECAPACITY;
+    return d2h(g, out_ids, g->inv, n);
+}
+
+fgi_status fgi_invalidate(fgi_graph* g, uint32_t n_roots, const uint32_t* roots, const uint8_t* immediately,
+                          uint32_t* out_ids, uint64_t cap, uint64_t* out_n, fgi_wave_stats* stats) {
+    if (!g || (n_roots && !roots)) return FGI_EINVAL;
+    hipSetDevice(g->device);
+    FGI_TRY(stage_roots(g, n_roots));
+    FGI_TRY(h2d(g, g->roots_buf, roots, n_roots));
+    if (immediately) FGI_TRY(h2d(g, g->imm_buf, immediately, n_roots));
+    FGI_TRY(run_wave(g, n_roots, g->roots_buf, immediately ? g->imm_buf : nullptr, stats));
+    return copy_ids(g, out_ids, cap, out_n);
+}
+
+fgi_status fgi_invalidate_dev(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
+                              uint32_t* out_ids_dev, uint64_t* out_n, fgi_wave_stats* stats) {
+    if (!g || (n_roots && !roots_dev)) return FGI_EINVAL;
+    hipSetDevice(g->device);
+    FGI_TRY(run_wave(g, n_roots, roots_dev, imm_dev, stats));
+    if (out_n) *out_n = g->last_wave_n;
+    if (out_ids_dev && g->last_wave_n) {
+        FGI_HIP(g, hipMemcpyAsync(out_ids_dev, g->inv, g->last_wave_n * 4, hipMemcpyDeviceToDevice, g->stream));
+        FGI_HIP(g, hipStreamSynchronize(g->stream));
+    }
+    return FGI_OK;
+}
+
+fgi_status fgi_wave_ids_dev(fgi_graph* g, const uint32_t** ids_dev, uint64_t* n) {
+    if (!g || !ids_dev) return FGI_EINVAL;
+    *ids_dev = g->inv;
+    if (n) *n = g->last_wave_n;
+    return FGI_OK;
+}
+
+fgi_status fgi_invalidate_all(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n, fgi_wave_stats* stats) {
+    if (!g) return FGI_EINVAL;
+    hipSetDevice(g->device);
+    FGI_TRY(stage_roots(g, g->n_slots));
+    FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, sizeof(unsigned long long), g->stream));
+    hipLaunchKernelGGL(k_invalidate_all_roots, dim3(nblk(g->n_slots)), dim3(256), 0, g->stream, g->n_slots,
+                       reinterpret_cast<const unsigned long long*>(g->node), g->roots_buf, g->misc_dev);
+    unsigned long long n = 0;
+    FGI_TRY(d2h(g, &n, g->misc_dev, 1));
+    FGI_TRY(run_wave(g, (uint32_t)n, g->roots_buf, nullptr, stats));
+    return copy_ids(g, out_ids, cap, out_n);
+}
+
+fgi_status fgi_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, const uint64_t* version,
+                             const uint8_t* has_delay, uint32_t* out_detached, fgi_wave_stats* stats) {
+    if (!g || (n && (!slot || !version))) return FGI_EINVAL;
+    if (n == 0) return FGI_OK;
+    {
+        std::vector<uint32_t> s(slot, slot + n);
+        std::sort(s.begin(), s.end());
+        for (uint32_t i = 0; i < n; ++i) {
+            if (s[i] >= g->n_slots) return set_err(g, FGI_EINVAL, "slot %u out of range", s[i]);
+            if (i && s[i] == s[i - 1]) return set_err(g, FGI_EINVAL, "slot %u repeated in one batch", s[i]);
+            if (version[i] == 0 || version[i] > kVMask) return set_err(g, FGI_EINVAL, "bad version at %u", i);
+        }
+    }
+    hipSetDevice(g->device);
+    hipStream_t st = g->stream;
+    Tmp ts, tv, td, tc, tr, tf, to;
+    uint32_t *ds, *droots, *dfree_h, *dout;
+    uint64_t* dv;
+    uint8_t *dd = nullptr, *dcls;
+    FGI_TRY(tmalloc(g, ts, &ds, n));
+    FGI_TRY(tmalloc(g, tv, &dv, n));
+    FGI_TRY(tmalloc(g, tc, &dcls, n));
+    FGI_TRY(tmalloc(g, tr, &droots, n));
+    FGI_TRY(tmalloc(g, to, &dout, n));
+    if (has_delay) {
+        FGI_TRY(tmalloc(g, td, &dd, n));
+        FGI_TRY(h2d(g, dd, has_delay, n));
+    }
+    FGI_TRY(h2d(g, ds, slot, n));
+    FGI_TRY(h2d(g, dv, version, n));
+    FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, 4 * sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_bc_classify, dim3(nblk(n)), dim3(256), 0, st, n, ds,
+                       reinterpret_cast<const unsigned long long*>(g->node), dcls, droots, g->misc_dev);
+    unsigned long long cnt[2];
+    FGI_TRY(d2h(g, cnt, g->misc_dev, 2));
+    if (cnt[1] > g->free_detached.size())
+        return set_err(g, FGI_ECAPACITY, "out of detached handles (%zu free, %llu needed)", g->free_detached.size(),
+                       cnt[1]);
+    // displacement cascade first (ComputedRegistry.cs:91-94), then detach + install
+    if (cnt[0]) FGI_TRY(run_wave(g, (uint32_t)cnt[0], droots, nullptr, stats));
+    std::vector<uint32_t> take(g->free_detached.end() - (ptrdiff_t)cnt[1], g->free_detached.end());
+    FGI_TRY(tmalloc(g, tf, &dfree_h, take.size() + 1));
+    FGI_TRY(h2d(g, dfree_h, take.data(), take.size()));
+    FGI_HIP(g, hipMemsetAsync(g->misc_dev + 2, 0, sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_bc_install, dim3(nblk(n)), dim3(256), 0, st, n, ds, dv, dd, dcls, dfree_h, g->misc_dev + 2,
+                       g->n_slots, reinterpret_cast<unsigned long long*>(g->node), g->row_off, g->row_len, g->row_cap,
+                       g->used_cnt, g->home, dout);
+    FGI_HIP(g, hipGetLastError());
+    std::vector<uint32_t> od(n);
+    FGI_TRY(d2h(g, od.data(), dout, n));
+    g->free_detached.resize(g->free_detached.size() - take.size());
+    if (out_detached) std::memcpy(out_detached, od.data(), n * sizeof(uint32_t));
+    return FGI_OK;
+}
+
+fgi_status fgi_add_used(fgi_graph* g, uint32_t n, const uint32_t* dependant, const uint32_t* used, uint32_t* out_result) {
+    if (!g || (n && (!dependant || !used))) return FGI_EINVAL;
+    for (uint32_t i = 0; i < n; ++i)
+        if (dependant[i] >= g->n_handles || used[i] >= g->n_handles)
+            return set_err(g, FGI_EINVAL, "handle out of range at %u", i);
+    if (n == 0) return FGI_OK;
+    hipSetDevice(g->device);
+    hipStream_t st = g->stream;
+    uint64_t hcap = 64;
+    while (hcap < 2ull * n) hcap <<= 1;
+    Tmp tdep, tuse, tres, thash, tcand, tpend, tovf;
+    uint32_t *ddep, *duse, *dres, *dpend, *dovf;
+    unsigned long long* dhash;
+    Cand* dcand;
+    FGI_TRY(tmalloc(g, tdep, &ddep, n));
+    FGI_TRY(tmalloc(g, tuse, &duse, n));
+    FGI_TRY(tmalloc(g, tres, &dres, n));
+    FGI_TRY(tmalloc(g, thash, &dhash, hcap));
+    FGI_TRY(tmalloc(g, tcand, &dcand, n));
+    FGI_TRY(tmalloc(g, tpend, &dpend, n));
+    FGI_TRY(tmalloc(g, tovf, &dovf, n));
+    FGI_TRY(h2d(g, ddep, dependant, n));
+    FGI_TRY(h2d(g, duse, used, n));
+    FGI_HIP(g, hipMemsetAsync(dhash, 0xFF, hcap * sizeof(unsigned long long), st));
+    FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, 8 * sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_au_classify, dim3(nblk(n)), dim3(256), 0, st, n, ddep, duse, g->n_slots, g->home,
+                       reinterpret_cast<unsigned long long*>(g->node), g->row_off, g->row_len, g->used_cnt, g->pool_col,
+                       g->pool_tag, dhash, hcap - 1, dres, dcand, g->misc_dev);
+    unsigned long long nc = 0;
+    FGI_TRY(d2h(g, &nc, g->misc_dev, 1));
+    if (nc) {
+        hipLaunchKernelGGL(k_au_reserve, dim3(nblk(nc)), dim3(256), 0, st, (uint64_t)nc, dcand, g->row_off, g->row_len,
+                           g->row_cap, g->used_cnt, g->pool_col, g->pool_tag, dpend, dovf, g->misc_dev + 1);
+        unsigned long long c2[2];
+        FGI_TRY(d2h(g, c2, g->misc_dev + 1, 2));
+        if (c2[1]) {   // some rows outgrew their capacity: relocate them to the pool top
+            hipLaunchKernelGGL(k_au_size, dim3(nblk(c2[1])), dim3(256), 0, st, (uint64_t)c2[1], dovf, g->row_len,
+                               g->misc_dev + 3);
+            unsigned long long need = 0;
+            FGI_TRY(d2h(g, &need, g->misc_dev + 3, 1));
+            FGI_TRY(ensure_pool(g, g->pool_top + need));
+            FGI_HIP(g, hipMemcpyAsync(g->pool_top_dev, &g->pool_top, sizeof(uint64_t), hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_au_relocate, dim3(nblk(c2[1] * 64)), dim3(256), 0, st, (uint64_t)c2[1], dovf,
+                               g->row_off, g->row_len, g->row_cap, g->pool_col, g->pool_tag, g->pool_top_dev);
+            hipLaunchKernelGGL(k_au_pending, dim3(nblk(nc)), dim3(256), 0, st, (uint64_t)nc, dcand, dpend, g->row_off,
+                               g->pool_col, g->pool_tag);
+            g->pool_top += need;
+            FGI_TRY(ensure_cstart(g, g->pool_top));
+        }
+    }
+    FGI_HIP(g, hipGetLastError());
+    if (out_result) FGI_TRY(d2h(g, out_result, dres, n));
+    else FGI_HIP(g, hipStreamSynchronize(st));
+    return FGI_OK;
+}
+
+fgi_status fgi_set_output(fgi_graph* g, uint32_t n, const uint32_t* handle, uint8_t* out_set, uint32_t* out_ids,
+                          uint64_t cap, uint64_t* out_n, fgi_wave_stats* stats) {
+    if (!g || (n && !handle)) return FGI_EINVAL;
+    if (out_n) *out_n = 0;
+    if (n == 0) return FGI_OK;
+    hipSetDevice(g->device);
+    hipStream_t st = g->stream;
+    Tmp th, ts, tr;
+    uint32_t *dh, *droots;
+    uint8_t* dset;
+    FGI_TRY(tmalloc(g, th, &dh, n));
+    FGI_TRY(tmalloc(g, ts, &dset, n));
+    FGI_TRY(tmalloc(g, tr, &droots, n));
+    FGI_TRY(h2d(g, dh, handle, n));
+    FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_set_output, dim3(nblk(n)), dim3(256), 0, st, n, dh, g->n_handles,
+                       reinterpret_cast<unsigned long long*>(g->node), dset, droots, g->misc_dev);
+    unsigned long long nr = 0;
+    FGI_TRY(d2h(g, &nr, g->misc_dev, 1));
+    if (out_set) FGI_TRY(d2h(g, out_set, dset, n));
+    g->last_wave_n = 0;
+    if (nr) FGI_TRY(run_wave(g, (uint32_t)nr, droots, nullptr, stats));   // Invalidate() (Computed.cs:153-156)
+    return copy_ids(g, out_ids, cap, out_n);
+}
+
+fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats) {
+    if (!g) return FGI_EINVAL;
+    hipSetDevice(g->device);
+    const auto t0 = std::chrono::steady_clock::now();
+    hipStream_t st = g->stream;
+    const uint32_t H = g->n_handles;
+    Tmp tl, to, ts;
+    uint32_t* newlen;
+    uint64_t* newoff;
+    FGI_TRY(tmalloc(g, tl, &newlen, H));
+    FGI_TRY(tmalloc(g, to, &newoff, H));
+    FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, 2 * sizeof(unsigned long long), st));
+    const uint32_t grid = std::min<uint64_t>(nblk((uint64_t)H * 64), 8192);
+    hipLaunchKernelGGL(k_prune_count, dim3(grid), dim3(256), 0, st, H, g->n_slots,
+                       reinterpret_cast<const unsigned long long*>(g->node), g->row_off, g->row_len, g->pool_col,
+                       g->pool_tag, newlen, g->misc_dev);
+    size_t tb = 0;
+    FGI_HIP(g, rocprim::exclusive_scan(nullptr, tb, newlen, newoff, (uint64_t)0, (size_t)H, rocprim::plus<uint64_t>(), st));
+    char* tmp;
+    FGI_TRY(tmalloc(g, ts, &tmp, tb));
+    FGI_HIP(g, rocprim::exclusive_scan(tmp, tb, newlen, newoff, (uint64_t)0, (size_t)H, rocprim::plus<uint64_t>(), st));
+    unsigned long long eo[2];
+    uint64_t last_off = 0;
+    uint32_t last_len = 0;
+    FGI_TRY(d2h(g, eo, g->misc_dev, 2));
+    FGI_TRY(d2h(g, &last_off, newoff + H - 1, 1));
+    FGI_TRY(d2h(g, &last_len, newlen + H - 1, 1));
+    const uint64_t total = last_off + last_len;
+    const uint64_t cap = std::max<uint64_t>(total, 1024);
+    uint32_t* ncol = nullptr;
+    uint64_t* ntag = nullptr;
+    FGI_TRY(dmalloc(g, &ncol, cap));
+    if (dmalloc(g, &ntag, cap) != FGI_OK) {
+        hipFree(ncol);
+        return FGI_ENOMEM;
+    }
+    hipLaunchKernelGGL(k_prune_scatter, dim3(grid), dim3(256), 0, st, H, g->n_slots,
+                       reinterpret_cast<const unsigned long long*>(g->node), g->row_off, g->row_len, g->pool_col,
+                       g->pool_tag, newoff, ncol, ntag);
+    hipLaunchKernelGGL(k_prune_rows, dim3(nblk(H)), dim3(256), 0, st, H, newoff, newlen, g->row_off, g->row_len,
+                       g->row_cap);
+    FGI_HIP(g, hipGetLastError());
+    FGI_HIP(g, hipStreamSynchronize(st));
+    if (stats) {
+        stats->old_edges = eo[0];
+        stats->new_edges = eo[1];
+        stats->pool_before = g->pool_top;
+        stats->pool_after = total;
+    }
+    dfree(g->pool_col);
+    dfree(g->pool_tag);
+    g->pool_col = ncol;
+    g->pool_tag = ntag;
+    g->pool_cap = cap;
+    g->pool_top = total;
+    g->pool_epoch++;
+    FGI_HIP(g, hipMemcpy(g->pool_top_dev, &g->pool_top, sizeof(uint64_t), hipMemcpyHostToDevice));
+    if (stats)
+        stats->kernel_ms =
+            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return FGI_OK;
+}
+
+fgi_status fgi_release(fgi_graph* g, uint32_t n, const uint32_t* handle) {
+    if (!g || (n && !handle)) return FGI_EINVAL;
+    hipSetDevice(g->device);
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t h = handle[i];
+        if (h < g->n_slots || h >= g->n_handles) return set_err(g, FGI_EINVAL, "handle %u is not detached", h);
+        if (std::find(g->free_detached.begin(), g->free_detached.end(), h) != g->free_detached.end())
+            return set_err(g, FGI_EINVAL, "handle %u released twice", h);
+        const uint64_t zero = 0;
+        const uint32_t z32 = 0;
+        FGI_TRY(h2d(g, g->node + h, &zero, 1));
+        FGI_TRY(h2d(g, g->row_len + h, &z32, 1));
+        FGI_TRY(h2d(g, g->row_cap + h, &z32, 1));
+        FGI_TRY(h2d(g, g->row_off + h, &zero, 1));
+        FGI_HIP(g, hipStreamSynchronize(g->stream));
+        g->free_detached.push_back(h);
+    }
+    return FGI_OK;
+}
+
+}  // extern "C"

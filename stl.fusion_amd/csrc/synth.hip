@@ -1,0 +1,129 @@
+// synth.hip — device generators for the benchmark workloads.
+// Same definitions as the CPU oracle's oracle/synth.cpp (checked equal in tests), written for the
+// device so a 256M-edge graph is generated and turned into rows in HBM in well under a second.
+#include <hip/hip_runtime.h>
+
+#include "fgi_internal.h"
+
+namespace fgi {
+namespace {
+
+__device__ __forceinline__ uint32_t scramble(uint64_t x, uint32_t scale, uint64_t seed) {
+    const uint64_t mask = (scale >= 64) ? ~0ull : ((1ull << scale) - 1);
+    const uint64_t k1 = sm64(seed ^ 0xA5A5A5A5A5A5A5A5ull) | 1ull;
+    const uint64_t k2 = sm64(seed ^ 0x5A5A5A5A5A5A5A5Aull) | 1ull;
+    const uint64_t c = sm64(seed ^ 0x0123456789ABCDEFull);
+    const uint32_t s1 = (scale + 1) / 2, s2 = scale / 2 ? scale / 2 : 1;
+    x = (x * k1) & mask;
+    x ^= x >> s1;
+    x = (x + c) & mask;
+    x = (x * k2) & mask;
+    x ^= x >> s2;
+    return (uint32_t)x;
+}
+
+__global__ void k_versions(uint32_t n, uint64_t seed, unsigned long long* node) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    if (s < n) node[s] = synth_version(seed, s) | kW_Consistent;
+}
+
+__global__ void k_gen_layered(uint32_t levels, uint32_t width, uint32_t fanout, uint64_t seed, uint64_t* keys) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t n = (uint64_t)(levels - 1) * width;
+    if (t >= n) return;
+    const uint32_t l = (uint32_t)(t / width) + 1, i = (uint32_t)(t % width);
+    uint32_t chosen[64];
+    uint32_t c = 0;
+    for (uint64_t attempt = 0; c < fanout; ++attempt) {
+        const uint64_t key = ((uint64_t)l << 56) ^ ((uint64_t)i << 20) ^ attempt;
+        const uint32_t j = (uint32_t)(sm64(seed ^ sm64(key)) % width);
+        bool dup = false;
+        for (uint32_t q = 0; q < c; ++q) dup |= (chosen[q] == j);
+        if (!dup) chosen[c++] = j;
+    }
+    const uint64_t d = (uint64_t)l * width + i;
+    for (uint32_t k = 0; k < fanout; ++k) {
+        const uint64_t s = (uint64_t)(l - 1) * width + chosen[k];
+        keys[t * fanout + k] = (s << 32) | d;
+    }
+}
+
+__global__ void k_gen_rmat(uint64_t m, uint32_t scale, uint64_t seed, uint64_t* keys) {
+    const uint64_t one = 1ull << 53;
+    const uint64_t tA = one / 100 * 57, tAB = one / 100 * 76, tABC = one / 100 * 95;
+    const uint64_t ks = sm64(seed);
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t s = 0, d = 0;
+        for (uint32_t l = 0; l < scale; ++l) {
+            const uint64_t u = sm64(ks ^ ((i << 6) | l)) >> 11;
+            const uint64_t bit = 1ull << (scale - 1 - l);
+            if (u >= tA) {
+                if (u < tAB) d |= bit;
+                else if (u < tABC) s |= bit;
+                else {
+                    s |= bit;
+                    d |= bit;
+                }
+            }
+        }
+        keys[i] = ((uint64_t)scramble(s, scale, seed) << 32) | scramble(d, scale, seed);
+    }
+}
+
+}  // namespace
+
+fgi_status synth_rmat_keys(fgi_graph* g, uint32_t scale, uint32_t edge_factor, uint64_t seed, uint64_t** keys,
+                           uint64_t* m) {
+    *m = (uint64_t)edge_factor << scale;
+    FGI_HIP(g, hipMalloc(reinterpret_cast<void**>(keys), *m * sizeof(uint64_t)));
+    hipLaunchKernelGGL(k_gen_rmat, dim3(8192), dim3(256), 0, g->stream, *m, scale, seed, *keys);
+    FGI_HIP(g, hipGetLastError());
+    return FGI_OK;
+}
+
+fgi_status synth_versions(fgi_graph* g, uint32_t n, uint64_t seed) {
+    FGI_HIP(g, hipMemsetAsync(g->node, 0, (size_t)g->n_handles * 8, g->stream));
+    hipLaunchKernelGGL(k_versions, dim3((n + 255) / 256), dim3(256), 0, g->stream, n, seed,
+                       reinterpret_cast<unsigned long long*>(g->node));
+    FGI_HIP(g, hipGetLastError());
+    return FGI_OK;
+}
+
+}  // namespace fgi
+
+using namespace fgi;
+
+extern "C" {
+
+fgi_status fgi_synth_layered(fgi_graph* g, uint32_t levels, uint32_t width, uint32_t fanout, uint64_t seed) {
+    if (!g || levels < 2 || width == 0 || fanout == 0 || fanout > 64 || fanout > width) return FGI_EINVAL;
+    const uint64_t n = (uint64_t)levels * width;
+    if (n > g->n_slots) return set_err(g, FGI_EINVAL, "graph needs %llu slots", (unsigned long long)n);
+    hipSetDevice(g->device);
+    FGI_TRY(synth_versions(g, (uint32_t)n, seed));
+    const uint64_t m = (uint64_t)(levels - 1) * width * fanout;
+    uint64_t* keys = nullptr;
+    FGI_HIP(g, hipMalloc(reinterpret_cast<void**>(&keys), m * sizeof(uint64_t)));
+    const uint64_t threads = (uint64_t)(levels - 1) * width;
+    hipLaunchKernelGGL(k_gen_layered, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, g->stream, levels, width,
+                       fanout, seed, keys);
+    fgi_status st = hipGetLastError() == hipSuccess ? build_rows_from_keys(g, m, keys, nullptr, seed, 0, 0) : FGI_EDEVICE;
+    hipFree(keys);
+    return st;
+}
+
+fgi_status fgi_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_factor, uint64_t seed, uint32_t stale_pct,
+                          uint64_t stale_seed) {
+    if (!g || scale == 0 || scale > 31 || edge_factor == 0 || stale_pct > 100) return FGI_EINVAL;
+    if ((1ull << scale) > g->n_slots) return set_err(g, FGI_EINVAL, "graph needs 2^%u slots", scale);
+    hipSetDevice(g->device);
+    FGI_TRY(synth_versions(g, 1u << scale, seed));
+    uint64_t* keys = nullptr;
+    uint64_t m = 0;
+    FGI_TRY(synth_rmat_keys(g, scale, edge_factor, seed, &keys, &m));
+    fgi_status st = build_rows_from_keys(g, m, keys, nullptr, seed, stale_pct, stale_seed);
+    hipFree(keys);
+    return st;
+}
+
+}  // extern "C"

@@ -1,0 +1,317 @@
+"""ctypes binding of the fgi C-ABI (include/fgi.h) — the MI355X cascading-invalidation engine.
+
+This is plumbing for tests and the bench; the drop-in host layers are the C++ mirror in
+``stl.fusion_amd/host/fusion.hpp`` and the C# ``[LibraryImport]`` stubs in INTEGRATION.md. The
+library is the in-tree ``stl.fusion_amd/lib/libfgi.so``; there is no fallback: if it is missing,
+or no GPU is present, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Tuple
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libfgi.so")
+
+OK, EINVAL, ENOMEM, ECAPACITY, EDEVICE, ESTATE, ENOTSUP = range(7)
+NONE = 0xFFFFFFFF
+COMPUTING, CONSISTENT, INVALIDATED = 0, 1, 2
+F_IOSO, F_DELAY_STARTED, F_HAS_DELAY = 4, 8, 16
+USED_ADDED, USED_DROPPED, USED_INVALIDATED, USED_ESTATE = range(4)
+
+_STATUS = {0: "FGI_OK", 1: "FGI_EINVAL", 2: "FGI_ENOMEM", 3: "FGI_ECAPACITY", 4: "FGI_EDEVICE",
+           5: "FGI_ESTATE", 6: "FGI_ENOTSUP"}
+
+
+class FgiError(RuntimeError):
+    def __init__(self, status: int, msg: str):
+        super().__init__(f"{_STATUS.get(status, status)}: {msg}")
+        self.status = status
+
+
+class Config(C.Structure):
+    _fields_ = [("struct_size", C.c_uint32), ("device", C.c_int32), ("n_slots", C.c_uint32),
+                ("n_detached", C.c_uint32), ("edge_capacity", C.c_uint64), ("rank", C.c_int32),
+                ("world", C.c_int32)]
+
+
+class WaveStats(C.Structure):
+    _fields_ = [("roots", C.c_uint64), ("levels", C.c_uint64), ("v_inv", C.c_uint64),
+                ("e_trav", C.c_uint64), ("e_match", C.c_uint64), ("n_flagged", C.c_uint64),
+                ("alg_bytes", C.c_uint64), ("kernel_ms", C.c_double), ("total_ms", C.c_double),
+                ("remote_msgs", C.c_uint64), ("f_total", C.c_uint64), ("expand_launches", C.c_uint64),
+                ("expand_ms", C.c_double), ("expand_bytes", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class PruneStats(C.Structure):
+    _fields_ = [("old_edges", C.c_uint64), ("new_edges", C.c_uint64), ("pool_before", C.c_uint64),
+                ("pool_after", C.c_uint64), ("kernel_ms", C.c_double)]
+
+
+_u32p = C.POINTER(C.c_uint32)
+_u64p = C.POINTER(C.c_uint64)
+_u8p = C.POINTER(C.c_uint8)
+_G = C.c_void_p
+
+# name -> argtypes (every function returns int fgi_status except fgi_last_error)
+SIGNATURES = {
+    "fgi_version": [_u32p, _u32p],
+    "fgi_create": [C.POINTER(Config), C.POINTER(C.c_void_p)],
+    "fgi_destroy": [_G],
+    "fgi_register_nodes": [_G, C.c_uint32, _u32p, _u64p, _u32p],
+    "fgi_load_edges": [_G, C.c_uint64, _u32p, _u32p, _u64p],
+    "fgi_get_state": [_G, C.c_uint32, _u32p, _u64p, _u32p],
+    "fgi_dump_states": [_G, _u64p, _u32p],
+    "fgi_get_used_by": [_G, C.c_uint32, _u32p, _u64p, C.c_uint64, _u64p],
+    "fgi_get_used_count": [_G, C.c_uint32, _u32p],
+    "fgi_get_degrees": [_G, _u32p, _u64p],
+    "fgi_begin_compute": [_G, C.c_uint32, _u32p, _u64p, _u8p, _u32p, C.POINTER(WaveStats)],
+    "fgi_add_used": [_G, C.c_uint32, _u32p, _u32p, _u32p],
+    "fgi_set_output": [_G, C.c_uint32, _u32p, _u8p, _u32p, C.c_uint64, _u64p, C.POINTER(WaveStats)],
+    "fgi_invalidate": [_G, C.c_uint32, _u32p, _u8p, _u32p, C.c_uint64, _u64p, C.POINTER(WaveStats)],
+    "fgi_invalidate_dev": [_G, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, _u64p, C.POINTER(WaveStats)],
+    "fgi_wave_ids_dev": [_G, C.POINTER(C.c_void_p), _u64p],
+    "fgi_invalidate_all": [_G, _u32p, C.c_uint64, _u64p, C.POINTER(WaveStats)],
+    "fgi_prune": [_G, C.POINTER(PruneStats)],
+    "fgi_release": [_G, C.c_uint32, _u32p],
+    "fgi_snapshot": [_G],
+    "fgi_restore": [_G],
+    "fgi_synth_layered": [_G, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint64],
+    "fgi_synth_rmat": [_G, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint64],
+    "fgi_export_edges": [_G, _u32p, _u32p, _u64p, C.c_uint64, _u64p],
+    "fgi_stream": [_G, C.POINTER(C.c_void_p)],
+    "fgi_part_unique_id": [_u8p],
+    "fgi_part_init": [_G, C.c_uint32, _u8p],
+    "fgi_part_synth_rmat": [_G, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint64],
+    "fgi_part_invalidate": [_G, C.c_uint32, C.c_void_p, C.c_void_p, _u64p, C.POINTER(WaveStats)],
+    "fgi_part_export_ids": [_G, _u32p, C.c_uint64, _u64p],
+}
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    """Load libfgi.so. Raises if it is missing: there is no CPU fallback for the engine."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FgiError(EDEVICE, f"{path} not built (run __graft_entry__.build())")
+    lib = C.CDLL(path)
+    for name, args in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = C.c_int
+    lib.fgi_last_error.argtypes = [_G]
+    lib.fgi_last_error.restype = C.c_char_p
+    _lib = lib
+    return lib
+
+
+def _ptr(a: Optional[np.ndarray], ct):
+    if a is None:
+        return None
+    return a.ctypes.data_as(C.POINTER(ct))
+
+
+def _u32(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint32))
+
+
+def _u64(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint64))
+
+
+def _u8(a) -> np.ndarray:
+    return np.ascontiguousarray(np.asarray(a, dtype=np.uint8))
+
+
+class Graph:
+    """One engine instance (one ComputedRegistry worth of nodes) on one device."""
+
+    def __init__(self, n_slots: int, n_detached: int = 0, edge_capacity: int = 0, device: int = 0,
+                 rank: int = 0, world: int = 1):
+        self.lib = load_library()
+        cfg = Config(C.sizeof(Config), device, n_slots, n_detached, edge_capacity, rank, world)
+        h = C.c_void_p()
+        st = self.lib.fgi_create(C.byref(cfg), C.byref(h))
+        if st != OK:
+            raise FgiError(st, f"fgi_create(n_slots={n_slots}) failed (is a GPU present?)")
+        self.h = h
+        self.n_slots = n_slots
+        self.n_detached = n_detached
+        self.n_handles = n_slots + n_detached
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.fgi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def _check(self, st: int, what: str):
+        if st != OK:
+            msg = self.lib.fgi_last_error(self.h)
+            raise FgiError(st, f"{what}: {msg.decode() if msg else ''}")
+
+    # ---- registry / import ----
+    def register_nodes(self, slots, versions, state_flags=None):
+        s, v = _u32(slots), _u64(versions)
+        f = None if state_flags is None else _u32(state_flags)
+        self._check(self.lib.fgi_register_nodes(self.h, len(s), _ptr(s, C.c_uint32), _ptr(v, C.c_uint64),
+                                                _ptr(f, C.c_uint32)), "register_nodes")
+
+    def load_edges(self, used, dependant, tags):
+        u, d, t = _u32(used), _u32(dependant), _u64(tags)
+        self._check(self.lib.fgi_load_edges(self.h, len(u), _ptr(u, C.c_uint32), _ptr(d, C.c_uint32),
+                                            _ptr(t, C.c_uint64)), "load_edges")
+
+    def synth_layered(self, levels, width, fanout, seed):
+        self._check(self.lib.fgi_synth_layered(self.h, levels, width, fanout, seed), "synth_layered")
+
+    def synth_rmat(self, scale, edge_factor, seed, stale_pct=0, stale_seed=0):
+        self._check(self.lib.fgi_synth_rmat(self.h, scale, edge_factor, seed, stale_pct, stale_seed), "synth_rmat")
+
+    # ---- queries ----
+    def get_state(self, handles) -> Tuple[np.ndarray, np.ndarray]:
+        h = _u32(handles)
+        v = np.zeros(len(h), np.uint64)
+        f = np.zeros(len(h), np.uint32)
+        self._check(self.lib.fgi_get_state(self.h, len(h), _ptr(h, C.c_uint32), _ptr(v, C.c_uint64),
+                                           _ptr(f, C.c_uint32)), "get_state")
+        return v, f
+
+    def dump_states(self) -> Tuple[np.ndarray, np.ndarray]:
+        v = np.zeros(self.n_handles, np.uint64)
+        f = np.zeros(self.n_handles, np.uint32)
+        self._check(self.lib.fgi_dump_states(self.h, _ptr(v, C.c_uint64), _ptr(f, C.c_uint32)), "dump_states")
+        return v, f
+
+    def used_by(self, handle) -> Tuple[np.ndarray, np.ndarray]:
+        n = C.c_uint64()
+        st = self.lib.fgi_get_used_by(self.h, handle, None, None, 0, C.byref(n))
+        if st not in (OK, ECAPACITY):
+            self._check(st, "used_by")
+        d = np.zeros(n.value, np.uint32)
+        t = np.zeros(n.value, np.uint64)
+        self._check(self.lib.fgi_get_used_by(self.h, handle, _ptr(d, C.c_uint32), _ptr(t, C.c_uint64), n.value,
+                                             C.byref(n)), "used_by")
+        return d, t
+
+    def used_count(self, handle) -> int:
+        c = C.c_uint32()
+        self._check(self.lib.fgi_get_used_count(self.h, handle, C.byref(c)), "used_count")
+        return c.value
+
+    def degrees(self) -> Tuple[np.ndarray, int]:
+        d = np.zeros(self.n_handles, np.uint32)
+        t = C.c_uint64()
+        self._check(self.lib.fgi_get_degrees(self.h, _ptr(d, C.c_uint32), C.byref(t)), "degrees")
+        return d, t.value
+
+    def export_edges(self):
+        n = C.c_uint64()
+        st = self.lib.fgi_export_edges(self.h, None, None, None, 0, C.byref(n))
+        if st not in (OK, ECAPACITY):
+            self._check(st, "export_edges")
+        u = np.zeros(n.value, np.uint32)
+        d = np.zeros(n.value, np.uint32)
+        t = np.zeros(n.value, np.uint64)
+        self._check(self.lib.fgi_export_edges(self.h, _ptr(u, C.c_uint32), _ptr(d, C.c_uint32), _ptr(t, C.c_uint64),
+                                              n.value, C.byref(n)), "export_edges")
+        return u, d, t
+
+    # ---- mutations ----
+    def begin_compute(self, slots, versions, has_delay=None, stats: Optional[WaveStats] = None) -> np.ndarray:
+        s, v = _u32(slots), _u64(versions)
+        hd = None if has_delay is None else _u8(has_delay)
+        out = np.zeros(len(s), np.uint32)
+        self._check(self.lib.fgi_begin_compute(self.h, len(s), _ptr(s, C.c_uint32), _ptr(v, C.c_uint64),
+                                               _ptr(hd, C.c_uint8), _ptr(out, C.c_uint32),
+                                               C.byref(stats) if stats is not None else None), "begin_compute")
+        return out
+
+    def add_used(self, dependant, used) -> np.ndarray:
+        d, u = _u32(dependant), _u32(used)
+        out = np.zeros(len(d), np.uint32)
+        self._check(self.lib.fgi_add_used(self.h, len(d), _ptr(d, C.c_uint32), _ptr(u, C.c_uint32),
+                                          _ptr(out, C.c_uint32)), "add_used")
+        return out
+
+    def set_output(self, handles, stats: Optional[WaveStats] = None):
+        h = _u32(handles)
+        out_set = np.zeros(len(h), np.uint8)
+        ids = np.zeros(self.n_handles, np.uint32)
+        n = C.c_uint64()
+        self._check(self.lib.fgi_set_output(self.h, len(h), _ptr(h, C.c_uint32), _ptr(out_set, C.c_uint8),
+                                            _ptr(ids, C.c_uint32), len(ids), C.byref(n),
+                                            C.byref(stats) if stats is not None else None), "set_output")
+        return out_set, ids[:n.value].copy()
+
+    def invalidate(self, roots, immediately=None, stats: Optional[WaveStats] = None) -> np.ndarray:
+        r = _u32(roots)
+        imm = None if immediately is None else _u8(immediately)
+        ids = np.zeros(self.n_handles, np.uint32)
+        n = C.c_uint64()
+        self._check(self.lib.fgi_invalidate(self.h, len(r), _ptr(r, C.c_uint32), _ptr(imm, C.c_uint8),
+                                            _ptr(ids, C.c_uint32), len(ids), C.byref(n),
+                                            C.byref(stats) if stats is not None else None), "invalidate")
+        return ids[:n.value].copy()
+
+    def invalidate_dev(self, n_roots: int, roots_ptr: int, imm_ptr: int = 0,
+                       stats: Optional[WaveStats] = None) -> int:
+        n = C.c_uint64()
+        self._check(self.lib.fgi_invalidate_dev(self.h, n_roots, C.c_void_p(roots_ptr),
+                                                C.c_void_p(imm_ptr) if imm_ptr else None, None, C.byref(n),
+                                                C.byref(stats) if stats is not None else None), "invalidate_dev")
+        return n.value
+
+    def invalidate_all(self, stats: Optional[WaveStats] = None) -> np.ndarray:
+        ids = np.zeros(self.n_handles, np.uint32)
+        n = C.c_uint64()
+        self._check(self.lib.fgi_invalidate_all(self.h, _ptr(ids, C.c_uint32), len(ids), C.byref(n),
+                                                C.byref(stats) if stats is not None else None), "invalidate_all")
+        return ids[:n.value].copy()
+
+    def prune(self) -> PruneStats:
+        ps = PruneStats()
+        self._check(self.lib.fgi_prune(self.h, C.byref(ps)), "prune")
+        return ps
+
+    def release(self, handles):
+        h = _u32(handles)
+        self._check(self.lib.fgi_release(self.h, len(h), _ptr(h, C.c_uint32)), "release")
+
+    def snapshot(self):
+        self._check(self.lib.fgi_snapshot(self.h), "snapshot")
+
+    def restore(self):
+        self._check(self.lib.fgi_restore(self.h), "restore")
+
+    def stream(self) -> int:
+        s = C.c_void_p()
+        self._check(self.lib.fgi_stream(self.h, C.byref(s)), "stream")
+        return s.value or 0
+
+
+def header_symbols(header_path: str) -> list:
+    """Names of every function declared in include/fgi.h (for the ABI export test)."""
+    import re
+    txt = open(header_path).read()
+    return sorted(set(re.findall(r"\b(fgi_[a-z0-9_]+)\s*\(", txt)) - {"fgi_status"})

@@ -1,0 +1,286 @@
+"""GPU parity: the HIP engine (through the C-ABI) against the CPU oracle on identical inputs.
+
+Bar: bit-exact — same invalidated set, same final (version, state, flags) for every slot, same
+V_inv / E_trav / E_match / flag counts, same `_usedBy` edge sets after a prune on both sides.
+"""
+import numpy as np
+import pytest
+
+import _pkg
+import fgo as O
+from harness import (COMPUTING, CONSISTENT, F_DS, F_HD, F_IOSO, INVALIDATED, assert_states_equal, build_pair,
+                     canon_edges, oracle_edges, random_states)
+
+pytestmark = pytest.mark.gpu
+
+
+def _edges_from_live(versions, flags, rng, m, n, stale_p=0.3):
+    # only Consistent nodes have `_usedBy` entries: AddUsedBy throws on a Computing node
+    # (Computed.cs:374-375) and an Invalidated node's set is cleared (Computed.cs:217)
+    live = np.nonzero((versions != 0) & ((flags & 3) == CONSISTENT))[0].astype(np.uint32)
+    src = rng.choice(live, m).astype(np.uint32)
+    dst = rng.integers(0, n, m).astype(np.uint32)
+    tags = versions[dst].astype(np.uint64).copy()
+    tags[tags == 0] = 7
+    stale = rng.random(m) < stale_p
+    tags[stale] += np.uint64(1)
+    return src, dst, tags
+
+
+def _compare_wave(g, o, n, roots, imm=None):
+    st = O.Stats()
+    o.clear_log()
+    o.invalidate_slots(roots, imm, stats=st)
+    ws = _pkg.load().WaveStats()
+    ids = g.invalidate(roots, imm, stats=ws)
+    oids = o.inv_log()
+    assert np.array_equal(np.sort(ids), np.sort(oids)), f"invalidated sets differ: {len(ids)} vs {len(oids)}"
+    assert len(np.unique(ids)) == len(ids), "a node was invalidated twice"
+    assert ws.v_inv == st.v_inv and ws.e_trav == st.e_trav and ws.e_match == st.e_match, \
+        (ws.v_inv, st.v_inv, ws.e_trav, st.e_trav, ws.e_match, st.e_match)
+    # n_flagged is informational: which visit sets a flag first is order-dependent
+    assert_states_equal(g, o, n)
+    return ids, ws
+
+
+def test_synth_layered_matches_cpu_definition(pkg, gpu_available):
+    levels, width, fanout, seed = 5, 300, 4, 0x5EED0001
+    g = pkg.Graph(levels * width)
+    g.synth_layered(levels, width, fanout, seed)
+    u, d, t = g.export_edges()
+    s, dd = O.gen_layered(levels, width, fanout, seed)
+    tt = O.gen_tags(s, dd, seed)
+    assert np.array_equal(canon_edges(u, d, t), canon_edges(s, dd, tt))
+    v, f = g.dump_states()
+    assert np.array_equal(v[:levels * width], O.version_of(seed, np.arange(levels * width)))
+    assert np.all(f[:levels * width] == CONSISTENT)
+
+
+@pytest.mark.parametrize("scale,ef,stale", [(10, 8, 0), (12, 16, 50)])
+def test_synth_rmat_matches_cpu_definition(pkg, gpu_available, scale, ef, stale):
+    seed, sseed = 0x5EED0024, 0x5EED00C0
+    g = pkg.Graph(1 << scale)
+    g.synth_rmat(scale, ef, seed, stale, sseed)
+    u, d, t = g.export_edges()
+    s, dd = O.gen_rmat(scale, ef, seed)
+    tt = O.gen_tags(s, dd, seed, stale, sseed)
+    assert np.array_equal(canon_edges(u, d, t), canon_edges(s, dd, tt))
+
+
+def _oracle_from_synth(n, seed, s, dd, tt):
+    o = O.Oracle(n)
+    o.load_graph(O.version_of(seed, np.arange(n)), None, s, dd, tt)
+    return o
+
+
+def test_wave_layered_config1_shape(pkg, gpu_available):
+    """BASELINE config 1 shape (fan-out 8, depth 6) at reduced width."""
+    levels, width, fanout, seed = 7, 2000, 8, 0x5EED0001
+    n = levels * width
+    g = pkg.Graph(n)
+    g.synth_layered(levels, width, fanout, seed)
+    s, dd = O.gen_layered(levels, width, fanout, seed)
+    o = _oracle_from_synth(n, seed, s, dd, O.gen_tags(s, dd, seed))
+    deg = np.bincount(s, minlength=n)
+    roots = O.gen_roots(20, width, 0x5EED1001, deg[:width])
+    ids, ws = _compare_wave(g, o, n, roots)
+    assert ws.levels >= 5 and len(ids) > 1000
+
+
+@pytest.mark.parametrize("stale", [0, 50])
+def test_wave_rmat(pkg, gpu_available, stale):
+    scale, ef, seed = 13, 16, 0x5EED0024
+    n = 1 << scale
+    g = pkg.Graph(n)
+    g.synth_rmat(scale, ef, seed, stale, 0x5EED00C0)
+    s, dd = O.gen_rmat(scale, ef, seed)
+    o = _oracle_from_synth(n, seed, s, dd, O.gen_tags(s, dd, seed, stale, 0x5EED00C0))
+    deg = np.bincount(s, minlength=n)
+    roots = O.gen_roots(64, n, 0x5EED1024, deg)
+    ids, ws = _compare_wave(g, o, n, roots)
+    assert len(ids) > 64
+    # second wave on the already-invalidated graph is a no-op
+    ids2, ws2 = _compare_wave(g, o, n, roots)
+    assert len(ids2) == 0
+
+
+def test_wave_mixed_states_and_immediately(pkg, gpu_available):
+    rng = np.random.default_rng(7)
+    n = 5000
+    versions, flags = random_states(n, rng)
+    src, dst, tags = _edges_from_live(versions, flags, rng, 40000, n)
+    g, o = build_pair(pkg, n, versions, flags, src, dst, tags)
+    assert_states_equal(g, o, n)
+    roots = rng.integers(0, n, 300).astype(np.uint32)   # duplicates and empty slots included
+    imm = (rng.random(300) < 0.3).astype(np.uint8)
+    _compare_wave(g, o, n, roots, imm)
+
+
+def test_hub_row_spans_many_chunks(pkg, gpu_available):
+    """One `Everything()`-style hub with 200k dependants (UserService.cs:178-179 shape)."""
+    n = 300_000
+    versions = O.version_of(3, np.arange(n))
+    flags = np.full(n, CONSISTENT, np.uint32)
+    dst = np.arange(1, 200_001, dtype=np.uint32)
+    src = np.zeros(len(dst), np.uint32)
+    tags = versions[dst].copy()
+    tags[::7] += np.uint64(1)     # some stale
+    # second level: each dependant feeds one more node
+    src2 = dst[:50_000]
+    dst2 = (dst[:50_000] + 200_000).astype(np.uint32) % n
+    src = np.concatenate([src, src2])
+    dst = np.concatenate([dst, dst2])
+    tags = np.concatenate([tags, versions[dst2]])
+    g, o = build_pair(pkg, n, versions, flags, src, dst, tags)
+    _compare_wave(g, o, n, np.array([0], np.uint32))
+
+
+def test_cycles_and_self_loops(pkg, gpu_available):
+    n = 1000
+    versions = O.version_of(5, np.arange(n))
+    flags = np.full(n, CONSISTENT, np.uint32)
+    src = np.arange(n, dtype=np.uint32)
+    dst = ((src + 1) % n).astype(np.uint32)            # one big cycle
+    src = np.concatenate([src, np.arange(0, n, 10, dtype=np.uint32)])
+    dst = np.concatenate([dst, np.arange(0, n, 10, dtype=np.uint32)])   # self loops
+    tags = versions[dst]
+    g, o = build_pair(pkg, n, versions, flags, src, dst, tags)
+    ids, ws = _compare_wave(g, o, n, np.array([17], np.uint32))
+    assert len(ids) == n and ws.levels == n
+
+
+def test_empty_and_noop_waves(pkg, gpu_available):
+    n = 100
+    versions = O.version_of(9, np.arange(n))
+    flags = np.full(n, CONSISTENT, np.uint32)
+    g, o = build_pair(pkg, n, versions, flags, np.zeros(0, np.uint32), np.zeros(0, np.uint32), np.zeros(0, np.uint64))
+    assert len(g.invalidate(np.zeros(0, np.uint32))) == 0
+    _compare_wave(g, o, n, np.array([3, 3, 3], np.uint32))   # no edges, duplicate root
+    _compare_wave(g, o, n, np.array([3], np.uint32))         # already invalidated
+
+
+def test_invalidate_all(pkg, gpu_available):
+    rng = np.random.default_rng(11)
+    n = 3000
+    versions, flags = random_states(n, rng)
+    src, dst, tags = _edges_from_live(versions, flags, rng, 20000, n)
+    g, o = build_pair(pkg, n, versions, flags, src, dst, tags)
+    st = O.Stats()
+    o.clear_log()
+    o.invalidate_everything(st)
+    ids = g.invalidate_all()
+    assert np.array_equal(np.sort(ids), np.sort(o.inv_log()))
+    assert_states_equal(g, o, n)
+
+
+def test_prune_matches_pruner(pkg, gpu_available):
+    rng = np.random.default_rng(13)
+    n = 4000
+    versions, flags = random_states(n, rng, p_delay=0.0)
+    src, dst, tags = _edges_from_live(versions, flags, rng, 30000, n, stale_p=0.5)
+    g, o = build_pair(pkg, n, versions, flags, src, dst, tags)
+    roots = rng.integers(0, n, 50).astype(np.uint32)
+    _compare_wave(g, o, n, roots)
+    ps = g.prune()
+    oe, ne = o.prune()
+    assert (ps.old_edges, ps.new_edges) != (0, 0)
+    assert ps.new_edges == ne
+    u, d, t = g.export_edges()
+    assert np.array_equal(canon_edges(u, d, t), oracle_edges(o, n))
+    # a wave after compaction still agrees
+    _compare_wave(g, o, n, rng.integers(0, n, 50).astype(np.uint32))
+
+
+class Pair:
+    """Engine + oracle driven by the same compute-method operations; handles mapped both ways."""
+
+    def __init__(self, pkg, n, n_detached=256):
+        self.g = pkg.Graph(n, n_detached=n_detached)
+        self.o = O.Oracle(n)
+        self.n = n
+        self.o2g = {}        # oracle node handle -> engine handle
+        self.home = {}       # engine detached handle -> slot
+
+    def begin(self, slots, versions, has_delay):
+        det = self.g.begin_compute(slots, versions, has_delay)
+        for s, v, hd, dh in zip(slots, versions, has_delay, det):
+            cur = self.o.current(int(s))
+            new, displaced = self.o.begin_compute(int(s), int(v), bool(hd))
+            if displaced != O.NONE and cur != O.NONE:
+                ost = self.o.node_info(displaced)[2] & 3
+                if ost != INVALIDATED:
+                    assert dh != 0xFFFFFFFF, "engine did not detach a surviving displaced node"
+                    self.o2g[displaced] = int(dh)
+                    self.home[int(dh)] = int(s)
+                else:
+                    self.o2g.pop(displaced, None)
+            self.o2g[new] = int(s)
+
+    def node(self, slot):
+        return self.o.last(slot)
+
+
+def test_compute_method_lifecycle_random(pkg, gpu_available):
+    """Random begin_compute / add_used / set_output / invalidate sequences (streaming-mix shape)."""
+    rng = np.random.default_rng(21)
+    n = 600
+    p = Pair(pkg, n)
+    versions = O.version_of(77, np.arange(n))
+    next_ver = versions.copy()
+    # everything starts Consistent via a compute + set_output round
+    slots = np.arange(n, dtype=np.uint32)
+    p.begin(slots, next_ver, (rng.random(n) < 0.1).astype(np.uint8))
+    p.g.set_output(slots)
+    for s in slots:
+        p.o.set_output(p.node(int(s)))
+    for step in range(25):
+        # 1. a batch of recomputations
+        k = int(rng.integers(5, 60))
+        bs = rng.choice(n, k, replace=False).astype(np.uint32)
+        next_ver[bs] += np.uint64(1000)
+        hd = (rng.random(k) < 0.15).astype(np.uint8)
+        p.begin(bs, next_ver[bs], hd)
+        # 2. dependency capture: each recomputed node uses a few others
+        dep, use = [], []
+        for s in bs:
+            for u in rng.choice(n, int(rng.integers(1, 5)), replace=False):
+                dep.append(int(s))
+                use.append(int(u))
+        dep = np.array(dep, np.uint32)
+        use = np.array(use, np.uint32)
+        res = p.g.add_used(dep, use)
+        ores = [p.o.add_used(p.node(int(d)), p.node(int(u))) for d, u in zip(dep, use)]
+        assert list(res) == ores, f"add_used results differ at step {step}"
+        # 3. some computations finish (in order; duplicates of a node are no-ops)
+        fin = bs[rng.random(len(bs)) < 0.8]
+        oset, ids = p.g.set_output(fin)
+        o_set = [p.o.set_output(p.node(int(s))) for s in fin]
+        assert list(oset) == o_set
+        # 4. an invalidation wave (immediately for some roots)
+        roots = rng.integers(0, n, 8).astype(np.uint32)
+        imm = (rng.random(8) < 0.25).astype(np.uint8)
+        p.o.clear_log()
+        p.o.invalidate_slots(roots, imm)
+        gids = p.g.invalidate(roots, imm)
+        assert np.array_equal(np.sort(gids), np.sort(p.o.inv_log())), f"step {step}"
+        assert_states_equal(p.g, p.o, n)
+        # 5. a delayed invalidation firing on detached nodes: Invalidate(true) on the object
+        det = [(oh, gh) for oh, gh in p.o2g.items() if gh >= n]
+        if det and step % 3 == 0:
+            oh, gh = det[int(rng.integers(0, len(det)))]
+            p.o.clear_log()
+            p.o.invalidate_nodes([oh], [1])
+            gids = p.g.invalidate(np.array([gh], np.uint32), np.array([1], np.uint8))
+            # engine ids are handles: a detached node reports its own handle, the oracle its slot
+            gslots = np.array([p.home.get(int(x), int(x)) for x in gids], np.uint32)
+            assert np.array_equal(np.sort(gslots), np.sort(p.o.inv_log()))
+            assert_states_equal(p.g, p.o, n)
+    # used counts and edge sets after a prune on both sides
+    for s in range(0, n, 37):
+        assert p.g.used_count(s) == p.o.used_count(p.node(s))
+    p.g.prune()
+    p.o.prune()
+    u, d, t = p.g.export_edges()
+    ge = canon_edges(u, d, t)
+    ge = ge[ge[:, 0] < n] if len(ge) else ge
+    assert np.array_equal(ge, oracle_edges(p.o, n))
