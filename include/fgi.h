@@ -98,6 +98,10 @@ typedef struct fgi_wave_stats {
     uint64_t expand_launches;  /* expand kernel launches that had work */
     double expand_ms;          /* summed device time of those launches (HIP events) */
     uint64_t expand_bytes;     /* algorithmic bytes of those launches */
+    uint64_t pull_levels;      /* levels run bottom-up */
+    uint64_t pull_edges;       /* dependency-list entries examined by pull levels */
+    double pull_ms;            /* device time of the pull kernels */
+    uint64_t pull_bytes;       /* algorithmic bytes of the pull kernels */
 } fgi_wave_stats;
 
 typedef struct fgi_prune_stats {
@@ -203,6 +207,16 @@ fgi_status fgi_export_edges(fgi_graph* g, uint32_t* used, uint32_t* dependant_sl
                             uint64_t cap, uint64_t* out_n);
 /* HIP stream the graph's kernels run on (as void* = hipStream_t) — for event timing in bench. */
 fgi_status fgi_stream(fgi_graph* g, void** stream);
+/* Traversal options (defaults in brackets). Results never depend on them; they exist so tests can
+ * pin each code path and benches can compare them.
+ *   FGI_OPT_DEAD_FILTER [1]  skip edges whose dependant was invalidated in an earlier level using
+ *                            a per-wave bitmap (E_match then counts examined edges only)
+ *   FGI_OPT_DIRECTION   [0]  0 auto (push/pull per level), 1 push only, 2 pull only
+ *   FGI_OPT_PULL_ALPHA  [14] auto: pull when frontier edges > total edges / alpha */
+#define FGI_OPT_DEAD_FILTER 1
+#define FGI_OPT_DIRECTION 2
+#define FGI_OPT_PULL_ALPHA 3
+fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value);
 
 /* ---- multi-GPU (1-D vertex-range partition, RCCL all-to-all frontier exchange) --------------- */
 /* RCCL unique id (128 bytes) made by rank 0 and broadcast by the caller (e.g. torch.distributed). */

@@ -81,7 +81,11 @@ struct LevelCtr {
     unsigned long long F;       // frontier entries (expandable = invalidated with |row| > 0)
     unsigned long long T;       // edges of the frontier (sum of row lengths)
     unsigned long long nchunks; // ceil(T / kChunk)
-    unsigned long long pad[5];
+    unsigned long long pull;    // 1 if this level runs bottom-up (pull)
+    unsigned long long mark_lo; // inv[] range marked into the bitmaps before this level
+    unsigned long long mark_hi;
+    unsigned long long ovf;     // pull: nodes whose dependency list continues in k_pull_long
+    unsigned long long pad;
 };
 
 struct WaveCtr {
@@ -89,7 +93,10 @@ struct WaveCtr {
     unsigned long long e_match;
     unsigned long long n_flagged;
     unsigned long long root_inv;    // winners of the roots kernel
-    unsigned long long pad[4];
+    unsigned long long marked;      // inv[] entries already marked in the dead bitmap
+    unsigned long long pull_cand;   // pull: slots whose dependency list was scanned
+    unsigned long long pull_edges;  // pull: dependency entries examined
+    unsigned long long pad[1];
     LevelCtr lvl[kRing];
 };
 
@@ -139,6 +146,29 @@ struct fgi_graph {
     uint64_t roots_cap = 0;
     uint64_t last_wave_n = 0;
 
+    // per-wave bitmaps over handles (bit set = node invalidated earlier in this wave / in the
+    // current frontier); read-only while a level expands, so they stay L2-resident
+    uint32_t* dead_bm = nullptr;
+    uint32_t* front_bm = nullptr;
+    uint64_t bm_words = 0;
+
+    // dependency-list cache for pull levels: for slot d, the handles whose `_usedBy` row holds
+    // (d, version(d)) (= the reference's d._used). Rebuilt from the rows when stale.
+    uint64_t* uin_off = nullptr;
+    uint32_t* uin_len = nullptr;
+    uint32_t* uin_src = nullptr;
+    uint64_t uin_cap = 0;
+    uint32_t* pull_ovf = nullptr;      // [n_slots]
+    uint64_t uin_epoch = 0;            // mut_epoch the cache was built at (0 = never)
+    uint64_t mut_epoch = 1;            // changes on every mutation of rows or versions
+    uint64_t epoch_counter = 1;
+    uint64_t snap_mut_epoch = 0;
+
+    // options (fgi_set_option)
+    int opt_dead_filter = 1;
+    int opt_direction = 0;
+    int opt_pull_alpha = 14;
+
     // generic scratch (sorts, batches)
     void* scratch = nullptr;
     size_t scratch_bytes = 0;
@@ -178,6 +208,10 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
 // edge is synth_version(ver_seed, dst) (+1 if stale by hash).
 fgi_status build_rows_from_keys(fgi_graph* g, uint64_t m, uint64_t* keys, uint64_t* tags,
                                 uint64_t ver_seed, uint32_t stale_pct, uint64_t stale_seed);
+// Build the pull dependency-list cache if the graph changed since it was built.
+fgi_status ensure_in_lists(fgi_graph* g);
+// Record a mutation of rows or versions (invalidates the dependency-list cache).
+inline void touch(fgi_graph* g) { g->mut_epoch = ++g->epoch_counter; }
 // Release multi-GPU resources (part.hip).
 fgi_status part_destroy(fgi_graph* g);
 // Append (used, dependant slot, tag) entries to rows (set semantics, no state checks).

@@ -462,6 +462,45 @@ __global__ void k_prune_rows(uint32_t n, const uint64_t* __restrict__ new_off, c
     row_cap[h] = newlen[h];
 }
 
+// ---- dependency-list cache (pull levels) ------------------------------------------------------
+// For every `_usedBy` entry (d, tag) of every row owner u with tag == version(d): d depends on u.
+// Inclusion depends only on rows and versions, never on node states, so the cache survives waves
+// and fgi_restore; every mutation of rows or versions invalidates it (touch()).
+__global__ void k_in_count(uint32_t n, const unsigned long long* __restrict__ node, const uint64_t* __restrict__ row_off,
+                           const uint32_t* __restrict__ row_len, const uint32_t* __restrict__ pool_col,
+                           const uint64_t* __restrict__ pool_tag, uint32_t* cnt) {
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t u = wave; u < n; u += nw) {
+        const uint32_t len = row_len[u];
+        const uint64_t o = row_off[u];
+        for (uint32_t k = lane; k < len; k += 64) {
+            const uint32_t d = pool_col[o + k];
+            const uint64_t t = pool_tag[o + k];
+            if (t != 0 && (node[d] & kVMask) == t) atomicAdd(&cnt[d], 1u);
+        }
+    }
+}
+
+__global__ void k_in_fill(uint32_t n, const unsigned long long* __restrict__ node, const uint64_t* __restrict__ row_off,
+                          const uint32_t* __restrict__ row_len, const uint32_t* __restrict__ pool_col,
+                          const uint64_t* __restrict__ pool_tag, const uint64_t* __restrict__ uin_off,
+                          uint32_t* cursor, uint32_t* uin_src) {
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t u = wave; u < n; u += nw) {
+        const uint32_t len = row_len[u];
+        const uint64_t o = row_off[u];
+        for (uint32_t k = lane; k < len; k += 64) {
+            const uint32_t d = pool_col[o + k];
+            const uint64_t t = pool_tag[o + k];
+            if (t != 0 && (node[d] & kVMask) == t) uin_src[uin_off[d] + atomicAdd(&cursor[d], 1u)] = (uint32_t)u;
+        }
+    }
+}
+
 __global__ void k_invalidate_all_roots(uint32_t n_slots, const unsigned long long* node, uint32_t* roots,
                                        unsigned long long* cnt) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -552,6 +591,44 @@ fgi_status ensure_pool(fgi_graph* g, uint64_t entries) {
     return ensure_cstart(g, cap);
 }
 
+fgi_status ensure_in_lists(fgi_graph* g) {
+    if (g->uin_epoch == g->mut_epoch && g->uin_src) return FGI_OK;
+    hipStream_t s = g->stream;
+    const uint32_t H = g->n_handles, N = g->n_slots;
+    const uint32_t grid = std::min<uint64_t>(nblk((uint64_t)H * 64), 16384);
+    FGI_HIP(g, hipMemsetAsync(g->uin_len, 0, (size_t)N * 4, s));
+    hipLaunchKernelGGL(k_in_count, dim3(grid), dim3(256), 0, s, H, reinterpret_cast<const unsigned long long*>(g->node),
+                       g->row_off, g->row_len, g->pool_col, g->pool_tag, g->uin_len);
+    Tmp ts, tc;
+    size_t tb = 0;
+    FGI_HIP(g, rocprim::exclusive_scan(nullptr, tb, g->uin_len, g->uin_off, (uint64_t)0, (size_t)N,
+                                       rocprim::plus<uint64_t>(), s));
+    char* tmp;
+    FGI_TRY(tmalloc(g, ts, &tmp, tb));
+    FGI_HIP(g, rocprim::exclusive_scan(tmp, tb, g->uin_len, g->uin_off, (uint64_t)0, (size_t)N,
+                                       rocprim::plus<uint64_t>(), s));
+    uint64_t last_off = 0;
+    uint32_t last_len = 0;
+    FGI_TRY(d2h(g, &last_off, g->uin_off + N - 1, 1));
+    FGI_TRY(d2h(g, &last_len, g->uin_len + N - 1, 1));
+    const uint64_t total = last_off + last_len;
+    if (total > g->uin_cap || !g->uin_src) {
+        dfree(g->uin_src);
+        const uint64_t cap = std::max<uint64_t>(total, 1024);
+        FGI_TRY(dmalloc(g, &g->uin_src, cap));
+        g->uin_cap = cap;
+    }
+    uint32_t* cursor;
+    FGI_TRY(tmalloc(g, tc, &cursor, N));
+    FGI_HIP(g, hipMemsetAsync(cursor, 0, (size_t)N * 4, s));
+    hipLaunchKernelGGL(k_in_fill, dim3(grid), dim3(256), 0, s, H, reinterpret_cast<const unsigned long long*>(g->node),
+                       g->row_off, g->row_len, g->pool_col, g->pool_tag, g->uin_off, cursor, g->uin_src);
+    FGI_HIP(g, hipGetLastError());
+    FGI_HIP(g, hipStreamSynchronize(s));
+    g->uin_epoch = g->mut_epoch;
+    return FGI_OK;
+}
+
 fgi_status build_rows_from_keys(fgi_graph* g, uint64_t m, uint64_t* keys, uint64_t* tags, uint64_t ver_seed,
                                 uint32_t stale_pct, uint64_t stale_seed) {
     hipStream_t s = g->stream;
@@ -563,6 +640,7 @@ fgi_status build_rows_from_keys(fgi_graph* g, uint64_t m, uint64_t* keys, uint64
     FGI_HIP(g, hipMemsetAsync(g->used_cnt, 0, (size_t)H * sizeof(uint32_t), s));
     g->pool_top = 0;
     g->pool_epoch++;
+    touch(g);
     if (m == 0) return FGI_OK;
     if (m >= 0xFFFFFFF0ull) return set_err(g, FGI_ENOTSUP, "more than 2^32 edges on one device");
     // 1. sort by (used, dependant) [, tag as payload]
@@ -649,8 +727,12 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
         dmalloc(g, &g->inv, H) || dmalloc(g, &g->fr_off[0], H) || dmalloc(g, &g->fr_off[1], H) ||
         dmalloc(g, &g->fr_len[0], H) || dmalloc(g, &g->fr_len[1], H) || dmalloc(g, &g->escan, H) ||
         dmalloc(g, &g->partials, kScanBlocks) || dmalloc(g, &g->ctr, 1) || dmalloc(g, &g->misc_dev, 16) ||
-        dmalloc(g, &g->pool_top_dev, 1))
+        dmalloc(g, &g->pool_top_dev, 1) || dmalloc(g, &g->uin_off, H) || dmalloc(g, &g->uin_len, H) ||
+        dmalloc(g, &g->pull_ovf, g->n_slots))
         return fail(FGI_ENOMEM);
+    g->bm_words = (H + 31) / 32 + 2;
+    if (dmalloc(g, &g->dead_bm, g->bm_words) || dmalloc(g, &g->front_bm, g->bm_words)) return fail(FGI_ENOMEM);
+    hipMemset(g->front_bm, 0, g->bm_words * 4);
     if (hipHostMalloc(reinterpret_cast<void**>(&g->ctr_host), sizeof(WaveCtr)) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&g->misc_host), 16 * sizeof(unsigned long long)) != hipSuccess)
         return fail(FGI_ENOMEM);
@@ -690,6 +772,12 @@ fgi_status fgi_destroy(fgi_graph* g) {
     }
     dfree(g->escan);
     dfree(g->cstart);
+    dfree(g->uin_off);
+    dfree(g->uin_len);
+    dfree(g->uin_src);
+    dfree(g->pull_ovf);
+    dfree(g->dead_bm);
+    dfree(g->front_bm);
     dfree(g->partials);
     dfree(g->ctr);
     dfree(g->roots_buf);
@@ -737,6 +825,7 @@ fgi_status fgi_register_nodes(fgi_graph* g, uint32_t n, const uint32_t* slot, co
     FGI_TRY(h2d(g, dv, version, n));
     if (state_flags) FGI_TRY(h2d(g, df, state_flags, n));
     FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, sizeof(unsigned long long), g->stream));
+    touch(g);
     hipLaunchKernelGGL(k_register, dim3(nblk(n)), dim3(256), 0, g->stream, n, ds, dv, df,
                        reinterpret_cast<unsigned long long*>(g->node), g->row_len, g->misc_dev);
     FGI_HIP(g, hipGetLastError());
@@ -883,6 +972,7 @@ fgi_status fgi_snapshot(fgi_graph* g) {
     FGI_HIP(g, hipMemcpyAsync(g->snap_used, g->used_cnt, H * 4, hipMemcpyDeviceToDevice, s));
     FGI_HIP(g, hipStreamSynchronize(s));
     g->snap_epoch = g->pool_epoch;
+    g->snap_mut_epoch = g->mut_epoch;
     return FGI_OK;
 }
 
@@ -900,7 +990,24 @@ fgi_status fgi_restore(fgi_graph* g) {
     FGI_HIP(g, hipMemcpyAsync(g->row_cap, g->snap_row_cap, H * 4, hipMemcpyDeviceToDevice, s));
     FGI_HIP(g, hipMemcpyAsync(g->used_cnt, g->snap_used, H * 4, hipMemcpyDeviceToDevice, s));
     FGI_HIP(g, hipStreamSynchronize(s));
+    g->mut_epoch = g->snap_mut_epoch;   // rows and versions are those of the snapshot again
     return FGI_OK;
+}
+
+fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
+    if (!g) return FGI_EINVAL;
+    switch (option) {
+    case FGI_OPT_DEAD_FILTER: g->opt_dead_filter = value ? 1 : 0; return FGI_OK;
+    case FGI_OPT_DIRECTION:
+        if (value < 0 || value > 2) return set_err(g, FGI_EINVAL, "direction must be 0, 1 or 2");
+        g->opt_direction = (int)value;
+        return FGI_OK;
+    case FGI_OPT_PULL_ALPHA:
+        if (value < 1) return set_err(g, FGI_EINVAL, "alpha must be >= 1");
+        g->opt_pull_alpha = (int)value;
+        return FGI_OK;
+    default: return set_err(g, FGI_EINVAL, "unknown option %d", option);
+    }
 }
 
 // ---- invalidation entry points ----------------------------------------------------------------
@@ -1011,6 +1118,7 @@ fgi_status fgi_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, con
     FGI_TRY(tmalloc(g, tf, &dfree_h, take.size() + 1));
     FGI_TRY(h2d(g, dfree_h, take.data(), take.size()));
     FGI_HIP(g, hipMemsetAsync(g->misc_dev + 2, 0, sizeof(unsigned long long), st));
+    touch(g);
     hipLaunchKernelGGL(k_bc_install, dim3(nblk(n)), dim3(256), 0, st, n, ds, dv, dd, dcls, dfree_h, g->misc_dev + 2,
                        g->n_slots, reinterpret_cast<unsigned long long*>(g->node), g->row_off, g->row_len, g->row_cap,
                        g->used_cnt, g->home, dout);
@@ -1053,6 +1161,7 @@ fgi_status fgi_add_used(fgi_graph* g, uint32_t n, const uint32_t* dependant, con
     unsigned long long nc = 0;
     FGI_TRY(d2h(g, &nc, g->misc_dev, 1));
     if (nc) {
+        touch(g);
         hipLaunchKernelGGL(k_au_reserve, dim3(nblk(nc)), dim3(256), 0, st, (uint64_t)nc, dcand, g->row_off, g->row_len,
                            g->row_cap, g->used_cnt, g->pool_col, g->pool_tag, dpend, dovf, g->misc_dev + 1);
         unsigned long long c2[2];
@@ -1159,6 +1268,7 @@ fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats) {
     g->pool_cap = cap;
     g->pool_top = total;
     g->pool_epoch++;
+    touch(g);
     FGI_HIP(g, hipMemcpy(g->pool_top_dev, &g->pool_top, sizeof(uint64_t), hipMemcpyHostToDevice));
     if (stats)
         stats->kernel_ms =
@@ -1182,6 +1292,7 @@ fgi_status fgi_release(fgi_graph* g, uint32_t n, const uint32_t* handle) {
         FGI_TRY(h2d(g, g->row_off + h, &zero, 1));
         FGI_HIP(g, hipStreamSynchronize(g->stream));
         g->free_detached.push_back(h);
+        touch(g);
     }
     return FGI_OK;
 }

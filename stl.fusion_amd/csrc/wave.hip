@@ -1,4 +1,4 @@
-// wave.hip — batched multi-root invalidation as a level-synchronous frontier BFS on gfx950.
+// wave.hip — batched multi-root invalidation as a level-synchronous, direction-optimizing BFS.
 //
 // Restates the cascade of Computed<T>.Invalidate (src/Stl.Fusion/Computed.cs:162-230):
 //   visit(dst, tag): the dst slot's current node n exists and n.Version == tag
@@ -11,24 +11,34 @@
 // exactly once however many frontier edges reach it. The union over roots is order-independent
 // (DESIGN.md §Semantics), so one BFS wave replaces the reference's sequence of per-root DFS.
 //
-// Per level L (all launches stream-ordered, no host round trip inside a group of levels):
-//   k_scan_reduce / k_scan_apply : exclusive scan of the frontier's row lengths (two passes over
-//                                  4 B/entry), chunk->first-entry map for load balancing
-//   k_expand                     : edge-parallel expansion, kChunk edges per block iteration;
-//                                  each edge: col (4 B) + tag (8 B) streamed non-temporally,
-//                                  node word (8 B) gathered, CAS on a version match. Winners are
-//                                  appended (wave-aggregated atomics) to the invalidated list and,
-//                                  with their row, to the next frontier.
+// Per level L (stream-ordered launches; the host only synchronises once per group of levels):
+//   k_scan_reduce / k_scan_apply : exclusive scan of the frontier's row lengths, chunk->entry map,
+//                                  level edge total, and the push/pull decision for the level
+//   k_mark                       : the previous level's winners -> dead bitmap (+ frontier bitmap)
+//   k_expand  (push levels)      : edge-parallel expansion of the frontier's `_usedBy` rows;
+//                                  edges to nodes already dead skip the tag load and the gather
+//   k_pull / k_pull_long (pull)  : every live slot scans its dependency list (the reference's
+//                                  `_used`: in-edges whose tag matches its version) for a parent
+//                                  in the frontier bitmap, with early exit (Beamer's bottom-up step)
+//   k_clear_front                : reset the frontier bitmap
 #include <hip/hip_runtime.h>
 
 #include <chrono>
+#include <cstdio>
+#include <cstdlib>
 
 #include "fgi_internal.h"
 
 namespace fgi {
 namespace {
 
+constexpr uint32_t kPullCap = 16;   // in-list entries a k_pull thread scans before handing off
+
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ bool bit_of(const uint32_t* __restrict__ bm, uint32_t h) {
+    return (bm[h >> 5] >> (h & 31)) & 1u;
+}
 
 // CAS state transition of one node word; w is a (possibly stale) observed value with the right
 // version. Returns 1 if this call moved Consistent -> Invalidated, 2 if it only set a flag.
@@ -71,7 +81,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 }
 
 // Reserve `n_inv` slots in the invalidated list and `n_fr` in the next frontier for this lane;
-// one atomic per list per wave. Returns the lane's bases.
+// one atomic per list per wave. Every lane of the wave must call it.
 __device__ __forceinline__ void wave_reserve(uint32_t n_inv, uint32_t n_fr, unsigned long long* inv_ctr,
                                              unsigned long long* fr_ctr, uint64_t& inv_base,
                                              uint64_t& fr_base) {
@@ -88,6 +98,129 @@ __device__ __forceinline__ void wave_reserve(uint32_t n_inv, uint32_t n_fr, unsi
     fr_base = b_fr + (ex >> 16);
 }
 
+// Append one (possibly absent) winner per lane: invalidated list + next frontier with its row.
+__device__ __forceinline__ void emit_one(bool win, uint32_t h, const uint64_t* __restrict__ row_off,
+                                         const uint32_t* __restrict__ row_len, uint32_t* __restrict__ inv,
+                                         uint64_t* __restrict__ nfr_off, uint32_t* __restrict__ nfr_len,
+                                         unsigned long long* inv_ctr, unsigned long long* fr_ctr) {
+    uint32_t len = 0;
+    uint64_t off = 0;
+    if (win) {
+        len = row_len[h];
+        off = row_off[h];
+    }
+    uint64_t ib, fb;
+    wave_reserve(win ? 1u : 0u, (win && len) ? 1u : 0u, inv_ctr, fr_ctr, ib, fb);
+    if (win) inv[ib] = h;
+    if (win && len) {
+        nfr_off[fb] = off;
+        nfr_len[fb] = len;
+    }
+}
+
+// Block-level emission: winners are staged in LDS and appended to the global lists in batches
+// (one pair of global atomics per batch instead of one per wave per iteration: the two list
+// counters are single words, and same-address atomics saturate at ~88/us chip-wide).
+constexpr uint32_t kEmitCap = 1024;
+struct Emit {
+    uint32_t n;
+    uint32_t pad;
+    unsigned long long base_inv, base_fr;
+    uint32_t wsum[kBlock / 64];
+    uint32_t h[kEmitCap];
+};
+
+__device__ __forceinline__ void emit_init(Emit& e) {
+    if (threadIdx.x == 0) e.n = 0;
+    __syncthreads();
+}
+
+// Every lane of the calling wave must call it (ballot); lanes beyond the LDS capacity fall back
+// to direct appends.
+__device__ __forceinline__ void emit_push(Emit& e, bool win, uint32_t h, const uint64_t* __restrict__ row_off,
+                                          const uint32_t* __restrict__ row_len, uint32_t* __restrict__ inv,
+                                          uint64_t* __restrict__ nfr_off, uint32_t* __restrict__ nfr_len,
+                                          unsigned long long* inv_ctr, unsigned long long* fr_ctr) {
+    const unsigned long long m = __ballot(win);
+    if (!m) return;
+    uint32_t base = 0;
+    if (lane_id() == 0) base = atomicAdd(&e.n, (uint32_t)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (win) {
+        const uint32_t idx = base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+        if (idx < kEmitCap) {
+            e.h[idx] = h;
+        } else {
+            inv[atomicAdd(inv_ctr, 1ull)] = h;
+            const uint32_t len = row_len[h];
+            if (len) {
+                const unsigned long long fb = atomicAdd(fr_ctr, 1ull);
+                nfr_off[fb] = row_off[h];
+                nfr_len[fb] = len;
+            }
+        }
+    }
+}
+
+// Block-uniform call. Flushes when at least `at` winners are staged (at = 1: flush anything).
+__device__ __forceinline__ void emit_flush(Emit& e, uint32_t at, const uint64_t* __restrict__ row_off,
+                                           const uint32_t* __restrict__ row_len, uint32_t* __restrict__ inv,
+                                           uint64_t* __restrict__ nfr_off, uint32_t* __restrict__ nfr_len,
+                                           unsigned long long* inv_ctr, unsigned long long* fr_ctr) {
+    __syncthreads();
+    const uint32_t n = e.n < kEmitCap ? e.n : kEmitCap;
+    __syncthreads();   // every thread has read e.n before any wave can push again
+    if (n < at || n == 0) return;   // uniform decision
+    constexpr int kPer = kEmitCap / kBlock;
+    uint32_t hh[kPer], len[kPer];
+    uint64_t off[kPer];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t i = threadIdx.x + k * kBlock;
+        hh[k] = 0;
+        len[k] = 0;
+        off[k] = 0;
+        if (i < n) {
+            hh[k] = e.h[i];
+            len[k] = row_len[hh[k]];
+            off[k] = row_off[hh[k]];
+            cnt += len[k] ? 1u : 0u;
+        }
+    }
+    uint32_t wtot;
+    const uint32_t wex = wave_excl_scan(cnt, wtot);
+    const uint32_t wid = threadIdx.x >> 6;
+    if (lane_id() == 0) e.wsum[wid] = wtot;
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (uint32_t k = 0; k < kBlock / 64; ++k) {
+        if (k < wid) before += e.wsum[k];
+        total += e.wsum[k];
+    }
+    if (threadIdx.x == 0) {
+        e.base_inv = atomicAdd(inv_ctr, (unsigned long long)n);
+        e.base_fr = total ? atomicAdd(fr_ctr, (unsigned long long)total) : 0ull;
+    }
+    __syncthreads();
+    uint64_t fb = e.base_fr + before + wex;
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const uint32_t i = threadIdx.x + k * kBlock;
+        if (i < n) {
+            inv[e.base_inv + i] = hh[k];
+            if (len[k]) {
+                nfr_off[fb] = off[k];
+                nfr_len[fb] = len[k];
+                ++fb;
+            }
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) e.n = 0;
+    __syncthreads();
+}
+
 // ---- roots (level 0) ------------------------------------------------------------------------
 // Roots are resolved like ComputedExt.TryUseExisting (Internal/ComputedExt.cs:25-35): the
 // handle's current node, no tag check; immediately[i] selects Invalidate(true).
@@ -99,32 +232,19 @@ __global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ r
                                                   uint32_t* __restrict__ inv, uint64_t* __restrict__ fr_off,
                                                   uint32_t* __restrict__ fr_len, WaveCtr* ctr) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t win = 0, flagged = 0, h = 0, len = 0;
-    uint64_t off = 0;
+    uint32_t win = 0, flagged = 0, h = 0;
     if (i < n) {
         h = roots[i];
         if (h < n_handles) {
             const unsigned long long w = node[h];
             if ((w & kVMask) != 0) {
                 const int r = visit_word(node + h, w, imm ? imm[i] != 0 : false);
-                if (r == 1) {
-                    win = 1;
-                    len = row_len[h];
-                    off = row_off[h];
-                } else if (r == 2) {
-                    flagged = 1;
-                }
+                win = (r == 1);
+                flagged = (r == 2);
             }
         }
     }
-    uint64_t ib, fb;
-    const uint32_t has_row = (win && len) ? 1u : 0u;
-    wave_reserve(win, has_row, &ctr->inv, &ctr->lvl[0].F, ib, fb);
-    if (win) inv[ib] = h;
-    if (has_row) {
-        fr_off[fb] = off;
-        fr_len[fb] = len;
-    }
+    emit_one(win, h, row_off, row_len, inv, fr_off, fr_len, &ctr->inv, &ctr->lvl[0].F);
     const uint32_t fs = wave_sum(flagged), ws = wave_sum(win);
     if (lane_id() == 0 && fs) atomicAdd(&ctr->n_flagged, (unsigned long long)fs);
     if (lane_id() == 0 && ws) atomicAdd(&ctr->root_inv, (unsigned long long)ws);
@@ -157,17 +277,16 @@ __global__ __launch_bounds__(kBlock) void k_scan_reduce(int L, const uint32_t* _
 }
 
 // Exclusive scan of fr_len into escan; records for every chunk of kChunk edges the frontier
-// entry holding its first edge (cstart), and the level's edge total.
+// entry holding its first edge (cstart), the level's edge total, and push-vs-pull.
 __global__ __launch_bounds__(kBlock) void k_scan_apply(int L, const uint32_t* __restrict__ fr_len,
                                                        const unsigned long long* __restrict__ partials,
                                                        uint64_t* __restrict__ escan, uint32_t* __restrict__ cstart,
-                                                       WaveCtr* ctr) {
+                                                       WaveCtr* ctr, int direction, uint64_t pull_threshold) {
     __shared__ unsigned long long s_red[kBlock / 64];
     __shared__ unsigned long long s_wave[kBlock / 64];
     LevelCtr& lc = ctr->lvl[L % kRing];
     const uint64_t F = lc.F;
     const uint64_t b = blockIdx.x, G = gridDim.x;
-    // prefix of partials before this block, and the grand total
     unsigned long long before = 0, all = 0;
     for (uint64_t k = threadIdx.x; k < G; k += blockDim.x) {
         const unsigned long long p = partials[k];
@@ -179,6 +298,8 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(int L, const uint32_t* __
     if (b == 0 && threadIdx.x == 0) {
         lc.T = all;
         lc.nchunks = (all + kChunk - 1) / kChunk;
+        // direction: 1 push only, 2 pull only, 0 auto (pull when the frontier's rows are heavy)
+        lc.pull = (F != 0 && (direction == 2 || (direction == 0 && all > pull_threshold))) ? 1ull : 0ull;
     }
     if (F == 0) return;
     const uint64_t lo = F * b / G, hi = F * (b + 1) / G;
@@ -187,7 +308,6 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(int L, const uint32_t* __
     for (uint64_t base = lo; base < hi; base += blockDim.x) {
         const uint64_t i = base + threadIdx.x;
         const unsigned long long v = (i < hi) ? fr_len[i] : 0ull;
-        // inclusive wave scan (64-bit)
         unsigned long long x = v;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -214,7 +334,38 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(int L, const uint32_t* __
     }
 }
 
-// ---- expansion --------------------------------------------------------------------------------
+// ---- bitmaps ----------------------------------------------------------------------------------
+// Nodes that won Consistent -> Invalidated since the last mark become dead (and frontier, on pull
+// levels). The range [marked, inv) is exactly the previous level's winners.
+__global__ __launch_bounds__(kBlock) void k_mark(int L, const uint32_t* __restrict__ inv, uint32_t* dead_bm,
+                                                 uint32_t* front_bm, WaveCtr* ctr) {
+    LevelCtr& lc = ctr->lvl[L % kRing];
+    const uint64_t lo = ctr->marked, hi = ctr->inv;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        lc.mark_lo = lo;
+        lc.mark_hi = hi;
+    }
+    const bool front = lc.pull != 0;
+    for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t h = inv[i];
+        atomicOr(dead_bm + (h >> 5), 1u << (h & 31));
+        if (front) atomicOr(front_bm + (h >> 5), 1u << (h & 31));
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_clear_front(int L, const uint32_t* __restrict__ inv, uint32_t* front_bm,
+                                                        WaveCtr* ctr) {
+    LevelCtr& lc = ctr->lvl[L % kRing];
+    const uint64_t lo = lc.mark_lo, hi = lc.mark_hi;
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctr->marked = hi;
+    if (!lc.pull) return;
+    for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
+         i += (uint64_t)gridDim.x * blockDim.x)
+        front_bm[inv[i] >> 5] = 0u;   // every set bit of the word belongs to this level's frontier
+}
+
+// ---- push: edge-parallel expansion ------------------------------------------------------------
 __device__ __forceinline__ uint32_t lds_upper_bound(const uint32_t* s, uint32_t n, uint32_t x) {
     uint32_t lo = 0, hi = n;   // first k with s[k] > x
     while (lo < hi) {
@@ -232,14 +383,18 @@ __global__ __launch_bounds__(kBlock) void k_expand(int L, const uint64_t* __rest
                                                    const uint64_t* __restrict__ pool_tag,
                                                    unsigned long long* node, const uint64_t* __restrict__ row_off,
                                                    const uint32_t* __restrict__ row_len,
+                                                   const uint32_t* __restrict__ dead_bm, int dead_filter,
                                                    uint32_t* __restrict__ inv, uint64_t* __restrict__ nfr_off,
                                                    uint32_t* __restrict__ nfr_len, WaveCtr* ctr) {
     __shared__ uint32_t s_rel[kChunk + 1];
     __shared__ uint64_t s_base[kChunk + 1];
+    __shared__ Emit em;
     LevelCtr& lc = ctr->lvl[L % kRing];
     LevelCtr& ln = ctr->lvl[(L + 1) % kRing];
     if (blockIdx.x == 0 && threadIdx.x < sizeof(LevelCtr) / 8)
         reinterpret_cast<unsigned long long*>(&ctr->lvl[(L + 2) % kRing])[threadIdx.x] = 0ull;
+    if (lc.pull) return;
+    emit_init(em);
     const uint64_t T = lc.T, F = lc.F, nch = lc.nchunks;
     uint32_t matched = 0, flagged = 0;
     for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
@@ -255,22 +410,35 @@ __global__ __launch_bounds__(kBlock) void k_expand(int L, const uint64_t* __rest
         }
         __syncthreads();
         uint32_t dst[kEPT];
-        uint64_t tag[kEPT];
+        uint64_t pos[kEPT];
 #pragma unroll
         for (int j = 0; j < kEPT; ++j) {
             const uint32_t local = threadIdx.x + j * kBlock;
             dst[j] = 0xFFFFFFFFu;
-            tag[j] = 0;
+            pos[j] = 0;
             if (local < clen) {
                 const uint32_t k = lds_upper_bound(s_rel, n, local) - 1;
-                const uint64_t p = s_base[k] + local;
-                dst[j] = __builtin_nontemporal_load(pool_col + p);
-                tag[j] = __builtin_nontemporal_load(pool_tag + p);
+                pos[j] = s_base[k] + local;
+                dst[j] = __builtin_nontemporal_load(pool_col + pos[j]);
             }
         }
+        // edges to nodes invalidated in an earlier level need neither the tag nor the gather
+        if (dead_filter) {
+#pragma unroll
+            for (int j = 0; j < kEPT; ++j)
+                if (dst[j] != 0xFFFFFFFFu && bit_of(dead_bm, dst[j])) dst[j] = 0xFFFFFFFFu;
+        }
+        uint64_t tag[kEPT];
         unsigned long long w[kEPT];
 #pragma unroll
-        for (int j = 0; j < kEPT; ++j) w[j] = (dst[j] != 0xFFFFFFFFu) ? node[dst[j]] : 0ull;
+        for (int j = 0; j < kEPT; ++j) {
+            tag[j] = 0;
+            w[j] = 0;
+            if (dst[j] != 0xFFFFFFFFu) {
+                tag[j] = __builtin_nontemporal_load(pool_tag + pos[j]);
+                w[j] = node[dst[j]];
+            }
+        }
         uint32_t win_mask = 0;
 #pragma unroll
         for (int j = 0; j < kEPT; ++j) {
@@ -281,39 +449,128 @@ __global__ __launch_bounds__(kBlock) void k_expand(int L, const uint64_t* __rest
                 else if (r == 2) ++flagged;
             }
         }
-        uint32_t lens[kEPT];
-        uint64_t offs[kEPT];
-        uint32_t n_inv = 0, n_fr = 0;
 #pragma unroll
-        for (int j = 0; j < kEPT; ++j) {
-            lens[j] = 0;
-            offs[j] = 0;
-            if (win_mask & (1u << j)) {
-                lens[j] = row_len[dst[j]];
-                offs[j] = row_off[dst[j]];
-                ++n_inv;
-                if (lens[j]) ++n_fr;
-            }
-        }
-        uint64_t ib, fb;
-        wave_reserve(n_inv, n_fr, &ctr->inv, &ln.F, ib, fb);
-#pragma unroll
-        for (int j = 0; j < kEPT; ++j) {
-            if (win_mask & (1u << j)) {
-                inv[ib++] = dst[j];
-                if (lens[j]) {
-                    nfr_off[fb] = offs[j];
-                    nfr_len[fb] = lens[j];
-                    ++fb;
-                }
-            }
-        }
-        __syncthreads();
+        for (int j = 0; j < kEPT; ++j)
+            emit_push(em, (win_mask >> j) & 1u, dst[j], row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
+        emit_flush(em, kEmitCap / 2, row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
     }
+    emit_flush(em, 1, row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
     const uint32_t ms = wave_sum(matched), fs = wave_sum(flagged);
     if (lane_id() == 0) {
         if (ms) atomicAdd(&ctr->e_match, (unsigned long long)ms);
         if (fs) atomicAdd(&ctr->n_flagged, (unsigned long long)fs);
+    }
+}
+
+// ---- pull: every live slot looks for a parent in the frontier ---------------------------------
+// uin_* is the dependency-list cache: for slot d, the handles u whose `_usedBy` row holds
+// (d, version(d)) — the reference's d._used (Computed.cs:36, 365-366). A parent in the frontier
+// bitmap (u invalidated in the previous level) means the push step would visit d from u.
+__global__ __launch_bounds__(kBlock) void k_pull(int L, uint32_t n_slots, const uint64_t* __restrict__ uin_off,
+                                                 const uint32_t* __restrict__ uin_len,
+                                                 const uint32_t* __restrict__ uin_src,
+                                                 const uint32_t* __restrict__ dead_bm,
+                                                 const uint32_t* __restrict__ front_bm, unsigned long long* node,
+                                                 const uint64_t* __restrict__ row_off,
+                                                 const uint32_t* __restrict__ row_len, uint32_t* __restrict__ inv,
+                                                 uint64_t* __restrict__ nfr_off, uint32_t* __restrict__ nfr_len,
+                                                 uint32_t* __restrict__ ovf, WaveCtr* ctr) {
+    __shared__ Emit em;
+    LevelCtr& lc = ctr->lvl[L % kRing];
+    LevelCtr& ln = ctr->lvl[(L + 1) % kRing];
+    if (!lc.pull) return;
+    emit_init(em);
+    uint32_t flagged = 0, cand = 0, examined = 0;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    const uint32_t n_iter = (n_slots + stride - 1) / stride;   // uniform trip count: flushes are block-wide
+    for (uint32_t it = 0; it < n_iter; ++it) {
+        const uint32_t d = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
+        bool win = false, long_list = false;
+        if (d < n_slots && !bit_of(dead_bm, d)) {
+            const uint32_t len = uin_len[d];
+            if (len) {
+                ++cand;
+                const uint64_t off = uin_off[d];
+                const uint32_t lim = len < kPullCap ? len : kPullCap;
+                bool found = false;
+                uint32_t k = 0;
+                for (; k < lim; ++k) {
+                    if (bit_of(front_bm, uin_src[off + k])) {
+                        found = true;
+                        ++k;
+                        break;
+                    }
+                }
+                examined += k;
+                if (found) {
+                    const int r = visit_word(node + d, node[d], false);
+                    win = (r == 1);
+                    flagged += (r == 2);
+                } else if (len > kPullCap) {
+                    long_list = true;
+                }
+            }
+        }
+        // long dependency lists continue in k_pull_long (one wave per node)
+        const unsigned long long lm = __ballot(long_list);
+        if (lm) {
+            unsigned long long base = 0;
+            if (lane_id() == 0) base = atomicAdd(&lc.ovf, (unsigned long long)__popcll(lm));
+            base = __shfl(base, 0, 64);
+            if (long_list) ovf[base + __popcll(lm & ((1ull << lane_id()) - 1ull))] = d;
+        }
+        emit_push(em, win, d, row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
+        emit_flush(em, kEmitCap - kBlock, row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
+    }
+    emit_flush(em, 1, row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
+    const uint32_t fs = wave_sum(flagged), cs = wave_sum(cand), es = wave_sum(examined);
+    if (lane_id() == 0) {
+        if (fs) atomicAdd(&ctr->n_flagged, (unsigned long long)fs);
+        if (cs) atomicAdd(&ctr->pull_cand, (unsigned long long)cs);
+        if (es) atomicAdd(&ctr->pull_edges, (unsigned long long)es);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_pull_long(int L, const uint64_t* __restrict__ uin_off,
+                                                      const uint32_t* __restrict__ uin_len,
+                                                      const uint32_t* __restrict__ uin_src,
+                                                      const uint32_t* __restrict__ front_bm, unsigned long long* node,
+                                                      const uint64_t* __restrict__ row_off,
+                                                      const uint32_t* __restrict__ row_len,
+                                                      uint32_t* __restrict__ inv, uint64_t* __restrict__ nfr_off,
+                                                      uint32_t* __restrict__ nfr_len,
+                                                      const uint32_t* __restrict__ ovf, WaveCtr* ctr) {
+    LevelCtr& lc = ctr->lvl[L % kRing];
+    LevelCtr& ln = ctr->lvl[(L + 1) % kRing];
+    if (!lc.pull) return;
+    const uint64_t n = lc.ovf;
+    const uint32_t lane = lane_id();
+    const uint64_t wave0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t nwaves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    uint32_t flagged = 0, examined = 0;
+    for (uint64_t q = wave0; q < n; q += nwaves) {
+        const uint32_t d = ovf[q];
+        const uint32_t len = uin_len[d];
+        const uint64_t off = uin_off[d];
+        bool found = false;
+        for (uint32_t base = kPullCap; base < len && !found; base += 64) {
+            const uint32_t k = base + lane;
+            const bool hit = k < len && bit_of(front_bm, uin_src[off + k]);
+            found = __ballot(hit) != 0;
+            examined += (k < len) ? 1 : 0;
+        }
+        bool win = false;
+        if (found && lane == 0) {
+            const int r = visit_word(node + d, node[d], false);
+            win = (r == 1);
+            flagged += (r == 2);
+        }
+        emit_one(win, d, row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
+    }
+    const uint32_t fs = wave_sum(flagged), es = wave_sum(examined);
+    if (lane == 0) {
+        if (fs) atomicAdd(&ctr->n_flagged, (unsigned long long)fs);
+        if (es) atomicAdd(&ctr->pull_edges, (unsigned long long)es);
     }
 }
 
@@ -323,9 +580,18 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                     fgi_wave_stats* stats) {
     const auto t0 = std::chrono::steady_clock::now();
     hipStream_t s = g->stream;
+    static const bool trace = getenv("FGI_TRACE") != nullptr;
+    const bool timing = stats != nullptr || trace;
     FGI_TRY(ensure_cstart(g, g->pool_top));
+    // Pull levels need the dependency-list cache. It is built lazily: while it is stale, levels
+    // run push-only; once a level group shows a frontier heavy enough to pull, the cache is
+    // (re)built and later groups may pull. Small waves (streaming mixes) never pay for it.
+    const int direction = g->opt_direction;
+    const uint64_t pull_threshold = g->pool_top / (uint64_t)(g->opt_pull_alpha > 0 ? g->opt_pull_alpha : 1);
+    if (direction == 2 && n_roots) FGI_TRY(ensure_in_lists(g));
+    bool allow_pull = direction != 1 && g->uin_src && g->uin_epoch == g->mut_epoch;
     FGI_HIP(g, hipMemsetAsync(g->ctr, 0, sizeof(WaveCtr), s));
-    const bool timing = stats != nullptr;
+    FGI_HIP(g, hipMemsetAsync(g->dead_bm, 0, g->bm_words * 4, s));
     if (timing) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
     if (n_roots) {
         const uint32_t nb = (n_roots + kBlock - 1) / kBlock;
@@ -333,56 +599,92 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                            reinterpret_cast<unsigned long long*>(g->node), g->row_off, g->row_len, g->inv,
                            g->fr_off[0], g->fr_len[0], g->ctr);
     }
-    // Persistent grid for the expansion: 6 resident 256-thread blocks per CU (LDS 24.6 KB each).
     int n_cu = 256;
     hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device);
-    const uint32_t expand_grid = (uint32_t)n_cu * 6;
+    const uint32_t expand_grid = (uint32_t)n_cu * 5;     // 5 resident blocks per CU (LDS 28.8 KB each)
+    const uint32_t pull_grid = (uint32_t)n_cu * 8;
+    const uint32_t mark_grid = (uint32_t)n_cu * 2;
     constexpr int kGroup = 4;
     int L = 0;
-    uint64_t levels = 0, e_trav = 0, f_total = 0;
-    double expand_ms = 0;
-    uint64_t expand_launches = 0;
+    uint64_t levels = 0, e_trav = 0, f_total = 0, pull_levels = 0;
+    double expand_ms = 0, pull_ms = 0;
+    uint64_t expand_launches = 0, expand_edges = 0, expand_f = 0;
     bool done = (n_roots == 0);
-    std::vector<int> ev_level;
     while (!done) {
         const int L0 = L;
+        const int dir_eff = allow_pull ? direction : 1;
         for (int k = 0; k < kGroup; ++k, ++L) {
             const int buf = L & 1;
             hipLaunchKernelGGL(k_scan_reduce, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->fr_len[buf], g->partials,
                                g->ctr);
             hipLaunchKernelGGL(k_scan_apply, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->fr_len[buf], g->partials,
-                               g->escan, g->cstart, g->ctr);
+                               g->escan, g->cstart, g->ctr, dir_eff, pull_threshold);
+            hipLaunchKernelGGL(k_mark, dim3(mark_grid), dim3(kBlock), 0, s, L, g->inv, g->dead_bm, g->front_bm, g->ctr);
             if (timing) {
-                while (g->ev.size() < 2 * (size_t)(L + 1)) {
+                while (g->ev.size() < 4 * (size_t)(L + 1)) {
                     hipEvent_t e;
                     FGI_HIP(g, hipEventCreate(&e));
                     g->ev.push_back(e);
                 }
-                FGI_HIP(g, hipEventRecord(g->ev[2 * L], s));
+                FGI_HIP(g, hipEventRecord(g->ev[4 * L], s));
             }
             hipLaunchKernelGGL(k_expand, dim3(expand_grid), dim3(kBlock), 0, s, L, g->fr_off[buf], g->escan, g->cstart,
                                g->pool_col, g->pool_tag, reinterpret_cast<unsigned long long*>(g->node), g->row_off,
-                               g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], g->ctr);
-            if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L + 1], s));
+                               g->row_len, g->dead_bm, g->opt_dead_filter, g->inv, g->fr_off[buf ^ 1],
+                               g->fr_len[buf ^ 1], g->ctr);
+            if (timing) FGI_HIP(g, hipEventRecord(g->ev[4 * L + 1], s));
+            if (dir_eff != 1) {
+                hipLaunchKernelGGL(k_pull, dim3(pull_grid), dim3(kBlock), 0, s, L, g->n_slots, g->uin_off, g->uin_len,
+                                   g->uin_src, g->dead_bm, g->front_bm, reinterpret_cast<unsigned long long*>(g->node),
+                                   g->row_off, g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], g->pull_ovf,
+                                   g->ctr);
+                hipLaunchKernelGGL(k_pull_long, dim3(pull_grid), dim3(kBlock), 0, s, L, g->uin_off, g->uin_len,
+                                   g->uin_src, g->front_bm, reinterpret_cast<unsigned long long*>(g->node), g->row_off,
+                                   g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], g->pull_ovf, g->ctr);
+            }
+            if (timing) FGI_HIP(g, hipEventRecord(g->ev[4 * L + 2], s));
+            hipLaunchKernelGGL(k_clear_front, dim3(mark_grid), dim3(kBlock), 0, s, L, g->inv, g->front_bm, g->ctr);
         }
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
         FGI_HIP(g, hipStreamSynchronize(s));
         for (int l = L0; l < L; ++l) {
             const LevelCtr& lc = g->ctr_host->lvl[l % kRing];
+            float ms_e = 0, ms_p = 0;
+            if (timing) {
+                // every expand launch counts (empty and pull levels too), so the average launch
+                // duration is the one rocprofv3 reports for k_expand
+                FGI_HIP(g, hipEventElapsedTime(&ms_e, g->ev[4 * l], g->ev[4 * l + 1]));
+                FGI_HIP(g, hipEventElapsedTime(&ms_p, g->ev[4 * l + 1], g->ev[4 * l + 2]));
+                expand_ms += ms_e;
+                pull_ms += ms_p;
+                ++expand_launches;
+            }
             if (lc.F) {
                 ++levels;
                 e_trav += lc.T;
                 f_total += lc.F;
-                if (timing) {
-                    float ms = 0;
-                    FGI_HIP(g, hipEventElapsedTime(&ms, g->ev[2 * l], g->ev[2 * l + 1]));
-                    expand_ms += ms;
-                    ++expand_launches;
+                if (lc.pull) {
+                    ++pull_levels;
+                } else {
+                    expand_edges += lc.T;
+                    expand_f += lc.F;
                 }
             }
+            if (trace)
+                fprintf(stderr, "[fgi] level %d %s: frontier %llu edges %llu expand %.3f ms pull %.3f ms ovf %llu\n", l,
+                        lc.pull ? "pull" : "push", (unsigned long long)lc.F, (unsigned long long)lc.T, ms_e, ms_p,
+                        (unsigned long long)lc.ovf);
         }
         if (g->ctr_host->lvl[L % kRing].F == 0) done = true;
+        if (!done && !allow_pull && direction == 0) {
+            bool heavy = false;
+            for (int l = L0; l < L; ++l) heavy |= g->ctr_host->lvl[l % kRing].T > pull_threshold;
+            if (heavy) {
+                FGI_TRY(ensure_in_lists(g));
+                allow_pull = true;
+            }
+        }
     }
     if (n_roots == 0) {
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
@@ -393,6 +695,10 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         FGI_HIP(g, hipEventSynchronize(g->ev_w1));
     }
     g->last_wave_n = g->ctr_host->inv;
+    if (trace)
+        fprintf(stderr, "[fgi] wave: %llu invalidated, pull candidates %llu, pull dependencies examined %llu\n",
+                (unsigned long long)g->ctr_host->inv, (unsigned long long)g->ctr_host->pull_cand,
+                (unsigned long long)g->ctr_host->pull_edges);
     if (stats) {
         const uint64_t v = g->ctr_host->inv;
         stats->roots += n_roots;
@@ -401,23 +707,24 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         stats->e_trav += e_trav;
         stats->e_match += g->ctr_host->e_match;
         stats->n_flagged += g->ctr_host->n_flagged;
-        // Algorithmic bytes of the wave:
-        //   per traversed edge     20 B  (col 4 + tag 8 + node-word gather 8)
-        //   per frontier entry     44 B  (fr_len 4 x2 scan passes, escan 8 w + 8 r, fr_off 8 r,
-        //                                 frontier write 12 by the producer)
-        //   per invalidated node   24 B  (CAS 8 + row_len/row_off gather 12 + list write 4)
-        //   per root                5 B
-        stats->alg_bytes += 20 * e_trav + 44 * f_total + 24 * v + 5ull * n_roots;
+        stats->pull_levels += pull_levels;
+        stats->pull_edges += g->ctr_host->pull_edges;
+        // Algorithmic bytes of the wave. Push level, per traversed edge:
+        // col 4 + tag 8 + node-word gather 8; per frontier entry: fr_len 4 x2, escan 8 w + 8 r,
+        // fr_off 8 r, written 12 by the producer. Pull level: per candidate with a dependency list
+        // uin_len 4 + uin_off 8, per examined dependency 4. Per invalidated node: CAS 8 + row
+        // gathers 12 + list write 4. Per root 5.
+        const uint64_t push_b = 20 * expand_edges + 44 * expand_f;
+        const uint64_t pull_b = 12 * g->ctr_host->pull_cand + 4 * g->ctr_host->pull_edges;
+        stats->alg_bytes += push_b + pull_b + 24 * v + 5ull * n_roots;
         float wave_ms = 0;
         hipEventElapsedTime(&wave_ms, g->ev_w0, g->ev_w1);
         stats->kernel_ms += wave_ms;
         stats->expand_ms += expand_ms;
+        stats->pull_ms += pull_ms;
         stats->expand_launches += expand_launches;
-        // expand kernel alone: edges 20 B, frontier entries read 16 B (escan + fr_off), winners
-        // 24 B (CAS + row gathers + list write), next-frontier entries written 12 B.
-        const uint64_t v_exp = v - g->ctr_host->root_inv;
-        const uint64_t f0 = g->ctr_host->lvl[0].F;   // level-0 frontier is written by k_roots
-        stats->expand_bytes += 20 * e_trav + 16 * f_total + 24 * v_exp + 12 * (f_total - f0);
+        stats->expand_bytes += 20 * expand_edges + 16 * expand_f;
+        stats->pull_bytes += pull_b;
         stats->f_total += f_total;
         stats->total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }

@@ -17,6 +17,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libfgi.so")
 
 OK, EINVAL, ENOMEM, ECAPACITY, EDEVICE, ESTATE, ENOTSUP = range(7)
+OPT_DEAD_FILTER, OPT_DIRECTION, OPT_PULL_ALPHA = 1, 2, 3
+DIR_AUTO, DIR_PUSH, DIR_PULL = 0, 1, 2
 NONE = 0xFFFFFFFF
 COMPUTING, CONSISTENT, INVALIDATED = 0, 1, 2
 F_IOSO, F_DELAY_STARTED, F_HAS_DELAY = 4, 8, 16
@@ -43,7 +45,8 @@ class WaveStats(C.Structure):
                 ("e_trav", C.c_uint64), ("e_match", C.c_uint64), ("n_flagged", C.c_uint64),
                 ("alg_bytes", C.c_uint64), ("kernel_ms", C.c_double), ("total_ms", C.c_double),
                 ("remote_msgs", C.c_uint64), ("f_total", C.c_uint64), ("expand_launches", C.c_uint64),
-                ("expand_ms", C.c_double), ("expand_bytes", C.c_uint64)]
+                ("expand_ms", C.c_double), ("expand_bytes", C.c_uint64), ("pull_levels", C.c_uint64),
+                ("pull_edges", C.c_uint64), ("pull_ms", C.c_double), ("pull_bytes", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -86,6 +89,7 @@ SIGNATURES = {
     "fgi_synth_rmat": [_G, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint64],
     "fgi_export_edges": [_G, _u32p, _u32p, _u64p, C.c_uint64, _u64p],
     "fgi_stream": [_G, C.POINTER(C.c_void_p)],
+    "fgi_set_option": [_G, C.c_int, C.c_int64],
     "fgi_part_unique_id": [_u8p],
     "fgi_part_init": [_G, C.c_uint32, _u8p],
     "fgi_part_synth_rmat": [_G, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint64],
@@ -303,6 +307,9 @@ class Graph:
 
     def restore(self):
         self._check(self.lib.fgi_restore(self.h), "restore")
+
+    def set_option(self, option: int, value: int):
+        self._check(self.lib.fgi_set_option(self.h, option, value), "set_option")
 
     def stream(self) -> int:
         s = C.c_void_p()
