@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -98,6 +99,13 @@ struct WaveCtr {
     unsigned long long pull_edges;  // pull: dependency entries examined
     unsigned long long pad[1];
     LevelCtr lvl[kRing];
+};
+
+// per-wave accounting of a partitioned wave
+struct PartWave {
+    std::chrono::steady_clock::time_point t0;
+    uint64_t n_roots = 0, levels = 0, e_trav = 0, f_total = 0, sent = 0, expand_launches = 0;
+    double expand_ms = 0;
 };
 
 // ---- host-side graph object -------------------------------------------------------------------
@@ -189,6 +197,7 @@ struct fgi_graph {
 
     // multi-GPU
     void* part = nullptr;
+    fgi::PartWave pw;
 
     std::string err;
 };
@@ -206,14 +215,43 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
 // Build rows from device edge keys (src << 32 | dst) + optional tags; pool must be empty.
 // Consumes `keys`/`tags` buffers (they may be overwritten). If tags == nullptr the tag of each
 // edge is synth_version(ver_seed, dst) (+1 if stale by hash).
+// src_base / dst_base translate partition-local ids to global ones (multi-GPU): keys hold
+// (local used handle << 32 | global dependant slot); tags and the stale hash use global ids.
 fgi_status build_rows_from_keys(fgi_graph* g, uint64_t m, uint64_t* keys, uint64_t* tags,
-                                uint64_t ver_seed, uint32_t stale_pct, uint64_t stale_seed);
+                                uint64_t ver_seed, uint32_t stale_pct, uint64_t stale_seed,
+                                uint32_t src_base = 0, uint32_t dst_base = 0);
 // Build the pull dependency-list cache if the graph changed since it was built.
 fgi_status ensure_in_lists(fgi_graph* g);
 // Record a mutation of rows or versions (invalidates the dependency-list cache).
 inline void touch(fgi_graph* g) { g->mut_epoch = ++g->epoch_counter; }
-// Release multi-GPU resources (part.hip).
+// ---- multi-GPU partition (part.hip) ----
+// Release multi-GPU resources.
 fgi_status part_destroy(fgi_graph* g);
+struct PartView {
+    uint32_t rank, world;
+    uint32_t base, n_local, n_global, block;   // this rank owns [base, base + n_local); block = ceil(N/world)
+    uint64_t* ver_all;          // [n_global] replica of every node's version (immutable during a wave)
+    uint32_t* sent_bm;          // [n_global bits] remote targets already sent in this wave
+    uint64_t sent_words;
+    uint32_t* send_buf;         // [world][block] outgoing target ids per owner
+    uint32_t* recv_buf;         // [world * block] incoming, concatenated
+    unsigned long long* send_cnt;   // [world] device counters
+};
+bool part_view(fgi_graph* g, PartView* v);
+// Exchange this level's messages: counts by all-gather, payload by grouped send/recv over RCCL.
+// Returns the number of target ids received (concatenated at recv_buf) and sent.
+fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent);
+// Sum of a device u64 over all ranks (RCCL all-reduce), returned on the host.
+fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out);
+// Partitioned wave over global root ids (wave.hip), and its phases.
+fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
+                         fgi_wave_stats* stats);
+fgi_status part_wave_begin(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev);
+const unsigned long long* part_level_frontier_dev(fgi_graph* g, int L);
+fgi_status part_level_launch(fgi_graph* g, int L);
+fgi_status part_level_apply(fgi_graph* g, int L, uint64_t n_recv, uint64_t n_sent);
+fgi_status part_level_account(fgi_graph* g, int L);
+fgi_status part_wave_end(fgi_graph* g, fgi_wave_stats* stats);
 // Append (used, dependant slot, tag) entries to rows (set semantics, no state checks).
 fgi_status append_edges(fgi_graph* g, uint64_t m, const uint32_t* used_dev, const uint32_t* dep_dev,
                         const uint64_t* tag_dev, const uint32_t* dep_handle_dev);

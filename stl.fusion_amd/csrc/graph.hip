@@ -111,18 +111,20 @@ __global__ void k_scatter_rows(uint64_t m, const uint64_t* __restrict__ keys, co
                                const uint32_t* __restrict__ keep, const uint32_t* __restrict__ pos,
                                uint64_t ver_seed, uint32_t stale_pct, uint64_t stale_seed, uint32_t* pool_col,
                                uint64_t* pool_tag, uint64_t* row_off, uint32_t* row_len, uint32_t* used_cnt,
-                               const unsigned long long* node, uint32_t n_slots) {
+                               const unsigned long long* node, uint32_t n_slots, uint32_t src_base,
+                               uint32_t dst_base) {
     const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= m) return;
     const uint64_t k = keys[e];
     const uint32_t src = (uint32_t)(k >> 32), dst = (uint32_t)k;
     const uint32_t p = pos[e];
     if (keep[e]) {
-        const uint64_t t = tags ? tags[e] : edge_tag(ver_seed, stale_pct, stale_seed, src, dst);
+        const uint64_t t = tags ? tags[e] : edge_tag(ver_seed, stale_pct, stale_seed, src + src_base, dst);
         pool_col[p] = dst;
         pool_tag[p] = t;
         // the forward link dependant._used += used exists iff the tag is the dependant's version
-        if (dst < n_slots && (node[dst] & kVMask) == t && t != 0) atomicAdd(&used_cnt[dst], 1u);
+        const uint32_t ld = dst - dst_base;
+        if (ld < n_slots && (node[ld] & kVMask) == t && t != 0) atomicAdd(&used_cnt[ld], 1u);
     }
     const bool first = (e == 0) || (uint32_t)(keys[e - 1] >> 32) != src;
     const bool last = (e + 1 == m) || (uint32_t)(keys[e + 1] >> 32) != src;
@@ -630,7 +632,7 @@ fgi_status ensure_in_lists(fgi_graph* g) {
 }
 
 fgi_status build_rows_from_keys(fgi_graph* g, uint64_t m, uint64_t* keys, uint64_t* tags, uint64_t ver_seed,
-                                uint32_t stale_pct, uint64_t stale_seed) {
+                                uint32_t stale_pct, uint64_t stale_seed, uint32_t src_base, uint32_t dst_base) {
     hipStream_t s = g->stream;
     const uint32_t H = g->n_handles;
     // reset all rows (the pool is rebuilt from scratch)
@@ -681,7 +683,7 @@ fgi_status build_rows_from_keys(fgi_graph* g, uint64_t m, uint64_t* keys, uint64
     FGI_TRY(ensure_pool(g, total));
     hipLaunchKernelGGL(k_scatter_rows, dim3(nblk(m)), dim3(256), 0, s, m, k2, t2, keep, pos, ver_seed, stale_pct,
                        stale_seed, g->pool_col, g->pool_tag, g->row_off, g->row_len, g->used_cnt,
-                       reinterpret_cast<const unsigned long long*>(g->node), g->n_slots);
+                       reinterpret_cast<const unsigned long long*>(g->node), g->n_slots, src_base, dst_base);
     hipLaunchKernelGGL(k_fix_rows, dim3(nblk(H)), dim3(256), 0, s, H, g->row_off, g->row_len, g->row_cap);
     FGI_HIP(g, hipGetLastError());
     FGI_HIP(g, hipStreamSynchronize(s));

@@ -1,14 +1,143 @@
-// part.hip — multi-GPU 1-D vertex-range partition with an RCCL all-to-all frontier exchange.
-// (Filled in after the single-device path; until then the entry points report FGI_ENOTSUP.)
+// part.hip — multi-GPU engine: 1-D vertex-range partition of the slots over the GPUs of one node
+// (one process per GPU), frontier exchange with RCCL over xGMI.
+//
+// Rank p owns slots [p*B, p*B + n_local), B = ceil(N / world): their node words and their
+// `_usedBy` rows (entries keep the GLOBAL dependant slot). Every rank also holds a replica of all
+// N versions (versions never change during a wave), so the rank that traverses an edge to a
+// remote slot checks the tag against the version itself and forwards only matching targets. A
+// per-wave "sent" bitmap forwards each remote target at most once per wave: a node's first visit
+// in a wave is the only one that can change it (Computed.cs:164-191 — later visits find it
+// Invalidated, or the flag already set), so dropping the repeats is exact.
+//
+// Per level: local push (k_expand<true>) -> counts all-gather (ncclAllGather) -> payload by
+// grouped ncclSend/ncclRecv -> owners apply the received targets (k_apply_recv) -> global
+// frontier size by ncclAllReduce (termination).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include <rocprim/device/device_scan.hpp>
 
 #include "fgi_internal.h"
 
 namespace fgi {
+
+struct PartState {
+    PartView v{};
+    ncclComm_t comm = nullptr;
+    unsigned long long* all_cnt = nullptr;     // [world * world] device
+    unsigned long long* all_cnt_host = nullptr;
+    unsigned long long* scalar = nullptr;      // device scratch for all-reduce
+    unsigned long long* scalar_host = nullptr;
+};
+
+static PartState* ps(fgi_graph* g) { return reinterpret_cast<PartState*>(g->part); }
+
 fgi_status part_destroy(fgi_graph* g) {
-    (void)g;
+    PartState* p = ps(g);
+    if (!p) return FGI_OK;
+    if (p->comm) ncclCommDestroy(p->comm);
+    hipFree(p->v.ver_all);
+    hipFree(p->v.sent_bm);
+    hipFree(p->v.send_buf);
+    hipFree(p->v.recv_buf);
+    hipFree(p->v.send_cnt);
+    hipFree(p->all_cnt);
+    hipFree(p->scalar);
+    if (p->all_cnt_host) hipHostFree(p->all_cnt_host);
+    if (p->scalar_host) hipHostFree(p->scalar_host);
+    delete p;
+    g->part = nullptr;
     return FGI_OK;
 }
+
+bool part_view(fgi_graph* g, PartView* v) {
+    PartState* p = ps(g);
+    if (!p) return false;
+    *v = p->v;
+    return true;
+}
+
+static fgi_status nccl_check(fgi_graph* g, ncclResult_t r, const char* what) {
+    if (r == ncclSuccess) return FGI_OK;
+    return set_err(g, FGI_EDEVICE, "%s: %s", what, ncclGetErrorString(r));
+}
+#define FGI_NCCL(g, call)                                                  \
+    do {                                                                   \
+        ncclResult_t _r = (call);                                          \
+        if (_r != ncclSuccess) return nccl_check((g), _r, #call);          \
+    } while (0)
+
+fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent) {
+    PartState* p = ps(g);
+    const uint32_t W = p->v.world, R = p->v.rank;
+    hipStream_t s = g->stream;
+    FGI_NCCL(g, ncclAllGather(p->v.send_cnt, p->all_cnt, W, ncclUint64, p->comm, s));
+    FGI_HIP(g, hipMemcpyAsync(p->all_cnt_host, p->all_cnt, (size_t)W * W * 8, hipMemcpyDeviceToHost, s));
+    FGI_HIP(g, hipStreamSynchronize(s));
+    const unsigned long long* c = p->all_cnt_host;   // c[q * W + r]: sent by q to r
+    uint64_t recv = 0, sent = 0;
+    FGI_NCCL(g, ncclGroupStart());
+    for (uint32_t q = 0; q < W; ++q) {
+        if (q == R) continue;
+        const uint64_t to_q = c[R * W + q], from_q = c[q * W + R];
+        if (to_q)
+            FGI_NCCL(g, ncclSend(p->v.send_buf + (uint64_t)q * p->v.block, to_q, ncclUint32, (int)q, p->comm, s));
+        if (from_q) FGI_NCCL(g, ncclRecv(p->v.recv_buf + recv, from_q, ncclUint32, (int)q, p->comm, s));
+        recv += from_q;
+        sent += to_q;
+    }
+    FGI_NCCL(g, ncclGroupEnd());
+    *n_recv = recv;
+    *n_sent = sent;
+    return FGI_OK;
+}
+
+fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out) {
+    PartState* p = ps(g);
+    hipStream_t s = g->stream;
+    FGI_NCCL(g, ncclAllReduce(dev_val, p->scalar, 1, ncclUint64, ncclSum, p->comm, s));
+    FGI_HIP(g, hipMemcpyAsync(p->scalar_host, p->scalar, 8, hipMemcpyDeviceToHost, s));
+    FGI_HIP(g, hipStreamSynchronize(s));
+    *out = *p->scalar_host;
+    return FGI_OK;
+}
+
+namespace {
+
+__global__ void k_versions_all(uint32_t n, uint64_t seed, uint64_t* ver) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) ver[i] = synth_version(seed, (uint32_t)i);
+}
+
+__global__ void k_versions_local(uint32_t n, uint32_t base, uint64_t seed, unsigned long long* node) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) node[i] = synth_version(seed, base + i) | kW_Consistent;
+}
+
+__global__ void k_own_flags(uint64_t m, const uint64_t* __restrict__ keys, uint32_t base, uint32_t n_local,
+                            uint32_t* flag) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < m) flag[e] = ((uint32_t)(keys[e] >> 32) - base) < n_local ? 1u : 0u;
+}
+
+__global__ void k_own_compact(uint64_t m, const uint64_t* __restrict__ keys, const uint32_t* __restrict__ flag,
+                              const uint32_t* __restrict__ pos, uint32_t base, uint64_t* out) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < m && flag[e]) {
+        const uint64_t k = keys[e];
+        out[pos[e]] = ((uint64_t)((uint32_t)(k >> 32) - base) << 32) | (uint32_t)k;
+    }
+}
+
+}  // namespace
+
+fgi_status synth_rmat_keys(fgi_graph* g, uint32_t scale, uint32_t edge_factor, uint64_t seed, uint64_t** keys,
+                           uint64_t* m);
+
 }  // namespace fgi
 
 using namespace fgi;
@@ -16,22 +145,244 @@ using namespace fgi;
 extern "C" {
 
 fgi_status fgi_part_unique_id(uint8_t* id128) {
-    (void)id128;
-    return FGI_ENOTSUP;
+    if (!id128) return FGI_EINVAL;
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return FGI_EDEVICE;
+    std::memcpy(id128, id.internal, NCCL_UNIQUE_ID_BYTES);
+    return FGI_OK;
 }
+
+static fgi_status part_alloc(fgi_graph* g, uint32_t n_global);
+
 fgi_status fgi_part_init(fgi_graph* g, uint32_t n_global, const uint8_t* id128) {
-    (void)n_global;
-    (void)id128;
-    return set_err(g, FGI_ENOTSUP, "multi-GPU partition not built");
+    if (!g || !id128) return FGI_EINVAL;
+    if (g->part) return set_err(g, FGI_ESTATE, "partition already initialised");
+    FGI_TRY(part_alloc(g, n_global));
+    PartState* p = ps(g);
+    ncclUniqueId id;
+    std::memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
+    ncclResult_t r = ncclCommInitRank(&p->comm, (int)p->v.world, id, g->rank);
+    if (r != ncclSuccess) {
+        part_destroy(g);
+        return set_err(g, FGI_EDEVICE, "ncclCommInitRank: %s", ncclGetErrorString(r));
+    }
+    return FGI_OK;
 }
-fgi_status fgi_part_synth_rmat(fgi_graph* g, uint32_t, uint32_t, uint64_t, uint32_t, uint64_t) {
-    return set_err(g, FGI_ENOTSUP, "multi-GPU partition not built");
+
+static fgi_status part_alloc(fgi_graph* g, uint32_t n_global) {
+    if (!g || g->world < 1 || g->rank < 0 || g->rank >= g->world) return FGI_EINVAL;
+    if ((uint32_t)g->world > 8) return set_err(g, FGI_ENOTSUP, "at most 8 partitions (one node)");
+    if (g->part) return set_err(g, FGI_ESTATE, "partition already initialised");
+    const uint32_t W = (uint32_t)g->world;
+    const uint32_t block = (uint32_t)(((uint64_t)n_global + W - 1) / W);
+    if (g->n_slots < block) return set_err(g, FGI_EINVAL, "graph has %u slots, partition needs %u", g->n_slots, block);
+    hipSetDevice(g->device);
+    PartState* p = new PartState();
+    g->part = p;
+    p->v.rank = (uint32_t)g->rank;
+    p->v.world = W;
+    p->v.n_global = n_global;
+    p->v.block = block;
+    p->v.base = (uint32_t)std::min<uint64_t>((uint64_t)block * g->rank, n_global);
+    p->v.n_local = (uint32_t)std::min<uint64_t>(block, n_global - p->v.base);
+    p->v.sent_words = (uint64_t)n_global / 32 + 2;
+    auto fail = [&](const char* what) {
+        part_destroy(g);
+        return set_err(g, FGI_ENOMEM, "partition allocation failed: %s", what);
+    };
+    if (hipMalloc(&p->v.ver_all, (size_t)n_global * 8) != hipSuccess) return fail("versions");
+    if (hipMalloc(&p->v.sent_bm, p->v.sent_words * 4) != hipSuccess) return fail("sent bitmap");
+    if (hipMalloc(&p->v.send_buf, (size_t)W * block * 4) != hipSuccess) return fail("send buffer");
+    if (hipMalloc(&p->v.recv_buf, (size_t)W * block * 4) != hipSuccess) return fail("recv buffer");
+    if (hipMalloc(&p->v.send_cnt, (size_t)W * 8) != hipSuccess) return fail("counts");
+    if (hipMalloc(&p->all_cnt, (size_t)W * W * 8) != hipSuccess) return fail("counts");
+    if (hipMalloc(&p->scalar, 8) != hipSuccess) return fail("scalar");
+    if (hipHostMalloc(reinterpret_cast<void**>(&p->all_cnt_host), (size_t)W * W * 8) != hipSuccess) return fail("host");
+    if (hipHostMalloc(reinterpret_cast<void**>(&p->scalar_host), 8) != hipSuccess) return fail("host");
+    return FGI_OK;
 }
-fgi_status fgi_part_invalidate(fgi_graph* g, uint32_t, const uint32_t*, const uint8_t*, uint64_t*, fgi_wave_stats*) {
-    return set_err(g, FGI_ENOTSUP, "multi-GPU partition not built");
+
+fgi_status fgi_part_init_local(fgi_graph* const* gs, uint32_t P, uint32_t n_global) {
+    if (!gs || P == 0) return FGI_EINVAL;
+    for (uint32_t r = 0; r < P; ++r) {
+        if (!gs[r] || gs[r]->rank != (int)r || gs[r]->world != (int)P) return FGI_EINVAL;
+        FGI_TRY(part_alloc(gs[r], n_global));
+    }
+    return FGI_OK;
 }
-fgi_status fgi_part_export_ids(fgi_graph* g, uint32_t*, uint64_t, uint64_t*) {
-    return set_err(g, FGI_ENOTSUP, "multi-GPU partition not built");
+
+// In-process driver: the same phases as run_part_wave, the exchange done by device copies.
+fgi_status fgi_part_local_invalidate(fgi_graph* const* gs, uint32_t P, uint32_t n_roots, const uint32_t* roots,
+                                     const uint8_t* immediately, fgi_wave_stats* stats) {
+    if (!gs || P == 0 || (n_roots && !roots)) return FGI_EINVAL;
+    for (uint32_t r = 0; r < P; ++r)
+        if (!gs[r] || !gs[r]->part || ps(gs[r])->v.world != P) return FGI_EINVAL;
+    std::vector<uint32_t*> rd(P, nullptr);
+    std::vector<uint8_t*> id(P, nullptr);
+    auto cleanup = [&]() {
+        for (uint32_t r = 0; r < P; ++r) {
+            hipSetDevice(gs[r]->device);
+            hipFree(rd[r]);
+            hipFree(id[r]);
+        }
+    };
+    fgi_status st = FGI_OK;
+    for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
+        fgi_graph* g = gs[r];
+        hipSetDevice(g->device);
+        if (n_roots) {
+            if (hipMalloc(&rd[r], n_roots * 4) != hipSuccess ||
+                (immediately && hipMalloc(&id[r], n_roots) != hipSuccess)) {
+                st = FGI_ENOMEM;
+                break;
+            }
+            hipMemcpy(rd[r], roots, n_roots * 4, hipMemcpyHostToDevice);
+            if (immediately) hipMemcpy(id[r], immediately, n_roots, hipMemcpyHostToDevice);
+        }
+        st = part_wave_begin(g, n_roots, rd[r], id[r]);
+    }
+    auto frontier_total = [&](int L, uint64_t* out) -> fgi_status {
+        uint64_t t = 0;
+        for (uint32_t r = 0; r < P; ++r) {
+            unsigned long long f = 0;
+            hipSetDevice(gs[r]->device);
+            FGI_HIP(gs[r], hipMemcpyAsync(&f, part_level_frontier_dev(gs[r], L), 8, hipMemcpyDeviceToHost, gs[r]->stream));
+            FGI_HIP(gs[r], hipStreamSynchronize(gs[r]->stream));
+            t += f;
+        }
+        *out = t;
+        return FGI_OK;
+    };
+    uint64_t f_global = 0;
+    if (st == FGI_OK) st = frontier_total(0, &f_global);
+    std::vector<unsigned long long> cnt((size_t)P * P);
+    for (int L = 0; st == FGI_OK && f_global != 0; ++L) {
+        for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
+            hipSetDevice(gs[r]->device);
+            st = part_level_launch(gs[r], L);
+        }
+        // counts: cnt[r * P + q] = targets rank r forwards to owner q
+        for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
+            hipSetDevice(gs[r]->device);
+            if (hipMemcpyAsync(&cnt[(size_t)r * P], ps(gs[r])->v.send_cnt, P * 8, hipMemcpyDeviceToHost,
+                               gs[r]->stream) != hipSuccess ||
+                hipStreamSynchronize(gs[r]->stream) != hipSuccess)
+                st = set_err(gs[r], FGI_EDEVICE, "count readback");
+        }
+        for (uint32_t q = 0; q < P && st == FGI_OK; ++q) {
+            fgi_graph* gq = gs[q];
+            hipSetDevice(gq->device);
+            uint64_t off = 0, sent = 0;
+            for (uint32_t r = 0; r < P; ++r) {
+                if (r == q) continue;
+                const uint64_t c = cnt[(size_t)r * P + q];
+                if (c && hipMemcpyAsync(ps(gq)->v.recv_buf + off, ps(gs[r])->v.send_buf + (uint64_t)q * ps(gs[r])->v.block,
+                                        c * 4, hipMemcpyDefault, gq->stream) != hipSuccess)
+                    st = set_err(gq, FGI_EDEVICE, "exchange copy");
+                off += c;
+            }
+            for (uint32_t x = 0; x < P; ++x)
+                if (x != q) sent += cnt[(size_t)q * P + x];
+            if (st == FGI_OK) st = part_level_apply(gq, L, off, sent);
+        }
+        if (st == FGI_OK) st = frontier_total(L + 1, &f_global);
+        for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
+            hipSetDevice(gs[r]->device);
+            st = part_level_account(gs[r], L);
+        }
+    }
+    for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
+        hipSetDevice(gs[r]->device);
+        st = part_wave_end(gs[r], stats ? stats + r : nullptr);
+    }
+    cleanup();
+    return st;
+}
+
+fgi_status fgi_part_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_factor, uint64_t seed, uint32_t stale_pct,
+                               uint64_t stale_seed) {
+    if (!g || !g->part || scale == 0 || scale > 31 || edge_factor == 0 || stale_pct > 100) return FGI_EINVAL;
+    PartState* p = ps(g);
+    if ((1ull << scale) != p->v.n_global) return set_err(g, FGI_EINVAL, "partition was initialised for %u slots",
+                                                         p->v.n_global);
+    hipSetDevice(g->device);
+    hipStream_t s = g->stream;
+    const uint32_t N = p->v.n_global;
+    FGI_HIP(g, hipMemsetAsync(g->node, 0, (size_t)g->n_handles * 8, s));
+    hipLaunchKernelGGL(k_versions_local, dim3((p->v.n_local + 255) / 256), dim3(256), 0, s, p->v.n_local, p->v.base,
+                       seed, reinterpret_cast<unsigned long long*>(g->node));
+    hipLaunchKernelGGL(k_versions_all, dim3((N + 255) / 256), dim3(256), 0, s, N, seed, p->v.ver_all);
+    // every rank generates the global edge sequence and keeps the rows of the slots it owns
+    uint64_t* keys = nullptr;
+    uint64_t m = 0;
+    FGI_TRY(synth_rmat_keys(g, scale, edge_factor, seed, &keys, &m));
+    uint32_t *flag = nullptr, *pos = nullptr;
+    uint64_t* own = nullptr;
+    void* tmp = nullptr;
+    auto cleanup = [&]() {
+        hipFree(keys);
+        hipFree(flag);
+        hipFree(pos);
+        hipFree(own);
+        hipFree(tmp);
+    };
+    fgi_status st = FGI_OK;
+    do {
+        if (hipMalloc(&flag, m * 4) != hipSuccess || hipMalloc(&pos, m * 4) != hipSuccess) {
+            st = set_err(g, FGI_ENOMEM, "partition filter buffers");
+            break;
+        }
+        const uint32_t nb = (uint32_t)((m + 255) / 256);
+        hipLaunchKernelGGL(k_own_flags, dim3(nb), dim3(256), 0, s, m, keys, p->v.base, p->v.n_local, flag);
+        size_t tb = 0;
+        rocprim::exclusive_scan(nullptr, tb, flag, pos, 0u, (size_t)m, rocprim::plus<uint32_t>(), s);
+        if (hipMalloc(&tmp, tb) != hipSuccess) {
+            st = set_err(g, FGI_ENOMEM, "scan temp");
+            break;
+        }
+        rocprim::exclusive_scan(tmp, tb, flag, pos, 0u, (size_t)m, rocprim::plus<uint32_t>(), s);
+        uint32_t lp = 0, lf = 0;
+        hipMemcpyAsync(&lp, pos + m - 1, 4, hipMemcpyDeviceToHost, s);
+        hipMemcpyAsync(&lf, flag + m - 1, 4, hipMemcpyDeviceToHost, s);
+        hipStreamSynchronize(s);
+        const uint64_t mo = (uint64_t)lp + lf;
+        if (hipMalloc(&own, (mo ? mo : 1) * 8) != hipSuccess) {
+            st = set_err(g, FGI_ENOMEM, "owned keys");
+            break;
+        }
+        hipLaunchKernelGGL(k_own_compact, dim3(nb), dim3(256), 0, s, m, keys, flag, pos, p->v.base, own);
+        if (hipStreamSynchronize(s) != hipSuccess) {
+            st = set_err(g, FGI_EDEVICE, "partition filter");
+            break;
+        }
+        hipFree(keys);
+        keys = nullptr;
+        st = build_rows_from_keys(g, mo, own, nullptr, seed, stale_pct, stale_seed, p->v.base, p->v.base);
+    } while (0);
+    cleanup();
+    return st;
+}
+
+fgi_status fgi_part_invalidate(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
+                               uint64_t* out_n, fgi_wave_stats* stats) {
+    if (!g || !g->part || (n_roots && !roots_dev)) return FGI_EINVAL;
+    hipSetDevice(g->device);
+    FGI_TRY(run_part_wave(g, n_roots, roots_dev, imm_dev, stats));
+    if (out_n) *out_n = g->last_wave_n;
+    return FGI_OK;
+}
+
+fgi_status fgi_part_export_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n) {
+    if (!g || !g->part) return FGI_EINVAL;
+    const uint64_t n = g->last_wave_n;
+    if (out_n) *out_n = n;
+    if (!out_ids) return FGI_OK;
+    if (n > cap) return FGI_ECAPACITY;
+    hipSetDevice(g->device);
+    FGI_HIP(g, hipMemcpy(out_ids, g->inv, n * 4, hipMemcpyDeviceToHost));
+    const uint32_t base = ps(g)->v.base;
+    for (uint64_t i = 0; i < n; ++i) out_ids[i] += base;   // local handle -> global slot
+    return FGI_OK;
 }
 
 }  // extern "C"

@@ -221,6 +221,66 @@ __device__ __forceinline__ void emit_flush(Emit& e, uint32_t at, const uint64_t*
     __syncthreads();
 }
 
+// ---- multi-GPU: remote targets staged per block and bucketed by owner ------------------------
+constexpr uint32_t kMaxWorld = 8;
+constexpr uint32_t kMsgCap = 1024;
+struct RemoteArgs {
+    uint32_t base, n_local, block, world;
+    const uint64_t* ver_all;
+    uint32_t* sent_bm;
+    uint32_t* send_buf;
+    unsigned long long* send_cnt;
+};
+template <bool PART> struct MsgEmit {
+    uint32_t n;
+    uint32_t cnt[kMaxWorld], cur[kMaxWorld];
+    unsigned long long base[kMaxWorld];
+    uint32_t d[kMsgCap];
+};
+template <> struct MsgEmit<false> {
+    uint32_t n;
+};
+
+__device__ __forceinline__ void msg_push(MsgEmit<true>& me, bool send, uint32_t dst, const RemoteArgs& ra) {
+    const unsigned long long m = __ballot(send);
+    if (!m) return;
+    uint32_t base = 0;
+    if (lane_id() == 0) base = atomicAdd(&me.n, (uint32_t)__popcll(m));
+    base = __shfl(base, 0, 64);
+    if (send) {
+        const uint32_t idx = base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+        if (idx < kMsgCap) {
+            me.d[idx] = dst;
+        } else {
+            const uint32_t q = dst / ra.block;
+            ra.send_buf[(uint64_t)q * ra.block + atomicAdd(&ra.send_cnt[q], 1ull)] = dst;
+        }
+    }
+}
+
+__device__ __forceinline__ void msg_flush(MsgEmit<true>& me, uint32_t at, const RemoteArgs& ra) {
+    __syncthreads();
+    const uint32_t n = me.n < kMsgCap ? me.n : kMsgCap;
+    if (threadIdx.x < kMaxWorld) {
+        me.cnt[threadIdx.x] = 0;
+        me.cur[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    if (n < at || n == 0) return;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) atomicAdd(&me.cnt[me.d[i] / ra.block], 1u);
+    __syncthreads();
+    if (threadIdx.x < ra.world && me.cnt[threadIdx.x])
+        me.base[threadIdx.x] = atomicAdd(&ra.send_cnt[threadIdx.x], (unsigned long long)me.cnt[threadIdx.x]);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) {
+        const uint32_t dst = me.d[i], q = dst / ra.block;
+        ra.send_buf[(uint64_t)q * ra.block + me.base[q] + atomicAdd(&me.cur[q], 1u)] = dst;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) me.n = 0;
+    __syncthreads();
+}
+
 // ---- roots (level 0) ------------------------------------------------------------------------
 // Roots are resolved like ComputedExt.TryUseExisting (Internal/ComputedExt.cs:25-35): the
 // handle's current node, no tag check; immediately[i] selects Invalidate(true).
@@ -376,6 +436,9 @@ __device__ __forceinline__ uint32_t lds_upper_bound(const uint32_t* s, uint32_t 
     return lo;
 }
 
+// PART: multi-GPU rank — dependant slots outside [ra.base, ra.base + ra.n_local) are remote: their
+// tag is checked against the version replica and matching targets are forwarded once per wave.
+template <bool PART>
 __global__ __launch_bounds__(kBlock) void k_expand(int L, const uint64_t* __restrict__ fr_off,
                                                    const uint64_t* __restrict__ escan,
                                                    const uint32_t* __restrict__ cstart,
@@ -385,16 +448,20 @@ __global__ __launch_bounds__(kBlock) void k_expand(int L, const uint64_t* __rest
                                                    const uint32_t* __restrict__ row_len,
                                                    const uint32_t* __restrict__ dead_bm, int dead_filter,
                                                    uint32_t* __restrict__ inv, uint64_t* __restrict__ nfr_off,
-                                                   uint32_t* __restrict__ nfr_len, WaveCtr* ctr) {
+                                                   uint32_t* __restrict__ nfr_len, WaveCtr* ctr, RemoteArgs ra) {
     __shared__ uint32_t s_rel[kChunk + 1];
     __shared__ uint64_t s_base[kChunk + 1];
     __shared__ Emit em;
+    __shared__ MsgEmit<PART> me;
     LevelCtr& lc = ctr->lvl[L % kRing];
     LevelCtr& ln = ctr->lvl[(L + 1) % kRing];
     if (blockIdx.x == 0 && threadIdx.x < sizeof(LevelCtr) / 8)
         reinterpret_cast<unsigned long long*>(&ctr->lvl[(L + 2) % kRing])[threadIdx.x] = 0ull;
     if (lc.pull) return;
     emit_init(em);
+    if constexpr (PART) {
+        if (threadIdx.x == 0) me.n = 0;
+    }
     const uint64_t T = lc.T, F = lc.F, nch = lc.nchunks;
     uint32_t matched = 0, flagged = 0;
     for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
@@ -421,6 +488,29 @@ __global__ __launch_bounds__(kBlock) void k_expand(int L, const uint64_t* __rest
                 pos[j] = s_base[k] + local;
                 dst[j] = __builtin_nontemporal_load(pool_col + pos[j]);
             }
+        }
+        // remote dependants (PART): forwarded at most once per wave, only on a version match
+        if constexpr (PART) {
+#pragma unroll
+            for (int j = 0; j < kEPT; ++j) {
+                bool send = false;
+                const uint32_t d = dst[j];
+                if (d != 0xFFFFFFFFu && d - ra.base >= ra.n_local) {
+                    if (!bit_of(ra.sent_bm, d)) {
+                        const uint64_t t = __builtin_nontemporal_load(pool_tag + pos[j]);
+                        if (t != 0 && ra.ver_all[d] == t) {
+                            ++matched;
+                            const uint32_t b = 1u << (d & 31);
+                            send = !(atomicOr(ra.sent_bm + (d >> 5), b) & b);
+                        }
+                    }
+                    dst[j] = 0xFFFFFFFFu;
+                }
+                msg_push(me, send, d, ra);
+            }
+#pragma unroll
+            for (int j = 0; j < kEPT; ++j)
+                if (dst[j] != 0xFFFFFFFFu) dst[j] -= ra.base;   // local handle
         }
         // edges to nodes invalidated in an earlier level need neither the tag nor the gather
         if (dead_filter) {
@@ -453,8 +543,10 @@ __global__ __launch_bounds__(kBlock) void k_expand(int L, const uint64_t* __rest
         for (int j = 0; j < kEPT; ++j)
             emit_push(em, (win_mask >> j) & 1u, dst[j], row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
         emit_flush(em, kEmitCap / 2, row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
+        if constexpr (PART) msg_flush(me, kMsgCap / 2, ra);
     }
     emit_flush(em, 1, row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
+    if constexpr (PART) msg_flush(me, 1, ra);
     const uint32_t ms = wave_sum(matched), fs = wave_sum(flagged);
     if (lane_id() == 0) {
         if (ms) atomicAdd(&ctr->e_match, (unsigned long long)ms);
@@ -574,6 +666,65 @@ __global__ __launch_bounds__(kBlock) void k_pull_long(int L, const uint64_t* __r
     }
 }
 
+// multi-GPU roots: every rank gets the global list and visits the slots it owns
+__global__ __launch_bounds__(kBlock) void k_part_roots(const uint32_t* __restrict__ roots, const uint8_t* __restrict__ imm,
+                                                       uint32_t n, uint32_t base, uint32_t n_local,
+                                                       unsigned long long* node, const uint64_t* __restrict__ row_off,
+                                                       const uint32_t* __restrict__ row_len,
+                                                       uint32_t* __restrict__ inv, uint64_t* __restrict__ fr_off,
+                                                       uint32_t* __restrict__ fr_len, WaveCtr* ctr) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t win = 0, flagged = 0, h = 0;
+    if (i < n) {
+        h = roots[i] - base;
+        if (h < n_local) {
+            const unsigned long long w = node[h];
+            if ((w & kVMask) != 0) {
+                const int r = visit_word(node + h, w, imm ? imm[i] != 0 : false);
+                win = (r == 1);
+                flagged = (r == 2);
+            }
+        }
+    }
+    emit_one(win, h, row_off, row_len, inv, fr_off, fr_len, &ctr->inv, &ctr->lvl[0].F);
+    const uint32_t fs = wave_sum(flagged), ws = wave_sum(win);
+    if (lane_id() == 0 && fs) atomicAdd(&ctr->n_flagged, (unsigned long long)fs);
+    if (lane_id() == 0 && ws) atomicAdd(&ctr->root_inv, (unsigned long long)ws);
+}
+
+// multi-GPU: apply the targets other ranks forwarded (their versions were checked by the sender)
+__global__ __launch_bounds__(kBlock) void k_apply_recv(int L, uint64_t n, const uint32_t* __restrict__ recv, uint32_t base,
+                                                       unsigned long long* node, const uint64_t* __restrict__ row_off,
+                                                       const uint32_t* __restrict__ row_len,
+                                                       uint32_t* __restrict__ inv, uint64_t* __restrict__ nfr_off,
+                                                       uint32_t* __restrict__ nfr_len, WaveCtr* ctr) {
+    __shared__ Emit em;
+    LevelCtr& ln = ctr->lvl[(L + 1) % kRing];
+    emit_init(em);
+    uint32_t flagged = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t n_iter = (n + stride - 1) / stride;
+    for (uint64_t it = 0; it < n_iter; ++it) {
+        const uint64_t i = it * stride + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+        bool win = false;
+        uint32_t h = 0;
+        if (i < n) {
+            h = recv[i] - base;
+            const unsigned long long w = node[h];
+            if ((w & kVMask) != 0) {
+                const int r = visit_word(node + h, w, false);
+                win = (r == 1);
+                flagged += (r == 2);
+            }
+        }
+        emit_push(em, win, h, row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
+        emit_flush(em, kEmitCap - kBlock, row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
+    }
+    emit_flush(em, 1, row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
+    const uint32_t fs = wave_sum(flagged);
+    if (lane_id() == 0 && fs) atomicAdd(&ctr->n_flagged, (unsigned long long)fs);
+}
+
 }  // namespace
 
 fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
@@ -628,10 +779,10 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                 }
                 FGI_HIP(g, hipEventRecord(g->ev[4 * L], s));
             }
-            hipLaunchKernelGGL(k_expand, dim3(expand_grid), dim3(kBlock), 0, s, L, g->fr_off[buf], g->escan, g->cstart,
-                               g->pool_col, g->pool_tag, reinterpret_cast<unsigned long long*>(g->node), g->row_off,
-                               g->row_len, g->dead_bm, g->opt_dead_filter, g->inv, g->fr_off[buf ^ 1],
-                               g->fr_len[buf ^ 1], g->ctr);
+            hipLaunchKernelGGL(k_expand<false>, dim3(expand_grid), dim3(kBlock), 0, s, L, g->fr_off[buf], g->escan,
+                               g->cstart, g->pool_col, g->pool_tag, reinterpret_cast<unsigned long long*>(g->node),
+                               g->row_off, g->row_len, g->dead_bm, g->opt_dead_filter, g->inv, g->fr_off[buf ^ 1],
+                               g->fr_len[buf ^ 1], g->ctr, RemoteArgs{});
             if (timing) FGI_HIP(g, hipEventRecord(g->ev[4 * L + 1], s));
             if (dir_eff != 1) {
                 hipLaunchKernelGGL(k_pull, dim3(pull_grid), dim3(kBlock), 0, s, L, g->n_slots, g->uin_off, g->uin_len,
@@ -729,6 +880,138 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         stats->total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     return FGI_OK;
+}
+
+// ---- multi-GPU wave, split into phases shared by the RCCL driver (one process per GPU) and the
+// in-process driver (several partitions of one graph on one device, exchange by device copies).
+fgi_status part_wave_begin(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev) {
+    PartView pv;
+    if (!part_view(g, &pv)) return set_err(g, FGI_ESTATE, "partition not initialised");
+    hipStream_t s = g->stream;
+    g->pw = PartWave{};
+    g->pw.t0 = std::chrono::steady_clock::now();
+    g->pw.n_roots = n_roots;
+    FGI_TRY(ensure_cstart(g, g->pool_top));
+    FGI_HIP(g, hipMemsetAsync(g->ctr, 0, sizeof(WaveCtr), s));
+    FGI_HIP(g, hipMemsetAsync(g->dead_bm, 0, g->bm_words * 4, s));
+    FGI_HIP(g, hipMemsetAsync(pv.sent_bm, 0, pv.sent_words * 4, s));
+    while (g->ev.size() < 2) {
+        hipEvent_t e;
+        FGI_HIP(g, hipEventCreate(&e));
+        g->ev.push_back(e);
+    }
+    FGI_HIP(g, hipEventRecord(g->ev_w0, s));
+    if (n_roots)
+        hipLaunchKernelGGL(k_part_roots, dim3((n_roots + kBlock - 1) / kBlock), dim3(kBlock), 0, s, roots_dev, imm_dev,
+                           n_roots, pv.base, pv.n_local, reinterpret_cast<unsigned long long*>(g->node), g->row_off,
+                           g->row_len, g->inv, g->fr_off[0], g->fr_len[0], g->ctr);
+    FGI_HIP(g, hipGetLastError());
+    return FGI_OK;
+}
+
+const unsigned long long* part_level_frontier_dev(fgi_graph* g, int L) { return &g->ctr->lvl[L % kRing].F; }
+
+fgi_status part_level_launch(fgi_graph* g, int L) {
+    PartView pv;
+    part_view(g, &pv);
+    hipStream_t s = g->stream;
+    int n_cu = 256;
+    hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device);
+    const uint32_t expand_grid = (uint32_t)n_cu * 4, mark_grid = (uint32_t)n_cu * 2;
+    const RemoteArgs ra{pv.base, pv.n_local, pv.block, pv.world, pv.ver_all, pv.sent_bm, pv.send_buf, pv.send_cnt};
+    const int buf = L & 1;
+    FGI_HIP(g, hipMemsetAsync(pv.send_cnt, 0, (size_t)pv.world * 8, s));
+    hipLaunchKernelGGL(k_scan_reduce, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->fr_len[buf], g->partials, g->ctr);
+    hipLaunchKernelGGL(k_scan_apply, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->fr_len[buf], g->partials, g->escan,
+                       g->cstart, g->ctr, 1, (uint64_t)0);
+    hipLaunchKernelGGL(k_mark, dim3(mark_grid), dim3(kBlock), 0, s, L, g->inv, g->dead_bm, g->front_bm, g->ctr);
+    FGI_HIP(g, hipEventRecord(g->ev[0], s));
+    hipLaunchKernelGGL(k_expand<true>, dim3(expand_grid), dim3(kBlock), 0, s, L, g->fr_off[buf], g->escan, g->cstart,
+                       g->pool_col, g->pool_tag, reinterpret_cast<unsigned long long*>(g->node), g->row_off, g->row_len,
+                       g->dead_bm, g->opt_dead_filter, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], g->ctr, ra);
+    FGI_HIP(g, hipEventRecord(g->ev[1], s));
+    FGI_HIP(g, hipGetLastError());
+    return FGI_OK;
+}
+
+fgi_status part_level_apply(fgi_graph* g, int L, uint64_t n_recv, uint64_t n_sent) {
+    PartView pv;
+    part_view(g, &pv);
+    hipStream_t s = g->stream;
+    int n_cu = 256;
+    hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device);
+    const int buf = L & 1;
+    if (n_recv)
+        hipLaunchKernelGGL(k_apply_recv, dim3(std::min<uint64_t>((n_recv + kBlock - 1) / kBlock, (uint64_t)n_cu * 8)),
+                           dim3(kBlock), 0, s, L, n_recv, pv.recv_buf, pv.base,
+                           reinterpret_cast<unsigned long long*>(g->node), g->row_off, g->row_len, g->inv,
+                           g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], g->ctr);
+    hipLaunchKernelGGL(k_clear_front, dim3((uint32_t)n_cu * 2), dim3(kBlock), 0, s, L, g->inv, g->front_bm, g->ctr);
+    FGI_HIP(g, hipGetLastError());
+    g->pw.sent += n_sent;
+    return FGI_OK;
+}
+
+// after the level's frontier total is known (the stream has been synchronised by then)
+fgi_status part_level_account(fgi_graph* g, int L) {
+    FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, g->stream));
+    FGI_HIP(g, hipStreamSynchronize(g->stream));
+    const LevelCtr& lc = g->ctr_host->lvl[L % kRing];
+    g->pw.levels++;
+    g->pw.e_trav += lc.T;
+    g->pw.f_total += lc.F;
+    float ms = 0;
+    FGI_HIP(g, hipEventElapsedTime(&ms, g->ev[0], g->ev[1]));
+    g->pw.expand_ms += ms;
+    g->pw.expand_launches++;
+    return FGI_OK;
+}
+
+fgi_status part_wave_end(fgi_graph* g, fgi_wave_stats* stats) {
+    hipStream_t s = g->stream;
+    FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
+    FGI_HIP(g, hipEventRecord(g->ev_w1, s));
+    FGI_HIP(g, hipStreamSynchronize(s));
+    g->last_wave_n = g->ctr_host->inv;
+    if (stats) {
+        const PartWave& w = g->pw;
+        const uint64_t v = g->ctr_host->inv;
+        stats->roots += w.n_roots;
+        stats->levels += w.levels;
+        stats->v_inv += v;
+        stats->e_trav += w.e_trav;
+        stats->e_match += g->ctr_host->e_match;
+        stats->n_flagged += g->ctr_host->n_flagged;
+        stats->remote_msgs += w.sent;
+        // as run_wave's push levels, plus 8 B per forwarded target (4 written + 4 received)
+        stats->alg_bytes += 20 * w.e_trav + 44 * w.f_total + 24 * v + 8 * w.sent + 5ull * w.n_roots;
+        float wave_ms = 0;
+        hipEventElapsedTime(&wave_ms, g->ev_w0, g->ev_w1);
+        stats->kernel_ms += wave_ms;
+        stats->expand_ms += w.expand_ms;
+        stats->expand_launches += w.expand_launches;
+        stats->expand_bytes += 20 * w.e_trav + 16 * w.f_total;
+        stats->f_total += w.f_total;
+        stats->total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w.t0).count();
+    }
+    return FGI_OK;
+}
+
+// One process per GPU: levels in lockstep over RCCL.
+fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
+                         fgi_wave_stats* stats) {
+    FGI_TRY(part_wave_begin(g, n_roots, roots_dev, imm_dev));
+    uint64_t f_global = 0;
+    FGI_TRY(part_allreduce_sum(g, part_level_frontier_dev(g, 0), &f_global));
+    for (int L = 0; f_global != 0; ++L) {
+        FGI_TRY(part_level_launch(g, L));
+        uint64_t n_recv = 0, n_sent = 0;
+        FGI_TRY(part_exchange(g, &n_recv, &n_sent));
+        FGI_TRY(part_level_apply(g, L, n_recv, n_sent));
+        FGI_TRY(part_allreduce_sum(g, part_level_frontier_dev(g, L + 1), &f_global));
+        FGI_TRY(part_level_account(g, L));
+    }
+    return part_wave_end(g, stats);
 }
 
 }  // namespace fgi

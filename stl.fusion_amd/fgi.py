@@ -95,6 +95,8 @@ SIGNATURES = {
     "fgi_part_synth_rmat": [_G, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint64],
     "fgi_part_invalidate": [_G, C.c_uint32, C.c_void_p, C.c_void_p, _u64p, C.POINTER(WaveStats)],
     "fgi_part_export_ids": [_G, _u32p, C.c_uint64, _u64p],
+    "fgi_part_init_local": [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32],
+    "fgi_part_local_invalidate": [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32, _u32p, _u8p, C.POINTER(WaveStats)],
 }
 
 _lib = None
@@ -315,6 +317,62 @@ class Graph:
         s = C.c_void_p()
         self._check(self.lib.fgi_stream(self.h, C.byref(s)), "stream")
         return s.value or 0
+
+
+    # ---- multi-GPU partition ----
+    def part_init(self, n_global: int, unique_id: bytes):
+        buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
+        self._check(self.lib.fgi_part_init(self.h, n_global, buf), "part_init")
+
+    def part_synth_rmat(self, scale, edge_factor, seed, stale_pct=0, stale_seed=0):
+        self._check(self.lib.fgi_part_synth_rmat(self.h, scale, edge_factor, seed, stale_pct, stale_seed),
+                    "part_synth_rmat")
+
+    def part_invalidate(self, n_roots: int, roots_ptr: int, imm_ptr: int = 0,
+                        stats: Optional[WaveStats] = None) -> int:
+        n = C.c_uint64()
+        self._check(self.lib.fgi_part_invalidate(self.h, n_roots, C.c_void_p(roots_ptr),
+                                                 C.c_void_p(imm_ptr) if imm_ptr else None, C.byref(n),
+                                                 C.byref(stats) if stats is not None else None), "part_invalidate")
+        return n.value
+
+    def part_export_ids(self) -> np.ndarray:
+        n = C.c_uint64()
+        st = self.lib.fgi_part_export_ids(self.h, None, 0, C.byref(n))
+        self._check(st, "part_export_ids")
+        out = np.zeros(n.value, np.uint32)
+        self._check(self.lib.fgi_part_export_ids(self.h, _ptr(out, C.c_uint32), n.value, C.byref(n)), "part_export_ids")
+        return out
+
+
+def part_unique_id() -> bytes:
+    lib = load_library()
+    buf = (C.c_uint8 * 128)()
+    st = lib.fgi_part_unique_id(buf)
+    if st != OK:
+        raise FgiError(st, "fgi_part_unique_id")
+    return bytes(buf)
+
+
+def part_init_local(graphs, n_global: int):
+    """Bind graphs (rank i of world len(graphs)) into an in-process partition group."""
+    lib = load_library()
+    arr = (C.c_void_p * len(graphs))(*[g.h.value for g in graphs])
+    st = lib.fgi_part_init_local(arr, len(graphs), n_global)
+    if st != OK:
+        raise FgiError(st, "fgi_part_init_local: " + (lib.fgi_last_error(graphs[0].h) or b"").decode())
+
+
+def part_local_invalidate(graphs, roots, immediately=None):
+    lib = load_library()
+    arr = (C.c_void_p * len(graphs))(*[g.h.value for g in graphs])
+    r = _u32(roots)
+    imm = None if immediately is None else _u8(immediately)
+    stats = (WaveStats * len(graphs))()
+    st = lib.fgi_part_local_invalidate(arr, len(graphs), len(r), _ptr(r, C.c_uint32), _ptr(imm, C.c_uint8), stats)
+    if st != OK:
+        raise FgiError(st, "fgi_part_local_invalidate")
+    return list(stats)
 
 
 def header_symbols(header_path: str) -> list:
