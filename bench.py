@@ -68,6 +68,10 @@ def cpu_baseline(threads: int, scale: int = 20, edge_factor: int = 16, roots: in
 
 
 def main():
+    # Libraries (RCCL prints a banner on communicator init) must not write to stdout: the driver
+    # reads exactly one JSON line from it. Route fd 1 to stderr and keep a handle on the real one.
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -75,6 +79,8 @@ def main():
     ap.add_argument("--config", default="rmat24")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-scale", type=int, default=20)
+    ap.add_argument("--partition", action="store_true",
+                    help="use the partitioned RCCL engine even at N=1 (it is always used for N>1)")
     args = ap.parse_args()
 
     import torch
@@ -91,21 +97,61 @@ def main():
 
     pkg = _pkg.load()
     from stl_fusion_amd import workloads as W
-    cfg = W.CONFIGS[args.config]
+    partitioned = world > 1 or args.partition
+    cfg = dict(W.CONFIGS[args.config])
+    if partitioned:
+        # weak scaling: R-MAT scale 24 + log2(N) keeps configs[1]'s 16M slots per GPU (N = 8 is
+        # scale 27, the node count of configs[2]); --config rmat27 runs configs[2] exactly.
+        if cfg["kind"] != "rmat":
+            raise SystemExit("the partitioned engine runs R-MAT workloads")
+        if args.config == "rmat24":
+            cfg["scale"] = 24 + (world - 1).bit_length()
     n = W.n_slots(cfg)
     t0 = time.time()
-    g = pkg.Graph(n, device=local_rank)
-    W.build(g, cfg)
-    roots = W.roots_for(g, cfg)
-    _, n_edges = g.degrees()
+    if partitioned:
+        block = -(-n // world)
+        g = pkg.Graph(block, device=local_rank, rank=rank, world=world)
+        uid = [pkg.fgi.part_unique_id() if rank == 0 else None]
+        if dist:
+            dist.broadcast_object_list(uid, src=0)
+        g.part_init(n, uid[0])
+        g.part_synth_rmat(cfg["scale"], cfg["edge_factor"], cfg["seed"], cfg.get("stale_pct", 0),
+                          cfg.get("stale_seed", 0))
+        n_local = min(block, n - rank * block)
+        deg_local, _ = g.degrees()
+        deg = torch.zeros(block * world, dtype=torch.int32, device=f"cuda:{local_rank}")
+        mine = torch.zeros(block, dtype=torch.int32, device=f"cuda:{local_rank}")
+        mine[:n_local] = torch.from_numpy(deg_local[:n_local].astype(np.int32)).to(mine.device)
+        if dist:
+            dist.all_gather_into_tensor(deg, mine)
+        else:
+            deg = mine
+        deg_all = deg.cpu().numpy()[:n]
+        roots = W.pick_roots(cfg["roots"], n, cfg["roots_seed"], deg_all)
+        n_edges = int(deg_all.astype(np.int64).sum())
+    else:
+        g = pkg.Graph(n, device=local_rank)
+        W.build(g, cfg)
+        roots = W.roots_for(g, cfg)
+        _, n_edges = g.degrees()
     build_s = time.time() - t0
     d_roots = torch.from_numpy(roots.astype(np.int32)).to(f"cuda:{local_rank}")
     g.snapshot()
-    log(f"[rank {rank}] built {args.config}: {n} slots, {n_edges} edges, {len(roots)} roots in {build_s:.1f}s")
+    log(f"[rank {rank}] built {args.config} (scale {cfg.get('scale')}): {n} slots, {n_edges} edges, "
+        f"{len(roots)} roots in {build_s:.1f}s, partitioned={partitioned}")
 
     def step(stats):
         g.restore()
+        if partitioned:
+            return g.part_invalidate(len(roots), d_roots.data_ptr(), 0, stats)
         return g.invalidate_dev(len(roots), d_roots.data_ptr(), 0, stats)
+
+    # the first wave may build the pull dependency-list cache (a per-topology index, like the
+    # rows themselves); it is timed separately and reported, never inside the timed steps
+    t_first = time.perf_counter()
+    step(pkg.WaveStats())
+    torch.cuda.synchronize()
+    first_wave_s = time.perf_counter() - t_first
 
     for _ in range(args.warmup):
         step(pkg.WaveStats())
@@ -133,7 +179,12 @@ def main():
 
     value = v_inv / elapsed
     gteps = e_trav / elapsed / 1e9
-    expand_gbs = (st.expand_bytes / (st.expand_ms * 1e-3) / 1e9) if st.expand_ms > 0 else 0.0
+    # roofline of the dominant kernel (the one with the larger summed device time)
+    if st.pull_ms > st.expand_ms:
+        kname, k_ms, k_bytes, k_launches = "k_pull", st.pull_ms, st.pull_bytes, st.pull_launches
+    else:
+        kname, k_ms, k_bytes, k_launches = "k_expand", st.expand_ms, st.expand_bytes, st.expand_launches
+    k_gbs = (k_bytes / (k_ms * 1e-3) / 1e9) if k_ms > 0 else 0.0
     wave_gbs = (st.alg_bytes / (st.kernel_ms * 1e-3) / 1e9) if st.kernel_ms > 0 else 0.0
     result = {
         "metric": METRIC,
@@ -155,7 +206,9 @@ def main():
                          "rmat27": "R-MAT scale 27, edge factor 8 (configs[2])",
                          "rmat24_churn": "configs[1] graph with 50% stale edges (configs[3])"}[args.config],
             "nodes": n, "edges": int(n_edges), "roots": int(len(roots)),
-            "parallelism": "single" if world == 1 else f"replicas{world}",
+            "parallelism": (f"vertex-partition x{world} (RCCL all-gather counts + send/recv frontier)"
+                            if partitioned else "single"),
+            "scale": cfg.get("scale"), "edge_factor": cfg.get("edge_factor"),
         },
         "gteps": gteps,
         "v_inv_per_step": st.v_inv // args.steps,
@@ -163,17 +216,23 @@ def main():
         "levels_per_step": st.levels / args.steps,
         "wave_kernel_ms": st.kernel_ms / args.steps,
         "wave_alg_gbs": wave_gbs,
+        "pull_levels_per_step": st.pull_levels / args.steps,
+        "remote_msgs_per_step": st.remote_msgs / args.steps,
+        "first_wave_s": first_wave_s,
+        "build_s": build_s,
         "roofline": {
             "bound": "hbm",
-            "kernel": "k_expand",
-            "achieved": expand_gbs,
+            "kernel": kname,
+            "achieved": k_gbs,
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
-            "frac": expand_gbs / HBM_PEAK_GBS,
+            "frac": k_gbs / HBM_PEAK_GBS,
             "traffic": None,
-            "launches_per_step": st.expand_launches / args.steps,
-            "avg_launch_ms": st.expand_ms / max(1, st.expand_launches),
-            "alg_bytes_per_launch": st.expand_bytes / max(1, st.expand_launches),
+            "launches_per_step": k_launches / args.steps,
+            "avg_launch_ms": k_ms / max(1, k_launches),
+            "alg_bytes_per_launch": k_bytes / max(1, k_launches),
+            "expand_ms_per_step": st.expand_ms / args.steps,
+            "pull_ms_per_step": st.pull_ms / args.steps,
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -197,7 +256,8 @@ def main():
         except Exception as e:  # the CPU leg must not hide the GPU number
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        json_out.write(json.dumps(result) + "\n")
+        json_out.flush()
     g.close()
     if dist:
         dist.destroy_process_group()

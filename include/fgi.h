@@ -100,8 +100,9 @@ typedef struct fgi_wave_stats {
     uint64_t expand_bytes;     /* algorithmic bytes of those launches */
     uint64_t pull_levels;      /* levels run bottom-up */
     uint64_t pull_edges;       /* dependency-list entries examined by pull levels */
-    double pull_ms;            /* device time of the pull kernels */
-    uint64_t pull_bytes;       /* algorithmic bytes of the pull kernels */
+    double pull_ms;            /* device time of the k_pull launches (HIP events) */
+    uint64_t pull_bytes;       /* algorithmic bytes of the k_pull launches */
+    uint64_t pull_launches;    /* k_pull launches (every level of a wave that may pull) */
 } fgi_wave_stats;
 
 typedef struct fgi_prune_stats {

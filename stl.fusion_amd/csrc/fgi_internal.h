@@ -97,7 +97,10 @@ struct WaveCtr {
     unsigned long long marked;      // inv[] entries already marked in the dead bitmap
     unsigned long long pull_cand;   // pull: slots whose dependency list was scanned
     unsigned long long pull_edges;  // pull: dependency entries examined
-    unsigned long long pad[1];
+    unsigned long long pull_live;   // pull: slots not yet dead when scanned
+    unsigned long long pull_win;    // pull: nodes invalidated by pull levels
+    unsigned long long pull_scan;   // pull: slots scanned (bitmap reads), summed over pull levels
+    unsigned long long pad[6];
     LevelCtr lvl[kRing];
 };
 
@@ -105,7 +108,9 @@ struct WaveCtr {
 struct PartWave {
     std::chrono::steady_clock::time_point t0;
     uint64_t n_roots = 0, levels = 0, e_trav = 0, f_total = 0, sent = 0, expand_launches = 0;
-    double expand_ms = 0;
+    uint64_t push_edges = 0, push_f = 0, pull_launches = 0, pull_levels = 0;
+    double expand_ms = 0, pull_ms = 0;
+    bool pulled = false;
 };
 
 // ---- host-side graph object -------------------------------------------------------------------
@@ -236,6 +241,9 @@ struct PartView {
     uint32_t* send_buf;         // [world][block] outgoing target ids per owner
     uint32_t* recv_buf;         // [world * block] incoming, concatenated
     unsigned long long* send_cnt;   // [world] device counters
+    uint32_t* front_global;     // [n_global bits] all-gathered frontier bitmap (pull levels)
+    uint64_t front_words_global;
+    unsigned long long* scratch_u64;
 };
 bool part_view(fgi_graph* g, PartView* v);
 // Exchange this level's messages: counts by all-gather, payload by grouped send/recv over RCCL.
@@ -248,8 +256,13 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
                          fgi_wave_stats* stats);
 fgi_status part_wave_begin(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev);
 const unsigned long long* part_level_frontier_dev(fgi_graph* g, int L);
-fgi_status part_level_launch(fgi_graph* g, int L);
+const unsigned long long* part_level_edges_dev(fgi_graph* g, int L);
+fgi_status part_level_scan(fgi_graph* g, int L);
+fgi_status part_level_mark(fgi_graph* g, int L, bool pull);
+fgi_status part_level_work(fgi_graph* g, int L, bool pull);
 fgi_status part_level_apply(fgi_graph* g, int L, uint64_t n_recv, uint64_t n_sent);
+// all-gather every rank's local frontier words into front_global (part.hip)
+fgi_status part_allgather_front(fgi_graph* g);
 fgi_status part_level_account(fgi_graph* g, int L);
 fgi_status part_wave_end(fgi_graph* g, fgi_wave_stats* stats);
 // Append (used, dependant slot, tag) entries to rows (set semantics, no state checks).

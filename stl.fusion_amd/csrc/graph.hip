@@ -987,6 +987,11 @@ fgi_status fgi_restore(fgi_graph* g) {
     const size_t H = g->n_handles;
     hipStream_t s = g->stream;
     FGI_HIP(g, hipMemcpyAsync(g->node, g->snap_node, H * 8, hipMemcpyDeviceToDevice, s));
+    if (g->mut_epoch == g->snap_mut_epoch) {
+        // nothing but waves ran since the snapshot: rows and |_used| counts are unchanged
+        FGI_HIP(g, hipStreamSynchronize(s));
+        return FGI_OK;
+    }
     FGI_HIP(g, hipMemcpyAsync(g->row_off, g->snap_row_off, H * 8, hipMemcpyDeviceToDevice, s));
     FGI_HIP(g, hipMemcpyAsync(g->row_len, g->snap_row_len, H * 4, hipMemcpyDeviceToDevice, s));
     FGI_HIP(g, hipMemcpyAsync(g->row_cap, g->snap_row_cap, H * 4, hipMemcpyDeviceToDevice, s));

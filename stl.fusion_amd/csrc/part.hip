@@ -19,6 +19,7 @@
 #include <cstring>
 #include <vector>
 
+#include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
 #include "fgi_internal.h"
@@ -47,6 +48,8 @@ fgi_status part_destroy(fgi_graph* g) {
     hipFree(p->v.send_cnt);
     hipFree(p->all_cnt);
     hipFree(p->scalar);
+    hipFree(p->v.front_global);
+    hipFree(p->v.scratch_u64);
     if (p->all_cnt_host) hipHostFree(p->all_cnt_host);
     if (p->scalar_host) hipHostFree(p->scalar_host);
     delete p;
@@ -96,6 +99,12 @@ fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent) {
     return FGI_OK;
 }
 
+fgi_status part_allgather_front(fgi_graph* g) {
+    PartState* p = ps(g);
+    FGI_NCCL(g, ncclAllGather(g->front_bm, p->v.front_global, p->v.block / 32, ncclUint32, p->comm, g->stream));
+    return FGI_OK;
+}
+
 fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out) {
     PartState* p = ps(g);
     hipStream_t s = g->stream;
@@ -133,10 +142,137 @@ __global__ void k_own_compact(uint64_t m, const uint64_t* __restrict__ keys, con
     }
 }
 
+// dependency lists of the owned slots from the global edge sequence: (dst_local << 32 | src_global)
+// for every non-stale edge whose dependant this rank owns
+__device__ __forceinline__ bool synth_stale(uint32_t stale_pct, uint64_t stale_seed, uint32_t src, uint32_t dst) {
+    return stale_pct && (sm64(stale_seed ^ sm64(((uint64_t)src << 32) | dst)) % 100) < stale_pct;
+}
+
+__global__ void k_in_part_flags(uint64_t m, const uint64_t* __restrict__ keys, uint32_t base, uint32_t n_local,
+                                uint32_t stale_pct, uint64_t stale_seed, uint32_t* flag) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    const uint64_t k = keys[e];
+    const uint32_t src = (uint32_t)(k >> 32), dst = (uint32_t)k;
+    flag[e] = (dst - base < n_local && !synth_stale(stale_pct, stale_seed, src, dst)) ? 1u : 0u;
+}
+
+__global__ void k_in_part_compact(uint64_t m, const uint64_t* __restrict__ keys, const uint32_t* __restrict__ flag,
+                                  const uint32_t* __restrict__ pos, uint32_t base, uint64_t* out) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < m && flag[e]) {
+        const uint64_t k = keys[e];
+        out[pos[e]] = ((uint64_t)((uint32_t)k - base) << 32) | (uint32_t)(k >> 32);
+    }
+}
+
+__global__ void k_in_part_unique(uint64_t m, const uint64_t* __restrict__ k, uint32_t* keep) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < m) keep[e] = (e == 0 || k[e] != k[e - 1]) ? 1u : 0u;
+}
+
+__global__ void k_in_part_rows(uint64_t m, const uint64_t* __restrict__ k, const uint32_t* __restrict__ keep,
+                               const uint32_t* __restrict__ pos, uint32_t* src_out, uint64_t* off, uint32_t* len) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    const uint32_t d = (uint32_t)(k[e] >> 32);
+    if (keep[e]) src_out[pos[e]] = (uint32_t)k[e];
+    if (e == 0 || (uint32_t)(k[e - 1] >> 32) != d) off[d] = pos[e];
+    if (e + 1 == m || (uint32_t)(k[e + 1] >> 32) != d) len[d] = pos[e] + keep[e];   // row end, fixed below
+}
+
+__global__ void k_in_part_fix(uint32_t n, const uint64_t* __restrict__ off, uint32_t* len) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d < n && len[d]) len[d] -= (uint32_t)off[d];
+}
+
 }  // namespace
 
 fgi_status synth_rmat_keys(fgi_graph* g, uint32_t scale, uint32_t edge_factor, uint64_t seed, uint64_t** keys,
                            uint64_t* m);
+
+// Builds g->uin_* for the owned slots from the global keys. flag/pos are caller scratch of m
+// entries; *tmp is a scan scratch the caller frees.
+static fgi_status part_build_in_lists(fgi_graph* g, const uint64_t* keys, uint64_t m, uint32_t stale_pct,
+                                      uint64_t stale_seed, uint32_t* flag, uint32_t* pos, void** tmp) {
+    PartState* p = ps(g);
+    hipStream_t s = g->stream;
+    const uint32_t nb = (uint32_t)((m + 255) / 256);
+    hipLaunchKernelGGL(k_in_part_flags, dim3(nb), dim3(256), 0, s, m, keys, p->v.base, p->v.n_local, stale_pct,
+                       stale_seed, flag);
+    size_t tb = 0;
+    rocprim::exclusive_scan(nullptr, tb, flag, pos, 0u, (size_t)m, rocprim::plus<uint32_t>(), s);
+    hipFree(*tmp);
+    *tmp = nullptr;
+    FGI_HIP(g, hipMalloc(tmp, tb));
+    rocprim::exclusive_scan(*tmp, tb, flag, pos, 0u, (size_t)m, rocprim::plus<uint32_t>(), s);
+    uint32_t lp = 0, lf = 0;
+    FGI_HIP(g, hipMemcpyAsync(&lp, pos + m - 1, 4, hipMemcpyDeviceToHost, s));
+    FGI_HIP(g, hipMemcpyAsync(&lf, flag + m - 1, 4, hipMemcpyDeviceToHost, s));
+    FGI_HIP(g, hipStreamSynchronize(s));
+    const uint64_t mi = (uint64_t)lp + lf;
+    FGI_HIP(g, hipMemsetAsync(g->uin_len, 0, (size_t)g->n_slots * 4, s));
+    FGI_HIP(g, hipMemsetAsync(g->uin_off, 0, (size_t)g->n_slots * 8, s));
+    if (mi == 0) {
+        if (!g->uin_src) FGI_HIP(g, hipMalloc(&g->uin_src, 1024 * 4));
+        return FGI_OK;
+    }
+    uint64_t *k1 = nullptr, *k2 = nullptr;
+    uint32_t *keep = nullptr, *kpos = nullptr;
+    void* st = nullptr;
+    fgi_status rc = FGI_OK;
+    do {
+        if (hipMalloc(&k1, mi * 8) != hipSuccess || hipMalloc(&k2, mi * 8) != hipSuccess ||
+            hipMalloc(&keep, mi * 4) != hipSuccess || hipMalloc(&kpos, mi * 4) != hipSuccess) {
+            rc = set_err(g, FGI_ENOMEM, "dependency-list build buffers");
+            break;
+        }
+        hipLaunchKernelGGL(k_in_part_compact, dim3(nb), dim3(256), 0, s, m, keys, flag, pos, p->v.base, k1);
+        size_t sb = 0;
+        rocprim::radix_sort_keys(nullptr, sb, k1, k2, (size_t)mi, 0, 64, s);
+        if (hipMalloc(&st, std::max(sb, (size_t)16)) != hipSuccess) {
+            rc = set_err(g, FGI_ENOMEM, "sort temp");
+            break;
+        }
+        rocprim::radix_sort_keys(st, sb, k1, k2, (size_t)mi, 0, 64, s);
+        const uint32_t nb2 = (uint32_t)((mi + 255) / 256);
+        hipLaunchKernelGGL(k_in_part_unique, dim3(nb2), dim3(256), 0, s, mi, k2, keep);
+        size_t tb2 = 0;
+        rocprim::exclusive_scan(nullptr, tb2, keep, kpos, 0u, (size_t)mi, rocprim::plus<uint32_t>(), s);
+        hipFree(st);
+        st = nullptr;
+        if (hipMalloc(&st, std::max(tb2, (size_t)16)) != hipSuccess) {
+            rc = set_err(g, FGI_ENOMEM, "scan temp");
+            break;
+        }
+        rocprim::exclusive_scan(st, tb2, keep, kpos, 0u, (size_t)mi, rocprim::plus<uint32_t>(), s);
+        uint32_t a = 0, b = 0;
+        hipMemcpyAsync(&a, kpos + mi - 1, 4, hipMemcpyDeviceToHost, s);
+        hipMemcpyAsync(&b, keep + mi - 1, 4, hipMemcpyDeviceToHost, s);
+        hipStreamSynchronize(s);
+        const uint64_t total = (uint64_t)a + b;
+        if (total > g->uin_cap || !g->uin_src) {
+            hipFree(g->uin_src);
+            g->uin_src = nullptr;
+            if (hipMalloc(&g->uin_src, std::max<uint64_t>(total, 1024) * 4) != hipSuccess) {
+                rc = set_err(g, FGI_ENOMEM, "dependency lists");
+                break;
+            }
+            g->uin_cap = std::max<uint64_t>(total, 1024);
+        }
+        hipLaunchKernelGGL(k_in_part_rows, dim3(nb2), dim3(256), 0, s, mi, k2, keep, kpos, g->uin_src, g->uin_off,
+                           g->uin_len);
+        hipLaunchKernelGGL(k_in_part_fix, dim3((g->n_slots + 255) / 256), dim3(256), 0, s, g->n_slots, g->uin_off,
+                           g->uin_len);
+        if (hipStreamSynchronize(s) != hipSuccess) rc = set_err(g, FGI_EDEVICE, "dependency-list build");
+    } while (0);
+    hipFree(k1);
+    hipFree(k2);
+    hipFree(keep);
+    hipFree(kpos);
+    hipFree(st);
+    return rc;
+}
 
 }  // namespace fgi
 
@@ -197,6 +333,10 @@ static fgi_status part_alloc(fgi_graph* g, uint32_t n_global) {
     if (hipMalloc(&p->v.send_cnt, (size_t)W * 8) != hipSuccess) return fail("counts");
     if (hipMalloc(&p->all_cnt, (size_t)W * W * 8) != hipSuccess) return fail("counts");
     if (hipMalloc(&p->scalar, 8) != hipSuccess) return fail("scalar");
+    p->v.front_words_global = (uint64_t)n_global / 32 + 2;
+    if (hipMalloc(&p->v.front_global, p->v.front_words_global * 4) != hipSuccess) return fail("frontier bitmap");
+    if (hipMemset(p->v.front_global, 0, p->v.front_words_global * 4) != hipSuccess) return fail("frontier bitmap");
+    if (hipMalloc(&p->v.scratch_u64, 8) != hipSuccess) return fail("scratch");
     if (hipHostMalloc(reinterpret_cast<void**>(&p->all_cnt_host), (size_t)W * W * 8) != hipSuccess) return fail("host");
     if (hipHostMalloc(reinterpret_cast<void**>(&p->scalar_host), 8) != hipSuccess) return fail("host");
     return FGI_OK;
@@ -254,20 +394,68 @@ fgi_status fgi_part_local_invalidate(fgi_graph* const* gs, uint32_t P, uint32_t 
         return FGI_OK;
     };
     uint64_t f_global = 0;
-    if (st == FGI_OK) st = frontier_total(0, &f_global);
+    if (st == FGI_OK) st = frontier_total(0, &f_global);   // level 0 frontier (the roots' winners)
     std::vector<unsigned long long> cnt((size_t)P * P);
-    for (int L = 0; st == FGI_OK && f_global != 0; ++L) {
-        for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
+    auto level_total = [&](const unsigned long long* (*field)(fgi_graph*, int), int L, uint64_t* out) -> fgi_status {
+        uint64_t t = 0;
+        for (uint32_t r = 0; r < P; ++r) {
+            unsigned long long f = 0;
             hipSetDevice(gs[r]->device);
-            st = part_level_launch(gs[r], L);
+            FGI_HIP(gs[r], hipMemcpyAsync(&f, field(gs[r], L), 8, hipMemcpyDeviceToHost, gs[r]->stream));
+            FGI_HIP(gs[r], hipStreamSynchronize(gs[r]->stream));
+            t += f;
         }
-        // counts: cnt[r * P + q] = targets rank r forwards to owner q
+        *out = t;
+        return FGI_OK;
+    };
+    bool allow_pull = true;
+    uint64_t e_global = 0;
+    for (uint32_t r = 0; r < P; ++r) {
+        allow_pull &= gs[r]->opt_direction != 1 && gs[r]->uin_src && gs[r]->uin_epoch == gs[r]->mut_epoch;
+        e_global += gs[r]->pool_top;
+    }
+    const int direction = gs[0]->opt_direction;
+    const uint64_t threshold = e_global / (uint64_t)(gs[0]->opt_pull_alpha > 0 ? gs[0]->opt_pull_alpha : 1);
+    for (int L = 0; st == FGI_OK && f_global != 0; ++L) {
+        uint64_t t_global = 0;
         for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
             hipSetDevice(gs[r]->device);
-            if (hipMemcpyAsync(&cnt[(size_t)r * P], ps(gs[r])->v.send_cnt, P * 8, hipMemcpyDeviceToHost,
-                               gs[r]->stream) != hipSuccess ||
-                hipStreamSynchronize(gs[r]->stream) != hipSuccess)
-                st = set_err(gs[r], FGI_EDEVICE, "count readback");
+            st = part_level_scan(gs[r], L);
+        }
+        if (st == FGI_OK) st = level_total(part_level_edges_dev, L, &t_global);
+        const bool pull = allow_pull && (direction == 2 || t_global > threshold);
+        for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
+            hipSetDevice(gs[r]->device);
+            st = part_level_mark(gs[r], L, pull);
+            if (st == FGI_OK) st = hipStreamSynchronize(gs[r]->stream) == hipSuccess ? FGI_OK : FGI_EDEVICE;
+        }
+        if (pull) {   // all-gather of the local frontier words into every rank's global bitmap
+            for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
+                hipSetDevice(gs[r]->device);
+                for (uint32_t q = 0; q < P && st == FGI_OK; ++q) {
+                    const uint32_t words = ps(gs[q])->v.block / 32;
+                    if (hipMemcpyAsync(ps(gs[r])->v.front_global + (uint64_t)q * words, gs[q]->front_bm, words * 4,
+                                       hipMemcpyDefault, gs[r]->stream) != hipSuccess)
+                        st = set_err(gs[r], FGI_EDEVICE, "frontier gather");
+                }
+            }
+        }
+        for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
+            hipSetDevice(gs[r]->device);
+            st = part_level_work(gs[r], L, pull);
+        }
+        if (!pull) {
+            // counts: cnt[r * P + q] = targets rank r forwards to owner q
+            for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
+                hipSetDevice(gs[r]->device);
+                if (hipMemcpyAsync(&cnt[(size_t)r * P], ps(gs[r])->v.send_cnt, P * 8, hipMemcpyDeviceToHost,
+                                   gs[r]->stream) != hipSuccess ||
+                    hipStreamSynchronize(gs[r]->stream) != hipSuccess)
+                    st = set_err(gs[r], FGI_EDEVICE, "count readback");
+            }
+        } else {
+            std::fill(cnt.begin(), cnt.end(), 0ull);
+            for (uint32_t r = 0; r < P; ++r) hipStreamSynchronize(gs[r]->stream);
         }
         for (uint32_t q = 0; q < P && st == FGI_OK; ++q) {
             fgi_graph* gq = gs[q];
@@ -285,7 +473,7 @@ fgi_status fgi_part_local_invalidate(fgi_graph* const* gs, uint32_t P, uint32_t 
                 if (x != q) sent += cnt[(size_t)q * P + x];
             if (st == FGI_OK) st = part_level_apply(gq, L, off, sent);
         }
-        if (st == FGI_OK) st = frontier_total(L + 1, &f_global);
+        if (st == FGI_OK) st = level_total(part_level_frontier_dev, L + 1, &f_global);
         for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
             hipSetDevice(gs[r]->device);
             st = part_level_account(gs[r], L);
@@ -355,9 +543,15 @@ fgi_status fgi_part_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_facto
             st = set_err(g, FGI_EDEVICE, "partition filter");
             break;
         }
+        // dependency lists of the owned slots (pull levels), while the global keys are at hand
+        if (p->v.block % 32 == 0) {
+            st = part_build_in_lists(g, keys, m, stale_pct, stale_seed, flag, pos, &tmp);
+            if (st != FGI_OK) break;
+        }
         hipFree(keys);
         keys = nullptr;
         st = build_rows_from_keys(g, mo, own, nullptr, seed, stale_pct, stale_seed, p->v.base, p->v.base);
+        g->uin_epoch = (p->v.block % 32 == 0) ? g->mut_epoch : 0;   // rows and lists of one edge set
     } while (0);
     cleanup();
     return st;

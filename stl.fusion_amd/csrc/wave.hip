@@ -572,13 +572,14 @@ __global__ __launch_bounds__(kBlock) void k_pull(int L, uint32_t n_slots, const 
     LevelCtr& ln = ctr->lvl[(L + 1) % kRing];
     if (!lc.pull) return;
     emit_init(em);
-    uint32_t flagged = 0, cand = 0, examined = 0;
+    uint32_t flagged = 0, cand = 0, examined = 0, live = 0, wins = 0;
     const uint32_t stride = gridDim.x * blockDim.x;
     const uint32_t n_iter = (n_slots + stride - 1) / stride;   // uniform trip count: flushes are block-wide
     for (uint32_t it = 0; it < n_iter; ++it) {
         const uint32_t d = it * stride + blockIdx.x * blockDim.x + threadIdx.x;
         bool win = false, long_list = false;
         if (d < n_slots && !bit_of(dead_bm, d)) {
+            ++live;
             const uint32_t len = uin_len[d];
             if (len) {
                 ++cand;
@@ -611,16 +612,21 @@ __global__ __launch_bounds__(kBlock) void k_pull(int L, uint32_t n_slots, const 
             base = __shfl(base, 0, 64);
             if (long_list) ovf[base + __popcll(lm & ((1ull << lane_id()) - 1ull))] = d;
         }
+        wins += win ? 1u : 0u;
         emit_push(em, win, d, row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
         emit_flush(em, kEmitCap - kBlock, row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
     }
     emit_flush(em, 1, row_off, row_len, inv, nfr_off, nfr_len, &ctr->inv, &ln.F);
     const uint32_t fs = wave_sum(flagged), cs = wave_sum(cand), es = wave_sum(examined);
+    const uint32_t ls = wave_sum(live), ws = wave_sum(wins);
     if (lane_id() == 0) {
         if (fs) atomicAdd(&ctr->n_flagged, (unsigned long long)fs);
         if (cs) atomicAdd(&ctr->pull_cand, (unsigned long long)cs);
         if (es) atomicAdd(&ctr->pull_edges, (unsigned long long)es);
+        if (ls) atomicAdd(&ctr->pull_live, (unsigned long long)ls);
+        if (ws) atomicAdd(&ctr->pull_win, (unsigned long long)ws);
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&ctr->pull_scan, (unsigned long long)n_slots);
 }
 
 __global__ __launch_bounds__(kBlock) void k_pull_long(int L, const uint64_t* __restrict__ uin_off,
@@ -759,20 +765,22 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     int L = 0;
     uint64_t levels = 0, e_trav = 0, f_total = 0, pull_levels = 0;
     double expand_ms = 0, pull_ms = 0;
-    uint64_t expand_launches = 0, expand_edges = 0, expand_f = 0;
+    uint64_t expand_launches = 0, expand_edges = 0, expand_f = 0, pull_launches = 0, pull_f = 0;
+    int dir_eff_of[kRing];
     bool done = (n_roots == 0);
     while (!done) {
         const int L0 = L;
         const int dir_eff = allow_pull ? direction : 1;
         for (int k = 0; k < kGroup; ++k, ++L) {
             const int buf = L & 1;
+            dir_eff_of[L % kRing] = dir_eff;
             hipLaunchKernelGGL(k_scan_reduce, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->fr_len[buf], g->partials,
                                g->ctr);
             hipLaunchKernelGGL(k_scan_apply, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->fr_len[buf], g->partials,
                                g->escan, g->cstart, g->ctr, dir_eff, pull_threshold);
             hipLaunchKernelGGL(k_mark, dim3(mark_grid), dim3(kBlock), 0, s, L, g->inv, g->dead_bm, g->front_bm, g->ctr);
             if (timing) {
-                while (g->ev.size() < 4 * (size_t)(L + 1)) {
+                while (g->ev.size() < 4 * (size_t)(L + 1) + 4) {
                     hipEvent_t e;
                     FGI_HIP(g, hipEventCreate(&e));
                     g->ev.push_back(e);
@@ -789,6 +797,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                                    g->uin_src, g->dead_bm, g->front_bm, reinterpret_cast<unsigned long long*>(g->node),
                                    g->row_off, g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], g->pull_ovf,
                                    g->ctr);
+                if (timing) FGI_HIP(g, hipEventRecord(g->ev[4 * L + 3], s));
                 hipLaunchKernelGGL(k_pull_long, dim3(pull_grid), dim3(kBlock), 0, s, L, g->uin_off, g->uin_len,
                                    g->uin_src, g->front_bm, reinterpret_cast<unsigned long long*>(g->node), g->row_off,
                                    g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], g->pull_ovf, g->ctr);
@@ -803,13 +812,16 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
             const LevelCtr& lc = g->ctr_host->lvl[l % kRing];
             float ms_e = 0, ms_p = 0;
             if (timing) {
-                // every expand launch counts (empty and pull levels too), so the average launch
-                // duration is the one rocprofv3 reports for k_expand
+                // every launch counts (empty and no-op levels too), so the average launch
+                // durations are the ones rocprofv3 reports for k_expand and k_pull
                 FGI_HIP(g, hipEventElapsedTime(&ms_e, g->ev[4 * l], g->ev[4 * l + 1]));
-                FGI_HIP(g, hipEventElapsedTime(&ms_p, g->ev[4 * l + 1], g->ev[4 * l + 2]));
                 expand_ms += ms_e;
-                pull_ms += ms_p;
                 ++expand_launches;
+                if (dir_eff_of[l % kRing] != 1) {
+                    FGI_HIP(g, hipEventElapsedTime(&ms_p, g->ev[4 * l + 1], g->ev[4 * l + 3]));
+                    pull_ms += ms_p;
+                    ++pull_launches;
+                }
             }
             if (lc.F) {
                 ++levels;
@@ -817,6 +829,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                 f_total += lc.F;
                 if (lc.pull) {
                     ++pull_levels;
+                    pull_f += lc.F;
                 } else {
                     expand_edges += lc.T;
                     expand_f += lc.F;
@@ -866,7 +879,13 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         // uin_len 4 + uin_off 8, per examined dependency 4. Per invalidated node: CAS 8 + row
         // gathers 12 + list write 4. Per root 5.
         const uint64_t push_b = 20 * expand_edges + 44 * expand_f;
-        const uint64_t pull_b = 12 * g->ctr_host->pull_cand + 4 * g->ctr_host->pull_edges;
+        // k_pull alone: dead-bitmap scan 1/8 B per slot, uin_len 4 B per live slot, uin_off 8 B per
+        // slot with a dependency list, 4 B per dependency examined (its frontier-bitmap probe is an
+        // L2 hit and not counted), and per winner 24 B (CAS 8 + row gathers 12 + list write 4)
+        // plus 12 B per next-frontier entry written.
+        const WaveCtr& c = *g->ctr_host;
+        const uint64_t pull_b = c.pull_scan / 8 + 4 * c.pull_live + 8 * c.pull_cand + 4 * c.pull_edges +
+                                36 * c.pull_win;
         stats->alg_bytes += push_b + pull_b + 24 * v + 5ull * n_roots;
         float wave_ms = 0;
         hipEventElapsedTime(&wave_ms, g->ev_w0, g->ev_w1);
@@ -876,6 +895,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         stats->expand_launches += expand_launches;
         stats->expand_bytes += 20 * expand_edges + 16 * expand_f;
         stats->pull_bytes += pull_b;
+        stats->pull_launches += pull_launches;
         stats->f_total += f_total;
         stats->total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
@@ -895,7 +915,7 @@ fgi_status part_wave_begin(fgi_graph* g, uint32_t n_roots, const uint32_t* roots
     FGI_HIP(g, hipMemsetAsync(g->ctr, 0, sizeof(WaveCtr), s));
     FGI_HIP(g, hipMemsetAsync(g->dead_bm, 0, g->bm_words * 4, s));
     FGI_HIP(g, hipMemsetAsync(pv.sent_bm, 0, pv.sent_words * 4, s));
-    while (g->ev.size() < 2) {
+    while (g->ev.size() < 3) {
         hipEvent_t e;
         FGI_HIP(g, hipEventCreate(&e));
         g->ev.push_back(e);
@@ -910,27 +930,66 @@ fgi_status part_wave_begin(fgi_graph* g, uint32_t n_roots, const uint32_t* roots
 }
 
 const unsigned long long* part_level_frontier_dev(fgi_graph* g, int L) { return &g->ctr->lvl[L % kRing].F; }
+const unsigned long long* part_level_edges_dev(fgi_graph* g, int L) { return &g->ctr->lvl[L % kRing].T; }
 
-fgi_status part_level_launch(fgi_graph* g, int L) {
+// scan of the local frontier (its edge total T decides push vs pull for every rank)
+fgi_status part_level_scan(fgi_graph* g, int L) {
     PartView pv;
     part_view(g, &pv);
     hipStream_t s = g->stream;
-    int n_cu = 256;
-    hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device);
-    const uint32_t expand_grid = (uint32_t)n_cu * 4, mark_grid = (uint32_t)n_cu * 2;
-    const RemoteArgs ra{pv.base, pv.n_local, pv.block, pv.world, pv.ver_all, pv.sent_bm, pv.send_buf, pv.send_cnt};
     const int buf = L & 1;
     FGI_HIP(g, hipMemsetAsync(pv.send_cnt, 0, (size_t)pv.world * 8, s));
     hipLaunchKernelGGL(k_scan_reduce, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->fr_len[buf], g->partials, g->ctr);
     hipLaunchKernelGGL(k_scan_apply, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->fr_len[buf], g->partials, g->escan,
                        g->cstart, g->ctr, 1, (uint64_t)0);
-    hipLaunchKernelGGL(k_mark, dim3(mark_grid), dim3(kBlock), 0, s, L, g->inv, g->dead_bm, g->front_bm, g->ctr);
-    FGI_HIP(g, hipEventRecord(g->ev[0], s));
-    hipLaunchKernelGGL(k_expand<true>, dim3(expand_grid), dim3(kBlock), 0, s, L, g->fr_off[buf], g->escan, g->cstart,
-                       g->pool_col, g->pool_tag, reinterpret_cast<unsigned long long*>(g->node), g->row_off, g->row_len,
-                       g->dead_bm, g->opt_dead_filter, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], g->ctr, ra);
-    FGI_HIP(g, hipEventRecord(g->ev[1], s));
     FGI_HIP(g, hipGetLastError());
+    return FGI_OK;
+}
+
+// marks the previous level's winners (dead; frontier bitmap on pull levels); on a pull level the
+// local frontier words front_bm[0, block/32) are then all-gathered into pv.front_global
+fgi_status part_level_mark(fgi_graph* g, int L, bool pull) {
+    hipStream_t s = g->stream;
+    int n_cu = 256;
+    hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device);
+    static const unsigned long long one = 1;
+    if (pull)
+        FGI_HIP(g, hipMemcpyAsync(&g->ctr->lvl[L % kRing].pull, &one, 8, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_mark, dim3((uint32_t)n_cu * 2), dim3(kBlock), 0, s, L, g->inv, g->dead_bm, g->front_bm, g->ctr);
+    FGI_HIP(g, hipGetLastError());
+    return FGI_OK;
+}
+
+// push: expand (remote targets staged for the exchange); pull: scan local dependency lists
+// against the global frontier bitmap
+fgi_status part_level_work(fgi_graph* g, int L, bool pull) {
+    PartView pv;
+    part_view(g, &pv);
+    hipStream_t s = g->stream;
+    int n_cu = 256;
+    hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device);
+    const RemoteArgs ra{pv.base, pv.n_local, pv.block, pv.world, pv.ver_all, pv.sent_bm, pv.send_buf, pv.send_cnt};
+    const int buf = L & 1;
+    FGI_HIP(g, hipEventRecord(g->ev[0], s));
+    // launched on pull levels too: it clears the counters of level L + 2 and returns
+    hipLaunchKernelGGL(k_expand<true>, dim3((uint32_t)n_cu * 4), dim3(kBlock), 0, s, L, g->fr_off[buf], g->escan,
+                       g->cstart, g->pool_col, g->pool_tag, reinterpret_cast<unsigned long long*>(g->node), g->row_off,
+                       g->row_len, g->dead_bm, g->opt_dead_filter, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1],
+                       g->ctr, ra);
+    FGI_HIP(g, hipEventRecord(g->ev[1], s));
+    if (pull) {
+        const uint32_t pull_grid = (uint32_t)n_cu * 8;
+        hipLaunchKernelGGL(k_pull, dim3(pull_grid), dim3(kBlock), 0, s, L, pv.n_local, g->uin_off, g->uin_len, g->uin_src,
+                           g->dead_bm, pv.front_global, reinterpret_cast<unsigned long long*>(g->node), g->row_off,
+                           g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], g->pull_ovf, g->ctr);
+        FGI_HIP(g, hipEventRecord(g->ev[2], s));
+        hipLaunchKernelGGL(k_pull_long, dim3(pull_grid), dim3(kBlock), 0, s, L, g->uin_off, g->uin_len, g->uin_src,
+                           pv.front_global, reinterpret_cast<unsigned long long*>(g->node), g->row_off, g->row_len,
+                           g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], g->pull_ovf, g->ctr);
+        FGI_HIP(g, hipMemsetAsync(pv.front_global, 0, pv.front_words_global * 4, s));
+    }
+    FGI_HIP(g, hipGetLastError());
+    g->pw.pulled = pull;
     return FGI_OK;
 }
 
@@ -960,10 +1019,17 @@ fgi_status part_level_account(fgi_graph* g, int L) {
     g->pw.levels++;
     g->pw.e_trav += lc.T;
     g->pw.f_total += lc.F;
+    if (!lc.pull) g->pw.push_edges += lc.T, g->pw.push_f += lc.F;
     float ms = 0;
     FGI_HIP(g, hipEventElapsedTime(&ms, g->ev[0], g->ev[1]));
     g->pw.expand_ms += ms;
     g->pw.expand_launches++;
+    if (g->pw.pulled) {
+        FGI_HIP(g, hipEventElapsedTime(&ms, g->ev[1], g->ev[2]));
+        g->pw.pull_ms += ms;
+        g->pw.pull_launches++;
+        g->pw.pull_levels++;
+    }
     return FGI_OK;
 }
 
@@ -983,14 +1049,22 @@ fgi_status part_wave_end(fgi_graph* g, fgi_wave_stats* stats) {
         stats->e_match += g->ctr_host->e_match;
         stats->n_flagged += g->ctr_host->n_flagged;
         stats->remote_msgs += w.sent;
-        // as run_wave's push levels, plus 8 B per forwarded target (4 written + 4 received)
-        stats->alg_bytes += 20 * w.e_trav + 44 * w.f_total + 24 * v + 8 * w.sent + 5ull * w.n_roots;
+        // as run_wave (push and pull levels), plus 8 B per forwarded target (written + received)
+        const WaveCtr& c = *g->ctr_host;
+        const uint64_t pull_b = c.pull_scan / 8 + 4 * c.pull_live + 8 * c.pull_cand + 4 * c.pull_edges +
+                                36 * c.pull_win;
+        stats->alg_bytes += 20 * w.push_edges + 44 * w.push_f + pull_b + 24 * v + 8 * w.sent + 5ull * w.n_roots;
+        stats->pull_levels += w.pull_levels;
+        stats->pull_edges += c.pull_edges;
+        stats->pull_ms += w.pull_ms;
+        stats->pull_bytes += pull_b;
+        stats->pull_launches += w.pull_launches;
         float wave_ms = 0;
         hipEventElapsedTime(&wave_ms, g->ev_w0, g->ev_w1);
         stats->kernel_ms += wave_ms;
         stats->expand_ms += w.expand_ms;
         stats->expand_launches += w.expand_launches;
-        stats->expand_bytes += 20 * w.e_trav + 16 * w.f_total;
+        stats->expand_bytes += 20 * w.push_edges + 16 * w.push_f;
         stats->f_total += w.f_total;
         stats->total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w.t0).count();
     }
@@ -1000,13 +1074,24 @@ fgi_status part_wave_end(fgi_graph* g, fgi_wave_stats* stats) {
 // One process per GPU: levels in lockstep over RCCL.
 fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                          fgi_wave_stats* stats) {
+    PartView pv;
+    part_view(g, &pv);
     FGI_TRY(part_wave_begin(g, n_roots, roots_dev, imm_dev));
-    uint64_t f_global = 0;
+    const bool allow_pull = g->opt_direction != 1 && g->uin_src && g->uin_epoch == g->mut_epoch;
+    uint64_t e_global = 0, f_global = 0, t_global = 0;
+    FGI_HIP(g, hipMemcpy(pv.scratch_u64, &g->pool_top, 8, hipMemcpyHostToDevice));
+    FGI_TRY(part_allreduce_sum(g, pv.scratch_u64, &e_global));
+    const uint64_t threshold = e_global / (uint64_t)(g->opt_pull_alpha > 0 ? g->opt_pull_alpha : 1);
     FGI_TRY(part_allreduce_sum(g, part_level_frontier_dev(g, 0), &f_global));
     for (int L = 0; f_global != 0; ++L) {
-        FGI_TRY(part_level_launch(g, L));
+        FGI_TRY(part_level_scan(g, L));
+        FGI_TRY(part_allreduce_sum(g, part_level_edges_dev(g, L), &t_global));
+        const bool pull = allow_pull && (g->opt_direction == 2 || t_global > threshold);
+        FGI_TRY(part_level_mark(g, L, pull));
+        if (pull) FGI_TRY(part_allgather_front(g));
+        FGI_TRY(part_level_work(g, L, pull));
         uint64_t n_recv = 0, n_sent = 0;
-        FGI_TRY(part_exchange(g, &n_recv, &n_sent));
+        if (!pull) FGI_TRY(part_exchange(g, &n_recv, &n_sent));
         FGI_TRY(part_level_apply(g, L, n_recv, n_sent));
         FGI_TRY(part_allreduce_sum(g, part_level_frontier_dev(g, L + 1), &f_global));
         FGI_TRY(part_level_account(g, L));

@@ -46,7 +46,8 @@ class WaveStats(C.Structure):
                 ("alg_bytes", C.c_uint64), ("kernel_ms", C.c_double), ("total_ms", C.c_double),
                 ("remote_msgs", C.c_uint64), ("f_total", C.c_uint64), ("expand_launches", C.c_uint64),
                 ("expand_ms", C.c_double), ("expand_bytes", C.c_uint64), ("pull_levels", C.c_uint64),
-                ("pull_edges", C.c_uint64), ("pull_ms", C.c_double), ("pull_bytes", C.c_uint64)]
+                ("pull_edges", C.c_uint64), ("pull_ms", C.c_double), ("pull_bytes", C.c_uint64),
+                ("pull_launches", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}

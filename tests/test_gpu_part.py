@@ -9,9 +9,10 @@ import fgo as O
 pytestmark = pytest.mark.gpu
 
 
+@pytest.mark.parametrize("direction", [0, 1, 2])      # auto, push only, pull only
 @pytest.mark.parametrize("P", [2, 3, 4, 8])
 @pytest.mark.parametrize("stale", [0, 50])
-def test_partitioned_wave_matches_oracle(pkg, gpu_available, P, stale):
+def test_partitioned_wave_matches_oracle(pkg, gpu_available, P, stale, direction):
     scale, ef, seed, sseed = 12, 16, 0x5EED0027, 0x5EED00C0
     n = 1 << scale
     block = -(-n // P)
@@ -19,6 +20,7 @@ def test_partitioned_wave_matches_oracle(pkg, gpu_available, P, stale):
     pkg.fgi.part_init_local(gs, n)
     for g in gs:
         g.part_synth_rmat(scale, ef, seed, stale, sseed)
+        g.set_option(2, direction)
     s, d = O.gen_rmat(scale, ef, seed)
     o = O.Oracle(n)
     o.load_graph(O.version_of(seed, np.arange(n)), None, s, d, O.gen_tags(s, d, seed, stale, sseed))
@@ -31,7 +33,10 @@ def test_partitioned_wave_matches_oracle(pkg, gpu_available, P, stale):
     assert np.array_equal(np.sort(ids), np.sort(o.inv_log()))
     assert sum(x.v_inv for x in stats) == st.v_inv
     assert sum(x.e_trav for x in stats) == st.e_trav
-    assert sum(x.remote_msgs for x in stats) > 0
+    if direction == 1:
+        assert sum(x.remote_msgs for x in stats) > 0
+    if direction == 2 and block % 32 == 0:
+        assert all(x.pull_levels == x.levels for x in stats)
     # final states, gathered from the owners
     ov, of = o.dump_states()
     for r, g in enumerate(gs):
