@@ -181,6 +181,9 @@ fgi_status fgi_invalidate_dev(fgi_graph* g, uint32_t n_roots, const uint32_t* ro
                               fgi_wave_stats* stats);
 /* Device pointer to the last wave's invalidated-slot list (valid until the next call). */
 fgi_status fgi_wave_ids_dev(fgi_graph* g, const uint32_t** ids_dev, uint64_t* n);
+/* Host copy of the last wave's invalidated handles — e.g. the displacement cascade of
+ * fgi_begin_compute, whose Invalidated handlers the host must still run. */
+fgi_status fgi_last_wave_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n);
 /* ComputedRegistry.InvalidateEverything (ComputedRegistry.cs:142-147). */
 fgi_status fgi_invalidate_all(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n,
                               fgi_wave_stats* stats);

@@ -1068,6 +1068,12 @@ fgi_status fgi_wave_ids_dev(fgi_graph* g, const uint32_t** ids_dev, uint64_t* n)
     return FGI_OK;
 }
 
+fgi_status fgi_last_wave_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n) {
+    if (!g) return FGI_EINVAL;
+    hipSetDevice(g->device);
+    return copy_ids(g, out_ids, cap, out_n);
+}
+
 fgi_status fgi_invalidate_all(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n, fgi_wave_stats* stats) {
     if (!g) return FGI_EINVAL;
     hipSetDevice(g->device);
@@ -1120,6 +1126,7 @@ fgi_status fgi_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, con
         return set_err(g, FGI_ECAPACITY, "out of detached handles (%zu free, %llu needed)", g->free_detached.size(),
                        cnt[1]);
     // displacement cascade first (ComputedRegistry.cs:91-94), then detach + install
+    g->last_wave_n = 0;
     if (cnt[0]) FGI_TRY(run_wave(g, (uint32_t)cnt[0], droots, nullptr, stats));
     std::vector<uint32_t> take(g->free_detached.end() - (ptrdiff_t)cnt[1], g->free_detached.end());
     FGI_TRY(tmalloc(g, tf, &dfree_h, take.size() + 1));

@@ -81,6 +81,7 @@ SIGNATURES = {
     "fgi_invalidate": [_G, C.c_uint32, _u32p, _u8p, _u32p, C.c_uint64, _u64p, C.POINTER(WaveStats)],
     "fgi_invalidate_dev": [_G, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, _u64p, C.POINTER(WaveStats)],
     "fgi_wave_ids_dev": [_G, C.POINTER(C.c_void_p), _u64p],
+    "fgi_last_wave_ids": [_G, _u32p, C.c_uint64, _u64p],
     "fgi_invalidate_all": [_G, _u32p, C.c_uint64, _u64p, C.POINTER(WaveStats)],
     "fgi_prune": [_G, C.POINTER(PruneStats)],
     "fgi_release": [_G, C.c_uint32, _u32p],
@@ -288,6 +289,15 @@ class Graph:
                                                 C.c_void_p(imm_ptr) if imm_ptr else None, None, C.byref(n),
                                                 C.byref(stats) if stats is not None else None), "invalidate_dev")
         return n.value
+
+    def last_wave_ids(self) -> np.ndarray:
+        """Handles invalidated by the last wave (e.g. begin_compute's displacement cascade)."""
+        n = C.c_uint64()
+        self._check(self.lib.fgi_last_wave_ids(self.h, None, 0, C.byref(n)), "last_wave_ids")
+        ids = np.zeros(n.value, np.uint32)
+        self._check(self.lib.fgi_last_wave_ids(self.h, _ptr(ids, C.c_uint32), len(ids), C.byref(n)),
+                    "last_wave_ids")
+        return ids
 
     def invalidate_all(self, stats: Optional[WaveStats] = None) -> np.ndarray:
         ids = np.zeros(self.n_handles, np.uint32)

@@ -3,7 +3,8 @@
 The reference (C#) holds no numeric golden vectors for the cascade; its pins are the behaviour
 tests listed in SURVEY.md §4 / §8(c). Each scenario below restates one of them over the slot
 model (a slot = a compute-method input, a node = one Computed instance) and checks the oracle.
-The engine-side counterparts are in tests/test_gpu_scenarios.py.
+Each World-based scenario takes the world factory as a default argument, so
+tests/test_gpu_scenarios.py replays the same function against the engine (through the C-ABI).
 """
 import numpy as np
 import pytest
@@ -18,8 +19,8 @@ ADDED, DROPPED, USED_INV, ESTATE = 0, 1, 2, 3
 class World:
     """A tiny compute-service world over the oracle: compute(slot, deps) = begin + AddUsed + set."""
 
-    def __init__(self, n=64):
-        self.o = O.Oracle(n)
+    def __init__(self, n=64, make=O.Oracle):
+        self.o = make(n)
         self.ver = {}
         self.next_v = 1000
 
@@ -45,20 +46,20 @@ class World:
         return sorted(self.o.inv_log().tolist())
 
 
-def test_counter_service_basic():
+def test_counter_service_basic(W=World):
     """CounterServiceTest.BasicTest (CounterServiceTest.cs:12-30): invalidation makes the computed
     inconsistent and removes it from the registry (GetExisting -> null)."""
-    w = World()
+    w = W()
     h = w.compute(0)
     assert w.o.current(0) == h and w.state(0) == K
     assert w.invalidate(0) == [0]
     assert w.state(0) == I and w.o.current(0) == O.NONE
 
 
-def test_counter_service_long_wait():
+def test_counter_service_long_wait(W=World):
     """CounterServiceTest.LongWaitTest (:32-58): invalidating a Computing node keeps it Computing
     and registered; once its output is set it becomes Invalidated and unregistered."""
-    w = World()
+    w = W()
     h, _ = w.begin(0)
     assert w.invalidate(0) == []
     assert w.o.current(0) == h and w.state(0) == C | IOSO
@@ -66,10 +67,10 @@ def test_counter_service_long_wait():
     assert w.state(0) == I and w.o.current(0) == O.NONE
 
 
-def test_counter_service_concurrent_wait():
+def test_counter_service_concurrent_wait(W=World):
     """CounterServiceTest.ConcurrentWaitTest (:60-98): a dependency that completes after the
     dependant is not recorded (AddUsed drops it, Computed.cs:351-364): Used.Length == 1."""
-    w = World()
+    w = W()
     x = w.compute(1)
     yh, _ = w.begin(2)                      # "y wait" still computing
     dh, _ = w.begin(3)                      # GetFirstNonZero(x, y)
@@ -83,11 +84,11 @@ def test_counter_service_concurrent_wait():
     assert w.o.used_count(dh2) == 2
 
 
-def test_simplest_provider_cascade_and_new_version():
+def test_simplest_provider_cascade_and_new_version(W=World):
     """SimplestProviderTest.BasicTest (SimplestProviderTest.cs:9-32) + EdgeCaseServiceTest
     (EdgeCaseServiceTest.cs:52): SetValue invalidates GetValue, which cascades to GetCharCount;
     recomputation produces a new version."""
-    w = World()
+    w = W()
     w.compute(0)                  # GetValue
     w.compute(1, deps=[0])        # GetCharCount uses GetValue
     v0 = w.ver[1]
@@ -97,20 +98,20 @@ def test_simplest_provider_cascade_and_new_version():
     assert w.ver[1] != v0 and w.state(1) == K
 
 
-def test_mutable_state_two_dependants():
+def test_mutable_state_two_dependants(W=World):
     """MutableStateTest.CounterServiceTest (MutableStateTest.cs:82-116): one root (the offset
     state) invalidates both Get("a") and Get("b")."""
-    w = World()
+    w = W()
     w.compute(0)
     w.compute(1, deps=[0])
     w.compute(2, deps=[0])
     assert w.invalidate(0) == [0, 1, 2]
 
 
-def test_user_provider_invalidate_everything_hub():
+def test_user_provider_invalidate_everything_hub(W=World):
     """UserProviderTest.InvalidateEverythingTest (UserProviderTest.cs:12-36): the Everything() hub
     (UserService.cs:178-179) invalidates every Get(id) and Count(); recomputed nodes are new."""
-    w = World(200)
+    w = W(200)
     w.compute(0)                                       # Everything()
     hs = [w.compute(s, deps=[0]) for s in range(1, 101)]   # Get(id) x100 + Count()
     assert w.invalidate(0) == list(range(0, 101))
@@ -119,19 +120,19 @@ def test_user_provider_invalidate_everything_hub():
     assert all(a != b for a, b in zip(hs, hs2))
 
 
-def test_nested_operation_multi_root_batch():
+def test_nested_operation_multi_root_batch(W=World):
     """NestedOperationLoggerTest.BasicTest (Extensions/NestedOperationLoggerTest.cs:11-38): one
     Computed.Invalidate() scope with several roots invalidates all of them."""
-    w = World()
+    w = W()
     for s in (0, 1, 2):
         w.compute(s)
     assert w.invalidate(0, 1, 2) == [0, 1, 2]
 
 
-def test_invalidation_delay_then_timer():
+def test_invalidation_delay_then_timer(W=World):
     """Computed.cs:186-198 + Timeouts.cs:22-28: a node with InvalidationDelay is only flagged
     (DelayStarted) by the cascade; the timer later calls Invalidate(true)."""
-    w = World()
+    w = W()
     w.compute(0)
     d = w.compute(1, deps=[0], delay=True)
     w.compute(2, deps=[1])
@@ -143,10 +144,10 @@ def test_invalidation_delay_then_timer():
     assert sorted(w.o.inv_log().tolist()) == [1, 2]
 
 
-def test_computing_immediately_quirk():
+def test_computing_immediately_quirk(W=World):
     """Computed.cs:175-176 / 187-188: Invalidate(true) on a Computing node with a delay sets both
     flags; after TrySetOutput the node stays Consistent (the delayed invalidation never runs)."""
-    w = World()
+    w = W()
     h, _ = w.begin(0, delay=True)
     w.o.invalidate_nodes([h], [1])
     assert w.state(0) == C | IOSO | DS | HD
@@ -155,10 +156,10 @@ def test_computing_immediately_quirk():
     assert w.invalidate(0) == [] and w.state(0) == K | DS | HD
 
 
-def test_add_used_by_on_invalidated_and_computing():
+def test_add_used_by_on_invalidated_and_computing(W=World):
     """Computed.cs:370-385: AddUsedBy on an Invalidated node invalidates the dependant (it gets
     InvalidateOnSetOutput while Computing); on a Computing node it throws."""
-    w = World()
+    w = W()
     u = w.compute(0)
     w.invalidate(0)
     dh, _ = w.begin(1)
@@ -170,10 +171,10 @@ def test_add_used_by_on_invalidated_and_computing():
     assert w.o.add_used(eh, ch) == ESTATE
 
 
-def test_register_displacement():
+def test_register_displacement(W=World):
     """ComputedRegistry.Register (ComputedRegistry.cs:83-97): a new computation of a slot
     invalidates the current Consistent node (cascading) before replacing it."""
-    w = World()
+    w = W()
     w.compute(0)
     w.compute(1, deps=[0])
     w.o.clear_log()
@@ -182,10 +183,10 @@ def test_register_displacement():
     assert w.o.current(0) == h and w.state(0) == C
 
 
-def test_register_displacement_with_delay_detaches():
+def test_register_displacement_with_delay_detaches(W=World):
     """A displaced node with an InvalidationDelay is only flagged and dropped from the registry;
     its dependants stay Consistent until its timer fires."""
-    w = World()
+    w = W()
     w.compute(0, delay=True)
     w.compute(1, deps=[0])
     w.o.clear_log()
@@ -198,9 +199,9 @@ def test_register_displacement_with_delay_detaches():
     assert w.state(0) == C        # the slot's current node is the new computation
 
 
-def test_stale_edges_do_not_cascade():
+def test_stale_edges_do_not_cascade(W=World):
     """Computed.cs:213-214: an entry whose version no longer matches is skipped."""
-    w = World()
+    w = W()
     w.compute(0)
     w.compute(1, deps=[0])
     w.compute(2)
@@ -212,9 +213,9 @@ def test_stale_edges_do_not_cascade():
     assert w.state(1) == K
 
 
-def test_prune_used_by_drops_only_stale_entries():
+def test_prune_used_by_drops_only_stale_entries(W=World):
     """PruneUsedBy (Computed.cs:400-419) keeps (input, version) entries whose computed is current."""
-    w = World()
+    w = W()
     w.compute(0)
     w.compute(1, deps=[0])
     w.compute(2, deps=[0])
@@ -226,10 +227,10 @@ def test_prune_used_by_drops_only_stale_entries():
     assert new <= old
 
 
-def test_hashsetslim3_set_semantics_and_spill():
+def test_hashsetslim3_set_semantics_and_spill(W=World):
     """HashSetSlim3 (HashSetSlim3.cs:31-95; HashSetSlimTest.cs:10-86): duplicates collapse, more
     than three entries spill to a hash set, removal works in both representations."""
-    w = World(64)
+    w = W(64)
     w.compute(0)
     hs = []
     for s in range(1, 11):
@@ -245,10 +246,10 @@ def test_hashsetslim3_set_semantics_and_spill():
     assert w.invalidate(0) == [0, 1, 2, 3, 4, 6, 7, 8, 9, 10]
 
 
-def test_cycle_terminates():
+def test_cycle_terminates(W=World):
     """AddUsed cannot close a cycle of current nodes (AddUsedBy throws on a Computing node), but
     imported graphs may hold one; the cascade still visits each node once."""
-    w = World()
+    w = W()
     a, _ = w.begin(0)
     b, _ = w.begin(1)
     w.o.set_output(b)
