@@ -134,8 +134,10 @@ fgi_status fgi_get_state(fgi_graph* g, uint32_t n, const uint32_t* handle, uint6
                          uint32_t* state_flags);
 /* Whole-table dump (n_slots + n_detached entries) — for parity checks. */
 fgi_status fgi_dump_states(fgi_graph* g, uint64_t* version, uint32_t* state_flags);
-/* IComputedImpl.UsedBy (Computed.cs:337-345): the live `_usedBy` entries of one node. An
- * Invalidated node reports none (its set was cleared, Computed.cs:217). */
+/* IComputedImpl.UsedBy (Computed.cs:337-345): the `_usedBy` entries of one node as the reference
+ * would hold them: an entry (d, t) whose node d@t was invalidated is gone (RemoveUsedBy,
+ * Computed.cs:387-398; the engine removes it lazily), and an Invalidated node reports none (its
+ * set was cleared, Computed.cs:217). fgi_export_edges shows the raw pool instead. */
 fgi_status fgi_get_used_by(fgi_graph* g, uint32_t handle, uint32_t* dependant_slot, uint64_t* tag,
                            uint64_t cap, uint64_t* out_n);
 /* IComputedImpl.Used.Length for a node (Computed.cs:327-335). */

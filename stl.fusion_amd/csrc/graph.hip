@@ -894,6 +894,33 @@ fgi_status fgi_dump_states(fgi_graph* g, uint64_t* version, uint32_t* state_flag
     return FGI_OK;
 }
 
+// Marks the row entries the reference would still hold. RemoveUsedBy (Computed.cs:387-398) drops
+// (d, t) from every dependency when d@t is invalidated; the engine drops such entries lazily
+// (version filter in the wave, compaction in fgi_prune), so the observable set is: entries whose
+// node d@t is still alive — the slot's current node at version t, or a detached node of slot d at
+// version t (displaced while Computing / delayed) — and not Invalidated.
+__global__ void k_used_by_live(uint32_t len, const uint32_t* __restrict__ col, const uint64_t* __restrict__ tag,
+                               const unsigned long long* __restrict__ node, uint32_t n_slots, uint32_t n_detached,
+                               const uint32_t* __restrict__ home, uint8_t* keep) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= len) return;
+    const uint32_t d = col[i];
+    const uint64_t t = tag[i];
+    bool k = false;
+    if (d < n_slots) {
+        const unsigned long long w = node[d];
+        if ((w & kVMask) == t) {
+            k = word_is_current(w);
+        } else {
+            for (uint32_t j = 0; j < n_detached && !k; ++j) {
+                const unsigned long long wd = node[n_slots + j];
+                k = home[j] == d && (wd & kVMask) == t && word_is_current(wd);
+            }
+        }
+    }
+    keep[i] = k ? 1 : 0;
+}
+
 fgi_status fgi_get_used_by(fgi_graph* g, uint32_t handle, uint32_t* dep, uint64_t* tag, uint64_t cap, uint64_t* out_n) {
     if (!g || handle >= g->n_handles) return FGI_EINVAL;
     hipSetDevice(g->device);
@@ -903,10 +930,31 @@ fgi_status fgi_get_used_by(fgi_graph* g, uint32_t handle, uint32_t* dep, uint64_
     FGI_TRY(d2h(g, &off, g->row_off + handle, 1));
     FGI_TRY(d2h(g, &len, g->row_len + handle, 1));
     if (!word_is_current(w)) len = 0;   // `_usedBy` of an Invalidated node is cleared (Computed.cs:217)
-    if (out_n) *out_n = len;
-    if (len > cap) return FGI_ECAPACITY;
-    if (dep) FGI_TRY(d2h(g, dep, g->pool_col + off, len));
-    if (tag) FGI_TRY(d2h(g, tag, g->pool_tag + off, len));
+    std::vector<uint32_t> d(len);
+    std::vector<uint64_t> t(len);
+    std::vector<uint8_t> keep(len);
+    if (len) {
+        Tmp tk;
+        uint8_t* dkeep = nullptr;
+        FGI_TRY(tmalloc(g, tk, &dkeep, len));
+        hipLaunchKernelGGL(k_used_by_live, dim3((len + 255) / 256), dim3(256), 0, g->stream, len, g->pool_col + off,
+                           g->pool_tag + off, reinterpret_cast<const unsigned long long*>(g->node), g->n_slots,
+                           g->n_detached, g->home, dkeep);
+        FGI_HIP(g, hipGetLastError());
+        FGI_TRY(d2h(g, d.data(), g->pool_col + off, len));
+        FGI_TRY(d2h(g, t.data(), g->pool_tag + off, len));
+        FGI_TRY(d2h(g, keep.data(), dkeep, len));
+    }
+    uint64_t n = 0;
+    for (uint32_t i = 0; i < len; ++i) n += keep[i];
+    if (out_n) *out_n = n;
+    if (n > cap) return FGI_ECAPACITY;
+    for (uint32_t i = 0, o = 0; i < len; ++i) {
+        if (!keep[i]) continue;
+        if (dep) dep[o] = d[i];
+        if (tag) tag[o] = t[i];
+        ++o;
+    }
     return FGI_OK;
 }
 

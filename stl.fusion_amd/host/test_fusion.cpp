@@ -166,14 +166,28 @@ static void register_displacement() {
     auto a2 = r.BeginCompute("a");
     CHECK(fa == 1 && fb == 1 && a->IsInvalidated() && b->IsInvalidated());
     CHECK(r.Get("a") == a2 && a2->State() == ConsistencyState::Computing);
-    // a displaced Computing node keeps working on a detached handle
+    // a displaced Computing node keeps working on a detached handle; Register's Invalidate()
+    // flagged it InvalidateOnSetOutput, so its completion invalidates it (Computed.cs:145-146)
     auto a3 = r.BeginCompute("a");
     CHECK(a2->Handle() != a3->Handle() && a2->State() == ConsistencyState::Computing);
-    CHECK(r.SetOutput(*a2) && a2->IsConsistent());
+    CHECK(a2->Flags() & FGI_F_INVALIDATE_ON_SET_OUTPUT);
     int f2 = 0;
     a2->OnInvalidated([&](Computed&) { ++f2; });
-    a2->Invalidate();
-    CHECK(a2->IsInvalidated() && f2 == 1 && a3->State() == ConsistencyState::Computing);
+    CHECK(r.SetOutput(*a2) && a2->IsInvalidated() && f2 == 1);
+    CHECK(a3->State() == ConsistencyState::Computing && r.Get("a") == a3);
+    // a displaced delayed node is detached Consistent; its timer invalidates it later
+    CHECK(r.SetOutput(*a3));
+    auto b3 = Compute(r, "b3", {a3});
+    r.BeginCompute("x");   // unrelated
+    ComputedRegistry r2(64);
+    auto d1 = Compute(r2, "d", {}, true);
+    auto top = Compute(r2, "top", {d1});
+    auto d2 = r2.BeginCompute("d");
+    CHECK(d1->IsConsistent() && (d1->Flags() & FGI_F_INVALIDATION_DELAY_STARTED) && top->IsConsistent());
+    CHECK(d1->Handle() != d2->Handle());
+    d1->Invalidate(true);
+    CHECK(d1->IsInvalidated() && top->IsInvalidated() && d2->State() == ConsistencyState::Computing);
+    (void)b3;
 }
 
 // ComputedGraphPruner pass (Internal/ComputedGraphPruner.cs:79-94)
