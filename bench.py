@@ -205,11 +205,12 @@ def main():
 
     value = v_inv / elapsed
     gteps = e_trav / elapsed / 1e9
-    # roofline of the dominant kernel (the one with the larger summed device time)
-    if st.pull_ms > st.expand_ms:
-        kname, k_ms, k_bytes, k_launches = "k_pull", st.pull_ms, st.pull_bytes, st.pull_launches
-    else:
-        kname, k_ms, k_bytes, k_launches = "k_expand", st.expand_ms, st.expand_bytes, st.expand_launches
+    # roofline of the dominant kernel: k_level (push and pull levels are one kernel; the split is
+    # reported beside it)
+    kname = "k_level"
+    k_ms = st.pull_ms + st.expand_ms
+    k_bytes = st.pull_bytes + st.expand_bytes
+    k_launches = st.pull_launches + st.expand_launches
     k_gbs = (k_bytes / (k_ms * 1e-3) / 1e9) if k_ms > 0 else 0.0
     traffic, traffic_src = profiled_traffic(kname, cfg.get("scale"), k_ms / max(1, k_launches))
     wave_gbs = (st.alg_bytes / (st.kernel_ms * 1e-3) / 1e9) if st.kernel_ms > 0 else 0.0
@@ -259,8 +260,12 @@ def main():
             "launches_per_step": k_launches / args.steps,
             "avg_launch_ms": k_ms / max(1, k_launches),
             "alg_bytes_per_launch": k_bytes / max(1, k_launches),
-            "expand_ms_per_step": st.expand_ms / args.steps,
-            "pull_ms_per_step": st.pull_ms / args.steps,
+            "push_levels": {"ms_per_step": st.expand_ms / args.steps,
+                            "launches_per_step": st.expand_launches / args.steps,
+                            "gbs": (st.expand_bytes / (st.expand_ms * 1e-3) / 1e9) if st.expand_ms > 0 else 0.0},
+            "pull_levels": {"ms_per_step": st.pull_ms / args.steps,
+                            "launches_per_step": st.pull_launches / args.steps,
+                            "gbs": (st.pull_bytes / (st.pull_ms * 1e-3) / 1e9) if st.pull_ms > 0 else 0.0},
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -77,6 +77,8 @@ constexpr int kScanBlocks = 1024;       // fixed grid of the two-pass frontier s
 constexpr int kBlock = 256;             // threads per block for the traversal kernels
 constexpr int kEPT = 8;                 // edges per thread per chunk
 constexpr int kChunk = kBlock * kEPT;   // edges per expand chunk
+constexpr uint32_t kStatBlocks = 4096;  // per-block statistics rows (grid limit of the hot kernels)
+constexpr int kStatCols = 8;
 
 struct LevelCtr {
     unsigned long long F;       // frontier entries (expandable = invalidated with |row| > 0)
@@ -85,8 +87,8 @@ struct LevelCtr {
     unsigned long long pull;    // 1 if this level runs bottom-up (pull)
     unsigned long long mark_lo; // inv[] range marked into the bitmaps before this level
     unsigned long long mark_hi;
-    unsigned long long ovf;     // pull: nodes whose dependency list continues in k_pull_long
-    unsigned long long pad;
+    unsigned long long pad0;
+    unsigned long long pad1;
 };
 
 struct WaveCtr {
@@ -100,7 +102,9 @@ struct WaveCtr {
     unsigned long long pull_live;   // pull: slots not yet dead when scanned
     unsigned long long pull_win;    // pull: nodes invalidated by pull levels
     unsigned long long pull_scan;   // pull: slots scanned (bitmap reads), summed over pull levels
-    unsigned long long pad[6];
+    unsigned long long pull_tail;   // pull: candidates whose head dependency missed (list scanned)
+    unsigned long long root_flagged;  // flag-only visits of the roots kernel
+    unsigned long long pad[4];
     LevelCtr lvl[kRing];
 };
 
@@ -153,6 +157,7 @@ struct fgi_graph {
     uint64_t cstart_cap = 0;
     unsigned long long* partials = nullptr;  // [kScanBlocks]
     fgi::WaveCtr* ctr = nullptr;
+    unsigned long long* blk_stats = nullptr;   // [kStatBlocks][kStatCols] per-block wave statistics
     fgi::WaveCtr* ctr_host = nullptr;  // pinned
     uint32_t* roots_buf = nullptr;     // staging for host roots
     uint8_t* imm_buf = nullptr;
@@ -162,16 +167,20 @@ struct fgi_graph {
     // per-wave bitmaps over handles (bit set = node invalidated earlier in this wave / in the
     // current frontier); read-only while a level expands, so they stay L2-resident
     uint32_t* dead_bm = nullptr;
-    uint32_t* front_bm = nullptr;
-    uint64_t bm_words = 0;
+    uint32_t* front_bm = nullptr;      // frontier bitmap (pull levels); multi-GPU: the local words
+    uint32_t* front_nx = nullptr;      // second frontier bitmap: pull level L reads fb[L&1] and
+                                       // writes its winners into fb[(L+1)&1]
+    uint64_t bm_words = 0;             // words per bitmap (even: pull levels store 64-bit words)
 
     // dependency-list cache for pull levels: for slot d, the handles whose `_usedBy` row holds
     // (d, version(d)) (= the reference's d._used). Rebuilt from the rows when stale.
     uint64_t* uin_off = nullptr;
     uint32_t* uin_len = nullptr;
     uint32_t* uin_src = nullptr;
+    uint64_t* uin_head = nullptr;      // [n_slots] the list's first two entries (lo | hi << 32, FGI_NONE
+                                       // if absent), probed first: lists are ordered by the number of
+                                       // dependencies of each entry, the ones a wave reaches earliest
     uint64_t uin_cap = 0;
-    uint32_t* pull_ovf = nullptr;      // [n_slots]
     uint64_t uin_epoch = 0;            // mut_epoch the cache was built at (0 = never)
     uint64_t mut_epoch = 1;            // changes on every mutation of rows or versions
     uint64_t epoch_counter = 1;
@@ -227,6 +236,8 @@ fgi_status build_rows_from_keys(fgi_graph* g, uint64_t m, uint64_t* keys, uint64
                                 uint32_t src_base = 0, uint32_t dst_base = 0);
 // Build the pull dependency-list cache if the graph changed since it was built.
 fgi_status ensure_in_lists(fgi_graph* g);
+// Copy the first two entries of every slot's list into uin_head.
+fgi_status build_in_heads(fgi_graph* g);
 // Record a mutation of rows or versions (invalidates the dependency-list cache).
 inline void touch(fgi_graph* g) { g->mut_epoch = ++g->epoch_counter; }
 // ---- multi-GPU partition (part.hip) ----

@@ -9,6 +9,8 @@
 #include <hip/hip_runtime.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_reduce.hpp>
+#include <rocprim/device/device_segmented_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
@@ -503,6 +505,38 @@ __global__ void k_in_fill(uint32_t n, const unsigned long long* __restrict__ nod
     }
 }
 
+__global__ void k_in_head(uint32_t n, const uint64_t* __restrict__ uin_off, const uint32_t* __restrict__ uin_len,
+                          const uint32_t* __restrict__ uin_src, uint64_t* head) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= n) return;
+    const uint32_t len = uin_len[d];
+    const uint64_t off = uin_off[d];
+    const uint32_t h0 = len > 0 ? uin_src[off] : FGI_NONE;
+    const uint32_t h1 = len > 1 ? uin_src[off + 1] : FGI_NONE;
+    head[d] = (uint64_t)h0 | ((uint64_t)h1 << 32);
+}
+
+// Sort keys of the dependency lists: (weight of the entry << ubits) | entry, weight = the entry's
+// own number of dependencies (its list length; 0 for detached handles).
+__global__ void k_in_keys(uint64_t m, const uint32_t* __restrict__ uin_src, const uint32_t* __restrict__ uin_len,
+                          uint32_t n_slots, uint32_t ubits, uint64_t* keys) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t u = uin_src[i];
+    const uint64_t w = u < n_slots ? uin_len[u] : 0u;
+    keys[i] = (w << ubits) | u;
+}
+
+__global__ void k_in_unkey(uint64_t m, const uint64_t* __restrict__ keys, uint32_t ubits, uint32_t* uin_src) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < m) uin_src[i] = (uint32_t)(keys[i] & ((1ull << ubits) - 1ull));
+}
+
+__global__ void k_in_ends(uint32_t n, const uint64_t* __restrict__ off, const uint32_t* __restrict__ len, uint64_t* end) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d < n) end[d] = off[d] + len[d];
+}
+
 __global__ void k_invalidate_all_roots(uint32_t n_slots, const unsigned long long* node, uint32_t* roots,
                                        unsigned long long* cnt) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -571,7 +605,13 @@ fgi_status ensure_cstart(fgi_graph* g, uint64_t total_edges) {
 
 fgi_status ensure_pool(fgi_graph* g, uint64_t entries) {
     if (g->pool_cap >= entries && g->pool_col) return FGI_OK;
-    const uint64_t cap = std::max<uint64_t>({entries, g->pool_cap + g->pool_cap / 2, (uint64_t)1024});
+    // pool positions are 32-bit inside the expand kernel's LDS chunk map: 2^32 entries (48 GB of
+    // pool) per device; beyond that, partition the graph over more devices
+    constexpr uint64_t kMaxPool = 1ull << 32;
+    if (entries > kMaxPool)
+        return set_err(g, FGI_ENOTSUP, "edge pool of %llu entries exceeds 2^32 per device", (unsigned long long)entries);
+    const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>({entries, g->pool_cap + g->pool_cap / 2, (uint64_t)1024}),
+                                            kMaxPool);
     uint32_t* col = nullptr;
     uint64_t* tag = nullptr;
     FGI_TRY(dmalloc(g, &col, cap));
@@ -626,8 +666,55 @@ fgi_status ensure_in_lists(fgi_graph* g) {
     hipLaunchKernelGGL(k_in_fill, dim3(grid), dim3(256), 0, s, H, reinterpret_cast<const unsigned long long*>(g->node),
                        g->row_off, g->row_len, g->pool_col, g->pool_tag, g->uin_off, cursor, g->uin_src);
     FGI_HIP(g, hipGetLastError());
+    // Order every list by the entries' own dependency counts (descending; ties by handle): the
+    // nodes a wave reaches first are the ones with many dependencies, so a pull level finds a
+    // parent in the frontier among the first entries (and in the two heads, most of the time).
+    if (total > 1) {
+        uint32_t ubits = 1;
+        while (ubits < 32 && (1ull << ubits) < H) ++ubits;
+        uint32_t max_len = 0;
+        {
+            Tmp tr, tm;
+            uint32_t* dmax;
+            FGI_TRY(tmalloc(g, tm, &dmax, 1));
+            size_t rb = 0;
+            FGI_HIP(g, rocprim::reduce(nullptr, rb, g->uin_len, dmax, 0u, (size_t)N, rocprim::maximum<uint32_t>(), s));
+            char* rt;
+            FGI_TRY(tmalloc(g, tr, &rt, rb));
+            FGI_HIP(g, rocprim::reduce(rt, rb, g->uin_len, dmax, 0u, (size_t)N, rocprim::maximum<uint32_t>(), s));
+            FGI_TRY(d2h(g, &max_len, dmax, 1));
+        }
+        uint32_t wbits = 1;
+        while (wbits < 32 && (1ull << wbits) <= max_len) ++wbits;
+        Tmp tk0, tk1, te, tt;
+        uint64_t *k0, *k1, *ends;
+        FGI_TRY(tmalloc(g, tk0, &k0, total));
+        FGI_TRY(tmalloc(g, tk1, &k1, total));
+        FGI_TRY(tmalloc(g, te, &ends, N));
+        hipLaunchKernelGGL(k_in_keys, dim3(nblk(total)), dim3(256), 0, s, total, g->uin_src, g->uin_len, N, ubits, k0);
+        hipLaunchKernelGGL(k_in_ends, dim3(nblk(N)), dim3(256), 0, s, N, g->uin_off, g->uin_len, ends);
+        size_t sb = 0;
+        FGI_HIP(g, rocprim::segmented_radix_sort_keys_desc(nullptr, sb, k0, k1, (unsigned)total, N, g->uin_off, ends, 0,
+                                                           ubits + wbits, s));
+        char* st;
+        FGI_TRY(tmalloc(g, tt, &st, sb));
+        FGI_HIP(g, rocprim::segmented_radix_sort_keys_desc(st, sb, k0, k1, (unsigned)total, N, g->uin_off, ends, 0,
+                                                           ubits + wbits, s));
+        hipLaunchKernelGGL(k_in_unkey, dim3(nblk(total)), dim3(256), 0, s, total, k1, ubits, g->uin_src);
+        FGI_HIP(g, hipGetLastError());
+        FGI_HIP(g, hipStreamSynchronize(s));
+    }
+    FGI_TRY(build_in_heads(g));
     FGI_HIP(g, hipStreamSynchronize(s));
     g->uin_epoch = g->mut_epoch;
+    return FGI_OK;
+}
+
+fgi_status build_in_heads(fgi_graph* g) {
+    const uint32_t N = g->n_slots;
+    hipLaunchKernelGGL(k_in_head, dim3(nblk(N)), dim3(256), 0, g->stream, N, g->uin_off, g->uin_len, g->uin_src,
+                       g->uin_head);
+    FGI_HIP(g, hipGetLastError());
     return FGI_OK;
 }
 
@@ -728,13 +815,17 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
         dmalloc(g, &g->row_cap, H) || dmalloc(g, &g->used_cnt, H) || dmalloc(g, &g->home, g->n_detached + 1) ||
         dmalloc(g, &g->inv, H) || dmalloc(g, &g->fr_off[0], H) || dmalloc(g, &g->fr_off[1], H) ||
         dmalloc(g, &g->fr_len[0], H) || dmalloc(g, &g->fr_len[1], H) || dmalloc(g, &g->escan, H) ||
-        dmalloc(g, &g->partials, kScanBlocks) || dmalloc(g, &g->ctr, 1) || dmalloc(g, &g->misc_dev, 16) ||
+        dmalloc(g, &g->partials, kScanBlocks) || dmalloc(g, &g->ctr, 1) ||
+        dmalloc(g, &g->blk_stats, (size_t)kStatBlocks * kStatCols) || dmalloc(g, &g->misc_dev, 16) ||
         dmalloc(g, &g->pool_top_dev, 1) || dmalloc(g, &g->uin_off, H) || dmalloc(g, &g->uin_len, H) ||
-        dmalloc(g, &g->pull_ovf, g->n_slots))
+        dmalloc(g, &g->uin_head, g->n_slots + 1))
         return fail(FGI_ENOMEM);
-    g->bm_words = (H + 31) / 32 + 2;
-    if (dmalloc(g, &g->dead_bm, g->bm_words) || dmalloc(g, &g->front_bm, g->bm_words)) return fail(FGI_ENOMEM);
+    g->bm_words = (H + 63) / 64 * 2 + 2;
+    if (dmalloc(g, &g->dead_bm, g->bm_words) || dmalloc(g, &g->front_bm, g->bm_words) ||
+        dmalloc(g, &g->front_nx, g->bm_words))
+        return fail(FGI_ENOMEM);
     hipMemset(g->front_bm, 0, g->bm_words * 4);
+    hipMemset(g->front_nx, 0, g->bm_words * 4);
     if (hipHostMalloc(reinterpret_cast<void**>(&g->ctr_host), sizeof(WaveCtr)) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&g->misc_host), 16 * sizeof(unsigned long long)) != hipSuccess)
         return fail(FGI_ENOMEM);
@@ -777,11 +868,13 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->uin_off);
     dfree(g->uin_len);
     dfree(g->uin_src);
-    dfree(g->pull_ovf);
+    dfree(g->uin_head);
     dfree(g->dead_bm);
     dfree(g->front_bm);
+    dfree(g->front_nx);
     dfree(g->partials);
     dfree(g->ctr);
+    dfree(g->blk_stats);
     dfree(g->roots_buf);
     dfree(g->imm_buf);
     dfree(g->misc_dev);

@@ -9,7 +9,7 @@
 // in a wave is the only one that can change it (Computed.cs:164-191 — later visits find it
 // Invalidated, or the flag already set), so dropping the repeats is exact.
 //
-// Per level: local push (k_expand<true>) -> counts all-gather (ncclAllGather) -> payload by
+// Per level: local push (k_level<true>) -> counts all-gather (ncclAllGather) -> payload by
 // grouped ncclSend/ncclRecv -> owners apply the received targets (k_apply_recv) -> global
 // frontier size by ncclAllReduce (termination).
 #include <hip/hip_runtime.h>
@@ -215,7 +215,7 @@ static fgi_status part_build_in_lists(fgi_graph* g, const uint64_t* keys, uint64
     FGI_HIP(g, hipMemsetAsync(g->uin_off, 0, (size_t)g->n_slots * 8, s));
     if (mi == 0) {
         if (!g->uin_src) FGI_HIP(g, hipMalloc(&g->uin_src, 1024 * 4));
-        return FGI_OK;
+        return build_in_heads(g);
     }
     uint64_t *k1 = nullptr, *k2 = nullptr;
     uint32_t *keep = nullptr, *kpos = nullptr;
@@ -264,6 +264,9 @@ static fgi_status part_build_in_lists(fgi_graph* g, const uint64_t* keys, uint64
                            g->uin_len);
         hipLaunchKernelGGL(k_in_part_fix, dim3((g->n_slots + 255) / 256), dim3(256), 0, s, g->n_slots, g->uin_off,
                            g->uin_len);
+        // global dependency ids carry no local weight: lists stay in id order
+        rc = build_in_heads(g);
+        if (rc != FGI_OK) break;
         if (hipStreamSynchronize(s) != hipSuccess) rc = set_err(g, FGI_EDEVICE, "dependency-list build");
     } while (0);
     hipFree(k1);

@@ -14,7 +14,9 @@ from typing import Optional, Tuple
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libfgi.so")
+# FGI_LIBRARY selects another in-tree build of the engine (e.g. an instrumented one); there is no
+# fallback: a missing library raises FgiError.
+LIB_PATH = os.environ.get("FGI_LIBRARY") or os.path.join(_HERE, "lib", "libfgi.so")
 
 OK, EINVAL, ENOMEM, ECAPACITY, EDEVICE, ESTATE, ENOTSUP = range(7)
 OPT_DEAD_FILTER, OPT_DIRECTION, OPT_PULL_ALPHA = 1, 2, 3

@@ -196,10 +196,10 @@ static void prune() {
     auto a = Compute(r, "a");
     auto b = Compute(r, "b", {a});
     Compute(r, "c", {a});
-    b->Invalidate();                      // a's entry for b is now stale
-    CHECK(a->UsedBy().size() == 2);
-    auto pr = r.Prune();
-    CHECK(pr.first >= 2 && a->UsedBy().size() == 1);
+    b->Invalidate();   // RemoveUsedBy: b's entry leaves a's set (lazily in the engine's pool)
+    CHECK(a->UsedBy().size() == 1);
+    auto pr = r.Prune();   // the pruner compacts the stale entry away
+    CHECK(pr.first == 2 && pr.second == 1 && a->UsedBy().size() == 1);
 }
 
 int main() {
