@@ -80,15 +80,23 @@ constexpr int kChunk = kBlock * kEPT;   // edges per expand chunk
 constexpr uint32_t kStatBlocks = 4096;  // per-block statistics rows (grid limit of the hot kernels)
 constexpr int kStatCols = 8;
 
+constexpr int kPullTile = 1024;        // slots per pull tile (one block iteration of a pull level)
+
 struct LevelCtr {
     unsigned long long F;       // frontier entries (expandable = invalidated with |row| > 0)
     unsigned long long T;       // edges of the frontier (sum of row lengths)
     unsigned long long nchunks; // ceil(T / kChunk)
     unsigned long long pull;    // 1 if this level runs bottom-up (pull)
-    unsigned long long mark_lo; // inv[] range marked into the bitmaps before this level
-    unsigned long long mark_hi;
+    unsigned long long mark_lo; // inv[] range of the previous level's winners (marked into the
+    unsigned long long mark_hi; //   frontier bitmap before a pull; appended here after a pull)
     unsigned long long pad0;
     unsigned long long pad1;
+};
+
+// Per pull tile (kPullTile slots): winners, expandable winners (|row| > 0), their row lengths.
+struct PullTile {
+    uint32_t w, e;
+    unsigned long long len;
 };
 
 struct WaveCtr {
@@ -163,10 +171,21 @@ struct fgi_graph {
     uint8_t* imm_buf = nullptr;
     uint64_t roots_cap = 0;
     uint64_t last_wave_n = 0;
+    int last_levels = 4;               // non-empty levels of the last wave (sizes the first level group)
 
-    // per-wave bitmaps over handles (bit set = node invalidated earlier in this wave / in the
-    // current frontier); read-only while a level expands, so they stay L2-resident
-    uint32_t* dead_bm = nullptr;
+    // Visit bitmap over handles: bit h set = node h was visited by a wave since the
+    // last fold. A visit's effect is a pure function of the node word, and every second visit is a
+    // no-op, so the pair (node word, visit bit) is the node's state; one atomicOr decides the first
+    // visitor. fold() applies the bits to the words before any mutation or state query.
+    uint32_t* vis_bm = nullptr;
+    bool v_dirty = false;              // vis_bm may hold set bits
+    // Expandable-class bitmap (Consistent, no delay: a first visit invalidates and expands), built
+    // from the node words; pull levels read it instead of the words (2 MB vs 128 MB at 16M slots).
+    uint32_t* cls_bm = nullptr;
+    bool cls_valid = false;
+    bool words_dirty = true;           // node words changed since the snapshot
+    fgi::PullTile* tiles = nullptr;    // per pull tile counts of the last pull level
+    uint64_t tiles_cap = 0;
     uint32_t* front_bm = nullptr;      // frontier bitmap (pull levels); multi-GPU: the local words
     uint32_t* front_nx = nullptr;      // second frontier bitmap: pull level L reads fb[L&1] and
                                        // writes its winners into fb[(L+1)&1]
@@ -180,6 +199,7 @@ struct fgi_graph {
     uint64_t* uin_head = nullptr;      // [n_slots] the list's first two entries (lo | hi << 32, FGI_NONE
                                        // if absent), probed first: lists are ordered by the number of
                                        // dependencies of each entry, the ones a wave reaches earliest
+    uint32_t* uin_more = nullptr;      // bitmap: the list has more than two entries
     uint64_t uin_cap = 0;
     uint64_t uin_epoch = 0;            // mut_epoch the cache was built at (0 = never)
     uint64_t mut_epoch = 1;            // changes on every mutation of rows or versions
@@ -240,6 +260,18 @@ fgi_status ensure_in_lists(fgi_graph* g);
 fgi_status build_in_heads(fgi_graph* g);
 // Record a mutation of rows or versions (invalidates the dependency-list cache).
 inline void touch(fgi_graph* g) { g->mut_epoch = ++g->epoch_counter; }
+// Record a change of node words (class bitmap rebuilt before the next wave; restore copies words).
+inline void note_words(fgi_graph* g) {
+    g->cls_valid = false;
+    g->words_dirty = true;
+}
+// Apply the visit bitmap to the node words and clear it (wave.hip). Every entry point that reads or
+// mutates node words outside a wave calls it first.
+fgi_status fold(fgi_graph* g);
+// Rebuild the expandable-class bitmap if node words changed (wave.hip).
+fgi_status ensure_cls(fgi_graph* g);
+// Pull tiles of a level over n slots with `grid` blocks.
+__host__ __device__ inline uint64_t pull_iters(uint64_t n, uint32_t grid) { return (n + (uint64_t)grid * kPullTile - 1) / ((uint64_t)grid * kPullTile); }
 // ---- multi-GPU partition (part.hip) ----
 // Release multi-GPU resources.
 fgi_status part_destroy(fgi_graph* g);

@@ -505,11 +505,14 @@ __global__ void k_in_fill(uint32_t n, const unsigned long long* __restrict__ nod
     }
 }
 
+// heads (first two entries) and the "more than two entries" bitmap, one 64-bit word per wave
 __global__ void k_in_head(uint32_t n, const uint64_t* __restrict__ uin_off, const uint32_t* __restrict__ uin_len,
-                          const uint32_t* __restrict__ uin_src, uint64_t* head) {
+                          const uint32_t* __restrict__ uin_src, uint64_t* head, unsigned long long* more64) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t len = d < n ? uin_len[d] : 0u;
+    const unsigned long long m = __ballot(len > 2);
+    if ((threadIdx.x & 63) == 0 && d < n) more64[d >> 6] = m;
     if (d >= n) return;
-    const uint32_t len = uin_len[d];
     const uint64_t off = uin_off[d];
     const uint32_t h0 = len > 0 ? uin_src[off] : FGI_NONE;
     const uint32_t h1 = len > 1 ? uin_src[off + 1] : FGI_NONE;
@@ -713,7 +716,7 @@ fgi_status ensure_in_lists(fgi_graph* g) {
 fgi_status build_in_heads(fgi_graph* g) {
     const uint32_t N = g->n_slots;
     hipLaunchKernelGGL(k_in_head, dim3(nblk(N)), dim3(256), 0, g->stream, N, g->uin_off, g->uin_len, g->uin_src,
-                       g->uin_head);
+                       g->uin_head, reinterpret_cast<unsigned long long*>(g->uin_more));
     FGI_HIP(g, hipGetLastError());
     return FGI_OK;
 }
@@ -815,17 +818,21 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
         dmalloc(g, &g->row_cap, H) || dmalloc(g, &g->used_cnt, H) || dmalloc(g, &g->home, g->n_detached + 1) ||
         dmalloc(g, &g->inv, H) || dmalloc(g, &g->fr_off[0], H) || dmalloc(g, &g->fr_off[1], H) ||
         dmalloc(g, &g->fr_len[0], H) || dmalloc(g, &g->fr_len[1], H) || dmalloc(g, &g->escan, H) ||
-        dmalloc(g, &g->partials, kScanBlocks) || dmalloc(g, &g->ctr, 1) ||
+        dmalloc(g, &g->partials, 4 * kScanBlocks) || dmalloc(g, &g->ctr, 1) ||
         dmalloc(g, &g->blk_stats, (size_t)kStatBlocks * kStatCols) || dmalloc(g, &g->misc_dev, 16) ||
         dmalloc(g, &g->pool_top_dev, 1) || dmalloc(g, &g->uin_off, H) || dmalloc(g, &g->uin_len, H) ||
         dmalloc(g, &g->uin_head, g->n_slots + 1))
         return fail(FGI_ENOMEM);
     g->bm_words = (H + 63) / 64 * 2 + 2;
-    if (dmalloc(g, &g->dead_bm, g->bm_words) || dmalloc(g, &g->front_bm, g->bm_words) ||
-        dmalloc(g, &g->front_nx, g->bm_words))
+    g->tiles_cap = (uint64_t)H / kPullTile + kStatBlocks + 1;
+    if (dmalloc(g, &g->vis_bm, g->bm_words) || dmalloc(g, &g->front_bm, g->bm_words) ||
+        dmalloc(g, &g->front_nx, g->bm_words) || dmalloc(g, &g->cls_bm, g->bm_words) ||
+        dmalloc(g, &g->uin_more, g->bm_words) || dmalloc(g, &g->tiles, g->tiles_cap))
         return fail(FGI_ENOMEM);
+    hipMemset(g->vis_bm, 0, g->bm_words * 4);
     hipMemset(g->front_bm, 0, g->bm_words * 4);
     hipMemset(g->front_nx, 0, g->bm_words * 4);
+    hipMemset(g->uin_more, 0, g->bm_words * 4);
     if (hipHostMalloc(reinterpret_cast<void**>(&g->ctr_host), sizeof(WaveCtr)) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&g->misc_host), 16 * sizeof(unsigned long long)) != hipSuccess)
         return fail(FGI_ENOMEM);
@@ -869,7 +876,10 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->uin_len);
     dfree(g->uin_src);
     dfree(g->uin_head);
-    dfree(g->dead_bm);
+    dfree(g->vis_bm);
+    dfree(g->cls_bm);
+    dfree(g->uin_more);
+    dfree(g->tiles);
     dfree(g->front_bm);
     dfree(g->front_nx);
     dfree(g->partials);
@@ -919,8 +929,10 @@ fgi_status fgi_register_nodes(fgi_graph* g, uint32_t n, const uint32_t* slot, co
     FGI_TRY(h2d(g, ds, slot, n));
     FGI_TRY(h2d(g, dv, version, n));
     if (state_flags) FGI_TRY(h2d(g, df, state_flags, n));
+    FGI_TRY(fold(g));
     FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, sizeof(unsigned long long), g->stream));
     touch(g);
+    note_words(g);
     hipLaunchKernelGGL(k_register, dim3(nblk(n)), dim3(256), 0, g->stream, n, ds, dv, df,
                        reinterpret_cast<unsigned long long*>(g->node), g->row_len, g->misc_dev);
     FGI_HIP(g, hipGetLastError());
@@ -939,6 +951,7 @@ fgi_status fgi_load_edges(fgi_graph* g, uint64_t m, const uint32_t* used, const 
         if (tag[e] == 0) return set_err(g, FGI_EINVAL, "edge %llu has tag 0 (LTags are positive)", (unsigned long long)e);
     }
     hipSetDevice(g->device);
+    FGI_TRY(fold(g));
     // existing live rows + the new entries, rebuilt in one sort (set semantics across both)
     Tmp tk, tt;
     uint64_t *keys, *tags, m0 = 0;
@@ -958,6 +971,7 @@ fgi_status fgi_get_state(fgi_graph* g, uint32_t n, const uint32_t* handle, uint6
         if (handle[i] >= g->n_handles) return set_err(g, FGI_EINVAL, "handle %u out of range", handle[i]);
     if (n == 0) return FGI_OK;
     hipSetDevice(g->device);
+    FGI_TRY(fold(g));
     Tmp th, tw;
     uint32_t* dh;
     unsigned long long* dw;
@@ -978,6 +992,7 @@ fgi_status fgi_get_state(fgi_graph* g, uint32_t n, const uint32_t* handle, uint6
 fgi_status fgi_dump_states(fgi_graph* g, uint64_t* version, uint32_t* state_flags) {
     if (!g) return FGI_EINVAL;
     hipSetDevice(g->device);
+    FGI_TRY(fold(g));
     std::vector<uint64_t> w(g->n_handles);
     FGI_TRY(d2h(g, w.data(), g->node, g->n_handles));
     for (uint32_t h = 0; h < g->n_handles; ++h) {
@@ -1017,6 +1032,7 @@ __global__ void k_used_by_live(uint32_t len, const uint32_t* __restrict__ col, c
 fgi_status fgi_get_used_by(fgi_graph* g, uint32_t handle, uint32_t* dep, uint64_t* tag, uint64_t cap, uint64_t* out_n) {
     if (!g || handle >= g->n_handles) return FGI_EINVAL;
     hipSetDevice(g->device);
+    FGI_TRY(fold(g));
     uint64_t w = 0, off = 0;
     uint32_t len = 0;
     FGI_TRY(d2h(g, &w, g->node + handle, 1));
@@ -1054,6 +1070,7 @@ fgi_status fgi_get_used_by(fgi_graph* g, uint32_t handle, uint32_t* dep, uint64_
 fgi_status fgi_get_used_count(fgi_graph* g, uint32_t handle, uint32_t* out) {
     if (!g || !out || handle >= g->n_handles) return FGI_EINVAL;
     hipSetDevice(g->device);
+    FGI_TRY(fold(g));
     uint64_t w = 0;
     uint32_t c = 0;
     FGI_TRY(d2h(g, &w, g->node + handle, 1));
@@ -1065,6 +1082,7 @@ fgi_status fgi_get_used_count(fgi_graph* g, uint32_t handle, uint32_t* out) {
 fgi_status fgi_get_degrees(fgi_graph* g, uint32_t* degree, uint64_t* total) {
     if (!g) return FGI_EINVAL;
     hipSetDevice(g->device);
+    FGI_TRY(fold(g));
     const uint32_t H = g->n_handles;
     std::vector<uint64_t> w(H);
     std::vector<uint32_t> len(H);
@@ -1083,6 +1101,7 @@ fgi_status fgi_get_degrees(fgi_graph* g, uint32_t* degree, uint64_t* total) {
 fgi_status fgi_export_edges(fgi_graph* g, uint32_t* used, uint32_t* dep, uint64_t* tag, uint64_t cap, uint64_t* out_n) {
     if (!g) return FGI_EINVAL;
     hipSetDevice(g->device);
+    FGI_TRY(fold(g));
     Tmp tk, tt;
     uint64_t *keys, *tags, m = 0;
     FGI_TRY(gather_live(g, tk, tt, &keys, &tags, 0, &m));
@@ -1108,6 +1127,7 @@ fgi_status fgi_snapshot(fgi_graph* g) {
             return FGI_ENOMEM;
     }
     hipStream_t s = g->stream;
+    FGI_TRY(fold(g));
     FGI_HIP(g, hipMemcpyAsync(g->snap_node, g->node, H * 8, hipMemcpyDeviceToDevice, s));
     FGI_HIP(g, hipMemcpyAsync(g->snap_row_off, g->row_off, H * 8, hipMemcpyDeviceToDevice, s));
     FGI_HIP(g, hipMemcpyAsync(g->snap_row_len, g->row_len, H * 4, hipMemcpyDeviceToDevice, s));
@@ -1116,18 +1136,28 @@ fgi_status fgi_snapshot(fgi_graph* g) {
     FGI_HIP(g, hipStreamSynchronize(s));
     g->snap_epoch = g->pool_epoch;
     g->snap_mut_epoch = g->mut_epoch;
+    g->words_dirty = false;
     return FGI_OK;
 }
 
 // Restores the node table; the edge pool is append-only between compactions, so the saved row
-// descriptors still address the saved rows unless fgi_prune / a bulk load ran in between.
+// descriptors still address the saved rows unless fgi_prune / a bulk load ran in between. A node's
+// state is its word plus its visit bit: waves only set bits, so after waves alone the words are the
+// snapshot's and clearing the bitmap restores every node; words are copied back only if something
+// else (a fold, a mutation, an immediate root) changed them.
 fgi_status fgi_restore(fgi_graph* g) {
     if (!g || !g->snap_node) return FGI_EINVAL;
     if (g->snap_epoch != g->pool_epoch) return set_err(g, FGI_ESTATE, "edge pool was rebuilt since the snapshot");
     hipSetDevice(g->device);
     const size_t H = g->n_handles;
     hipStream_t s = g->stream;
-    FGI_HIP(g, hipMemcpyAsync(g->node, g->snap_node, H * 8, hipMemcpyDeviceToDevice, s));
+    if (g->words_dirty) {
+        FGI_HIP(g, hipMemcpyAsync(g->node, g->snap_node, H * 8, hipMemcpyDeviceToDevice, s));
+        g->words_dirty = false;
+        g->cls_valid = false;
+    }
+    if (g->v_dirty) FGI_HIP(g, hipMemsetAsync(g->vis_bm, 0, g->bm_words * 4, s));
+    g->v_dirty = false;
     if (g->mut_epoch == g->snap_mut_epoch) {
         // nothing but waves ran since the snapshot: rows and |_used| counts are unchanged
         FGI_HIP(g, hipStreamSynchronize(s));
@@ -1219,6 +1249,7 @@ fgi_status fgi_invalidate_all(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uin
     if (!g) return FGI_EINVAL;
     hipSetDevice(g->device);
     FGI_TRY(stage_roots(g, g->n_slots));
+    FGI_TRY(fold(g));
     FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, sizeof(unsigned long long), g->stream));
     hipLaunchKernelGGL(k_invalidate_all_roots, dim3(nblk(g->n_slots)), dim3(256), 0, g->stream, g->n_slots,
                        reinterpret_cast<const unsigned long long*>(g->node), g->roots_buf, g->misc_dev);
@@ -1258,6 +1289,7 @@ fgi_status fgi_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, con
     }
     FGI_TRY(h2d(g, ds, slot, n));
     FGI_TRY(h2d(g, dv, version, n));
+    FGI_TRY(fold(g));
     FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, 4 * sizeof(unsigned long long), st));
     hipLaunchKernelGGL(k_bc_classify, dim3(nblk(n)), dim3(256), 0, st, n, ds,
                        reinterpret_cast<const unsigned long long*>(g->node), dcls, droots, g->misc_dev);
@@ -1272,8 +1304,10 @@ fgi_status fgi_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, con
     std::vector<uint32_t> take(g->free_detached.end() - (ptrdiff_t)cnt[1], g->free_detached.end());
     FGI_TRY(tmalloc(g, tf, &dfree_h, take.size() + 1));
     FGI_TRY(h2d(g, dfree_h, take.data(), take.size()));
+    FGI_TRY(fold(g));   // the displacement cascade's visits
     FGI_HIP(g, hipMemsetAsync(g->misc_dev + 2, 0, sizeof(unsigned long long), st));
     touch(g);
+    note_words(g);
     hipLaunchKernelGGL(k_bc_install, dim3(nblk(n)), dim3(256), 0, st, n, ds, dv, dd, dcls, dfree_h, g->misc_dev + 2,
                        g->n_slots, reinterpret_cast<unsigned long long*>(g->node), g->row_off, g->row_len, g->row_cap,
                        g->used_cnt, g->home, dout);
@@ -1308,6 +1342,8 @@ fgi_status fgi_add_used(fgi_graph* g, uint32_t n, const uint32_t* dependant, con
     FGI_TRY(tmalloc(g, tovf, &dovf, n));
     FGI_TRY(h2d(g, ddep, dependant, n));
     FGI_TRY(h2d(g, duse, used, n));
+    FGI_TRY(fold(g));
+    note_words(g);   // may set InvalidateOnSetOutput (Computed.cs:376-378)
     FGI_HIP(g, hipMemsetAsync(dhash, 0xFF, hcap * sizeof(unsigned long long), st));
     FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, 8 * sizeof(unsigned long long), st));
     hipLaunchKernelGGL(k_au_classify, dim3(nblk(n)), dim3(256), 0, st, n, ddep, duse, g->n_slots, g->home,
@@ -1356,6 +1392,8 @@ fgi_status fgi_set_output(fgi_graph* g, uint32_t n, const uint32_t* handle, uint
     FGI_TRY(tmalloc(g, ts, &dset, n));
     FGI_TRY(tmalloc(g, tr, &droots, n));
     FGI_TRY(h2d(g, dh, handle, n));
+    FGI_TRY(fold(g));
+    note_words(g);
     FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, sizeof(unsigned long long), st));
     hipLaunchKernelGGL(k_set_output, dim3(nblk(n)), dim3(256), 0, st, n, dh, g->n_handles,
                        reinterpret_cast<unsigned long long*>(g->node), dset, droots, g->misc_dev);
@@ -1371,6 +1409,7 @@ fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats) {
     if (!g) return FGI_EINVAL;
     hipSetDevice(g->device);
     const auto t0 = std::chrono::steady_clock::now();
+    FGI_TRY(fold(g));
     hipStream_t st = g->stream;
     const uint32_t H = g->n_handles;
     Tmp tl, to, ts;
@@ -1434,6 +1473,8 @@ fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats) {
 fgi_status fgi_release(fgi_graph* g, uint32_t n, const uint32_t* handle) {
     if (!g || (n && !handle)) return FGI_EINVAL;
     hipSetDevice(g->device);
+    FGI_TRY(fold(g));
+    if (n) note_words(g);
     for (uint32_t i = 0; i < n; ++i) {
         const uint32_t h = handle[i];
         if (h < g->n_slots || h >= g->n_handles) return set_err(g, FGI_EINVAL, "handle %u is not detached", h);

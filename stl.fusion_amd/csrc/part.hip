@@ -419,7 +419,9 @@ fgi_status fgi_part_local_invalidate(fgi_graph* const* gs, uint32_t P, uint32_t 
     }
     const int direction = gs[0]->opt_direction;
     const uint64_t threshold = e_global / (uint64_t)(gs[0]->opt_pull_alpha > 0 ? gs[0]->opt_pull_alpha : 1);
-    for (int L = 0; st == FGI_OK && f_global != 0; ++L) {
+    int L = 0;
+    bool last_pull = false;
+    for (; st == FGI_OK && f_global != 0; ++L) {
         uint64_t t_global = 0;
         for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
             hipSetDevice(gs[r]->device);
@@ -481,6 +483,12 @@ fgi_status fgi_part_local_invalidate(fgi_graph* const* gs, uint32_t P, uint32_t 
             hipSetDevice(gs[r]->device);
             st = part_level_account(gs[r], L);
         }
+        last_pull = pull;
+    }
+    // the last level's pull winners (without rows) are collected into the invalidated list
+    for (uint32_t r = 0; r < P && st == FGI_OK && last_pull; ++r) {
+        hipSetDevice(gs[r]->device);
+        st = part_level_scan(gs[r], L);
     }
     for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
         hipSetDevice(gs[r]->device);
@@ -500,6 +508,9 @@ fgi_status fgi_part_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_facto
     hipStream_t s = g->stream;
     const uint32_t N = p->v.n_global;
     FGI_HIP(g, hipMemsetAsync(g->node, 0, (size_t)g->n_handles * 8, s));
+    FGI_HIP(g, hipMemsetAsync(g->vis_bm, 0, g->bm_words * 4, s));   // a new node table
+    g->v_dirty = false;
+    note_words(g);
     hipLaunchKernelGGL(k_versions_local, dim3((p->v.n_local + 255) / 256), dim3(256), 0, s, p->v.n_local, p->v.base,
                        seed, reinterpret_cast<unsigned long long*>(g->node));
     hipLaunchKernelGGL(k_versions_all, dim3((N + 255) / 256), dim3(256), 0, s, N, seed, p->v.ver_all);

@@ -7,20 +7,22 @@
 //     Computing                : flags |= InvalidateOnSetOutput          (173-178)
 //     Consistent, hasDelay     : flags |= InvalidationDelayStarted once  (186-191; timer host-side)
 //     Consistent, no delay     : state := Invalidated, expand every `_usedBy` entry (185, 212-216)
-// Each rule is one 64-bit CAS on the packed node word, so a node is invalidated (and expanded)
-// exactly once however many frontier edges reach it. The union over roots is order-independent
-// (DESIGN.md §Semantics), so one BFS wave replaces the reference's sequence of per-root DFS.
+// Every rule is idempotent (a second visit is always a no-op) and its effect depends only on the
+// node word, which no wave changes. So a wave records visits in a bitmap: one atomicOr per visit
+// decides the first visitor, and the first visitor of a node of the expandable class (Consistent,
+// no delay) is its one invalidation winner. fold() applies the bits to the words before anything
+// else reads them. The union over roots is order-independent, so one
+// BFS wave replaces the reference's sequence of per-root DFS.
 //
-// Per level L (stream-ordered launches; the host only synchronises once per group of levels):
-//   k_level_begin : push/pull decision for the level (from the frontier totals F and T that the
-//                   previous level's emitters accumulated), dead/frontier bitmap upkeep for the
-//                   previous level's push winners, partial sums of the frontier's row lengths
-//   k_scan_apply  : (push levels) exclusive scan of the row lengths and the chunk->entry map
-//   k_level       : push — edge-parallel expansion of the frontier's `_usedBy` rows (edges to
-//                   nodes already dead skip the tag load and the gather); or pull — every live
-//                   slot probes its dependency list (the reference's `_used`: in-edges whose tag
-//                   matches its version) for a parent in the frontier bitmap, head first, with
-//                   early exit (Beamer's bottom-up step), storing its winners' bitmap words itself
+// Per level L (stream-ordered launches; the host synchronises once per group of levels):
+//   k_level_begin : push/pull decision for the level, frontier bitmap upkeep for the previous
+//                   level's push winners, partial sums of the frontier's row lengths; after a pull
+//                   level: partial sums of its per-tile winner counts (collect, pass 1)
+//   k_scan_apply  : push — exclusive scan of the row lengths and the chunk->entry map; after a pull
+//                   level: the winners bitmap -> invalidated list + frontier list (collect, pass 2)
+//   k_level       : push — edge-parallel expansion of the frontier's `_usedBy` rows; or pull — every
+//                   live slot probes its dependency list (the reference's `_used`) for a parent in
+//                   the frontier bitmap (Beamer's bottom-up step), writing only bitmaps and counts
 // Multi-GPU levels (run_part_wave) use k_scan_reduce / k_scan_apply / k_mark / k_level<true> /
 // k_apply_recv / k_clear_front, with the exchange between them.
 #include <hip/hip_runtime.h>
@@ -34,34 +36,45 @@
 namespace fgi {
 namespace {
 
-constexpr uint32_t kPullCap = 16;   // list entries one lane scans; longer lists go to the whole wave
-
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
 __device__ __forceinline__ bool bit_of(const uint32_t* __restrict__ bm, uint32_t h) {
     return (bm[h >> 5] >> (h & 31)) & 1u;
 }
 
-// CAS state transition of one node word; w is a (possibly stale) observed value with the right
-// version. Returns 1 if this call moved Consistent -> Invalidated, 2 if it only set a flag.
-__device__ __forceinline__ int visit_word(unsigned long long* p, unsigned long long w, bool imm) {
-    while (true) {
-        const uint32_t st = word_state(w);
-        unsigned long long nw;
-        if (st == FGI_INVALIDATED) return 0;
-        if (st == FGI_COMPUTING) {
-            nw = w | kW_IOSO | (imm ? kW_DS : 0ull);
-            if (nw == w) return 0;
-        } else if (imm || !(w & kW_HasDelay)) {
-            nw = (w & (kVMask | kW_HasDelay)) | kW_Invalidated;   // canonical: flags cleared
-        } else {
-            if (w & kW_DS) return 0;
-            nw = w | kW_DS;
-        }
-        const unsigned long long prev = atomicCAS(p, w, nw);
-        if (prev == w) return word_state(nw) == FGI_INVALIDATED ? 1 : 2;
-        w = prev;
-    }
+// Effect of a node's first visit in a wave: 1 = Consistent -> Invalidated (expands), 2 = a flag
+// is newly set (Computing: InvalidateOnSetOutput; Consistent with delay: InvalidationDelayStarted),
+// 0 = nothing (Invalidated, or the flag was already set).
+__device__ __forceinline__ int first_visit(unsigned long long w) {
+    const uint32_t st = word_state(w);
+    if (st == FGI_CONSISTENT) return (w & kW_HasDelay) ? ((w & kW_DS) ? 0 : 2) : 1;
+    if (st == FGI_COMPUTING) return (w & kW_IOSO) ? 0 : 2;
+    return 0;
+}
+
+// The node word after a (non-immediate) visit: canonical, flags of an Invalidated node cleared.
+__host__ __device__ __forceinline__ unsigned long long visited_word(unsigned long long w) {
+    if ((w & kVMask) == 0) return w;
+    const uint32_t st = word_state(w);
+    if (st == FGI_COMPUTING) return w | kW_IOSO;
+    if (st == FGI_CONSISTENT)
+        return (w & kW_HasDelay) ? (w | kW_DS) : ((w & (kVMask | kW_HasDelay)) | kW_Invalidated);
+    return w;
+}
+
+// Invalidate(immediately: true) on a canonical word (Computed.cs:162-191: the delay is ignored).
+__device__ __forceinline__ unsigned long long imm_word(unsigned long long w) {
+    const uint32_t st = word_state(w);
+    if (st == FGI_COMPUTING) return w | kW_IOSO | kW_DS;
+    if (st == FGI_CONSISTENT) return (w & (kVMask | kW_HasDelay)) | kW_Invalidated;
+    return w;
+}
+
+// One visit of node h (word w, version already matched): a single atomicOr on the visit bitmap.
+__device__ __forceinline__ int visit_bit(uint32_t* vis, uint32_t h, unsigned long long w) {
+    const uint32_t b = 1u << (h & 31);
+    if (atomicOr(vis + (h >> 5), b) & b) return 0;
+    return first_visit(w);
 }
 
 __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) {
@@ -76,11 +89,29 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) 
     return x - v;
 }
 
+__device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long long v) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const unsigned long long y = __shfl_up(v, d, 64);
+        if (lane >= (uint32_t)d) v += y;
+    }
+    return v;
+}
+
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
     return v;
 }
+
+__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+
+__device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
 // Where a level's winners go: the invalidated list (all winners) and the next frontier (winners
 // with a non-empty row, with that row's offset/length); the next level's F and T accumulate in ln.
@@ -112,20 +143,14 @@ __device__ __forceinline__ void wave_reserve(uint32_t n_inv, uint32_t n_fr, unsi
     fr_base = b_fr + (ex >> 16);
 }
 
-__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
-}
-
 // Per-block statistics: hot kernels keep their counters per block (plain read-modify-write of the
-// block's own row by one thread, launches of a wave are stream-ordered) instead of per-wave
-// atomics on a few words: a single device-scope word saturates near 88 atomics/us, so 6,000 waves
-// adding to it would serialise for ~70 us. k_stats_reduce folds the rows into WaveCtr.
+// block's own column entry by one thread, launches of a wave are stream-ordered) instead of per-wave
+// atomics on a few words: a single device-scope word saturates near 88 atomics/us. Column-major
+// ([column][block]) so k_stats_reduce sweeps each column coalesced.
 enum : int { kStEMatch, kStFlagged, kStPullCand, kStPullEdges, kStPullLive, kStPullWin, kStPullTail, kStPullScan, kStats };
 static_assert(kStats == kStatCols, "statistics columns");
 
-// Block-uniform call: adds each thread's v[k] into the block's row.
+// Block-uniform call: adds each thread's v[k] into the block's entries.
 __device__ __forceinline__ void block_stats_add(unsigned long long* blk, unsigned long long (*s)[kStats],
                                                 const uint32_t (&v)[kStats]) {
     const uint32_t wid = threadIdx.x >> 6;
@@ -139,8 +164,8 @@ __device__ __forceinline__ void block_stats_add(unsigned long long* blk, unsigne
     __syncthreads();
     if (threadIdx.x < kStats) {
         unsigned long long t = 0;
-        for (uint32_t q = 0; q < kBlock / 64; ++q) t += s[q][threadIdx.x];
-        if (t) blk[(uint64_t)blockIdx.x * kStats + threadIdx.x] += t;
+        for (uint32_t q = 0; q < blockDim.x / 64; ++q) t += s[q][threadIdx.x];
+        if (t) blk[(uint64_t)threadIdx.x * kStatBlocks + blockIdx.x] += t;
     }
 }
 
@@ -163,10 +188,8 @@ __device__ __forceinline__ void emit_one(bool win, uint32_t h, const Out& o) {
     if (lane_id() == 0 && ls) atomicAdd(&o.ln->T, ls);
 }
 
-// Block-level emission: winners are staged in LDS and appended to the global lists in batches
-// (one pair of global atomics per batch instead of one per wave per iteration: the two list
-// counters are single words, and same-address atomics saturate at ~88/us chip-wide). The staging
-// buffer (CAP entries) is passed separately: pull levels stage into the expand LDS arrays.
+// Block-level emission (push levels): winners are staged in LDS and appended to the global lists
+// in batches (one pair of global atomics per batch instead of one per wave per iteration).
 constexpr uint32_t kEmitCap = 1024;
 struct Emit {
     uint32_t n;
@@ -191,7 +214,7 @@ __device__ __forceinline__ void emit_push(Emit& e, uint32_t* buf, bool win, uint
     if (lane_id() == 0) base = atomicAdd(&e.n, (uint32_t)__popcll(m));
     base = __shfl(base, 0, 64);
     if (win) {
-        const uint32_t idx = base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+        const uint32_t idx = base + (uint32_t)__popcll(m & lanemask_lt());
         if (idx < CAP) {
             buf[idx] = h;
         } else {
@@ -297,7 +320,7 @@ __device__ __forceinline__ void msg_push(MsgEmit<true>& me, bool send, uint32_t 
     if (lane_id() == 0) base = atomicAdd(&me.n, (uint32_t)__popcll(m));
     base = __shfl(base, 0, 64);
     if (send) {
-        const uint32_t idx = base + (uint32_t)__popcll(m & ((1ull << lane_id()) - 1ull));
+        const uint32_t idx = base + (uint32_t)__popcll(m & lanemask_lt());
         if (idx < kMsgCap) {
             me.d[idx] = dst;
         } else {
@@ -332,19 +355,40 @@ __device__ __forceinline__ void msg_flush(MsgEmit<true>& me, uint32_t at, const 
 
 // ---- roots (level 0) ------------------------------------------------------------------------
 // Roots are resolved like ComputedExt.TryUseExisting (Internal/ComputedExt.cs:25-35): the
-// handle's current node, no tag check; immediately[i] selects Invalidate(true).
-__global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ roots,
-                                                  const uint8_t* __restrict__ imm, uint32_t n,
-                                                  uint32_t n_handles, unsigned long long* node, Out o,
-                                                  WaveCtr* ctr) {
+// handle's current node, no tag check. Global root ids; this device owns [base, base + n_range).
+// IMM = 1: only the roots with immediately[i] set (Invalidate(true) ignores the delay, so it can
+// change the node word; CAS on the word with the visit bit folded in), launched before IMM = 0,
+// which visits the other roots through the visit bitmap.
+template <int IMM>
+__global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ roots, const uint8_t* __restrict__ imm,
+                                                  uint32_t n, uint32_t base, uint32_t n_range, unsigned long long* node,
+                                                  uint32_t* vis, Out o, WaveCtr* ctr) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t win = 0, flagged = 0, h = 0;
     if (i < n) {
-        h = roots[i];
-        if (h < n_handles) {
-            const unsigned long long w = node[h];
+        h = roots[i] - base;
+        const bool is_imm = imm ? imm[i] != 0 : false;
+        if (h < n_range && is_imm == (IMM != 0)) {
+            unsigned long long w = node[h];
             if ((w & kVMask) != 0) {
-                const int r = visit_word(node + h, w, imm ? imm[i] != 0 : false);
+                int r = 0;
+                if (IMM) {
+                    const bool v = bit_of(vis, h);
+                    while (true) {
+                        const unsigned long long cw = v ? visited_word(w) : w;
+                        const unsigned long long nw = imm_word(cw);
+                        if (nw == cw) break;
+                        const unsigned long long prev = atomicCAS(node + h, w, nw);
+                        if (prev == w) {
+                            r = (word_state(nw) == FGI_INVALIDATED) ? 1 : 2;
+                            break;
+                        }
+                        w = prev;
+                    }
+                    if (r == 1) atomicOr(vis + (h >> 5), 1u << (h & 31));
+                } else {
+                    r = visit_bit(vis, h, w);
+                }
                 win = (r == 1);
                 flagged = (r == 2);
             }
@@ -357,6 +401,9 @@ __global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ r
 }
 
 // ---- frontier scan ----------------------------------------------------------------------------
+constexpr int kScanThreads = 512;   // threads per block of the collect / scan kernel (k_scan_apply)
+constexpr int kMaxWaves = kScanThreads / 64;
+
 __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, unsigned long long* s_red) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -379,47 +426,223 @@ __device__ __forceinline__ void scan_partial(uint64_t F, const uint32_t* __restr
     if (threadIdx.x == 0) partials[b] = s;
 }
 
-// multi-GPU levels: partial sums of the frontier's row lengths
+// ---- collect: a pull level's winners bitmap -> invalidated list (+ next frontier) -------------
+// The pull level counted its winners per tile (kPullTile slots; tile t = iteration * pgrid + block,
+// slots [it * pgrid * kPullTile + block * kPullTile, +kPullTile)). Pass 1 sums the tiles of every
+// block of the collect grid; pass 2 turns each tile's bitmap words into list entries at offsets
+// from those sums — deterministic, no atomics. Entries come out in tile order.
+struct CollectArgs {
+    const PullTile* __restrict__ tiles;
+    uint64_t n_tiles;
+    uint32_t pgrid, n_slots;
+    uint32_t* fb;                // winners bitmap of the pull level
+    int clear_fb;                // multi-GPU: the words are scratch, cleared after reading
+    const uint64_t* __restrict__ row_off;
+    const uint32_t* __restrict__ row_len;
+    uint32_t* inv;
+    uint64_t* fr_off;
+    uint32_t* fr_len;
+    uint64_t* escan;
+    uint32_t* cstart;
+    unsigned long long* part3;   // [3][G] pass-1 sums: winners, expandable winners, row lengths
+};
+
+__device__ __forceinline__ void collect_pass1(const CollectArgs& c, unsigned long long* s_red) {
+    const uint64_t b = blockIdx.x, G = gridDim.x;
+    const uint64_t lo = c.n_tiles * b / G, hi = c.n_tiles * (b + 1) / G;
+    unsigned long long w = 0, e = 0, l = 0;
+    for (uint64_t t = lo + threadIdx.x; t < hi; t += blockDim.x) {
+        const PullTile x = c.tiles[t];
+        w += x.w;
+        e += x.e;
+        l += x.len;
+    }
+    w = block_sum(w, s_red);
+    e = block_sum(e, s_red);
+    l = block_sum(l, s_red);
+    if (threadIdx.x == 0) {
+        c.part3[b] = w;
+        c.part3[G + b] = e;
+        c.part3[2 * G + b] = l;
+    }
+}
+
+// One tile by one wave: 16 bitmap words (1,024 slots); entries at bw (inv), be / bl (frontier
+// index / edge offset). write_fr: also the frontier entries, their scan and the chunk map.
+__device__ __forceinline__ void collect_tile(const CollectArgs& c, uint64_t t, uint64_t bw, uint64_t be, uint64_t bl,
+                                             bool write_fr) {
+    constexpr int kWords = kPullTile / 64;
+    const uint32_t lane = lane_id();
+    const uint64_t it = t / c.pgrid, bb = t % c.pgrid;
+    const uint64_t s0 = it * (uint64_t)c.pgrid * kPullTile + bb * kPullTile;
+    unsigned long long* fb64 = reinterpret_cast<unsigned long long*>(c.fb);
+    unsigned long long wd = 0;
+    if (lane < kWords && s0 + (uint64_t)lane * 64 < c.n_slots) {
+        wd = fb64[s0 / 64 + lane];
+        if (c.clear_fb && wd) fb64[s0 / 64 + lane] = 0ull;
+    }
+    unsigned long long bits[kWords];
+#pragma unroll
+    for (int r = 0; r < kWords; ++r) bits[r] = __shfl(wd, r, 64);
+    uint32_t rl[kWords];
+    uint64_t ro[kWords];
+#pragma unroll
+    for (int r = 0; r < kWords; ++r)
+        rl[r] = (write_fr && ((bits[r] >> lane) & 1ull)) ? c.row_len[s0 + r * 64 + lane] : 0u;
+#pragma unroll
+    for (int r = 0; r < kWords; ++r) ro[r] = rl[r] ? c.row_off[s0 + r * 64 + lane] : 0ull;
+#pragma unroll
+    for (int r = 0; r < kWords; ++r) {
+        if (!bits[r]) continue;   // uniform
+        const uint32_t slot = (uint32_t)(s0 + r * 64 + lane);
+        const bool bit = (bits[r] >> lane) & 1ull;
+        if (bit) c.inv[bw + __popcll(bits[r] & lanemask_lt())] = slot;
+        bw += __popcll(bits[r]);
+        if (!write_fr) continue;
+        const bool e = rl[r] != 0;
+        const unsigned long long me = __ballot(e);
+        const unsigned long long x = rl[r];
+        const unsigned long long incl = wave_incl_scan64(x);
+        if (e) {
+            const uint64_t idx = be + __popcll(me & lanemask_lt());
+            const uint64_t es = bl + incl - x;
+            c.fr_off[idx] = ro[r];
+            c.fr_len[idx] = rl[r];
+            c.escan[idx] = es;
+            const uint64_t c_lo = (es + kChunk - 1) / kChunk, c_hi = (es + x - 1) / kChunk;
+            for (uint64_t k = c_lo; k <= c_hi; ++k) c.cstart[k] = (uint32_t)idx;
+        }
+        be += __popcll(me);
+        bl += __shfl(incl, 63, 64);
+    }
+}
+
+// Pass 2 (kScanThreads-thread blocks, same grid as pass 1); block 0 publishes the level's totals.
+// single: the push/pull decision for this level is made here and the frontier list is written
+// only for a push; multi-GPU levels always write it (the drivers decide after an all-reduce).
+__device__ __forceinline__ void collect_pass2(const CollectArgs& c, LevelCtr& lc, WaveCtr* ctr, bool single,
+                                              int direction, uint64_t pull_threshold, uint32_t* fb_nxt,
+                                              uint64_t slot_words, unsigned long long* s_red) {
+    __shared__ unsigned long long s_w[kMaxWaves], s_e[kMaxWaves], s_l[kMaxWaves];
+    const uint64_t b = blockIdx.x, G = gridDim.x;
+    unsigned long long bw = 0, be = 0, bl = 0, tw = 0, te = 0, tl = 0;
+    for (uint64_t k = threadIdx.x; k < G; k += blockDim.x) {
+        const unsigned long long w = c.part3[k], e = c.part3[G + k], l = c.part3[2 * G + k];
+        tw += w;
+        te += e;
+        tl += l;
+        if (k < b) {
+            bw += w;
+            be += e;
+            bl += l;
+        }
+    }
+    bw = block_sum(bw, s_red);
+    be = block_sum(be, s_red);
+    bl = block_sum(bl, s_red);
+    tw = block_sum(tw, s_red);
+    te = block_sum(te, s_red);
+    tl = block_sum(tl, s_red);
+    const uint64_t inv_base = lc.mark_lo;   // set by pass 1's kernel
+    const bool pull = single && te != 0 && (direction == 2 || (direction == 0 && tl > pull_threshold));
+    const bool write_fr = !pull;
+    __syncthreads();   // block 0's threads have all read lc.mark_lo before thread 0 writes lc
+    if (b == 0 && threadIdx.x == 0) {
+        lc.F = te;
+        lc.T = tl;
+        lc.nchunks = (tl + kChunk - 1) / kChunk;
+        lc.pull = pull ? 1ull : 0ull;
+        lc.mark_hi = inv_base + tw;
+        ctr->inv = inv_base + tw;
+    }
+    // a push level after a pull: the next frontier bitmap (last written by the pull before) is
+    // cleared so a later push->pull switch marks into an empty one
+    if (single && !pull) {
+        const uint64_t nthr = G * blockDim.x;
+        for (uint64_t w = b * blockDim.x + threadIdx.x; w < slot_words; w += nthr) fb_nxt[w] = 0u;
+    }
+    const uint64_t lo = c.n_tiles * b / G, hi = c.n_tiles * (b + 1) / G;
+    const uint32_t W = blockDim.x >> 6, wid = threadIdx.x >> 6;
+    uint64_t rw = inv_base + bw, re = be, rl = bl;
+    for (uint64_t base = lo; base < hi; base += W) {   // block-uniform
+        const uint64_t t = base + wid;
+        PullTile x{0, 0, 0ull};
+        if (t < hi) x = c.tiles[t];
+        if (lane_id() == 0) {
+            s_w[wid] = x.w;
+            s_e[wid] = x.e;
+            s_l[wid] = x.len;
+        }
+        __syncthreads();
+        uint64_t ow = 0, oe = 0, ol = 0, aw = 0, ae = 0, al = 0;
+        for (uint32_t k = 0; k < W; ++k) {
+            if (k < wid) {
+                ow += s_w[k];
+                oe += s_e[k];
+                ol += s_l[k];
+            }
+            aw += s_w[k];
+            ae += s_e[k];
+            al += s_l[k];
+        }
+        __syncthreads();
+        if (t < hi && x.w != 0) collect_tile(c, t, rw + ow, re + oe, rl + ol, write_fr);
+        rw += aw;
+        re += ae;
+        rl += al;
+    }
+}
+
+// multi-GPU levels: partial sums of the frontier's row lengths, or collect pass 1 after a pull
 __global__ __launch_bounds__(kBlock) void k_scan_reduce(int L, const uint32_t* __restrict__ fr_len,
                                                         unsigned long long* __restrict__ partials,
-                                                        WaveCtr* ctr) {
+                                                        WaveCtr* ctr, CollectArgs ca) {
     __shared__ unsigned long long s_red[kBlock / 64];
+    if (L > 0 && ctr->lvl[(L + kRing - 1) % kRing].pull) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) ctr->lvl[L % kRing].mark_lo = ctr->inv;
+        collect_pass1(ca, s_red);
+        return;
+    }
     scan_partial(ctr->lvl[L % kRing].F, fr_len, partials, s_red);
 }
 
 // Single-GPU level prologue (one launch, grid kScanBlocks):
-//  - the push/pull decision for level L from the frontier totals F, T its producers accumulated;
-//  - bitmap upkeep for the previous level's winners inv[mark_hi(L-1), inv): winners of a push level
-//    (or the roots) are marked dead here, and into the frontier bitmap fb_cur if level L pulls;
-//    winners of a pull level were marked by the pull itself. fb_nxt (written by a pull at level
-//    L) is cleared when level L pushes, so a later push->pull switch finds it empty;
-//  - on push levels, the partial sums of the frontier's row lengths for k_scan_apply.
+//  - after a push level (or the roots): the push/pull decision for level L from the frontier
+//    totals F, T its producers accumulated; its winners inv[mark_hi(L-1), inv) are marked into the
+//    frontier bitmap fb_cur if level L pulls; fb_nxt is cleared when level L pushes, so a later
+//    push->pull switch finds it empty; partial sums of the frontier's row lengths on a push;
+//  - after a pull level: collect pass 1 (the decision follows in k_scan_apply).
 __global__ __launch_bounds__(kBlock) void k_level_begin(int L, WaveCtr* ctr, const uint32_t* __restrict__ inv,
-                                                        uint32_t* dead_bm, uint32_t* fb_cur, uint32_t* fb_nxt,
-                                                        uint64_t bm_words, uint64_t slot_words,
-                                                        const uint32_t* __restrict__ fr_len,
+                                                        uint32_t* fb_cur, uint32_t* fb_nxt, uint64_t bm_words,
+                                                        uint64_t slot_words, const uint32_t* __restrict__ fr_len,
                                                         unsigned long long* __restrict__ partials, int direction,
-                                                        uint64_t pull_threshold) {
+                                                        uint64_t pull_threshold, CollectArgs ca) {
     __shared__ unsigned long long s_red[kBlock / 64];
     LevelCtr& lc = ctr->lvl[L % kRing];
-    const uint64_t F = lc.F, T = lc.T;
-    const bool pull = F != 0 && (direction == 2 || (direction == 0 && T > pull_threshold));
-    const bool prev_pull = L > 0 && ctr->lvl[(L + kRing - 1) % kRing].pull != 0;
-    const uint64_t lo = L > 0 ? ctr->lvl[(L + kRing - 1) % kRing].mark_hi : 0ull;
-    const uint64_t hi = ctr->inv;
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    const bool prev_pull = L > 0 && ctr->lvl[(L + kRing - 1) % kRing].pull != 0;
+    if (prev_pull) {
+        if (tid == 0) lc.mark_lo = ctr->inv;
+        // words past the slots (detached handles) are never written by a pull: keep them zero
+        for (uint64_t w = slot_words + tid; w < bm_words; w += nthr) fb_nxt[w] = 0u;
+        collect_pass1(ca, s_red);
+        return;
+    }
+    const uint64_t F = lc.F, T = lc.T;
+    const bool pull = F != 0 && (direction == 2 || (direction == 0 && T > pull_threshold));
+    const uint64_t lo = L > 0 ? ctr->lvl[(L + kRing - 1) % kRing].mark_hi : 0ull;
+    const uint64_t hi = ctr->inv;
     if (tid == 0) {
         lc.pull = pull ? 1ull : 0ull;
         lc.nchunks = (T + kChunk - 1) / kChunk;
         lc.mark_lo = lo;
         lc.mark_hi = hi;
     }
-    if (!prev_pull) {
+    if (pull) {
         for (uint64_t i = lo + tid; i < hi; i += nthr) {
             const uint32_t h = inv[i];
-            atomicOr(dead_bm + (h >> 5), 1u << (h & 31));
-            if (pull) atomicOr(fb_cur + (h >> 5), 1u << (h & 31));
+            atomicOr(fb_cur + (h >> 5), 1u << (h & 31));
         }
     }
     // a pull at level L stores every slot word of fb_nxt; the words past the slots (detached
@@ -431,13 +654,19 @@ __global__ __launch_bounds__(kBlock) void k_level_begin(int L, WaveCtr* ctr, con
 // Exclusive scan of fr_len into escan; records for every chunk of kChunk edges the frontier
 // entry holding its first edge (cstart). decide = 1 (multi-GPU levels): also sets T, nchunks and
 // a push decision (the driver overrides it for pull levels); decide = 0: k_level_begin decided.
-__global__ __launch_bounds__(kBlock) void k_scan_apply(int L, const uint32_t* __restrict__ fr_len,
-                                                       const unsigned long long* __restrict__ partials,
-                                                       uint64_t* __restrict__ escan, uint32_t* __restrict__ cstart,
-                                                       WaveCtr* ctr, int decide) {
-    __shared__ unsigned long long s_red[kBlock / 64];
-    __shared__ unsigned long long s_wave[kBlock / 64];
+// After a pull level: collect pass 2 instead. kScanThreads-thread blocks.
+__global__ __launch_bounds__(kScanThreads) void k_scan_apply(int L, const uint32_t* __restrict__ fr_len,
+                                                     const unsigned long long* __restrict__ partials,
+                                                     uint64_t* __restrict__ escan, uint32_t* __restrict__ cstart,
+                                                     WaveCtr* ctr, int decide, CollectArgs ca, int direction,
+                                                     uint64_t pull_threshold, uint32_t* fb_nxt, uint64_t slot_words) {
+    __shared__ unsigned long long s_red[kMaxWaves];
+    __shared__ unsigned long long s_wave[kMaxWaves];
     LevelCtr& lc = ctr->lvl[L % kRing];
+    if (L > 0 && ctr->lvl[(L + kRing - 1) % kRing].pull) {
+        collect_pass2(ca, lc, ctr, !decide, direction, pull_threshold, fb_nxt, slot_words, s_red);
+        return;
+    }
     const uint64_t F = lc.F;
     if (!decide && (lc.pull || F == 0)) return;
     const uint64_t b = blockIdx.x, G = gridDim.x;
@@ -488,31 +717,53 @@ __global__ __launch_bounds__(kBlock) void k_scan_apply(int L, const uint32_t* __
 }
 
 // ---- multi-GPU bitmaps ------------------------------------------------------------------------
-// Nodes that won Consistent -> Invalidated since the last mark become dead (and frontier, on pull
-// levels). The range [marked, inv) is exactly the previous level's winners.
-__global__ __launch_bounds__(kBlock) void k_mark(int L, const uint32_t* __restrict__ inv, uint32_t* dead_bm,
-                                                 uint32_t* front_bm, WaveCtr* ctr) {
+// The previous level's winners (pushed, received or collected after a pull: the range [marked,
+// inv)) become the frontier bitmap of a pull level.
+__global__ __launch_bounds__(kBlock) void k_mark(int L, const uint32_t* __restrict__ inv, uint32_t* front_bm,
+                                                 WaveCtr* ctr) {
     LevelCtr& lc = ctr->lvl[L % kRing];
     const uint64_t lo = ctr->marked, hi = ctr->inv;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         lc.mark_lo = lo;
         lc.mark_hi = hi;
     }
-    const bool front = lc.pull != 0;
+    if (!lc.pull) return;
     for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t h = inv[i];
-        atomicOr(dead_bm + (h >> 5), 1u << (h & 31));
-        if (front) atomicOr(front_bm + (h >> 5), 1u << (h & 31));
+        atomicOr(front_bm + (h >> 5), 1u << (h & 31));
+    }
+}
+
+// Tile totals of a pull level into the next level's F and T, and its winner count into pad0
+// (winners still to be collected into the invalidated list; one block).
+__device__ __forceinline__ void tile_totals(const PullTile* __restrict__ tiles, uint64_t n_tiles, LevelCtr& ln,
+                                            unsigned long long* s_red) {
+    unsigned long long w = 0, e = 0, l = 0;
+    for (uint64_t t = threadIdx.x; t < n_tiles; t += blockDim.x) {
+        w += tiles[t].w;
+        e += tiles[t].e;
+        l += tiles[t].len;
+    }
+    w = block_sum(w, s_red);
+    e = block_sum(e, s_red);
+    l = block_sum(l, s_red);
+    if (threadIdx.x == 0) {
+        ln.F = e;
+        ln.T = l;
+        ln.pad0 = w;
     }
 }
 
 __global__ __launch_bounds__(kBlock) void k_clear_front(int L, const uint32_t* __restrict__ inv, uint32_t* front_bm,
-                                                        WaveCtr* ctr) {
+                                                        WaveCtr* ctr, const PullTile* __restrict__ tiles,
+                                                        uint64_t n_tiles) {
+    __shared__ unsigned long long s_red[kBlock / 64];
     LevelCtr& lc = ctr->lvl[L % kRing];
     const uint64_t lo = lc.mark_lo, hi = lc.mark_hi;
     if (blockIdx.x == 0 && threadIdx.x == 0) ctr->marked = hi;
     if (!lc.pull) return;
+    if (blockIdx.x == 0) tile_totals(tiles, n_tiles, ctr->lvl[(L + 1) % kRing], s_red);
     for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
          i += (uint64_t)gridDim.x * blockDim.x)
         front_bm[inv[i] >> 5] = 0u;   // every set bit of the word belongs to this level's frontier
@@ -535,16 +786,15 @@ struct ExpandArgs {
     const uint32_t* __restrict__ cstart;
     const uint32_t* __restrict__ pool_col;
     const uint64_t* __restrict__ pool_tag;
-    const uint32_t* __restrict__ dead_bm;
     int dead_filter;
 };
 
 // PART: multi-GPU rank — dependant slots outside [ra.base, ra.base + ra.n_local) are remote: their
 // tag is checked against the version replica and matching targets are forwarded once per wave.
 template <bool PART>
-__device__ __forceinline__ void expand_level(const LevelCtr& lc, const ExpandArgs& x, unsigned long long* node,
-                                             const Out& o, Emit& em, uint32_t* eb, MsgEmit<PART>& me, uint32_t* s_rel,
-                                             uint32_t* s_base, unsigned long long* blk,
+__device__ __forceinline__ void expand_level(const LevelCtr& lc, const ExpandArgs& x, const unsigned long long* node,
+                                             uint32_t* vis, const Out& o, Emit& em, uint32_t* eb, MsgEmit<PART>& me,
+                                             uint32_t* s_rel, uint32_t* s_base, unsigned long long* blk,
                                              unsigned long long (*s_st)[kStats], const RemoteArgs& ra) {
     if constexpr (PART) {
         if (threadIdx.x == 0) me.n = 0;
@@ -599,11 +849,12 @@ __device__ __forceinline__ void expand_level(const LevelCtr& lc, const ExpandArg
             for (int j = 0; j < kEPT; ++j)
                 if (dst[j] != 0xFFFFFFFFu) dst[j] -= ra.base;   // local handle
         }
-        // edges to nodes invalidated in an earlier level need neither the tag nor the gather
+        // edges to nodes visited earlier need neither the tag nor the gather (the bitmap is read
+        // without synchronisation: a stale 0 only costs the gather and an atomic that finds the bit)
         if (x.dead_filter) {
 #pragma unroll
             for (int j = 0; j < kEPT; ++j)
-                if (dst[j] != 0xFFFFFFFFu && bit_of(x.dead_bm, dst[j])) dst[j] = 0xFFFFFFFFu;
+                if (dst[j] != 0xFFFFFFFFu && bit_of(vis, dst[j])) dst[j] = 0xFFFFFFFFu;
         }
         uint64_t tag[kEPT];
         unsigned long long w[kEPT];
@@ -621,7 +872,7 @@ __device__ __forceinline__ void expand_level(const LevelCtr& lc, const ExpandArg
         for (int j = 0; j < kEPT; ++j) {
             if (tag[j] != 0 && (w[j] & kVMask) == tag[j]) {
                 ++matched;
-                const int r = visit_word(node + dst[j], w[j], false);
+                const int r = visit_bit(vis, dst[j], w[j]);
                 if (r == 1) win_mask |= 1u << j;
                 else if (r == 2) ++flagged;
             }
@@ -647,200 +898,231 @@ struct PullArgs {
     const uint32_t* __restrict__ uin_len;
     const uint32_t* __restrict__ uin_src;
     const uint64_t* __restrict__ uin_head;   // first two list entries (lo | hi << 32)
+    const uint32_t* __restrict__ uin_more;   // bitmap: the list has more than two entries
     const uint32_t* __restrict__ front_rd;   // frontier bitmap (handles; multi-GPU: global ids)
-    uint32_t* front_wr;                      // single GPU: next frontier bitmap, stored whole
-    uint32_t* dead_bm;
+    uint32_t* front_wr;                      // this level's winners, stored whole per tile
+    const uint32_t* __restrict__ cls;        // expandable-class bitmap
+    const uint32_t* __restrict__ row_len;
+    PullTile* tiles;
 };
 
-// Each wave owns kPS x 64 consecutive slots (2 x kPS bitmap words); a lane handles kPS slots 64
-// apart, so every step issues kPS independent loads (dead word, head, frontier bit, node word, CAS)
-// per lane. A live slot probes the two heads of its list first (lists are ordered so that the
-// entries a wave reaches earliest come first), then the next kPullCap entries of a list that
-// missed (4 loads in flight), and the rest of a longer list with the whole wave. The
-// wave stores its winners' dead bits and next-frontier words itself — no atomics, no marking pass.
-constexpr uint32_t kPS = 4;
-#ifndef FGI_DIAG
-#define FGI_DIAG 0   // instrumented builds only (make diag): bits switch parts of the pull off
-#endif
-constexpr uint32_t kPullEmitCap = 2048;   // staged in the expand LDS array s_base (8 KB)
+// A block owns tile (it, block) of every iteration: kPullTile consecutive slots, kPS per lane
+// (64 apart), so a lane issues kPS independent loads of each kind. Per slot: the visit, class and
+// "more" bitmap words (one 64-bit word per 64 slots), the two list heads and the row length, all
+// unconditional and coalesced; then the frontier bits of the heads (L2); a hit is a visit. The
+// wave's visits and wins go to LDS as 64-bit ballot words; slots whose heads missed but whose
+// list goes on are queued in LDS and scanned at the flush by 8-lane groups (8 entries per probe
+// step, early exit). The flush (every kMaxIter iterations and at the end) writes the owned
+// visit and frontier words and the per-tile counts — a pull level does no global atomics.
+constexpr uint32_t kPS = kPullTile / kBlock;
+constexpr uint32_t kMaxIter = 16;           // iterations buffered in LDS between flushes
+constexpr uint32_t kTailCap = kChunk;       // queued slots (s_rel)
+constexpr uint32_t kTileWords = kPullTile / 64;
+static_assert(kPS == 4 && kTileWords == 16, "pull geometry");
 
-__device__ __forceinline__ bool probe_tail(const PullArgs& p, uint64_t off, uint32_t len, uint32_t& examined) {
-    const uint32_t lim = len < kPullCap ? len : kPullCap;
-    bool hit = false;
-    for (uint32_t k = 0; k < lim && !hit; k += 4) {
-        uint32_t u[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) u[j] = (k + j < lim) ? p.uin_src[off + k + j] : FGI_NONE;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (u[j] != FGI_NONE) {
-                ++examined;
-                hit |= bit_of(p.front_rd, u[j]);
+__device__ __forceinline__ void pull_flush(const PullArgs& p, const unsigned long long* node, uint32_t* vis,
+                                           uint32_t it_base, uint32_t nbuf, const uint32_t* q, uint32_t nq,
+                                           unsigned long long* s_vm, unsigned long long* s_wm, uint32_t* s_cw,
+                                           uint32_t* s_ce, unsigned long long* s_cl, uint32_t& flagged,
+                                           uint32_t& examined, uint32_t& wins, uint32_t& tails) {
+    const uint64_t stride = (uint64_t)gridDim.x * kPullTile;
+    const uint32_t lane = lane_id(), sub = lane & 7, grp = threadIdx.x >> 3;
+    __syncthreads();
+    // queued slots: 8 lanes per slot, entries 2.. of its list
+    for (uint32_t e = grp; e < nq; e += blockDim.x / 8) {
+        const uint32_t d = q[e];
+        const uint32_t len = p.uin_len[d];
+        const uint64_t off = p.uin_off[d];
+        bool found = false;
+        for (uint32_t r = 2; r < len && !found; r += 8) {   // group-uniform
+            const uint32_t i = r + sub;
+            const bool x = i < len && bit_of(p.front_rd, p.uin_src[off + i]);
+            examined += (i < len) ? 1u : 0u;
+            found = ((__ballot(x) >> (lane & ~7u)) & 0xFFull) != 0;
+        }
+        if (found && sub == 0) {
+            const uint64_t it = d / stride;
+            const uint32_t k = (uint32_t)(it - it_base);
+            const uint32_t wq = (uint32_t)((d - it * stride - (uint64_t)blockIdx.x * kPullTile) >> 6);
+            const unsigned long long bit = 1ull << (d & 63);
+            atomicOr(&s_vm[k * kTileWords + wq], bit);
+            if (bit_of(p.cls, d)) {
+                atomicOr(&s_wm[k * kTileWords + wq], bit);
+                const uint32_t rl = p.row_len[d];
+                atomicAdd(&s_cw[k], 1u);
+                if (rl) {
+                    atomicAdd(&s_ce[k], 1u);
+                    atomicAdd(&s_cl[k], (unsigned long long)rl);
+                }
+                ++wins;
+            } else {
+                flagged += first_visit(node[d]) == 2 ? 1u : 0u;
             }
         }
+        tails += sub == 0 ? 1u : 0u;
     }
-    return hit;
+    __syncthreads();
+    unsigned long long* vis64 = reinterpret_cast<unsigned long long*>(vis);
+    unsigned long long* fw64 = reinterpret_cast<unsigned long long*>(p.front_wr);
+    for (uint32_t i = threadIdx.x; i < nbuf * kTileWords; i += blockDim.x) {
+        const uint32_t k = i / kTileWords, wq = i % kTileWords;
+        const uint64_t s = (it_base + k) * stride + (uint64_t)blockIdx.x * kPullTile + (uint64_t)wq * 64;
+        if (s < p.n_slots) {
+            const unsigned long long vm = s_vm[i];
+            if (vm) vis64[s >> 6] |= vm;   // the block owns these words during the level
+            fw64[s >> 6] = s_wm[i];
+        }
+    }
+    for (uint32_t k = threadIdx.x; k < nbuf; k += blockDim.x) {
+        p.tiles[(uint64_t)(it_base + k) * gridDim.x + blockIdx.x] = PullTile{s_cw[k], s_ce[k], s_cl[k]};
+        s_cw[k] = 0;
+        s_ce[k] = 0;
+        s_cl[k] = 0;
+    }
+    __syncthreads();
 }
 
-__device__ __forceinline__ void pull_level(const PullArgs& p, unsigned long long* node, const Out& o, Emit& em,
-                                           uint32_t* eb, unsigned long long* blk, unsigned long long (*s_st)[kStats]) {
-    uint32_t flagged = 0, cand = 0, examined = 0, live = 0, wins = 0, tails = 0;
-    const uint32_t lane = lane_id();
-    const uint32_t per_block = kBlock * kPS;
-    const uint32_t stride = gridDim.x * per_block;
-    const uint32_t n_iter = (p.n_slots + stride - 1) / stride;   // uniform trip count: flushes are block-wide
-    for (uint32_t it = 0; it < n_iter; ++it) {
-        const uint32_t d0 = it * stride + blockIdx.x * per_block + (threadIdx.x >> 6) * (64 * kPS);
-        uint32_t d[kPS];
-        uint64_t hd[kPS];
-        bool lv[kPS], hit[kPS], long_rest[kPS];
-#pragma unroll
-        for (int j = 0; j < (int)kPS; ++j) {
-            d[j] = d0 + j * 64 + lane;
-            const uint32_t dw = d[j] < p.n_slots ? p.dead_bm[d[j] >> 5] : 0xFFFFFFFFu;
-            lv[j] = d[j] < p.n_slots && !((dw >> (d[j] & 31)) & 1u);
-        }
-        constexpr uint64_t kNoHeads = ((uint64_t)FGI_NONE << 32) | FGI_NONE;
-#pragma unroll
-        for (int j = 0; j < (int)kPS; ++j)
-            hd[j] = lv[j] ? ((FGI_DIAG & 32) ? (uint64_t)((d[j] * 2654435761u) % p.n_slots) | ((uint64_t)FGI_NONE << 32)
-                                             : p.uin_head[d[j]])
-                          : kNoHeads;
-#pragma unroll
-        for (int j = 0; j < (int)kPS; ++j) {
-            live += lv[j] ? 1u : 0u;
-            hit[j] = false;
-            long_rest[j] = false;
-            const uint32_t h0 = (uint32_t)hd[j], h1 = (uint32_t)(hd[j] >> 32);
-            if (h0 != FGI_NONE) {
-                ++cand;
-                ++examined;
-                if (FGI_DIAG & 16) {
-                    hit[j] = ((h0 * 2654435761u) >> 31) != 0;
-                } else {
-                    const bool b0 = bit_of(p.front_rd, h0);
-                    const bool b1 = h1 != FGI_NONE && bit_of(p.front_rd, h1);
-                    examined += (!b0 && h1 != FGI_NONE) ? 1u : 0u;
-                    hit[j] = b0 || b1;
-                }
-            }
-        }
-        // both heads missed: the next kPullCap entries of the list, then the whole wave on the rest
-#pragma unroll
-        for (int j = 0; j < (int)kPS && !(FGI_DIAG & 4); ++j) {
-            uint32_t len = 0;
-            uint64_t off = 0;
-            if ((uint32_t)hd[j] != FGI_NONE && !hit[j]) {
-                len = p.uin_len[d[j]];
-                if (len > 2) {
-                    off = p.uin_off[d[j]];
-                    ++tails;
-                    hit[j] = probe_tail(p, off + 2, len - 2, examined);
-                    long_rest[j] = !hit[j] && len > 2 + kPullCap;
-                }
-            }
-            unsigned long long lm = __ballot(long_rest[j]);
-            while (lm) {
-                const int l = __ffsll((long long)lm) - 1;
-                lm &= lm - 1;
-                const uint64_t lo = __shfl(off, l, 64);
-                const uint32_t ln = __shfl(len, l, 64);
-                bool f = false;
-                for (uint32_t b = 2 + kPullCap; b < ln && !f; b += 64) {
-                    const uint32_t k = b + lane;
-                    const bool x = k < ln && bit_of(p.front_rd, p.uin_src[lo + k]);
-                    examined += (k < ln) ? 1u : 0u;
-                    f = __ballot(x) != 0;
-                }
-                if ((int)lane == l) hit[j] = f;
-            }
-        }
-        unsigned long long w[kPS];
-#pragma unroll
-        for (int j = 0; j < (int)kPS; ++j) w[j] = (hit[j] && !(FGI_DIAG & 2)) ? node[d[j]] : 0ull;
-        bool win[kPS];
-#pragma unroll
-        for (int j = 0; j < (int)kPS; ++j) {
-            win[j] = (FGI_DIAG & 2) ? hit[j] : false;
-            if (hit[j] && !(FGI_DIAG & 2)) {
-                const int r = visit_word(node + d[j], w[j], false);
-                win[j] = (r == 1);
-                flagged += (r == 2);
-            }
-            wins += win[j] ? 1u : 0u;
-        }
-        if (p.front_wr && !(FGI_DIAG & 8)) {
-#pragma unroll
-            for (int j = 0; j < (int)kPS; ++j) {
-                const unsigned long long wm = __ballot(win[j]);
-                const uint32_t u0 = d0 + j * 64;
-                if (lane == 0 && u0 < p.n_slots) {
-                    unsigned long long* dp = reinterpret_cast<unsigned long long*>(p.dead_bm) + (u0 >> 6);
-                    if (wm) *dp |= wm;
-                    reinterpret_cast<unsigned long long*>(p.front_wr)[u0 >> 6] = wm;
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < (int)kPS; ++j) emit_push<kPullEmitCap>(em, eb, (FGI_DIAG & 1) ? false : win[j], d[j], o);
-        // at most kPS x kBlock winners per step
-        emit_flush<kPullEmitCap>(em, eb, kPullEmitCap - kPS * kBlock, o);
+__device__ __forceinline__ void pull_level(const PullArgs& p, const unsigned long long* node, uint32_t* vis,
+                                           uint32_t* lds_q, unsigned long long* lds_buf, unsigned long long* blk,
+                                           unsigned long long (*s_st)[kStats]) {
+    uint32_t flagged = 0, cand = 0, examined = 0, live = 0, wins = 0, tails = 0, examined_tail = 0, wins_tail = 0;
+    const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
+    const uint64_t stride = (uint64_t)gridDim.x * kPullTile;
+    const uint32_t n_iter = (uint32_t)pull_iters(p.n_slots, gridDim.x);
+    unsigned long long* s_vm = lds_buf;                                   // [kMaxIter][16]
+    unsigned long long* s_wm = s_vm + kMaxIter * kTileWords;              // [kMaxIter][16]
+    unsigned long long* s_cl = s_wm + kMaxIter * kTileWords;              // [kMaxIter]
+    uint32_t* s_cw = reinterpret_cast<uint32_t*>(s_cl + kMaxIter);        // [kMaxIter]
+    uint32_t* s_ce = s_cw + kMaxIter;                                     // [kMaxIter]
+    uint32_t* s_qn = s_ce + kMaxIter;
+    if (threadIdx.x < kMaxIter) {
+        s_cw[threadIdx.x] = 0;
+        s_ce[threadIdx.x] = 0;
+        s_cl[threadIdx.x] = 0;
     }
-    emit_flush<kPullEmitCap>(em, eb, 1, o);
+    if (threadIdx.x == 0) *s_qn = 0;
+    __syncthreads();
+    constexpr uint64_t kNoHeads = ~0ull;
+    uint32_t it_base = 0;
+    for (uint32_t it = 0; it < n_iter; ++it) {
+        const uint32_t k = it - it_base;
+        const uint64_t s0 = (uint64_t)it * stride + (uint64_t)blockIdx.x * kPullTile;
+        const uint64_t d0 = s0 + wid * (64 * kPS);
+        // bitmap words are loaded per lane as the 32-bit word holding the lane's bit (the two
+        // halves of a wave read two addresses; 64-bit words would cost twice the registers)
+        uint32_t vw[kPS], cw[kPS], mw[kPS], rl[kPS];
+        uint64_t hd[kPS];
+#pragma unroll
+        for (int j = 0; j < (int)kPS; ++j) {
+            const uint64_t d = d0 + j * 64 + lane;
+            const bool in = d < p.n_slots;
+            vw[j] = in ? vis[d >> 5] : ~0u;
+            cw[j] = in ? p.cls[d >> 5] : 0u;
+            mw[j] = in ? p.uin_more[d >> 5] : 0u;
+            hd[j] = in ? __builtin_nontemporal_load(p.uin_head + d) : kNoHeads;
+            rl[j] = in ? p.row_len[d] : 0u;
+        }
+        bool hit[kPS], tail[kPS];
+#pragma unroll
+        for (int j = 0; j < (int)kPS; ++j) {
+            const uint64_t d = d0 + j * 64 + lane;
+            const bool lv = d < p.n_slots && !((vw[j] >> (lane & 31)) & 1u);
+            const uint32_t h0 = (uint32_t)hd[j], h1 = (uint32_t)(hd[j] >> 32);
+            const bool c = lv && h0 != FGI_NONE;
+            bool b0 = false, b1 = false;
+            if (c) {
+                b0 = bit_of(p.front_rd, h0);
+                b1 = h1 != FGI_NONE && bit_of(p.front_rd, h1);
+            }
+            // statistics as wave-uniform counts (scalar registers), reported by lane 0
+            live += (uint32_t)__popcll(__ballot(lv));
+            cand += (uint32_t)__popcll(__ballot(c));
+            examined += (uint32_t)__popcll(__ballot(c)) + (uint32_t)__popcll(__ballot(c && h1 != FGI_NONE && !b0));
+            hit[j] = b0 || b1;
+            tail[j] = c && !hit[j] && ((mw[j] >> (lane & 31)) & 1u);
+        }
+        uint32_t nw = 0, ne = 0;
+        unsigned long long nl = 0;
+        uint32_t q_end = 0;
+#pragma unroll
+        for (int j = 0; j < (int)kPS; ++j) {
+            const uint64_t d = d0 + j * 64 + lane;
+            const bool win = hit[j] && ((cw[j] >> (lane & 31)) & 1u);
+            if (hit[j] && !win) flagged += first_visit(node[d]) == 2 ? 1u : 0u;
+            const unsigned long long vm = __ballot(hit[j]), wm = __ballot(win);
+            if (lane == 0) {
+                s_vm[k * kTileWords + wid * kPS + j] = vm;
+                s_wm[k * kTileWords + wid * kPS + j] = wm;
+            }
+            nw += (uint32_t)__popcll(wm);
+            ne += (uint32_t)__popcll(__ballot(win && rl[j]));
+            nl += win ? rl[j] : 0u;
+            const unsigned long long tm = __ballot(tail[j]);
+            if (tm) {
+                uint32_t qb = 0;
+                if (lane == 0) qb = atomicAdd(s_qn, (uint32_t)__popcll(tm));
+                qb = __shfl(qb, 0, 64);
+                if (tail[j]) lds_q[qb + __popcll(tm & lanemask_lt())] = (uint32_t)d;
+                q_end = qb + (uint32_t)__popcll(tm);
+            }
+        }
+        wins += nw;
+        nl = wave_sum64(nl);
+        if (lane == 0) {
+            if (nw) atomicAdd(&s_cw[k], nw);
+            if (ne) atomicAdd(&s_ce[k], ne);
+            if (nl) atomicAdd(&s_cl[k], nl);
+        }
+        // flush when the LDS buffers are full, the queue could overflow next time, or at the end
+        const bool full = k + 1 == kMaxIter || it + 1 == n_iter;
+        if (__syncthreads_or(full || q_end > kTailCap - kPullTile)) {
+            const uint32_t nq = *s_qn;
+            pull_flush(p, node, vis, it_base, k + 1, lds_q, nq, s_vm, s_wm, s_cw, s_ce, s_cl, flagged, examined_tail,
+                       wins_tail, tails);
+            if (threadIdx.x == 0) *s_qn = 0;
+            __syncthreads();
+            it_base = it + 1;
+        }
+    }
     const uint32_t scan = (blockIdx.x == 0 && threadIdx.x == 0) ? p.n_slots : 0u;
-    const uint32_t v[kStats] = {0, flagged, cand, examined, live, wins, tails, scan};
+    // cand, live, wins and the head probes of `examined` are wave-uniform counts; the tail probes
+    // and flag counts are per lane
+    const bool l0 = lane == 0;
+    const uint32_t v[kStats] = {0, flagged, l0 ? cand : 0u, examined_tail + (l0 ? examined : 0u), l0 ? live : 0u,
+                                wins_tail + (l0 ? wins : 0u), tails, scan};
     block_stats_add(blk, s_st, v);
 }
 
 // One level's traversal: push (expand) or pull, as decided for the level on the device.
 template <bool PART>
-__global__ __launch_bounds__(kBlock) void k_level(int L, ExpandArgs x, PullArgs p, unsigned long long* node, Out o,
-                                                  WaveCtr* ctr, unsigned long long* blk, RemoteArgs ra) {
+__global__ __launch_bounds__(kBlock, 6) void k_level(int L, ExpandArgs x, PullArgs p, const unsigned long long* node,
+                                                  uint32_t* vis, Out o, WaveCtr* ctr, unsigned long long* blk,
+                                                  RemoteArgs ra) {
     __shared__ uint32_t s_rel[kChunk + 1];
-    __shared__ uint32_t s_base[kChunk + 1];
+    __shared__ __align__(16) uint32_t s_base[kChunk + 2];
     __shared__ Emit em;
     __shared__ uint32_t eb[kEmitCap];
     __shared__ MsgEmit<PART> me;
     __shared__ unsigned long long s_st[kBlock / 64][kStats];
-    static_assert(kChunk + 1 >= kPullEmitCap, "pull staging");
+    static_assert((2 * kMaxIter * kTileWords + kMaxIter) * 8 + 3 * kMaxIter * 4 + 4 <= (kChunk + 2) * 4, "pull LDS");
     const LevelCtr& lc = ctr->lvl[L % kRing];
     o.ln = &ctr->lvl[(L + 1) % kRing];
     if (blockIdx.x == 0 && threadIdx.x < sizeof(LevelCtr) / 8)
         reinterpret_cast<unsigned long long*>(&ctr->lvl[(L + 2) % kRing])[threadIdx.x] = 0ull;
     // multi-GPU pull levels run on every rank (parents may be remote); otherwise no frontier, no work
     if (!lc.pull && lc.F == 0) return;
-    emit_init(em);
-    if (lc.pull) pull_level(p, node, o, em, s_base, blk, s_st);
-    else expand_level<PART>(lc, x, node, o, em, eb, me, s_rel, s_base, blk, s_st, ra);
-}
-
-// multi-GPU roots: every rank gets the global list and visits the slots it owns
-__global__ __launch_bounds__(kBlock) void k_part_roots(const uint32_t* __restrict__ roots, const uint8_t* __restrict__ imm,
-                                                       uint32_t n, uint32_t base, uint32_t n_local,
-                                                       unsigned long long* node, Out o, WaveCtr* ctr) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t win = 0, flagged = 0, h = 0;
-    if (i < n) {
-        h = roots[i] - base;
-        if (h < n_local) {
-            const unsigned long long w = node[h];
-            if ((w & kVMask) != 0) {
-                const int r = visit_word(node + h, w, imm ? imm[i] != 0 : false);
-                win = (r == 1);
-                flagged = (r == 2);
-            }
-        }
+    if (lc.pull) {
+        pull_level(p, node, vis, s_rel, reinterpret_cast<unsigned long long*>(s_base), blk, s_st);
+    } else {
+        emit_init(em);
+        expand_level<PART>(lc, x, node, vis, o, em, eb, me, s_rel, s_base, blk, s_st, ra);
     }
-    emit_one(win, h, o);
-    const uint32_t fs = wave_sum(flagged), ws = wave_sum(win);
-    if (lane_id() == 0 && fs) atomicAdd(&ctr->root_flagged, (unsigned long long)fs);
-    if (lane_id() == 0 && ws) atomicAdd(&ctr->root_inv, (unsigned long long)ws);
 }
 
 // multi-GPU: apply the targets other ranks forwarded (their versions were checked by the sender)
 __global__ __launch_bounds__(kBlock) void k_apply_recv(int L, uint64_t n, const uint32_t* __restrict__ recv, uint32_t base,
-                                                       unsigned long long* node, Out o, WaveCtr* ctr,
-                                                       unsigned long long* blk) {
+                                                       const unsigned long long* node, uint32_t* vis, Out o,
+                                                       WaveCtr* ctr, unsigned long long* blk) {
     __shared__ unsigned long long s_st[kBlock / 64][kStats];
     __shared__ Emit em;
     __shared__ uint32_t eb[kEmitCap];
@@ -857,7 +1139,7 @@ __global__ __launch_bounds__(kBlock) void k_apply_recv(int L, uint64_t n, const 
             h = recv[i] - base;
             const unsigned long long w = node[h];
             if ((w & kVMask) != 0) {
-                const int r = visit_word(node + h, w, false);
+                const int r = visit_bit(vis, h, w);
                 win = (r == 1);
                 flagged += (r == 2);
             }
@@ -870,30 +1152,117 @@ __global__ __launch_bounds__(kBlock) void k_apply_recv(int L, uint64_t n, const 
     block_stats_add(blk, s_st, v);
 }
 
-// Folds the per-block statistics rows into the wave counters (one block; idempotent, so it can
-// run after every level group).
-__global__ __launch_bounds__(kBlock) void k_stats_reduce(const unsigned long long* __restrict__ blk, WaveCtr* ctr) {
+// Folds the per-block statistics into the wave counters: one block per column (coalesced sweeps).
+// Block kStats: if level L_next follows a pull level, its F and T from the pull's tiles (the host
+// reads them to decide termination before k_level_begin(L_next) has run).
+__global__ __launch_bounds__(kBlock) void k_stats_reduce(const unsigned long long* __restrict__ blk, WaveCtr* ctr,
+                                                         int L_next, const PullTile* __restrict__ tiles,
+                                                         uint64_t n_tiles) {
     __shared__ unsigned long long s_red[kBlock / 64];
+    const int k = blockIdx.x;
+    if (k == kStats) {
+        if (L_next > 0 && ctr->lvl[(L_next + kRing - 1) % kRing].pull)
+            tile_totals(tiles, n_tiles, ctr->lvl[L_next % kRing], s_red);
+        return;
+    }
     unsigned long long* dst[kStats] = {&ctr->e_match,   &ctr->n_flagged, &ctr->pull_cand, &ctr->pull_edges,
                                        &ctr->pull_live, &ctr->pull_win,  &ctr->pull_tail, &ctr->pull_scan};
-    for (int k = 0; k < kStats; ++k) {
-        unsigned long long t = 0;
-        for (uint32_t b = threadIdx.x; b < kStatBlocks; b += blockDim.x) t += blk[(uint64_t)b * kStats + k];
-        t = block_sum(t, s_red);
-        if (threadIdx.x == 0) *dst[k] = t + (k == kStFlagged ? ctr->root_flagged : 0ull);
+    const unsigned long long* col = blk + (uint64_t)k * kStatBlocks;
+    unsigned long long t = 0;
+#pragma unroll
+    for (uint32_t b = 0; b < kStatBlocks / kBlock; ++b) t += col[b * kBlock + threadIdx.x];
+    t = block_sum(t, s_red);
+    if (threadIdx.x == 0) *dst[k] = t + (k == kStFlagged ? ctr->root_flagged : 0ull);
+}
+
+// ---- fold / class bitmap -----------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_fold(uint32_t n, const uint32_t* __restrict__ vis,
+                                                 unsigned long long* node) {
+    for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n; h += (uint64_t)gridDim.x * blockDim.x)
+        if (bit_of(vis, (uint32_t)h)) node[h] = visited_word(node[h]);
+}
+
+__global__ __launch_bounds__(kBlock) void k_build_cls(uint32_t n, const unsigned long long* __restrict__ node,
+                                                      unsigned long long* cls64) {
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t lim = ((uint64_t)n + 63) / 64 * 64;
+    for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < lim; h += nthr) {
+        bool c = false;
+        if (h < n) {
+            const unsigned long long w = node[h];
+            c = (w & kVMask) != 0 && word_state(w) == FGI_CONSISTENT && !(w & kW_HasDelay);
+        }
+        const unsigned long long m = __ballot(c);
+        if (lane_id() == 0) cls64[h >> 6] = m;
     }
 }
 
 }  // namespace
 
-// Algorithmic bytes of the pull levels of a wave (k_level on pull levels): per slot scanned the
-// dead-bitmap read and the next-frontier store (1/8 B each); per live slot its head (4 B); per
-// head miss the list's offset and length (12 B) and 4 B per further dependency examined (the
-// frontier-bitmap probes hit L2 and are not counted); per winner CAS 8 + row gathers 12 + list
-// write 4 + frontier entry 12.
+fgi_status fold(fgi_graph* g) {
+    if (!g->v_dirty) return FGI_OK;
+    const uint32_t H = g->n_handles;
+    hipLaunchKernelGGL(k_fold, dim3(std::min<uint32_t>((H + kBlock - 1) / kBlock, 8192)), dim3(kBlock), 0, g->stream, H,
+                       g->vis_bm, reinterpret_cast<unsigned long long*>(g->node));
+    FGI_HIP(g, hipGetLastError());
+    FGI_HIP(g, hipMemsetAsync(g->vis_bm, 0, g->bm_words * 4, g->stream));
+    g->v_dirty = false;
+    note_words(g);
+    return FGI_OK;
+}
+
+fgi_status ensure_cls(fgi_graph* g) {
+    if (g->cls_valid) return FGI_OK;
+    const uint32_t H = g->n_handles;
+    hipLaunchKernelGGL(k_build_cls, dim3(std::min<uint32_t>((H + kBlock - 1) / kBlock + 1, 8192)), dim3(kBlock), 0,
+                       g->stream, H, reinterpret_cast<const unsigned long long*>(g->node),
+                       reinterpret_cast<unsigned long long*>(g->cls_bm));
+    FGI_HIP(g, hipGetLastError());
+    g->cls_valid = true;
+    return FGI_OK;
+}
+
+// Algorithmic bytes of the pull levels of a wave (k_level on pull levels): per slot scanned its
+// two list heads and row length (12 B) and the visit / class / "more" / frontier words (1/2 B);
+// per queued slot its list offset and length (12 B) and 4 B per further dependency examined (the
+// frontier-bitmap probes hit L2 and are not counted). Winners cost only bitmap bits and counts.
 static uint64_t pull_level_bytes(const WaveCtr& c) {
-    const uint64_t tail_deps = c.pull_edges > c.pull_cand ? c.pull_edges - c.pull_cand : 0;
-    return c.pull_scan / 4 + 4 * c.pull_live + 12 * c.pull_tail + 4 * tail_deps + 36 * c.pull_win;
+    const uint64_t head_probes = c.pull_cand;   // >= 1 examined per candidate in the head step
+    const uint64_t tail_deps = c.pull_edges > head_probes ? c.pull_edges - head_probes : 0;
+    return c.pull_scan * 12 + c.pull_scan / 2 + 12 * c.pull_tail + 4 * tail_deps;
+}
+
+// Flags of the per-level timing events (FGI_EVENT_FLAGS overrides, for measurement). Without the
+// system-scope fence a record costs ~1 us instead of ~6 us between kernels (profiles/, e1).
+static unsigned event_flags() {
+    static const unsigned f = getenv("FGI_EVENT_FLAGS") ? (unsigned)strtoul(getenv("FGI_EVENT_FLAGS"), nullptr, 0)
+                                                       : (unsigned)hipEventDisableSystemFence;
+    return f;
+}
+
+static CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, uint32_t pgrid, uint32_t* fb, int clear, int buf) {
+    CollectArgs c;
+    c.tiles = g->tiles;
+    c.n_tiles = pull_iters(n_slots, pgrid) * pgrid;
+    c.pgrid = pgrid;
+    c.n_slots = n_slots;
+    c.fb = fb;
+    c.clear_fb = clear;
+    c.row_off = g->row_off;
+    c.row_len = g->row_len;
+    c.inv = g->inv;
+    c.fr_off = g->fr_off[buf];
+    c.fr_len = g->fr_len[buf];
+    c.escan = g->escan;
+    c.cstart = g->cstart;
+    c.part3 = g->partials + kScanBlocks;
+    return c;
+}
+
+static uint32_t level_grid_for(fgi_graph* g, uint32_t per_cu) {
+    int n_cu = 256;
+    hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device);
+    return std::min<uint32_t>((uint32_t)n_cu * per_cu, kStatBlocks);
 }
 
 fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
@@ -901,8 +1270,10 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     const auto t0 = std::chrono::steady_clock::now();
     hipStream_t s = g->stream;
     static const bool trace = getenv("FGI_TRACE") != nullptr;
-    const bool timing = stats != nullptr || trace;
+    static const bool no_level_events = getenv("FGI_NO_LEVEL_EVENTS") != nullptr;   // measurement only
+    const bool timing = (stats != nullptr || trace) && !no_level_events;
     FGI_TRY(ensure_cstart(g, g->pool_top));
+    FGI_TRY(ensure_cls(g));
     // Pull levels need the dependency-list cache. It is built lazily: while it is stale, levels
     // run push-only; once a level group shows a frontier heavy enough to pull, the cache is
     // (re)built and later groups may pull. Small waves (streaming mixes) never pay for it.
@@ -913,21 +1284,28 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     uint32_t* fb[2] = {g->front_bm, g->front_nx};
     FGI_HIP(g, hipMemsetAsync(g->ctr, 0, sizeof(WaveCtr), s));
     FGI_HIP(g, hipMemsetAsync(g->blk_stats, 0, sizeof(unsigned long long) * kStatBlocks * kStatCols, s));
-    FGI_HIP(g, hipMemsetAsync(g->dead_bm, 0, g->bm_words * 4, s));
     FGI_HIP(g, hipMemsetAsync(fb[0], 0, g->bm_words * 4, s));
-    if (timing) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
+    if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
     Out o{g->row_off, g->row_len, g->inv, g->fr_off[0], g->fr_len[0], &g->ctr->inv, &g->ctr->lvl[0]};
     if (n_roots) {
+        g->v_dirty = true;
         const uint32_t nb = (n_roots + kBlock - 1) / kBlock;
-        hipLaunchKernelGGL(k_roots, dim3(nb), dim3(kBlock), 0, s, roots_dev, imm_dev, n_roots, g->n_handles,
-                           reinterpret_cast<unsigned long long*>(g->node), o, g->ctr);
+        auto* node = reinterpret_cast<unsigned long long*>(g->node);
+        if (imm_dev) {
+            hipLaunchKernelGGL(k_roots<1>, dim3(nb), dim3(kBlock), 0, s, roots_dev, imm_dev, n_roots, 0u, g->n_handles,
+                               node, g->vis_bm, o, g->ctr);
+        }
+        hipLaunchKernelGGL(k_roots<0>, dim3(nb), dim3(kBlock), 0, s, roots_dev, imm_dev, n_roots, 0u, g->n_handles, node,
+                           g->vis_bm, o, g->ctr);
     }
-    int n_cu = 256;
-    hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device);
-    // 6 resident blocks per CU (LDS 20.6 KB, 76 VGPRs); per-block statistics rows bound the grid
-    const uint32_t level_grid = std::min<uint32_t>((uint32_t)n_cu * 6, kStatBlocks);
+    // 6 resident blocks per CU; per-block statistics bound the grid
+    const uint32_t level_grid = level_grid_for(g, 6);
     const uint64_t slot_words = ((uint64_t)g->n_slots + 63) / 64 * 2;
-    constexpr int kGroup = 4;
+    const uint64_t n_tiles = pull_iters(g->n_slots, level_grid) * level_grid;
+    // Levels run in groups between host synchronisations (one ~30 us round trip each); the first
+    // group is sized by the previous wave's depth, so a repeated workload syncs once per wave and an
+    // overshoot costs only empty levels (three ~4 us launches each).
+    int group = std::min(8, std::max(2, g->last_levels));
     int L = 0;
     uint64_t levels = 0, e_trav = 0, f_total = 0, pull_levels = 0;
     double expand_ms = 0, pull_ms = 0;
@@ -936,31 +1314,33 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     while (!done) {
         const int L0 = L;
         const int dir_eff = allow_pull ? direction : 1;
-        for (int k = 0; k < kGroup; ++k, ++L) {
+        for (int k = 0; k < group; ++k, ++L) {
             const int buf = L & 1;
-            hipLaunchKernelGGL(k_level_begin, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->ctr, g->inv, g->dead_bm,
-                               fb[buf], fb[buf ^ 1], g->bm_words, slot_words, g->fr_len[buf], g->partials, dir_eff,
-                               pull_threshold);
-            hipLaunchKernelGGL(k_scan_apply, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->fr_len[buf], g->partials,
-                               g->escan, g->cstart, g->ctr, 0);
+            const CollectArgs ca = collect_args(g, g->n_slots, level_grid, fb[buf], 0, buf);
+            hipLaunchKernelGGL(k_level_begin, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->ctr, g->inv, fb[buf],
+                               fb[buf ^ 1], g->bm_words, slot_words, g->fr_len[buf], g->partials, dir_eff,
+                               pull_threshold, ca);
+            hipLaunchKernelGGL(k_scan_apply, dim3(kScanBlocks), dim3(kScanThreads), 0, s, L, g->fr_len[buf], g->partials,
+                               g->escan, g->cstart, g->ctr, 0, ca, dir_eff, pull_threshold, fb[buf ^ 1], slot_words);
             if (timing) {
                 while (g->ev.size() < 2 * (size_t)(L + 1) + 2) {
                     hipEvent_t e;
-                    FGI_HIP(g, hipEventCreate(&e));
+                    FGI_HIP(g, hipEventCreateWithFlags(&e, event_flags()));
                     g->ev.push_back(e);
                 }
                 FGI_HIP(g, hipEventRecord(g->ev[2 * L], s));
             }
-            const ExpandArgs xa{g->fr_off[buf], g->escan, g->cstart, g->pool_col, g->pool_tag, g->dead_bm,
-                                g->opt_dead_filter};
-            const PullArgs pa{g->n_slots, g->uin_off, g->uin_len, g->uin_src, g->uin_head, fb[buf], fb[buf ^ 1],
-                              g->dead_bm};
+            const ExpandArgs xa{g->fr_off[buf], g->escan, g->cstart, g->pool_col, g->pool_tag, g->opt_dead_filter};
+            const PullArgs pa{g->n_slots, g->uin_off, g->uin_len, g->uin_src, g->uin_head, g->uin_more,
+                              fb[buf],    fb[buf ^ 1], g->cls_bm, g->row_len, g->tiles};
             Out ol{g->row_off, g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv, nullptr};
             hipLaunchKernelGGL(k_level<false>, dim3(level_grid), dim3(kBlock), 0, s, L, xa, pa,
-                               reinterpret_cast<unsigned long long*>(g->node), ol, g->ctr, g->blk_stats, RemoteArgs{});
+                               reinterpret_cast<const unsigned long long*>(g->node), g->vis_bm, ol, g->ctr,
+                               g->blk_stats, RemoteArgs{});
             if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L + 1], s));
         }
-        hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(kBlock), 0, s, g->blk_stats, g->ctr);
+        hipLaunchKernelGGL(k_stats_reduce, dim3(kStats + 1), dim3(kBlock), 0, s, g->blk_stats, g->ctr, L, g->tiles,
+                           n_tiles);
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
         FGI_HIP(g, hipStreamSynchronize(s));
@@ -994,7 +1374,25 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                 fprintf(stderr, "[fgi] level %d %s: frontier %llu edges %llu k_level %.3f ms\n", l,
                         lc.pull ? "pull" : "push", (unsigned long long)lc.F, (unsigned long long)lc.T, ms);
         }
-        if (g->ctr_host->lvl[L % kRing].F == 0) done = true;
+        if (g->ctr_host->lvl[L % kRing].F == 0) {
+            done = true;
+            // a last pull level's winners (all without rows) are still only in its bitmap: run
+            // level L's collect (k_level_begin + k_scan_apply; there is nothing to traverse)
+            if (L > 0 && g->ctr_host->lvl[(L - 1) % kRing].pull && g->ctr_host->lvl[L % kRing].pad0) {
+                const int buf = L & 1;
+                const CollectArgs ca = collect_args(g, g->n_slots, level_grid, fb[buf], 0, buf);
+                hipLaunchKernelGGL(k_level_begin, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->ctr, g->inv, fb[buf],
+                                   fb[buf ^ 1], g->bm_words, slot_words, g->fr_len[buf], g->partials, dir_eff,
+                                   pull_threshold, ca);
+                hipLaunchKernelGGL(k_scan_apply, dim3(kScanBlocks), dim3(kScanThreads), 0, s, L, g->fr_len[buf],
+                                   g->partials, g->escan, g->cstart, g->ctr, 0, ca, dir_eff, pull_threshold,
+                                   fb[buf ^ 1], slot_words);
+                FGI_HIP(g, hipGetLastError());
+                FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
+                FGI_HIP(g, hipStreamSynchronize(s));
+            }
+        }
+        group = 4;
         if (!done && !allow_pull && direction == 0) {
             bool heavy = false;
             for (int l = L0; l <= L; ++l) heavy |= g->ctr_host->lvl[l % kRing].T > pull_threshold;
@@ -1005,19 +1403,22 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         }
     }
     if (n_roots == 0) {
-        hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(kBlock), 0, s, g->blk_stats, g->ctr);
+        hipLaunchKernelGGL(k_stats_reduce, dim3(kStats + 1), dim3(kBlock), 0, s, g->blk_stats, g->ctr, 0, g->tiles,
+                           n_tiles);
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
         FGI_HIP(g, hipStreamSynchronize(s));
     }
-    if (timing) {
+    if (timing || stats) {
         FGI_HIP(g, hipEventRecord(g->ev_w1, s));
         FGI_HIP(g, hipEventSynchronize(g->ev_w1));
     }
+    if (imm_dev && n_roots) note_words(g);   // immediate roots changed node words
     g->last_wave_n = g->ctr_host->inv;
+    if (n_roots) g->last_levels = (int)levels;
     const WaveCtr& c = *g->ctr_host;
     if (trace)
         fprintf(stderr,
-                "[fgi] wave: %llu invalidated; pull: live %llu, candidates %llu, head misses %llu, dependencies "
+                "[fgi] wave: %llu invalidated; pull: live %llu, candidates %llu, queued %llu, dependencies "
                 "examined %llu, winners %llu\n",
                 (unsigned long long)c.inv, (unsigned long long)c.pull_live, (unsigned long long)c.pull_cand,
                 (unsigned long long)c.pull_tail, (unsigned long long)c.pull_edges, (unsigned long long)c.pull_win);
@@ -1031,12 +1432,12 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         stats->n_flagged += c.n_flagged;
         stats->pull_levels += pull_levels;
         stats->pull_edges += c.pull_edges;
-        // Algorithmic bytes (DESIGN.md §Roofline). Push level, per traversed edge: col 4 + tag 8 +
+        // Algorithmic bytes (DESIGN.md §3). Push level, per traversed edge: col 4 + tag 8 +
         // node-word gather 8; per frontier entry: fr_len 4 x2, escan 8 w + 8 r, fr_off 8 r, written
-        // 12 by the producer. Per invalidated node: CAS 8 + row gathers 12 + list write 4. Per root 5.
+        // 12 by the producer. Per invalidated node: row gathers 12 + list write 4. Per root 5.
         const uint64_t push_b = 20 * expand_edges + 44 * expand_f;
         const uint64_t pull_b = pull_level_bytes(c);
-        stats->alg_bytes += push_b + pull_b + 24 * v + 5ull * n_roots;
+        stats->alg_bytes += push_b + pull_b + 16 * v + 5ull * n_roots;
         float wave_ms = 0;
         hipEventElapsedTime(&wave_ms, g->ev_w0, g->ev_w1);
         stats->kernel_ms += wave_ms;
@@ -1054,6 +1455,8 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
 
 // ---- multi-GPU wave, split into phases shared by the RCCL driver (one process per GPU) and the
 // in-process driver (several partitions of one graph on one device, exchange by device copies).
+static uint32_t part_grid(fgi_graph* g) { return level_grid_for(g, 5); }
+
 fgi_status part_wave_begin(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev) {
     PartView pv;
     if (!part_view(g, &pv)) return set_err(g, FGI_ESTATE, "partition not initialised");
@@ -1062,21 +1465,28 @@ fgi_status part_wave_begin(fgi_graph* g, uint32_t n_roots, const uint32_t* roots
     g->pw.t0 = std::chrono::steady_clock::now();
     g->pw.n_roots = n_roots;
     FGI_TRY(ensure_cstart(g, g->pool_top));
+    FGI_TRY(ensure_cls(g));
     FGI_HIP(g, hipMemsetAsync(g->ctr, 0, sizeof(WaveCtr), s));
     FGI_HIP(g, hipMemsetAsync(g->blk_stats, 0, sizeof(unsigned long long) * kStatBlocks * kStatCols, s));
-    FGI_HIP(g, hipMemsetAsync(g->dead_bm, 0, g->bm_words * 4, s));
     FGI_HIP(g, hipMemsetAsync(pv.sent_bm, 0, pv.sent_words * 4, s));
     while (g->ev.size() < 3) {
         hipEvent_t e;
-        FGI_HIP(g, hipEventCreate(&e));
+        FGI_HIP(g, hipEventCreateWithFlags(&e, event_flags()));
         g->ev.push_back(e);
     }
     FGI_HIP(g, hipEventRecord(g->ev_w0, s));
-    if (n_roots)
-        hipLaunchKernelGGL(k_part_roots, dim3((n_roots + kBlock - 1) / kBlock), dim3(kBlock), 0, s, roots_dev, imm_dev,
-                           n_roots, pv.base, pv.n_local, reinterpret_cast<unsigned long long*>(g->node),
-                           Out{g->row_off, g->row_len, g->inv, g->fr_off[0], g->fr_len[0], &g->ctr->inv, &g->ctr->lvl[0]},
-                           g->ctr);
+    g->v_dirty = true;
+    const Out o{g->row_off, g->row_len, g->inv, g->fr_off[0], g->fr_len[0], &g->ctr->inv, &g->ctr->lvl[0]};
+    auto* node = reinterpret_cast<unsigned long long*>(g->node);
+    if (n_roots) {
+        const uint32_t nb = (n_roots + kBlock - 1) / kBlock;
+        if (imm_dev)
+            hipLaunchKernelGGL(k_roots<1>, dim3(nb), dim3(kBlock), 0, s, roots_dev, imm_dev, n_roots, pv.base, pv.n_local,
+                               node, g->vis_bm, o, g->ctr);
+        hipLaunchKernelGGL(k_roots<0>, dim3(nb), dim3(kBlock), 0, s, roots_dev, imm_dev, n_roots, pv.base, pv.n_local,
+                           node, g->vis_bm, o, g->ctr);
+        if (imm_dev) note_words(g);
+    }
     FGI_HIP(g, hipGetLastError());
     return FGI_OK;
 }
@@ -1084,22 +1494,24 @@ fgi_status part_wave_begin(fgi_graph* g, uint32_t n_roots, const uint32_t* roots
 const unsigned long long* part_level_frontier_dev(fgi_graph* g, int L) { return &g->ctr->lvl[L % kRing].F; }
 const unsigned long long* part_level_edges_dev(fgi_graph* g, int L) { return &g->ctr->lvl[L % kRing].T; }
 
-// scan of the local frontier (its edge total T decides push vs pull for every rank)
+// scan of the local frontier (its edge total T decides push vs pull for every rank); after a pull
+// level, the local winners bitmap becomes the invalidated-list tail and the frontier list first
 fgi_status part_level_scan(fgi_graph* g, int L) {
     PartView pv;
     part_view(g, &pv);
     hipStream_t s = g->stream;
     const int buf = L & 1;
+    const CollectArgs ca = collect_args(g, pv.n_local, part_grid(g), g->front_nx, 1, buf);
     FGI_HIP(g, hipMemsetAsync(pv.send_cnt, 0, (size_t)pv.world * 8, s));
-    hipLaunchKernelGGL(k_scan_reduce, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->fr_len[buf], g->partials, g->ctr);
-    hipLaunchKernelGGL(k_scan_apply, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->fr_len[buf], g->partials, g->escan,
-                       g->cstart, g->ctr, 1);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->fr_len[buf], g->partials, g->ctr, ca);
+    hipLaunchKernelGGL(k_scan_apply, dim3(kScanBlocks), dim3(kScanThreads), 0, s, L, g->fr_len[buf], g->partials, g->escan,
+                       g->cstart, g->ctr, 1, ca, 1, ~0ull, g->front_nx, (uint64_t)0);
     FGI_HIP(g, hipGetLastError());
     return FGI_OK;
 }
 
-// marks the previous level's winners (dead; frontier bitmap on pull levels); on a pull level the
-// local frontier words front_bm[0, block/32) are then all-gathered into pv.front_global
+// marks the previous level's winners into the local frontier bitmap on a pull level; the local
+// frontier words front_bm[0, block/32) are then all-gathered into pv.front_global
 fgi_status part_level_mark(fgi_graph* g, int L, bool pull) {
     hipStream_t s = g->stream;
     int n_cu = 256;
@@ -1107,7 +1519,7 @@ fgi_status part_level_mark(fgi_graph* g, int L, bool pull) {
     static const unsigned long long one = 1;
     if (pull)
         FGI_HIP(g, hipMemcpyAsync(&g->ctr->lvl[L % kRing].pull, &one, 8, hipMemcpyHostToDevice, s));
-    hipLaunchKernelGGL(k_mark, dim3((uint32_t)n_cu * 2), dim3(kBlock), 0, s, L, g->inv, g->dead_bm, g->front_bm, g->ctr);
+    hipLaunchKernelGGL(k_mark, dim3((uint32_t)n_cu * 2), dim3(kBlock), 0, s, L, g->inv, g->front_bm, g->ctr);
     FGI_HIP(g, hipGetLastError());
     return FGI_OK;
 }
@@ -1118,16 +1530,15 @@ fgi_status part_level_work(fgi_graph* g, int L, bool pull) {
     PartView pv;
     part_view(g, &pv);
     hipStream_t s = g->stream;
-    int n_cu = 256;
-    hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device);
     const RemoteArgs ra{pv.base, pv.n_local, pv.block, pv.world, pv.ver_all, pv.sent_bm, pv.send_buf, pv.send_cnt};
     const int buf = L & 1;
     FGI_HIP(g, hipEventRecord(g->ev[0], s));
-    const ExpandArgs xa{g->fr_off[buf], g->escan, g->cstart, g->pool_col, g->pool_tag, g->dead_bm, g->opt_dead_filter};
-    const PullArgs pa{pv.n_local, g->uin_off, g->uin_len, g->uin_src, g->uin_head, pv.front_global, nullptr, g->dead_bm};
+    const ExpandArgs xa{g->fr_off[buf], g->escan, g->cstart, g->pool_col, g->pool_tag, g->opt_dead_filter};
+    const PullArgs pa{pv.n_local,      g->uin_off,  g->uin_len, g->uin_src,  g->uin_head, g->uin_more,
+                      pv.front_global, g->front_nx, g->cls_bm,  g->row_len, g->tiles};
     const Out o{g->row_off, g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv, nullptr};
-    hipLaunchKernelGGL(k_level<true>, dim3((uint32_t)n_cu * 5), dim3(kBlock), 0, s, L, xa, pa,
-                       reinterpret_cast<unsigned long long*>(g->node), o, g->ctr, g->blk_stats, ra);
+    hipLaunchKernelGGL(k_level<true>, dim3(part_grid(g)), dim3(kBlock), 0, s, L, xa, pa,
+                       reinterpret_cast<const unsigned long long*>(g->node), g->vis_bm, o, g->ctr, g->blk_stats, ra);
     FGI_HIP(g, hipEventRecord(g->ev[1], s));
     if (pull) FGI_HIP(g, hipMemsetAsync(pv.front_global, 0, pv.front_words_global * 4, s));
     FGI_HIP(g, hipGetLastError());
@@ -1145,11 +1556,13 @@ fgi_status part_level_apply(fgi_graph* g, int L, uint64_t n_recv, uint64_t n_sen
     if (n_recv)
         hipLaunchKernelGGL(k_apply_recv, dim3(std::min<uint64_t>((n_recv + kBlock - 1) / kBlock, (uint64_t)n_cu * 8)),
                            dim3(kBlock), 0, s, L, n_recv, pv.recv_buf, pv.base,
-                           reinterpret_cast<unsigned long long*>(g->node),
+                           reinterpret_cast<const unsigned long long*>(g->node), g->vis_bm,
                            Out{g->row_off, g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv,
                                nullptr},
                            g->ctr, g->blk_stats);
-    hipLaunchKernelGGL(k_clear_front, dim3((uint32_t)n_cu * 2), dim3(kBlock), 0, s, L, g->inv, g->front_bm, g->ctr);
+    const uint64_t n_tiles = pull_iters(pv.n_local, part_grid(g)) * part_grid(g);
+    hipLaunchKernelGGL(k_clear_front, dim3((uint32_t)n_cu * 2), dim3(kBlock), 0, s, L, g->inv, g->front_bm, g->ctr,
+                       g->tiles, n_tiles);
     FGI_HIP(g, hipGetLastError());
     g->pw.sent += n_sent;
     return FGI_OK;
@@ -1179,7 +1592,8 @@ fgi_status part_level_account(fgi_graph* g, int L) {
 
 fgi_status part_wave_end(fgi_graph* g, fgi_wave_stats* stats) {
     hipStream_t s = g->stream;
-    hipLaunchKernelGGL(k_stats_reduce, dim3(1), dim3(kBlock), 0, s, g->blk_stats, g->ctr);
+    hipLaunchKernelGGL(k_stats_reduce, dim3(kStats + 1), dim3(kBlock), 0, s, g->blk_stats, g->ctr, 0, g->tiles,
+                       (uint64_t)0);
     FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
     FGI_HIP(g, hipEventRecord(g->ev_w1, s));
     FGI_HIP(g, hipStreamSynchronize(s));
@@ -1197,7 +1611,7 @@ fgi_status part_wave_end(fgi_graph* g, fgi_wave_stats* stats) {
         // as run_wave (push and pull levels), plus 8 B per forwarded target (written + received)
         const WaveCtr& c = *g->ctr_host;
         const uint64_t pull_b = pull_level_bytes(c);
-        stats->alg_bytes += 20 * w.push_edges + 44 * w.push_f + pull_b + 24 * v + 8 * w.sent + 5ull * w.n_roots;
+        stats->alg_bytes += 20 * w.push_edges + 44 * w.push_f + pull_b + 16 * v + 8 * w.sent + 5ull * w.n_roots;
         stats->pull_levels += w.pull_levels;
         stats->pull_edges += c.pull_edges;
         stats->pull_ms += w.pull_ms;
@@ -1227,7 +1641,9 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     FGI_TRY(part_allreduce_sum(g, pv.scratch_u64, &e_global));
     const uint64_t threshold = e_global / (uint64_t)(g->opt_pull_alpha > 0 ? g->opt_pull_alpha : 1);
     FGI_TRY(part_allreduce_sum(g, part_level_frontier_dev(g, 0), &f_global));
-    for (int L = 0; f_global != 0; ++L) {
+    int L = 0;
+    bool last_pull = false;
+    for (; f_global != 0; ++L) {
         FGI_TRY(part_level_scan(g, L));
         FGI_TRY(part_allreduce_sum(g, part_level_edges_dev(g, L), &t_global));
         const bool pull = allow_pull && (g->opt_direction == 2 || t_global > threshold);
@@ -1239,7 +1655,10 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
         FGI_TRY(part_level_apply(g, L, n_recv, n_sent));
         FGI_TRY(part_allreduce_sum(g, part_level_frontier_dev(g, L + 1), &f_global));
         FGI_TRY(part_level_account(g, L));
+        last_pull = pull;
     }
+    // the last level's pull winners (without rows) are collected into the invalidated list
+    if (last_pull) FGI_TRY(part_level_scan(g, L));
     return part_wave_end(g, stats);
 }
 
