@@ -158,7 +158,7 @@ struct fgi_graph {
 
     // wave workspace
     uint32_t* inv = nullptr;           // [n_handles] invalidated handles of the last wave
-    uint64_t* fr_off[2] = {nullptr, nullptr};
+    uint32_t* fr_h[2] = {nullptr, nullptr};    // frontier lists: handles (row offsets are gathered by the push)
     uint32_t* fr_len[2] = {nullptr, nullptr};
     uint64_t* escan = nullptr;         // [n_handles]
     uint32_t* cstart = nullptr;        // [cstart_cap]

@@ -114,12 +114,11 @@ __device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
 __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
 // Where a level's winners go: the invalidated list (all winners) and the next frontier (winners
-// with a non-empty row, with that row's offset/length); the next level's F and T accumulate in ln.
+// with a non-empty row: handle and row length); the next level's F and T accumulate in ln.
 struct Out {
-    const uint64_t* __restrict__ row_off;
     const uint32_t* __restrict__ row_len;
     uint32_t* __restrict__ inv;
-    uint64_t* __restrict__ nfr_off;
+    uint32_t* __restrict__ nfr_h;
     uint32_t* __restrict__ nfr_len;
     unsigned long long* inv_ctr;
     LevelCtr* ln;
@@ -171,17 +170,12 @@ __device__ __forceinline__ void block_stats_add(unsigned long long* blk, unsigne
 
 // Append one (possibly absent) winner per lane. Every lane of the wave must call it.
 __device__ __forceinline__ void emit_one(bool win, uint32_t h, const Out& o) {
-    uint32_t len = 0;
-    uint64_t off = 0;
-    if (win) {
-        len = o.row_len[h];
-        off = o.row_off[h];
-    }
+    const uint32_t len = win ? o.row_len[h] : 0u;
     uint64_t ib, fb;
     wave_reserve(win ? 1u : 0u, (win && len) ? 1u : 0u, o.inv_ctr, &o.ln->F, ib, fb);
     if (win) o.inv[ib] = h;
     if (win && len) {
-        o.nfr_off[fb] = off;
+        o.nfr_h[fb] = h;
         o.nfr_len[fb] = len;
     }
     const unsigned long long ls = wave_sum64(len);
@@ -222,7 +216,7 @@ __device__ __forceinline__ void emit_push(Emit& e, uint32_t* buf, bool win, uint
             const uint32_t len = o.row_len[h];
             if (len) {
                 const unsigned long long fb = atomicAdd(&o.ln->F, 1ull);
-                o.nfr_off[fb] = o.row_off[h];
+                o.nfr_h[fb] = h;
                 o.nfr_len[fb] = len;
                 atomicAdd(&o.ln->T, (unsigned long long)len);
             }
@@ -282,7 +276,7 @@ __device__ __forceinline__ void emit_flush(Emit& e, uint32_t* buf, uint32_t at, 
             o.inv[e.base_inv + i] = h;
             const uint32_t len = o.row_len[h];
             if (len) {
-                o.nfr_off[fb] = o.row_off[h];
+                o.nfr_h[fb] = h;
                 o.nfr_len[fb] = len;
                 ++fb;
             }
@@ -437,10 +431,9 @@ struct CollectArgs {
     uint32_t pgrid, n_slots;
     uint32_t* fb;                // winners bitmap of the pull level
     int clear_fb;                // multi-GPU: the words are scratch, cleared after reading
-    const uint64_t* __restrict__ row_off;
     const uint32_t* __restrict__ row_len;
     uint32_t* inv;
-    uint64_t* fr_off;
+    uint32_t* fr_h;
     uint32_t* fr_len;
     uint64_t* escan;
     uint32_t* cstart;
@@ -481,23 +474,20 @@ __device__ __forceinline__ void collect_tile(const CollectArgs& c, uint64_t t, u
         wd = fb64[s0 / 64 + lane];
         if (c.clear_fb && wd) fb64[s0 / 64 + lane] = 0ull;
     }
-    unsigned long long bits[kWords];
+    // lane l holds bit l of every word (slot s0 + r * 64 + l), packed into one register
+    uint32_t mine = 0;
 #pragma unroll
-    for (int r = 0; r < kWords; ++r) bits[r] = __shfl(wd, r, 64);
+    for (int r = 0; r < kWords; ++r) mine |= (uint32_t)((__shfl(wd, r, 64) >> lane) & 1ull) << r;
     uint32_t rl[kWords];
-    uint64_t ro[kWords];
 #pragma unroll
-    for (int r = 0; r < kWords; ++r)
-        rl[r] = (write_fr && ((bits[r] >> lane) & 1ull)) ? c.row_len[s0 + r * 64 + lane] : 0u;
-#pragma unroll
-    for (int r = 0; r < kWords; ++r) ro[r] = rl[r] ? c.row_off[s0 + r * 64 + lane] : 0ull;
+    for (int r = 0; r < kWords; ++r) rl[r] = (write_fr && ((mine >> r) & 1u)) ? c.row_len[s0 + r * 64 + lane] : 0u;
 #pragma unroll
     for (int r = 0; r < kWords; ++r) {
-        if (!bits[r]) continue;   // uniform
+        const unsigned long long bits = __shfl(wd, r, 64);
+        if (!bits) continue;   // uniform
         const uint32_t slot = (uint32_t)(s0 + r * 64 + lane);
-        const bool bit = (bits[r] >> lane) & 1ull;
-        if (bit) c.inv[bw + __popcll(bits[r] & lanemask_lt())] = slot;
-        bw += __popcll(bits[r]);
+        if ((mine >> r) & 1u) c.inv[bw + __popcll(bits & lanemask_lt())] = slot;
+        bw += __popcll(bits);
         if (!write_fr) continue;
         const bool e = rl[r] != 0;
         const unsigned long long me = __ballot(e);
@@ -506,7 +496,7 @@ __device__ __forceinline__ void collect_tile(const CollectArgs& c, uint64_t t, u
         if (e) {
             const uint64_t idx = be + __popcll(me & lanemask_lt());
             const uint64_t es = bl + incl - x;
-            c.fr_off[idx] = ro[r];
+            c.fr_h[idx] = slot;
             c.fr_len[idx] = rl[r];
             c.escan[idx] = es;
             const uint64_t c_lo = (es + kChunk - 1) / kChunk, c_hi = (es + x - 1) / kChunk;
@@ -781,7 +771,8 @@ __device__ __forceinline__ uint32_t lds_upper_bound(const uint32_t* s, uint32_t 
 }
 
 struct ExpandArgs {
-    const uint64_t* __restrict__ fr_off;
+    const uint32_t* __restrict__ fr_h;
+    const uint64_t* __restrict__ row_off;
     const uint64_t* __restrict__ escan;
     const uint32_t* __restrict__ cstart;
     const uint32_t* __restrict__ pool_col;
@@ -810,7 +801,7 @@ __device__ __forceinline__ void expand_level(const LevelCtr& lc, const ExpandArg
         for (uint32_t k = threadIdx.x; k < n; k += kBlock) {
             const uint64_t es = x.escan[i0 + k];
             s_rel[k] = es > cbase ? (uint32_t)(es - cbase) : 0u;
-            s_base[k] = (uint32_t)(x.fr_off[i0 + k] + cbase - es);   // pool positions < 2^32
+            s_base[k] = (uint32_t)(x.row_off[x.fr_h[i0 + k]] + cbase - es);   // pool positions < 2^32
         }
         __syncthreads();
         uint32_t dst[kEPT];
@@ -1248,10 +1239,9 @@ static CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, uint32_t pgrid, 
     c.n_slots = n_slots;
     c.fb = fb;
     c.clear_fb = clear;
-    c.row_off = g->row_off;
     c.row_len = g->row_len;
     c.inv = g->inv;
-    c.fr_off = g->fr_off[buf];
+    c.fr_h = g->fr_h[buf];
     c.fr_len = g->fr_len[buf];
     c.escan = g->escan;
     c.cstart = g->cstart;
@@ -1286,7 +1276,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     FGI_HIP(g, hipMemsetAsync(g->blk_stats, 0, sizeof(unsigned long long) * kStatBlocks * kStatCols, s));
     FGI_HIP(g, hipMemsetAsync(fb[0], 0, g->bm_words * 4, s));
     if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
-    Out o{g->row_off, g->row_len, g->inv, g->fr_off[0], g->fr_len[0], &g->ctr->inv, &g->ctr->lvl[0]};
+    Out o{g->row_len, g->inv, g->fr_h[0], g->fr_len[0], &g->ctr->inv, &g->ctr->lvl[0]};
     if (n_roots) {
         g->v_dirty = true;
         const uint32_t nb = (n_roots + kBlock - 1) / kBlock;
@@ -1330,10 +1320,10 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                 }
                 FGI_HIP(g, hipEventRecord(g->ev[2 * L], s));
             }
-            const ExpandArgs xa{g->fr_off[buf], g->escan, g->cstart, g->pool_col, g->pool_tag, g->opt_dead_filter};
+            const ExpandArgs xa{g->fr_h[buf], g->row_off, g->escan, g->cstart, g->pool_col, g->pool_tag, g->opt_dead_filter};
             const PullArgs pa{g->n_slots, g->uin_off, g->uin_len, g->uin_src, g->uin_head, g->uin_more,
                               fb[buf],    fb[buf ^ 1], g->cls_bm, g->row_len, g->tiles};
-            Out ol{g->row_off, g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv, nullptr};
+            Out ol{g->row_len, g->inv, g->fr_h[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv, nullptr};
             hipLaunchKernelGGL(k_level<false>, dim3(level_grid), dim3(kBlock), 0, s, L, xa, pa,
                                reinterpret_cast<const unsigned long long*>(g->node), g->vis_bm, ol, g->ctr,
                                g->blk_stats, RemoteArgs{});
@@ -1476,7 +1466,7 @@ fgi_status part_wave_begin(fgi_graph* g, uint32_t n_roots, const uint32_t* roots
     }
     FGI_HIP(g, hipEventRecord(g->ev_w0, s));
     g->v_dirty = true;
-    const Out o{g->row_off, g->row_len, g->inv, g->fr_off[0], g->fr_len[0], &g->ctr->inv, &g->ctr->lvl[0]};
+    const Out o{g->row_len, g->inv, g->fr_h[0], g->fr_len[0], &g->ctr->inv, &g->ctr->lvl[0]};
     auto* node = reinterpret_cast<unsigned long long*>(g->node);
     if (n_roots) {
         const uint32_t nb = (n_roots + kBlock - 1) / kBlock;
@@ -1533,10 +1523,10 @@ fgi_status part_level_work(fgi_graph* g, int L, bool pull) {
     const RemoteArgs ra{pv.base, pv.n_local, pv.block, pv.world, pv.ver_all, pv.sent_bm, pv.send_buf, pv.send_cnt};
     const int buf = L & 1;
     FGI_HIP(g, hipEventRecord(g->ev[0], s));
-    const ExpandArgs xa{g->fr_off[buf], g->escan, g->cstart, g->pool_col, g->pool_tag, g->opt_dead_filter};
+    const ExpandArgs xa{g->fr_h[buf], g->row_off, g->escan, g->cstart, g->pool_col, g->pool_tag, g->opt_dead_filter};
     const PullArgs pa{pv.n_local,      g->uin_off,  g->uin_len, g->uin_src,  g->uin_head, g->uin_more,
                       pv.front_global, g->front_nx, g->cls_bm,  g->row_len, g->tiles};
-    const Out o{g->row_off, g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv, nullptr};
+    const Out o{g->row_len, g->inv, g->fr_h[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv, nullptr};
     hipLaunchKernelGGL(k_level<true>, dim3(part_grid(g)), dim3(kBlock), 0, s, L, xa, pa,
                        reinterpret_cast<const unsigned long long*>(g->node), g->vis_bm, o, g->ctr, g->blk_stats, ra);
     FGI_HIP(g, hipEventRecord(g->ev[1], s));
@@ -1557,7 +1547,7 @@ fgi_status part_level_apply(fgi_graph* g, int L, uint64_t n_recv, uint64_t n_sen
         hipLaunchKernelGGL(k_apply_recv, dim3(std::min<uint64_t>((n_recv + kBlock - 1) / kBlock, (uint64_t)n_cu * 8)),
                            dim3(kBlock), 0, s, L, n_recv, pv.recv_buf, pv.base,
                            reinterpret_cast<const unsigned long long*>(g->node), g->vis_bm,
-                           Out{g->row_off, g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv,
+                           Out{g->row_len, g->inv, g->fr_h[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv,
                                nullptr},
                            g->ctr, g->blk_stats);
     const uint64_t n_tiles = pull_iters(pv.n_local, part_grid(g)) * part_grid(g);
