@@ -430,6 +430,7 @@ struct CollectArgs {
     uint64_t n_tiles;
     uint32_t pgrid, n_slots;
     uint32_t* fb;                // winners bitmap of the pull level
+    uint32_t n_handles;          // rows: row_len has n_handles entries
     int clear_fb;                // multi-GPU: the words are scratch, cleared after reading
     const uint32_t* __restrict__ row_len;
     uint32_t* inv;
@@ -460,50 +461,93 @@ __device__ __forceinline__ void collect_pass1(const CollectArgs& c, unsigned lon
     }
 }
 
-// One tile by one wave: 16 bitmap words (1,024 slots); entries at bw (inv), be / bl (frontier
-// index / edge offset). write_fr: also the frontier entries, their scan and the chunk map.
+// One tile by one wave: lane l owns the 16 slots s0 + 16l .. s0 + 16l + 15 (one 16-bit chunk of the
+// winners bitmap). Two wave scans place every lane's entries (winners; expandable winners and their
+// row lengths); the entries are staged in the wave's LDS buffer and stored coalesced, in slot order,
+// at bw (inv) and be / bl (frontier index / edge offset). write_fr: also the frontier entries, their
+// scan and the chunk map.
 __device__ __forceinline__ void collect_tile(const CollectArgs& c, uint64_t t, uint64_t bw, uint64_t be, uint64_t bl,
-                                             bool write_fr) {
-    constexpr int kWords = kPullTile / 64;
+                                             bool write_fr, uint32_t* __restrict__ stage) {
     const uint32_t lane = lane_id();
-    const uint64_t it = t / c.pgrid, bb = t % c.pgrid;
-    const uint64_t s0 = it * (uint64_t)c.pgrid * kPullTile + bb * kPullTile;
-    unsigned long long* fb64 = reinterpret_cast<unsigned long long*>(c.fb);
-    unsigned long long wd = 0;
-    if (lane < kWords && s0 + (uint64_t)lane * 64 < c.n_slots) {
-        wd = fb64[s0 / 64 + lane];
-        if (c.clear_fb && wd) fb64[s0 / 64 + lane] = 0ull;
+    const uint64_t s0 = t * kPullTile;   // tile t = it * pgrid + block covers slots [t * kPullTile, +kPullTile)
+    const uint64_t base = s0 + 16ull * lane;
+    uint16_t* fb16 = reinterpret_cast<uint16_t*>(c.fb);
+    uint32_t m = 0;
+    if (base < c.n_slots) {
+        m = fb16[base / 16];
+        if (c.clear_fb && m) fb16[base / 16] = 0;
     }
-    // lane l holds bit l of every word (slot s0 + r * 64 + l), packed into one register
-    uint32_t mine = 0;
+    uint32_t rl[16];
+    uint32_t em = 0, len = 0;
 #pragma unroll
-    for (int r = 0; r < kWords; ++r) mine |= (uint32_t)((__shfl(wd, r, 64) >> lane) & 1ull) << r;
-    uint32_t rl[kWords];
+    for (int k = 0; k < 16; ++k) rl[k] = 0;
+    if (write_fr && m) {
+        if (base + 16 <= c.n_handles) {
+            const uint4* p = reinterpret_cast<const uint4*>(c.row_len + base);
 #pragma unroll
-    for (int r = 0; r < kWords; ++r) rl[r] = (write_fr && ((mine >> r) & 1u)) ? c.row_len[s0 + r * 64 + lane] : 0u;
+            for (int q = 0; q < 4; ++q) {
+                const uint4 v = p[q];
+                rl[4 * q] = v.x;
+                rl[4 * q + 1] = v.y;
+                rl[4 * q + 2] = v.z;
+                rl[4 * q + 3] = v.w;
+            }
+        } else {
 #pragma unroll
-    for (int r = 0; r < kWords; ++r) {
-        const unsigned long long bits = __shfl(wd, r, 64);
-        if (!bits) continue;   // uniform
-        const uint32_t slot = (uint32_t)(s0 + r * 64 + lane);
-        if ((mine >> r) & 1u) c.inv[bw + __popcll(bits & lanemask_lt())] = slot;
-        bw += __popcll(bits);
-        if (!write_fr) continue;
-        const bool e = rl[r] != 0;
-        const unsigned long long me = __ballot(e);
-        const unsigned long long x = rl[r];
-        const unsigned long long incl = wave_incl_scan64(x);
-        if (e) {
-            const uint64_t idx = be + __popcll(me & lanemask_lt());
-            const uint64_t es = bl + incl - x;
-            c.fr_h[idx] = slot;
-            c.fr_len[idx] = rl[r];
-            c.escan[idx] = es;
-            const uint64_t c_lo = (es + kChunk - 1) / kChunk, c_hi = (es + x - 1) / kChunk;
-            for (uint64_t k = c_lo; k <= c_hi; ++k) c.cstart[k] = (uint32_t)idx;
+            for (int k = 0; k < 16; ++k) rl[k] = ((m >> k) & 1u) ? c.row_len[base + k] : 0u;
         }
-        be += __popcll(me);
-        bl += __shfl(incl, 63, 64);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (!((m >> k) & 1u)) rl[k] = 0;
+            em |= (rl[k] != 0 ? 1u : 0u) << k;
+            len += rl[k];
+        }
+    }
+    uint32_t tot_p, tot_l;
+    const uint32_t pw = wave_excl_scan((uint32_t)__popc(m) | ((uint32_t)__popc(em) << 16), tot_p);
+    const uint32_t pl = write_fr ? wave_excl_scan(len, tot_l) : 0u;
+    const uint32_t n_w = tot_p & 0xFFFFu, n_e = tot_p >> 16;
+    // winners -> inv
+    {
+        uint32_t o = pw & 0xFFFFu;
+        for (uint32_t mm = m; mm; mm &= mm - 1) stage[o++] = (uint32_t)base + (uint32_t)(__ffs(mm) - 1);
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i = lane; i < n_w; i += 64) c.inv[bw + i] = stage[i];
+        __builtin_amdgcn_wave_barrier();
+    }
+    if (!write_fr || n_e == 0) return;
+    // expandable winners -> fr_h, fr_len, escan (+ cstart for every chunk whose first edge they hold)
+    const uint32_t pe = pw >> 16;
+    {
+        uint32_t o = pe;
+        for (uint32_t mm = em; mm; mm &= mm - 1) stage[o++] = (uint32_t)base + (uint32_t)(__ffs(mm) - 1);
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i = lane; i < n_e; i += 64) c.fr_h[be + i] = stage[i];
+        __builtin_amdgcn_wave_barrier();
+    }
+    {
+        uint32_t o = pe;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if (rl[k]) stage[o++] = rl[k];
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i = lane; i < n_e; i += 64) c.fr_len[be + i] = stage[i];
+        __builtin_amdgcn_wave_barrier();
+    }
+    {
+        uint32_t o = pe, r = pl;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            if (!rl[k]) continue;
+            const uint64_t es = bl + r, idx = be + o;
+            const uint64_t c_lo = (es + kChunk - 1) / kChunk, c_hi = (es + rl[k] - 1) / kChunk;
+            for (uint64_t q = c_lo; q <= c_hi; ++q) c.cstart[q] = (uint32_t)idx;
+            stage[o++] = r;
+            r += rl[k];
+        }
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i = lane; i < n_e; i += 64) c.escan[be + i] = bl + stage[i];
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
@@ -514,6 +558,7 @@ __device__ __forceinline__ void collect_pass2(const CollectArgs& c, LevelCtr& lc
                                               int direction, uint64_t pull_threshold, uint32_t* fb_nxt,
                                               uint64_t slot_words, unsigned long long* s_red) {
     __shared__ unsigned long long s_w[kMaxWaves], s_e[kMaxWaves], s_l[kMaxWaves];
+    __shared__ uint32_t s_stage[kMaxWaves][kPullTile];   // per-wave staging of one tile's entries
     const uint64_t b = blockIdx.x, G = gridDim.x;
     unsigned long long bw = 0, be = 0, bl = 0, tw = 0, te = 0, tl = 0;
     for (uint64_t k = threadIdx.x; k < G; k += blockDim.x) {
@@ -576,7 +621,7 @@ __device__ __forceinline__ void collect_pass2(const CollectArgs& c, LevelCtr& lc
             al += s_l[k];
         }
         __syncthreads();
-        if (t < hi && x.w != 0) collect_tile(c, t, rw + ow, re + oe, rl + ol, write_fr);
+        if (t < hi && x.w != 0) collect_tile(c, t, rw + ow, re + oe, rl + ol, write_fr, s_stage[wid]);
         rw += aw;
         re += ae;
         rl += al;
@@ -645,7 +690,7 @@ __global__ __launch_bounds__(kBlock) void k_level_begin(int L, WaveCtr* ctr, con
 // entry holding its first edge (cstart). decide = 1 (multi-GPU levels): also sets T, nchunks and
 // a push decision (the driver overrides it for pull levels); decide = 0: k_level_begin decided.
 // After a pull level: collect pass 2 instead. kScanThreads-thread blocks.
-__global__ __launch_bounds__(kScanThreads) void k_scan_apply(int L, const uint32_t* __restrict__ fr_len,
+__global__ __launch_bounds__(kScanThreads, 4) void k_scan_apply(int L, const uint32_t* __restrict__ fr_len,
                                                      const unsigned long long* __restrict__ partials,
                                                      uint64_t* __restrict__ escan, uint32_t* __restrict__ cstart,
                                                      WaveCtr* ctr, int decide, CollectArgs ca, int direction,
@@ -1238,6 +1283,7 @@ static CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, uint32_t pgrid, 
     c.pgrid = pgrid;
     c.n_slots = n_slots;
     c.fb = fb;
+    c.n_handles = g->n_handles;
     c.clear_fb = clear;
     c.row_len = g->row_len;
     c.inv = g->inv;
