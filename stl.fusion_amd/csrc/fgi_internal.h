@@ -80,6 +80,8 @@ constexpr int kChunk = kBlock * kEPT;   // edges per expand chunk
 constexpr uint32_t kStatBlocks = 4096;  // per-block statistics rows (grid limit of the hot kernels)
 constexpr int kStatCols = 8;
 
+constexpr int kProbeBlocks = 2048;     // FGI_PROBE (measurement only): blocks and phases stamped
+constexpr int kProbePhases = 16;
 constexpr int kPullTile = 1024;        // slots per pull tile (one block iteration of a pull level)
 
 struct LevelCtr {
@@ -157,8 +159,9 @@ struct fgi_graph {
     uint64_t pool_epoch = 0;           // bumped on compaction (invalidates snapshots)
 
     // wave workspace
+    unsigned long long* probe = nullptr;   // FGI_PROBE: [kProbeBlocks][kProbePhases] timestamps
     uint32_t* inv = nullptr;           // [n_handles] invalidated handles of the last wave
-    uint32_t* fr_h[2] = {nullptr, nullptr};    // frontier lists: handles (row offsets are gathered by the push)
+    uint32_t* fr_off[2] = {nullptr, nullptr};  // frontier lists: row offsets (pool positions < 2^32)
     uint32_t* fr_len[2] = {nullptr, nullptr};
     uint64_t* escan = nullptr;         // [n_handles]
     uint32_t* cstart = nullptr;        // [cstart_cap]

@@ -816,7 +816,7 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
     const size_t H = g->n_handles;
     if (dmalloc(g, &g->node, H) || dmalloc(g, &g->row_off, H) || dmalloc(g, &g->row_len, H) ||
         dmalloc(g, &g->row_cap, H) || dmalloc(g, &g->used_cnt, H) || dmalloc(g, &g->home, g->n_detached + 1) ||
-        dmalloc(g, &g->inv, H) || dmalloc(g, &g->fr_h[0], H) || dmalloc(g, &g->fr_h[1], H) ||
+        dmalloc(g, &g->inv, H) || dmalloc(g, &g->fr_off[0], H) || dmalloc(g, &g->fr_off[1], H) ||
         dmalloc(g, &g->fr_len[0], H) || dmalloc(g, &g->fr_len[1], H) || dmalloc(g, &g->escan, H) ||
         dmalloc(g, &g->partials, 4 * kScanBlocks) || dmalloc(g, &g->ctr, 1) ||
         dmalloc(g, &g->blk_stats, (size_t)kStatBlocks * kStatCols) || dmalloc(g, &g->misc_dev, 16) ||
@@ -866,8 +866,9 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->pool_tag);
     dfree(g->pool_top_dev);
     dfree(g->inv);
+    dfree(g->probe);
     for (int i = 0; i < 2; ++i) {
-        dfree(g->fr_h[i]);
+        dfree(g->fr_off[i]);
         dfree(g->fr_len[i]);
     }
     dfree(g->escan);

@@ -27,7 +27,9 @@
 // k_apply_recv / k_clear_front, with the exchange between them.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
+#include <vector>
 #include <cstdio>
 #include <cstdlib>
 
@@ -114,11 +116,12 @@ __device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
 __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
 // Where a level's winners go: the invalidated list (all winners) and the next frontier (winners
-// with a non-empty row: handle and row length); the next level's F and T accumulate in ln.
+// with a non-empty row: row offset and length); the next level's F and T accumulate in ln.
 struct Out {
+    const uint64_t* __restrict__ row_off;
     const uint32_t* __restrict__ row_len;
     uint32_t* __restrict__ inv;
-    uint32_t* __restrict__ nfr_h;
+    uint32_t* __restrict__ nfr_off;   // row offsets (edge pool positions < 2^32)
     uint32_t* __restrict__ nfr_len;
     unsigned long long* inv_ctr;
     LevelCtr* ln;
@@ -171,11 +174,12 @@ __device__ __forceinline__ void block_stats_add(unsigned long long* blk, unsigne
 // Append one (possibly absent) winner per lane. Every lane of the wave must call it.
 __device__ __forceinline__ void emit_one(bool win, uint32_t h, const Out& o) {
     const uint32_t len = win ? o.row_len[h] : 0u;
+    const uint32_t off = (win && len) ? (uint32_t)o.row_off[h] : 0u;
     uint64_t ib, fb;
     wave_reserve(win ? 1u : 0u, (win && len) ? 1u : 0u, o.inv_ctr, &o.ln->F, ib, fb);
     if (win) o.inv[ib] = h;
     if (win && len) {
-        o.nfr_h[fb] = h;
+        o.nfr_off[fb] = off;
         o.nfr_len[fb] = len;
     }
     const unsigned long long ls = wave_sum64(len);
@@ -185,6 +189,7 @@ __device__ __forceinline__ void emit_one(bool win, uint32_t h, const Out& o) {
 // Block-level emission (push levels): winners are staged in LDS and appended to the global lists
 // in batches (one pair of global atomics per batch instead of one per wave per iteration).
 constexpr uint32_t kEmitCap = 1024;
+constexpr uint32_t kChunkEmitCap = 2 * kChunk;   // push levels: staged over the chunk map
 struct Emit {
     uint32_t n;
     uint32_t pad;
@@ -216,7 +221,7 @@ __device__ __forceinline__ void emit_push(Emit& e, uint32_t* buf, bool win, uint
             const uint32_t len = o.row_len[h];
             if (len) {
                 const unsigned long long fb = atomicAdd(&o.ln->F, 1ull);
-                o.nfr_h[fb] = h;
+                o.nfr_off[fb] = (uint32_t)o.row_off[h];
                 o.nfr_len[fb] = len;
                 atomicAdd(&o.ln->T, (unsigned long long)len);
             }
@@ -258,11 +263,12 @@ __device__ __forceinline__ void emit_flush(Emit& e, uint32_t* buf, uint32_t at, 
         if (k < wid) before += e.wsum[k];
         total += e.wsum[k];
     }
-    if (threadIdx.x == 0) {
+    // the three counters from three waves, so the atomics are in flight together
+    if (threadIdx.x == 0) e.base_inv = atomicAdd(o.inv_ctr, (unsigned long long)n);
+    if (threadIdx.x == 64) e.base_fr = total ? atomicAdd(&o.ln->F, (unsigned long long)total) : 0ull;
+    if (threadIdx.x == 128) {
         unsigned long long tl = 0;
         for (uint32_t k = 0; k < kBlock / 64; ++k) tl += e.wlen[k];
-        e.base_inv = atomicAdd(o.inv_ctr, (unsigned long long)n);
-        e.base_fr = total ? atomicAdd(&o.ln->F, (unsigned long long)total) : 0ull;
         if (tl) atomicAdd(&o.ln->T, tl);
     }
     __syncthreads();
@@ -276,7 +282,7 @@ __device__ __forceinline__ void emit_flush(Emit& e, uint32_t* buf, uint32_t at, 
             o.inv[e.base_inv + i] = h;
             const uint32_t len = o.row_len[h];
             if (len) {
-                o.nfr_h[fb] = h;
+                o.nfr_off[fb] = (uint32_t)o.row_off[h];
                 o.nfr_len[fb] = len;
                 ++fb;
             }
@@ -434,7 +440,8 @@ struct CollectArgs {
     int clear_fb;                // multi-GPU: the words are scratch, cleared after reading
     const uint32_t* __restrict__ row_len;
     uint32_t* inv;
-    uint32_t* fr_h;
+    const uint64_t* __restrict__ row_off;
+    uint32_t* fr_off;
     uint32_t* fr_len;
     uint64_t* escan;
     uint32_t* cstart;
@@ -516,15 +523,8 @@ __device__ __forceinline__ void collect_tile(const CollectArgs& c, uint64_t t, u
         __builtin_amdgcn_wave_barrier();
     }
     if (!write_fr || n_e == 0) return;
-    // expandable winners -> fr_h, fr_len, escan (+ cstart for every chunk whose first edge they hold)
+    // expandable winners -> fr_len, escan (+ cstart for every chunk whose first edge they hold), fr_off
     const uint32_t pe = pw >> 16;
-    {
-        uint32_t o = pe;
-        for (uint32_t mm = em; mm; mm &= mm - 1) stage[o++] = (uint32_t)base + (uint32_t)(__ffs(mm) - 1);
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t i = lane; i < n_e; i += 64) c.fr_h[be + i] = stage[i];
-        __builtin_amdgcn_wave_barrier();
-    }
     {
         uint32_t o = pe;
 #pragma unroll
@@ -547,6 +547,21 @@ __device__ __forceinline__ void collect_tile(const CollectArgs& c, uint64_t t, u
         }
         __builtin_amdgcn_wave_barrier();
         for (uint32_t i = lane; i < n_e; i += 64) c.escan[be + i] = bl + stage[i];
+        __builtin_amdgcn_wave_barrier();
+    }
+    {
+        // row offsets of the expandable slots only (sparse: a whole 128-B run per lane would fetch
+        // mostly unused offsets); low words suffice, pool positions are < 2^32
+        const uint32_t* off32 = reinterpret_cast<const uint32_t*>(c.row_off);
+        uint32_t ro[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) ro[k] = ((em >> k) & 1u) ? off32[2 * (base + k)] : 0u;
+        uint32_t o = pe;
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            if ((em >> k) & 1u) stage[o++] = ro[k];
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i = lane; i < n_e; i += 64) c.fr_off[be + i] = stage[i];
         __builtin_amdgcn_wave_barrier();
     }
 }
@@ -816,14 +831,22 @@ __device__ __forceinline__ uint32_t lds_upper_bound(const uint32_t* s, uint32_t 
 }
 
 struct ExpandArgs {
-    const uint32_t* __restrict__ fr_h;
-    const uint64_t* __restrict__ row_off;
+    const uint32_t* __restrict__ fr_off;
     const uint64_t* __restrict__ escan;
     const uint32_t* __restrict__ cstart;
     const uint32_t* __restrict__ pool_col;
     const uint64_t* __restrict__ pool_tag;
     int dead_filter;
+    unsigned long long* probe;   // measurement only (FGI_PROBE): per-block phase timestamps, else null
 };
+
+// FGI_PROBE: all of the block's memory operations drained, then a 100 MHz timestamp for phase k
+__device__ __forceinline__ void probe_at(unsigned long long* pr, int k) {
+    if (!pr) return;
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < kProbeBlocks) pr[blockIdx.x * kProbePhases + k] = __builtin_amdgcn_s_memrealtime();
+}
 
 // PART: multi-GPU rank — dependant slots outside [ra.base, ra.base + ra.n_local) are remote: their
 // tag is checked against the version replica and matching targets are forwarded once per wave.
@@ -837,18 +860,32 @@ __device__ __forceinline__ void expand_level(const LevelCtr& lc, const ExpandArg
     }
     const uint64_t T = lc.T, F = lc.F, nch = lc.nchunks;
     uint32_t matched = 0, flagged = 0;
+    probe_at(x.probe, 1);
     for (uint64_t c = blockIdx.x; c < nch; c += gridDim.x) {
         const uint64_t cbase = c * kChunk;
         const uint32_t clen = (uint32_t)((T - cbase) < (uint64_t)kChunk ? (T - cbase) : (uint64_t)kChunk);
         const uint32_t i0 = x.cstart[c];
         const uint32_t i1 = (c + 1 < nch) ? x.cstart[c + 1] : (uint32_t)(F - 1);
         const uint32_t n = i1 - i0 + 1;
-        for (uint32_t k = threadIdx.x; k < n; k += kBlock) {
-            const uint64_t es = x.escan[i0 + k];
-            s_rel[k] = es > cbase ? (uint32_t)(es - cbase) : 0u;
-            s_base[k] = (uint32_t)(x.row_off[x.fr_h[i0 + k]] + cbase - es);   // pool positions < 2^32
+        // n <= kChunk + 1 entries: every load issued before the first use
+        uint64_t fes[kEPT + 1];
+        uint32_t fof[kEPT + 1];
+#pragma unroll
+        for (int j = 0; j <= kEPT; ++j) {
+            const uint32_t k = threadIdx.x + j * kBlock;
+            fes[j] = k < n ? x.escan[i0 + k] : 0ull;
+            fof[j] = k < n ? x.fr_off[i0 + k] : 0u;
+        }
+#pragma unroll
+        for (int j = 0; j <= kEPT; ++j) {
+            const uint32_t k = threadIdx.x + j * kBlock;
+            if (k < n) {
+                s_rel[k] = fes[j] > cbase ? (uint32_t)(fes[j] - cbase) : 0u;
+                s_base[k] = (uint32_t)((uint64_t)fof[j] + cbase - fes[j]);   // pool positions < 2^32
+            }
         }
         __syncthreads();
+        probe_at(x.probe, 2);
         uint32_t dst[kEPT];
         uint64_t pos[kEPT];
 #pragma unroll
@@ -862,6 +899,7 @@ __device__ __forceinline__ void expand_level(const LevelCtr& lc, const ExpandArg
                 dst[j] = __builtin_nontemporal_load(x.pool_col + pos[j]);
             }
         }
+        probe_at(x.probe, 3);
         // remote dependants (PART): forwarded at most once per wave, only on a version match
         if constexpr (PART) {
 #pragma unroll
@@ -892,6 +930,7 @@ __device__ __forceinline__ void expand_level(const LevelCtr& lc, const ExpandArg
             for (int j = 0; j < kEPT; ++j)
                 if (dst[j] != 0xFFFFFFFFu && bit_of(vis, dst[j])) dst[j] = 0xFFFFFFFFu;
         }
+        probe_at(x.probe, 4);
         uint64_t tag[kEPT];
         unsigned long long w[kEPT];
 #pragma unroll
@@ -903,6 +942,7 @@ __device__ __forceinline__ void expand_level(const LevelCtr& lc, const ExpandArg
                 w[j] = node[dst[j]];
             }
         }
+        probe_at(x.probe, 5);
         uint32_t win_mask = 0;
 #pragma unroll
         for (int j = 0; j < kEPT; ++j) {
@@ -913,15 +953,22 @@ __device__ __forceinline__ void expand_level(const LevelCtr& lc, const ExpandArg
                 else if (r == 2) ++flagged;
             }
         }
+        probe_at(x.probe, 6);
+        // the chunk's winners (at most kChunk) are staged over the chunk map, flushed before the
+        // next chunk refills it
+        __syncthreads();
 #pragma unroll
-        for (int j = 0; j < kEPT; ++j) emit_push<kEmitCap>(em, eb, (win_mask >> j) & 1u, dst[j], o);
-        emit_flush<kEmitCap>(em, eb, kEmitCap / 2, o);
+        for (int j = 0; j < kEPT; ++j) emit_push<kChunkEmitCap>(em, eb, (win_mask >> j) & 1u, dst[j], o);
+        probe_at(x.probe, 7);
+        emit_flush<kChunkEmitCap>(em, eb, 1, o);
+        probe_at(x.probe, 8);
         if constexpr (PART) msg_flush(me, kMsgCap / 2, ra);
     }
-    emit_flush<kEmitCap>(em, eb, 1, o);
+    probe_at(x.probe, 9);
     if constexpr (PART) msg_flush(me, 1, ra);
     const uint32_t v[kStats] = {matched, flagged, 0, 0, 0, 0, 0, 0};
     block_stats_add(blk, s_st, v);
+    probe_at(x.probe, 10);
 }
 
 // ---- pull: every live slot looks for a parent in the frontier ---------------------------------
@@ -1134,13 +1181,16 @@ template <bool PART>
 __global__ __launch_bounds__(kBlock, 6) void k_level(int L, ExpandArgs x, PullArgs p, const unsigned long long* node,
                                                   uint32_t* vis, Out o, WaveCtr* ctr, unsigned long long* blk,
                                                   RemoteArgs ra) {
-    __shared__ uint32_t s_rel[kChunk + 1];
-    __shared__ __align__(16) uint32_t s_base[kChunk + 2];
+    // push: the chunk map (s_rel, s_base), then the chunk's winners over it; pull: queue + buffers
+    __shared__ __align__(16) uint32_t s_x[kChunkEmitCap + 8];
+    uint32_t* s_rel = s_x;                    // [kChunk + 1]
+    uint32_t* s_base = s_x + kChunk + 4;      // [kChunk + 2], 16-byte aligned
     __shared__ Emit em;
-    __shared__ uint32_t eb[kEmitCap];
     __shared__ MsgEmit<PART> me;
     __shared__ unsigned long long s_st[kBlock / 64][kStats];
     static_assert((2 * kMaxIter * kTileWords + kMaxIter) * 8 + 3 * kMaxIter * 4 + 4 <= (kChunk + 2) * 4, "pull LDS");
+    if (x.probe && threadIdx.x == 0 && blockIdx.x < kProbeBlocks)
+        x.probe[blockIdx.x * kProbePhases] = __builtin_amdgcn_s_memrealtime();
     const LevelCtr& lc = ctr->lvl[L % kRing];
     o.ln = &ctr->lvl[(L + 1) % kRing];
     if (blockIdx.x == 0 && threadIdx.x < sizeof(LevelCtr) / 8)
@@ -1151,7 +1201,7 @@ __global__ __launch_bounds__(kBlock, 6) void k_level(int L, ExpandArgs x, PullAr
         pull_level(p, node, vis, s_rel, reinterpret_cast<unsigned long long*>(s_base), blk, s_st);
     } else {
         emit_init(em);
-        expand_level<PART>(lc, x, node, vis, o, em, eb, me, s_rel, s_base, blk, s_st, ra);
+        expand_level<PART>(lc, x, node, vis, o, em, s_x, me, s_rel, s_base, blk, s_st, ra);
     }
 }
 
@@ -1276,6 +1326,34 @@ static unsigned event_flags() {
     return f;
 }
 
+// FGI_PROBE (measurement only): median per-phase offsets (us) of a push level's stamped blocks
+static fgi_status probe_report(fgi_graph* g, int L, uint32_t grid) {
+    std::vector<unsigned long long> h((size_t)kProbeBlocks * kProbePhases);
+    FGI_HIP(g, hipStreamSynchronize(g->stream));
+    FGI_HIP(g, hipMemcpy(h.data(), g->probe, h.size() * 8, hipMemcpyDeviceToHost));
+    const uint32_t nb = std::min<uint32_t>(grid, kProbeBlocks);
+    unsigned long long t0 = ~0ull, t_end = 0;
+    for (uint32_t b = 0; b < nb; ++b)
+        if (h[(size_t)b * kProbePhases]) {
+            t0 = std::min(t0, h[(size_t)b * kProbePhases]);
+            t_end = std::max(t_end, h[(size_t)b * kProbePhases + 10]);
+        }
+    fprintf(stderr, "[probe] level %d span %.2f us; median phase stamps (us after first block start):", L,
+            t0 == ~0ull ? 0.0 : (t_end - t0) / 100.0);
+    for (int k = 0; k <= 10; ++k) {
+        std::vector<double> v;
+        for (uint32_t b = 0; b < nb; ++b) {
+            const unsigned long long x = h[(size_t)b * kProbePhases + k];
+            if (x && h[(size_t)b * kProbePhases + 2]) v.push_back((x - t0) / 100.0);   // blocks with a chunk
+        }
+        if (v.empty()) continue;
+        std::sort(v.begin(), v.end());
+        fprintf(stderr, " p%d=%.2f/%.2f", k, v[v.size() / 2], v.back());
+    }
+    fprintf(stderr, "\n");
+    return FGI_OK;
+}
+
 static CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, uint32_t pgrid, uint32_t* fb, int clear, int buf) {
     CollectArgs c;
     c.tiles = g->tiles;
@@ -1287,7 +1365,8 @@ static CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, uint32_t pgrid, 
     c.clear_fb = clear;
     c.row_len = g->row_len;
     c.inv = g->inv;
-    c.fr_h = g->fr_h[buf];
+    c.row_off = g->row_off;
+    c.fr_off = g->fr_off[buf];
     c.fr_len = g->fr_len[buf];
     c.escan = g->escan;
     c.cstart = g->cstart;
@@ -1307,6 +1386,8 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     hipStream_t s = g->stream;
     static const bool trace = getenv("FGI_TRACE") != nullptr;
     static const bool no_level_events = getenv("FGI_NO_LEVEL_EVENTS") != nullptr;   // measurement only
+    static const bool probe = getenv("FGI_PROBE") != nullptr;                        // measurement only
+    if (probe && !g->probe) FGI_HIP(g, hipMalloc(&g->probe, sizeof(unsigned long long) * kProbeBlocks * kProbePhases));
     const bool timing = (stats != nullptr || trace) && !no_level_events;
     FGI_TRY(ensure_cstart(g, g->pool_top));
     FGI_TRY(ensure_cls(g));
@@ -1322,7 +1403,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     FGI_HIP(g, hipMemsetAsync(g->blk_stats, 0, sizeof(unsigned long long) * kStatBlocks * kStatCols, s));
     FGI_HIP(g, hipMemsetAsync(fb[0], 0, g->bm_words * 4, s));
     if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
-    Out o{g->row_len, g->inv, g->fr_h[0], g->fr_len[0], &g->ctr->inv, &g->ctr->lvl[0]};
+    Out o{g->row_off, g->row_len, g->inv, g->fr_off[0], g->fr_len[0], &g->ctr->inv, &g->ctr->lvl[0]};
     if (n_roots) {
         g->v_dirty = true;
         const uint32_t nb = (n_roots + kBlock - 1) / kBlock;
@@ -1366,14 +1447,17 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                 }
                 FGI_HIP(g, hipEventRecord(g->ev[2 * L], s));
             }
-            const ExpandArgs xa{g->fr_h[buf], g->row_off, g->escan, g->cstart, g->pool_col, g->pool_tag, g->opt_dead_filter};
+            if (probe) FGI_HIP(g, hipMemsetAsync(g->probe, 0, sizeof(unsigned long long) * kProbeBlocks * kProbePhases, s));
+            const ExpandArgs xa{g->fr_off[buf], g->escan,    g->cstart,
+                                g->pool_col, g->pool_tag, g->opt_dead_filter, probe ? g->probe : nullptr};
             const PullArgs pa{g->n_slots, g->uin_off, g->uin_len, g->uin_src, g->uin_head, g->uin_more,
                               fb[buf],    fb[buf ^ 1], g->cls_bm, g->row_len, g->tiles};
-            Out ol{g->row_len, g->inv, g->fr_h[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv, nullptr};
+            Out ol{g->row_off, g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv, nullptr};
             hipLaunchKernelGGL(k_level<false>, dim3(level_grid), dim3(kBlock), 0, s, L, xa, pa,
                                reinterpret_cast<const unsigned long long*>(g->node), g->vis_bm, ol, g->ctr,
                                g->blk_stats, RemoteArgs{});
             if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L + 1], s));
+            if (probe) FGI_TRY(probe_report(g, L, level_grid));
         }
         hipLaunchKernelGGL(k_stats_reduce, dim3(kStats + 1), dim3(kBlock), 0, s, g->blk_stats, g->ctr, L, g->tiles,
                            n_tiles);
@@ -1512,7 +1596,7 @@ fgi_status part_wave_begin(fgi_graph* g, uint32_t n_roots, const uint32_t* roots
     }
     FGI_HIP(g, hipEventRecord(g->ev_w0, s));
     g->v_dirty = true;
-    const Out o{g->row_len, g->inv, g->fr_h[0], g->fr_len[0], &g->ctr->inv, &g->ctr->lvl[0]};
+    const Out o{g->row_off, g->row_len, g->inv, g->fr_off[0], g->fr_len[0], &g->ctr->inv, &g->ctr->lvl[0]};
     auto* node = reinterpret_cast<unsigned long long*>(g->node);
     if (n_roots) {
         const uint32_t nb = (n_roots + kBlock - 1) / kBlock;
@@ -1569,10 +1653,10 @@ fgi_status part_level_work(fgi_graph* g, int L, bool pull) {
     const RemoteArgs ra{pv.base, pv.n_local, pv.block, pv.world, pv.ver_all, pv.sent_bm, pv.send_buf, pv.send_cnt};
     const int buf = L & 1;
     FGI_HIP(g, hipEventRecord(g->ev[0], s));
-    const ExpandArgs xa{g->fr_h[buf], g->row_off, g->escan, g->cstart, g->pool_col, g->pool_tag, g->opt_dead_filter};
+    const ExpandArgs xa{g->fr_off[buf], g->escan, g->cstart, g->pool_col, g->pool_tag, g->opt_dead_filter, nullptr};
     const PullArgs pa{pv.n_local,      g->uin_off,  g->uin_len, g->uin_src,  g->uin_head, g->uin_more,
                       pv.front_global, g->front_nx, g->cls_bm,  g->row_len, g->tiles};
-    const Out o{g->row_len, g->inv, g->fr_h[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv, nullptr};
+    const Out o{g->row_off, g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv, nullptr};
     hipLaunchKernelGGL(k_level<true>, dim3(part_grid(g)), dim3(kBlock), 0, s, L, xa, pa,
                        reinterpret_cast<const unsigned long long*>(g->node), g->vis_bm, o, g->ctr, g->blk_stats, ra);
     FGI_HIP(g, hipEventRecord(g->ev[1], s));
@@ -1593,7 +1677,7 @@ fgi_status part_level_apply(fgi_graph* g, int L, uint64_t n_recv, uint64_t n_sen
         hipLaunchKernelGGL(k_apply_recv, dim3(std::min<uint64_t>((n_recv + kBlock - 1) / kBlock, (uint64_t)n_cu * 8)),
                            dim3(kBlock), 0, s, L, n_recv, pv.recv_buf, pv.base,
                            reinterpret_cast<const unsigned long long*>(g->node), g->vis_bm,
-                           Out{g->row_len, g->inv, g->fr_h[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv,
+                           Out{g->row_off, g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv,
                                nullptr},
                            g->ctr, g->blk_stats);
     const uint64_t n_tiles = pull_iters(pv.n_local, part_grid(g)) * part_grid(g);
