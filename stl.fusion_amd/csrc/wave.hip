@@ -987,6 +987,7 @@ struct PullArgs {
     const uint32_t* __restrict__ cls;        // expandable-class bitmap
     const uint32_t* __restrict__ row_len;
     PullTile* tiles;
+    unsigned long long* probe;   // measurement only (FGI_PROBE)
 };
 
 // A block owns tile (it, block) of every iteration: kPullTile consecutive slots, kPS per lane
@@ -1065,6 +1066,27 @@ __device__ __forceinline__ void pull_flush(const PullArgs& p, const unsigned lon
     __syncthreads();
 }
 
+// One iteration's per-slot words of a wave (kPS slots per lane, 64 apart): visit, class and "more"
+// bitmap words (the 32-bit word holding the lane's bit), the two list heads and the row length.
+struct PullSlots {
+    uint32_t vw[kPS], cw[kPS], mw[kPS], rl[kPS];
+    uint64_t hd[kPS];
+};
+
+__device__ __forceinline__ void pull_load(const PullArgs& p, const uint32_t* vis, uint64_t d0, uint32_t lane,
+                                          PullSlots& x) {
+#pragma unroll
+    for (int j = 0; j < (int)kPS; ++j) {
+        const uint64_t d = d0 + j * 64 + lane;
+        const bool in = d < p.n_slots;
+        x.vw[j] = in ? vis[d >> 5] : ~0u;
+        x.cw[j] = in ? p.cls[d >> 5] : 0u;
+        x.mw[j] = in ? p.uin_more[d >> 5] : 0u;
+        x.hd[j] = in ? __builtin_nontemporal_load(p.uin_head + d) : ~0ull;
+        x.rl[j] = in ? p.row_len[d] : 0u;
+    }
+}
+
 __device__ __forceinline__ void pull_level(const PullArgs& p, const unsigned long long* node, uint32_t* vis,
                                            uint32_t* lds_q, unsigned long long* lds_buf, unsigned long long* blk,
                                            unsigned long long (*s_st)[kStats]) {
@@ -1085,44 +1107,43 @@ __device__ __forceinline__ void pull_level(const PullArgs& p, const unsigned lon
     }
     if (threadIdx.x == 0) *s_qn = 0;
     __syncthreads();
-    constexpr uint64_t kNoHeads = ~0ull;
     uint32_t it_base = 0;
+    // the slot words of iteration it + 1 are loaded while iteration it waits for its frontier bits
+    PullSlots cur;
+    pull_load(p, vis, (uint64_t)blockIdx.x * kPullTile + wid * (64 * kPS), lane, cur);
     for (uint32_t it = 0; it < n_iter; ++it) {
         const uint32_t k = it - it_base;
         const uint64_t s0 = (uint64_t)it * stride + (uint64_t)blockIdx.x * kPullTile;
         const uint64_t d0 = s0 + wid * (64 * kPS);
-        // bitmap words are loaded per lane as the 32-bit word holding the lane's bit (the two
-        // halves of a wave read two addresses; 64-bit words would cost twice the registers)
-        uint32_t vw[kPS], cw[kPS], mw[kPS], rl[kPS];
-        uint64_t hd[kPS];
-#pragma unroll
-        for (int j = 0; j < (int)kPS; ++j) {
-            const uint64_t d = d0 + j * 64 + lane;
-            const bool in = d < p.n_slots;
-            vw[j] = in ? vis[d >> 5] : ~0u;
-            cw[j] = in ? p.cls[d >> 5] : 0u;
-            mw[j] = in ? p.uin_more[d >> 5] : 0u;
-            hd[j] = in ? __builtin_nontemporal_load(p.uin_head + d) : kNoHeads;
-            rl[j] = in ? p.row_len[d] : 0u;
-        }
-        bool hit[kPS], tail[kPS];
+        const uint32_t* vw = cur.vw;
+        const uint32_t* cw = cur.cw;
+        const uint32_t* mw = cur.mw;
+        const uint32_t* rl = cur.rl;
+        bool c[kPS];
+        uint32_t f0[kPS], f1[kPS];
 #pragma unroll
         for (int j = 0; j < (int)kPS; ++j) {
             const uint64_t d = d0 + j * 64 + lane;
             const bool lv = d < p.n_slots && !((vw[j] >> (lane & 31)) & 1u);
-            const uint32_t h0 = (uint32_t)hd[j], h1 = (uint32_t)(hd[j] >> 32);
-            const bool c = lv && h0 != FGI_NONE;
-            bool b0 = false, b1 = false;
-            if (c) {
-                b0 = bit_of(p.front_rd, h0);
-                b1 = h1 != FGI_NONE && bit_of(p.front_rd, h1);
-            }
-            // statistics as wave-uniform counts (scalar registers), reported by lane 0
+            const uint32_t h0 = (uint32_t)cur.hd[j], h1 = (uint32_t)(cur.hd[j] >> 32);
+            c[j] = lv && h0 != FGI_NONE;
+            f0[j] = c[j] ? p.front_rd[h0 >> 5] : 0u;
+            f1[j] = (c[j] && h1 != FGI_NONE) ? p.front_rd[h1 >> 5] : 0u;
             live += (uint32_t)__popcll(__ballot(lv));
-            cand += (uint32_t)__popcll(__ballot(c));
-            examined += (uint32_t)__popcll(__ballot(c)) + (uint32_t)__popcll(__ballot(c && h1 != FGI_NONE && !b0));
+        }
+        PullSlots nxt;
+        pull_load(p, vis, d0 + stride, lane, nxt);
+        bool hit[kPS], tail[kPS];
+#pragma unroll
+        for (int j = 0; j < (int)kPS; ++j) {
+            const uint32_t h0 = (uint32_t)cur.hd[j], h1 = (uint32_t)(cur.hd[j] >> 32);
+            const bool b0 = c[j] && ((f0[j] >> (h0 & 31)) & 1u);
+            const bool b1 = c[j] && h1 != FGI_NONE && ((f1[j] >> (h1 & 31)) & 1u);
+            // statistics as wave-uniform counts (scalar registers), reported by lane 0
+            cand += (uint32_t)__popcll(__ballot(c[j]));
+            examined += (uint32_t)__popcll(__ballot(c[j])) + (uint32_t)__popcll(__ballot(c[j] && h1 != FGI_NONE && !b0));
             hit[j] = b0 || b1;
-            tail[j] = c && !hit[j] && ((mw[j] >> (lane & 31)) & 1u);
+            tail[j] = c[j] && !hit[j] && ((mw[j] >> (lane & 31)) & 1u);
         }
         uint32_t nw = 0, ne = 0;
         unsigned long long nl = 0;
@@ -1156,16 +1177,20 @@ __device__ __forceinline__ void pull_level(const PullArgs& p, const unsigned lon
             if (ne) atomicAdd(&s_ce[k], ne);
             if (nl) atomicAdd(&s_cl[k], nl);
         }
+        if (it == 0) probe_at(p.probe, 1);
         // flush when the LDS buffers are full, the queue could overflow next time, or at the end
         const bool full = k + 1 == kMaxIter || it + 1 == n_iter;
         if (__syncthreads_or(full || q_end > kTailCap - kPullTile)) {
             const uint32_t nq = *s_qn;
+            probe_at(p.probe, it + 1 == n_iter ? 4 : 2);
             pull_flush(p, node, vis, it_base, k + 1, lds_q, nq, s_vm, s_wm, s_cw, s_ce, s_cl, flagged, examined_tail,
                        wins_tail, tails);
             if (threadIdx.x == 0) *s_qn = 0;
             __syncthreads();
+            probe_at(p.probe, it + 1 == n_iter ? 5 : 3);
             it_base = it + 1;
         }
+        cur = nxt;
     }
     const uint32_t scan = (blockIdx.x == 0 && threadIdx.x == 0) ? p.n_slots : 0u;
     // cand, live, wins and the head probes of `examined` are wave-uniform counts; the tail probes
@@ -1174,11 +1199,12 @@ __device__ __forceinline__ void pull_level(const PullArgs& p, const unsigned lon
     const uint32_t v[kStats] = {0, flagged, l0 ? cand : 0u, examined_tail + (l0 ? examined : 0u), l0 ? live : 0u,
                                 wins_tail + (l0 ? wins : 0u), tails, scan};
     block_stats_add(blk, s_st, v);
+    probe_at(p.probe, 10);
 }
 
 // One level's traversal: push (expand) or pull, as decided for the level on the device.
 template <bool PART>
-__global__ __launch_bounds__(kBlock, 6) void k_level(int L, ExpandArgs x, PullArgs p, const unsigned long long* node,
+__global__ __launch_bounds__(kBlock, 5) void k_level(int L, ExpandArgs x, PullArgs p, const unsigned long long* node,
                                                   uint32_t* vis, Out o, WaveCtr* ctr, unsigned long long* blk,
                                                   RemoteArgs ra) {
     // push: the chunk map (s_rel, s_base), then the chunk's winners over it; pull: queue + buffers
@@ -1189,8 +1215,8 @@ __global__ __launch_bounds__(kBlock, 6) void k_level(int L, ExpandArgs x, PullAr
     __shared__ MsgEmit<PART> me;
     __shared__ unsigned long long s_st[kBlock / 64][kStats];
     static_assert((2 * kMaxIter * kTileWords + kMaxIter) * 8 + 3 * kMaxIter * 4 + 4 <= (kChunk + 2) * 4, "pull LDS");
-    if (x.probe && threadIdx.x == 0 && blockIdx.x < kProbeBlocks)
-        x.probe[blockIdx.x * kProbePhases] = __builtin_amdgcn_s_memrealtime();
+    if ((x.probe || p.probe) && threadIdx.x == 0 && blockIdx.x < kProbeBlocks)
+        (x.probe ? x.probe : p.probe)[blockIdx.x * kProbePhases] = __builtin_amdgcn_s_memrealtime();
     const LevelCtr& lc = ctr->lvl[L % kRing];
     o.ln = &ctr->lvl[(L + 1) % kRing];
     if (blockIdx.x == 0 && threadIdx.x < sizeof(LevelCtr) / 8)
@@ -1344,7 +1370,8 @@ static fgi_status probe_report(fgi_graph* g, int L, uint32_t grid) {
         std::vector<double> v;
         for (uint32_t b = 0; b < nb; ++b) {
             const unsigned long long x = h[(size_t)b * kProbePhases + k];
-            if (x && h[(size_t)b * kProbePhases + 2]) v.push_back((x - t0) / 100.0);   // blocks with a chunk
+            if (x && (h[(size_t)b * kProbePhases + 2] || h[(size_t)b * kProbePhases + 4]))
+                v.push_back((x - t0) / 100.0);   // blocks with a chunk (push) / pulling blocks
         }
         if (v.empty()) continue;
         std::sort(v.begin(), v.end());
@@ -1415,8 +1442,8 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         hipLaunchKernelGGL(k_roots<0>, dim3(nb), dim3(kBlock), 0, s, roots_dev, imm_dev, n_roots, 0u, g->n_handles, node,
                            g->vis_bm, o, g->ctr);
     }
-    // 6 resident blocks per CU; per-block statistics bound the grid
-    const uint32_t level_grid = level_grid_for(g, 6);
+    // 5 resident blocks per CU (k_level launch bounds); per-block statistics bound the grid
+    const uint32_t level_grid = level_grid_for(g, 5);
     const uint64_t slot_words = ((uint64_t)g->n_slots + 63) / 64 * 2;
     const uint64_t n_tiles = pull_iters(g->n_slots, level_grid) * level_grid;
     // Levels run in groups between host synchronisations (one ~30 us round trip each); the first
@@ -1450,8 +1477,9 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
             if (probe) FGI_HIP(g, hipMemsetAsync(g->probe, 0, sizeof(unsigned long long) * kProbeBlocks * kProbePhases, s));
             const ExpandArgs xa{g->fr_off[buf], g->escan,    g->cstart,
                                 g->pool_col, g->pool_tag, g->opt_dead_filter, probe ? g->probe : nullptr};
-            const PullArgs pa{g->n_slots, g->uin_off, g->uin_len, g->uin_src, g->uin_head, g->uin_more,
-                              fb[buf],    fb[buf ^ 1], g->cls_bm, g->row_len, g->tiles};
+            const PullArgs pa{g->n_slots, g->uin_off, g->uin_len, g->uin_src,  g->uin_head,
+                              g->uin_more, fb[buf], fb[buf ^ 1], g->cls_bm, g->row_len,
+                              g->tiles,   probe ? g->probe : nullptr};
             Out ol{g->row_off, g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv, nullptr};
             hipLaunchKernelGGL(k_level<false>, dim3(level_grid), dim3(kBlock), 0, s, L, xa, pa,
                                reinterpret_cast<const unsigned long long*>(g->node), g->vis_bm, ol, g->ctr,
@@ -1553,9 +1581,10 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         stats->pull_levels += pull_levels;
         stats->pull_edges += c.pull_edges;
         // Algorithmic bytes. Push level, per traversed edge: col 4 + tag 8 +
-        // node-word gather 8; per frontier entry: fr_len 4 x2, escan 8 w + 8 r, fr_off 8 r, written
-        // 12 by the producer. Per invalidated node: row gathers 12 + list write 4. Per root 5.
-        const uint64_t push_b = 20 * expand_edges + 44 * expand_f;
+        // node-word gather 8; per frontier entry: fr_len 4 x2, escan 8 w + 8 r, fr_off 4 r, written
+        // 8 (offset, length) by the producer. Per invalidated node: row gathers 12 + list write 4.
+        // Per root 5.
+        const uint64_t push_b = 20 * expand_edges + 36 * expand_f;
         const uint64_t pull_b = pull_level_bytes(c);
         stats->alg_bytes += push_b + pull_b + 16 * v + 5ull * n_roots;
         float wave_ms = 0;
@@ -1655,7 +1684,7 @@ fgi_status part_level_work(fgi_graph* g, int L, bool pull) {
     FGI_HIP(g, hipEventRecord(g->ev[0], s));
     const ExpandArgs xa{g->fr_off[buf], g->escan, g->cstart, g->pool_col, g->pool_tag, g->opt_dead_filter, nullptr};
     const PullArgs pa{pv.n_local,      g->uin_off,  g->uin_len, g->uin_src,  g->uin_head, g->uin_more,
-                      pv.front_global, g->front_nx, g->cls_bm,  g->row_len, g->tiles};
+                      pv.front_global, g->front_nx, g->cls_bm,  g->row_len, g->tiles, nullptr};
     const Out o{g->row_off, g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv, nullptr};
     hipLaunchKernelGGL(k_level<true>, dim3(part_grid(g)), dim3(kBlock), 0, s, L, xa, pa,
                        reinterpret_cast<const unsigned long long*>(g->node), g->vis_bm, o, g->ctr, g->blk_stats, ra);
@@ -1731,7 +1760,7 @@ fgi_status part_wave_end(fgi_graph* g, fgi_wave_stats* stats) {
         // as run_wave (push and pull levels), plus 8 B per forwarded target (written + received)
         const WaveCtr& c = *g->ctr_host;
         const uint64_t pull_b = pull_level_bytes(c);
-        stats->alg_bytes += 20 * w.push_edges + 44 * w.push_f + pull_b + 16 * v + 8 * w.sent + 5ull * w.n_roots;
+        stats->alg_bytes += 20 * w.push_edges + 36 * w.push_f + pull_b + 16 * v + 8 * w.sent + 5ull * w.n_roots;
         stats->pull_levels += w.pull_levels;
         stats->pull_edges += c.pull_edges;
         stats->pull_ms += w.pull_ms;
