@@ -218,10 +218,14 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *   FGI_OPT_DEAD_FILTER [1]  skip edges whose dependant was invalidated in an earlier level using
  *                            a per-wave bitmap (E_match then counts examined edges only)
  *   FGI_OPT_DIRECTION   [0]  0 auto (push/pull per level), 1 push only, 2 pull only
- *   FGI_OPT_PULL_ALPHA  [14] auto: pull when frontier edges > total edges / alpha */
+ *   FGI_OPT_PULL_ALPHA  [14] auto: pull when frontier edges > total edges / alpha
+ *   FGI_OPT_LEVEL_TIMING [1] with a stats argument, time every level's traversal launch with HIP
+ *                            events (per-kernel figures for the roofline); 0 keeps only the
+ *                            wave-boundary events, so measured waves carry no per-level markers */
 #define FGI_OPT_DEAD_FILTER 1
 #define FGI_OPT_DIRECTION 2
 #define FGI_OPT_PULL_ALPHA 3
+#define FGI_OPT_LEVEL_TIMING 4
 fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value);
 
 /* ---- multi-GPU (1-D vertex-range partition, RCCL all-to-all frontier exchange) --------------- */

@@ -1185,6 +1185,7 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
         if (value < 1) return set_err(g, FGI_EINVAL, "alpha must be >= 1");
         g->opt_pull_alpha = (int)value;
         return FGI_OK;
+    case FGI_OPT_LEVEL_TIMING: g->opt_level_timing = value ? 1 : 0; return FGI_OK;
     default: return set_err(g, FGI_EINVAL, "unknown option %d", option);
     }
 }

@@ -1415,7 +1415,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     static const bool no_level_events = getenv("FGI_NO_LEVEL_EVENTS") != nullptr;   // measurement only
     static const bool probe = getenv("FGI_PROBE") != nullptr;                        // measurement only
     if (probe && !g->probe) FGI_HIP(g, hipMalloc(&g->probe, sizeof(unsigned long long) * kProbeBlocks * kProbePhases));
-    const bool timing = (stats != nullptr || trace) && !no_level_events;
+    const bool timing = (stats != nullptr || trace) && !no_level_events && g->opt_level_timing;
     FGI_TRY(ensure_cstart(g, g->pool_top));
     FGI_TRY(ensure_cls(g));
     // Pull levels need the dependency-list cache. It is built lazily: while it is stale, levels
@@ -1681,14 +1681,14 @@ fgi_status part_level_work(fgi_graph* g, int L, bool pull) {
     hipStream_t s = g->stream;
     const RemoteArgs ra{pv.base, pv.n_local, pv.block, pv.world, pv.ver_all, pv.sent_bm, pv.send_buf, pv.send_cnt};
     const int buf = L & 1;
-    FGI_HIP(g, hipEventRecord(g->ev[0], s));
+    if (g->opt_level_timing) FGI_HIP(g, hipEventRecord(g->ev[0], s));
     const ExpandArgs xa{g->fr_off[buf], g->escan, g->cstart, g->pool_col, g->pool_tag, g->opt_dead_filter, nullptr};
     const PullArgs pa{pv.n_local,      g->uin_off,  g->uin_len, g->uin_src,  g->uin_head, g->uin_more,
                       pv.front_global, g->front_nx, g->cls_bm,  g->row_len, g->tiles, nullptr};
     const Out o{g->row_off, g->row_len, g->inv, g->fr_off[buf ^ 1], g->fr_len[buf ^ 1], &g->ctr->inv, nullptr};
     hipLaunchKernelGGL(k_level<true>, dim3(part_grid(g)), dim3(kBlock), 0, s, L, xa, pa,
                        reinterpret_cast<const unsigned long long*>(g->node), g->vis_bm, o, g->ctr, g->blk_stats, ra);
-    FGI_HIP(g, hipEventRecord(g->ev[1], s));
+    if (g->opt_level_timing) FGI_HIP(g, hipEventRecord(g->ev[1], s));
     if (pull) FGI_HIP(g, hipMemsetAsync(pv.front_global, 0, pv.front_words_global * 4, s));
     FGI_HIP(g, hipGetLastError());
     g->pw.pulled = pull;
@@ -1727,7 +1727,7 @@ fgi_status part_level_account(fgi_graph* g, int L) {
     g->pw.f_total += lc.F;
     if (!lc.pull) g->pw.push_edges += lc.T, g->pw.push_f += lc.F;
     float ms = 0;
-    FGI_HIP(g, hipEventElapsedTime(&ms, g->ev[0], g->ev[1]));
+    if (g->opt_level_timing) FGI_HIP(g, hipEventElapsedTime(&ms, g->ev[0], g->ev[1]));
     if (g->pw.pulled) {
         g->pw.pull_ms += ms;
         g->pw.pull_launches++;
