@@ -48,6 +48,9 @@ def cpu_baseline(threads: int, scale: int = 20, edge_factor: int = 16, roots: in
     r = fgo.gen_roots(roots, n, 0x5EED1024, deg)
     o.snapshot()
     build_s = time.time() - t0
+    for k, v in (("FGI_PULL_ALPHA", "OPT_PULL_ALPHA"), ("FGI_PULL_BETA", "OPT_PULL_BETA")):
+        if os.environ.get(k):   # measurement knobs (results never depend on them)
+            g.set_option(getattr(pkg.fgi, v), int(os.environ[k]))
 
     def timed(th):
         o.restore()
@@ -161,6 +164,9 @@ def main():
         roots = W.roots_for(g, cfg)
         _, n_edges = g.degrees()
     build_s = time.time() - t0
+    for k, v in (("FGI_PULL_ALPHA", "OPT_PULL_ALPHA"), ("FGI_PULL_BETA", "OPT_PULL_BETA")):
+        if os.environ.get(k):   # measurement knobs (results never depend on them)
+            g.set_option(getattr(pkg.fgi, v), int(os.environ[k]))
     d_roots = torch.from_numpy(roots.astype(np.int32)).to(f"cuda:{local_rank}")
     g.snapshot()
     log(f"[rank {rank}] built {args.config} (scale {cfg.get('scale')}): {n} slots, {n_edges} edges, "

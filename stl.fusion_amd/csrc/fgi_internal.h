@@ -213,6 +213,7 @@ struct fgi_graph {
     int opt_dead_filter = 1;
     int opt_direction = 0;
     int opt_pull_alpha = 14;
+    int opt_pull_beta = 24;           // after a pull, pull again while the frontier exceeds n / beta
     int opt_level_timing = 1;         // HIP events around each level's k_level launch (statistics)
 
     // generic scratch (sorts, batches)

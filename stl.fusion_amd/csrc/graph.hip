@@ -1186,6 +1186,10 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
         g->opt_pull_alpha = (int)value;
         return FGI_OK;
     case FGI_OPT_LEVEL_TIMING: g->opt_level_timing = value ? 1 : 0; return FGI_OK;
+    case FGI_OPT_PULL_BETA:
+        if (value < 0) return set_err(g, FGI_EINVAL, "beta must be >= 0");
+        g->opt_pull_beta = (int)value;
+        return FGI_OK;
     default: return set_err(g, FGI_EINVAL, "unknown option %d", option);
     }
 }

@@ -446,6 +446,7 @@ struct CollectArgs {
     uint64_t* escan;
     uint32_t* cstart;
     unsigned long long* part3;   // [3][G] pass-1 sums: winners, expandable winners, row lengths
+    uint64_t stay_pull_f;        // a pull level is followed by another while the frontier exceeds this
 };
 
 __device__ __forceinline__ void collect_pass1(const CollectArgs& c, unsigned long long* s_red) {
@@ -594,7 +595,11 @@ __device__ __forceinline__ void collect_pass2(const CollectArgs& c, LevelCtr& lc
     te = block_sum(te, s_red);
     tl = block_sum(tl, s_red);
     const uint64_t inv_base = lc.mark_lo;   // set by pass 1's kernel
-    const bool pull = single && te != 0 && (direction == 2 || (direction == 0 && tl > pull_threshold));
+    // Beamer's two rules: pull when the frontier's edges exceed E / alpha; after a pull, keep pulling
+    // while the frontier holds more than n / beta nodes (a large frontier of short rows is cheaper
+    // to pull than to expand edge by edge)
+    const bool pull = single && te != 0 &&
+                      (direction == 2 || (direction == 0 && (tl > pull_threshold || te > c.stay_pull_f)));
     const bool write_fr = !pull;
     __syncthreads();   // block 0's threads have all read lc.mark_lo before thread 0 writes lc
     if (b == 0 && threadIdx.x == 0) {
@@ -1389,6 +1394,7 @@ static CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, uint32_t pgrid, 
     c.n_slots = n_slots;
     c.fb = fb;
     c.n_handles = g->n_handles;
+    c.stay_pull_f = g->opt_pull_beta > 0 ? n_slots / (uint64_t)g->opt_pull_beta : ~0ull;
     c.clear_fb = clear;
     c.row_len = g->row_len;
     c.inv = g->inv;

@@ -19,7 +19,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FGI_LIBRARY") or os.path.join(_HERE, "lib", "libfgi.so")
 
 OK, EINVAL, ENOMEM, ECAPACITY, EDEVICE, ESTATE, ENOTSUP = range(7)
-OPT_DEAD_FILTER, OPT_DIRECTION, OPT_PULL_ALPHA, OPT_LEVEL_TIMING = 1, 2, 3, 4
+OPT_DEAD_FILTER, OPT_DIRECTION, OPT_PULL_ALPHA, OPT_LEVEL_TIMING, OPT_PULL_BETA = 1, 2, 3, 4, 5
 DIR_AUTO, DIR_PUSH, DIR_PULL = 0, 1, 2
 NONE = 0xFFFFFFFF
 COMPUTING, CONSISTENT, INVALIDATED = 0, 1, 2
