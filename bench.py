@@ -48,9 +48,6 @@ def cpu_baseline(threads: int, scale: int = 20, edge_factor: int = 16, roots: in
     r = fgo.gen_roots(roots, n, 0x5EED1024, deg)
     o.snapshot()
     build_s = time.time() - t0
-    for k, v in (("FGI_PULL_ALPHA", "OPT_PULL_ALPHA"), ("FGI_PULL_BETA", "OPT_PULL_BETA")):
-        if os.environ.get(k):   # measurement knobs (results never depend on them)
-            g.set_option(getattr(pkg.fgi, v), int(os.environ[k]))
 
     def timed(th):
         o.restore()
