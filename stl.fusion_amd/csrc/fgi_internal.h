@@ -149,6 +149,7 @@ struct fgi_graph {
     uint32_t* used_cnt = nullptr;
     uint32_t* home = nullptr;          // [n_detached]: home slot of a detached handle
     std::vector<uint32_t> free_detached;  // host free list of detached handles
+    std::vector<uint64_t> seen_bits;      // host scratch bitmap over slots (batch duplicate checks)
 
     // edge pool
     uint32_t* pool_col = nullptr;

@@ -1270,13 +1270,22 @@ fgi_status fgi_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, con
     if (!g || (n && (!slot || !version))) return FGI_EINVAL;
     if (n == 0) return FGI_OK;
     {
-        std::vector<uint32_t> s(slot, slot + n);
-        std::sort(s.begin(), s.end());
-        for (uint32_t i = 0; i < n; ++i) {
-            if (s[i] >= g->n_slots) return set_err(g, FGI_EINVAL, "slot %u out of range", s[i]);
-            if (i && s[i] == s[i - 1]) return set_err(g, FGI_EINVAL, "slot %u repeated in one batch", s[i]);
-            if (version[i] == 0 || version[i] > kVMask) return set_err(g, FGI_EINVAL, "bad version at %u", i);
+        // O(n) validation over a reusable slot bitmap (cleared again bit by bit)
+        std::vector<uint64_t>& seen = g->seen_bits;
+        if (seen.size() < ((size_t)g->n_slots + 63) / 64) seen.assign(((size_t)g->n_slots + 63) / 64, 0);
+        uint32_t bad = FGI_NONE;
+        const char* why = nullptr;
+        uint32_t i = 0;
+        for (; i < n; ++i) {
+            const uint32_t x = slot[i];
+            if (x >= g->n_slots) { why = "slot out of range"; bad = x; break; }
+            if (version[i] == 0 || version[i] > kVMask) { why = "bad version"; bad = i; break; }
+            const uint64_t m = 1ull << (x & 63);
+            if (seen[x >> 6] & m) { why = "slot repeated in one batch"; bad = x; break; }
+            seen[x >> 6] |= m;
         }
+        for (uint32_t j = 0; j < i; ++j) seen[slot[j] >> 6] = 0;
+        if (why) return set_err(g, FGI_EINVAL, "%s (%u)", why, bad);
     }
     hipSetDevice(g->device);
     hipStream_t st = g->stream;

@@ -91,16 +91,6 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t& total) 
     return x - v;
 }
 
-__device__ __forceinline__ unsigned long long wave_incl_scan64(unsigned long long v) {
-    const uint32_t lane = lane_id();
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const unsigned long long y = __shfl_up(v, d, 64);
-        if (lane >= (uint32_t)d) v += y;
-    }
-    return v;
-}
-
 __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 #pragma unroll
     for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
@@ -1547,7 +1537,9 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
             }
         }
         group = 4;
-        if (!done && !allow_pull && direction == 0) {
+        // also when the wave is already done (its level groups are sized from the previous wave's
+        // depth, so a repeated wave after a mutation finishes in one group): the next wave pulls
+        if (!allow_pull && direction == 0) {
             bool heavy = false;
             for (int l = L0; l <= L; ++l) heavy |= g->ctr_host->lvl[l % kRing].T > pull_threshold;
             if (heavy) {

@@ -71,3 +71,71 @@ def roots_for(graph, cfg: dict) -> np.ndarray:
     deg, _ = graph.degrees()
     rng = cfg.get("roots_range", n_slots(cfg))
     return pick_roots(cfg["roots"], rng, cfg["roots_seed"], deg[:rng])
+
+
+# BASELINE.json configs[4]: streaming mix — hub slots (PseudoGet(tenant, prefix)-like,
+# samples/TodoApp InMemoryKeyValueStore.cs:100-112) each used by `leaves_per_hub` leaf compute
+# methods; per round the leaves invalidated in the previous round are recomputed
+# (ComputeMethodFunctionBase.cs:19-53: new version -> Computing -> AddUsed(hub) -> TrySetOutput),
+# then a wave invalidates `hubs_per_round` random hubs. 1% of leaves have an invalidation delay
+# (TodoApp ITodos.GetSummary, InvalidationDelay = 1, samples/TodoApp/Abstractions/ITodos.cs:51):
+# a wave only starts their delay; the host timer fires them next round with immediately = true.
+STREAM = dict(hubs=10_000, leaves_per_hub=1_000, rounds=100, hubs_per_round=100, delay_pct=1,
+              seed=0x5EED00E0)
+
+
+class StreamMix:
+    """Deterministic operation schedule of the streaming mix. Slots: hubs [0, H), leaves
+    [H, H + H*L); leaf H + h*L + j uses hub h. Versions are minted on the host (a new version is the
+    old one + 2: odd, positive, != old — LTagVersionGenerator.NextVersion's contract,
+    src/Stl/Versioning/Providers/LTagVersionGenerator.cs:13-20)."""
+
+    def __init__(self, hubs, leaves_per_hub, hubs_per_round, delay_pct, seed):
+        self.H, self.L, self.k, self.seed = hubs, leaves_per_hub, hubs_per_round, seed
+        self.n = hubs + hubs * leaves_per_hub
+        slots = np.arange(self.n, dtype=np.uint64)
+        self.version = (splitmix64(slots ^ np.uint64(seed)) & np.uint64((1 << 54) - 1)) | np.uint64(1)
+        leaf = np.arange(hubs * leaves_per_hub, dtype=np.uint64)
+        h = splitmix64(leaf ^ np.uint64(seed ^ 0xDE1A))
+        self.has_delay = np.zeros(self.n, np.uint8)
+        self.has_delay[hubs:] = ((h % np.uint64(100)) < np.uint64(delay_pct)).astype(np.uint8)
+        self.round = 0
+
+    def initial_edges(self):
+        """(used, dependant, tag) of every leaf -> hub dependency, for fgi_load_edges."""
+        leaf = np.arange(self.H, self.n, dtype=np.uint32)
+        hub = ((leaf - self.H) // self.L).astype(np.uint32)
+        return hub, leaf, self.version[leaf]
+
+    def state_flags(self):
+        """Initial flags: everything Consistent (state 1), hasDelay bit 4 on delayed leaves."""
+        return (np.uint32(1) | (self.has_delay.astype(np.uint32) << np.uint32(4))).astype(np.uint32)
+
+    def roots(self, r):
+        """Distinct hubs for round r's wave."""
+        ks = np.arange(self.k * 4, dtype=np.uint64) + np.uint64(r * self.k * 4)
+        c = (splitmix64(ks + np.uint64(self.seed)) % np.uint64(self.H)).astype(np.int64)
+        _, first = np.unique(c, return_index=True)
+        return c[np.sort(first)][: self.k].astype(np.uint32)
+
+    def children(self, hubs):
+        hubs = np.asarray(hubs, np.int64)
+        return (self.H + hubs[:, None] * self.L + np.arange(self.L)[None, :]).ravel().astype(np.uint32)
+
+    def delayed_children(self, hubs):
+        c = self.children(hubs)
+        return c[self.has_delay[c] != 0]
+
+    def new_versions(self, slots):
+        self.version[slots] += np.uint64(2)
+        return self.version[slots]
+
+    def plan(self, prev_roots):
+        """Round r's recompute work after round r-1's wave on `prev_roots`: the delayed leaves whose
+        timers fire (Invalidate(immediately: true)), the hubs to recompute, and every leaf of those
+        hubs (the wave invalidated the undelayed ones, the timers the rest)."""
+        prev = np.asarray(prev_roots, np.uint32)
+        return self.delayed_children(prev), prev, self.children(prev)
+
+    def hub_of(self, leaves):
+        return ((np.asarray(leaves, np.int64) - self.H) // self.L).astype(np.uint32)
