@@ -1,0 +1,159 @@
+"""CPU model of the partitioned wave's exchange protocol (stl.fusion_amd/csrc/part.hip), run over a
+real torch.distributed process group (gloo) — test infrastructure for the N>1 path, which the GPU
+engine runs over RCCL. Same decomposition as part.hip:
+
+- rank p owns slots [p*B, p*B + n_local), B = ceil(N / world): their node states and `_usedBy`
+  rows (entries keep GLOBAL dependant ids); every rank holds a replica of all N versions;
+- push level: expand the owned frontier; owned targets are visited locally; a remote target whose
+  tag matches its replicated version is forwarded once per wave (per-wave "sent" bitmap: only a
+  node's first visit in a wave can change it, Computed.cs:164-191), counts + payload exchanged
+  (ncclAllGather + ncclSend/Recv on the GPU; all_gather here), owners apply them;
+- pull level: the frontier bitmap is all-gathered and every rank pulls its own unvisited slots
+  over their dependency lists (global parent ids), stopping at the first parent in the frontier;
+- termination: all_reduce(sum) of the next frontier size.
+
+Visits follow SURVEY.md §8(a) R0 (Computed.cs:162-230): Invalidated -> no-op; Computing -> flag
+InvalidateOnSetOutput; Consistent without delay -> Invalidated + expand; Consistent with delay ->
+InvalidationDelayStarted. Roots: the slot's current node, Invalidate(immediately).
+"""
+import numpy as np
+import torch
+import torch.distributed as dist
+
+COMPUTING, CONSISTENT, INVALIDATED = 0, 1, 2
+F_IOSO, F_DS, F_HD = 4, 8, 16
+
+
+class RankModel:
+    def __init__(self, rank, world, n, versions, flags, src, dst, tags):
+        self.rank, self.world, self.n = rank, world, n
+        self.B = -(-n // world)
+        self.lo = rank * self.B
+        self.hi = min(n, self.lo + self.B)
+        self.ver_all = versions.astype(np.uint64)           # replicated, immutable during a wave
+        self.flags = flags[self.lo:self.hi].astype(np.uint32).copy()
+        self.ver = versions[self.lo:self.hi].astype(np.uint64).copy()
+        mine = (src >= self.lo) & (src < self.hi)
+        s, d, t = src[mine], dst[mine], tags[mine]
+        # set semantics of `_usedBy` (HashSetSlim3): duplicate (dst, tag) entries collapse
+        key = np.unique(np.stack([s.astype(np.uint64), d.astype(np.uint64), t], 1), axis=0)
+        self.rows = {}
+        for a, b, c in key:
+            self.rows.setdefault(int(a), []).append((int(b), int(c)))
+        # dependency lists for pull: owned dependant d -> global parents whose row holds (d, ver[d])
+        own_d = (dst >= self.lo) & (dst < self.hi)
+        self.deps = {}
+        for a, b, c in zip(src[own_d], dst[own_d], tags[own_d]):
+            if c == versions[b]:
+                self.deps.setdefault(int(b), set()).add(int(a))
+        self.sent = np.zeros(n, bool)
+        self.inv = []
+
+    def owner(self, slot):
+        return slot // self.B
+
+    def _visit(self, slot, immediately=False):
+        """First visit of an owned node; returns True if it was invalidated (expands)."""
+        i = slot - self.lo
+        f = int(self.flags[i])
+        if self.ver[i] == 0:
+            return False
+        st = f & 3
+        if st == INVALIDATED:
+            return False
+        if st == COMPUTING:
+            f |= F_IOSO
+            if immediately:
+                f |= F_DS
+            self.flags[i] = f
+            return False
+        if (f & F_HD) and not immediately:
+            self.flags[i] = f | F_DS
+            return False
+        self.flags[i] = INVALIDATED | (f & F_HD)   # canonical flags of an Invalidated node
+        self.inv.append(slot)
+        return True
+
+    def _matches(self, slot, tag):
+        return self.ver_all[slot] == tag   # replicated versions; the owner checks the state
+
+    def wave(self, roots, immediately=None, direction="push", alpha=14):
+        self.sent[:] = False
+        visited = set()
+        front = []
+        for k, r in enumerate(roots):
+            r = int(r)
+            if self.lo <= r < self.hi and r not in visited:
+                visited.add(r)
+                imm = bool(immediately[k]) if immediately is not None else False
+                if self._visit(r, imm):
+                    front.append(r)
+        e_total = torch.tensor([sum(len(v) for v in self.rows.values())], dtype=torch.int64)
+        dist.all_reduce(e_total)
+        levels = 0
+        while True:
+            n_front = torch.tensor([len(front)], dtype=torch.int64)
+            dist.all_reduce(n_front)                       # termination (ncclAllReduce)
+            if int(n_front) == 0:
+                break
+            edges = torch.tensor([sum(len(self.rows.get(u, ())) for u in front)], dtype=torch.int64)
+            dist.all_reduce(edges)
+            pull = direction == "pull" or (direction == "auto" and int(edges) > int(e_total) // alpha)
+            nxt = []
+            if pull:
+                bm = np.zeros(self.n, bool)
+                bm[np.asarray(front, np.int64)] = True
+                parts = [torch.zeros(self.n, dtype=torch.bool) for _ in range(self.world)]
+                dist.all_gather(parts, torch.from_numpy(bm))   # frontier bitmap all-gather
+                gfront = np.logical_or.reduce([p.numpy() for p in parts])
+                for d, ps in self.deps.items():
+                    if d in visited:
+                        continue
+                    if any(gfront[p] for p in ps):
+                        visited.add(d)
+                        if self._visit(d):
+                            nxt.append(d)
+            else:
+                out = [[] for _ in range(self.world)]
+                for u in front:
+                    for d, t in self.rows.get(u, ()):
+                        if not self._matches(d, t):
+                            continue
+                        q = self.owner(d)
+                        if q == self.rank:
+                            if d not in visited:
+                                visited.add(d)
+                                if self._visit(d):
+                                    nxt.append(d)
+                        elif not self.sent[d]:
+                            self.sent[d] = True
+                            out[q].append(d)
+                # counts then payload (ncclAllGather of counts + ncclSend/ncclRecv on the GPU)
+                cnt = torch.tensor([len(o) for o in out], dtype=torch.int64)
+                all_cnt = [torch.zeros(self.world, dtype=torch.int64) for _ in range(self.world)]
+                dist.all_gather(all_cnt, cnt)
+                width = max(1, int(max(int(c.max()) for c in all_cnt)))
+                pay = torch.full((self.world, width), -1, dtype=torch.int64)
+                for q, o in enumerate(out):
+                    if o:
+                        pay[q, :len(o)] = torch.tensor(o, dtype=torch.int64)
+                all_pay = [torch.zeros_like(pay) for _ in range(self.world)]
+                dist.all_gather(all_pay, pay)
+                for r in range(self.world):
+                    c = int(all_cnt[r][self.rank])
+                    for d in all_pay[r][self.rank, :c].tolist():
+                        if d not in visited:
+                            visited.add(d)
+                            if self._visit(d):
+                                nxt.append(d)
+            front = nxt
+            levels += 1
+        return levels
+
+    def gather_results(self):
+        """Union of the invalidated sets and the owners' final flags, on every rank."""
+        inv = [None] * self.world
+        dist.all_gather_object(inv, sorted(self.inv))
+        fl = [None] * self.world
+        dist.all_gather_object(fl, self.flags.tolist())
+        return sorted(x for part in inv for x in part), np.concatenate([np.asarray(f, np.uint32) for f in fl])
