@@ -17,6 +17,7 @@
 
 #include <chrono>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/fgi.h"
@@ -150,6 +151,10 @@ struct fgi_graph {
     uint32_t* home = nullptr;          // [n_detached]: home slot of a detached handle
     std::vector<uint32_t> free_detached;  // host free list of detached handles
     std::vector<uint64_t> seen_bits;      // host scratch bitmap over slots (batch duplicate checks)
+    // device temporaries of the mutation calls, kept for reuse (same stream, so reuse is ordered
+    // after the previous user) instead of a hipMalloc + hipFree (an implicit device sync) per call
+    std::vector<std::pair<size_t, void*>> tmp_cache;
+    size_t tmp_cached = 0;
 
     // edge pool
     uint32_t* pool_col = nullptr;

@@ -58,16 +58,62 @@ void dfree(T*& p) {
 }
 
 // RAII device temporaries for non-hot-path operations
+// Device temporaries of one ABI call. Small ones (power-of-two size classes up to kTmpKeepMax,
+// kTmpKeepTotal in all) go back to the graph's cache when the call ends; every user of a
+// temporary runs on the graph's stream, so a later reuse is ordered after it.
+constexpr size_t kTmpKeepMax = 64ull << 20;
+constexpr size_t kTmpKeepTotal = 512ull << 20;
+
+void tmp_release(fgi_graph* g, void* p, size_t bytes) {
+    if (g && bytes <= kTmpKeepMax && g->tmp_cached + bytes <= kTmpKeepTotal) {
+        g->tmp_cache.emplace_back(bytes, p);
+        g->tmp_cached += bytes;
+        return;
+    }
+    hipFree(p);
+}
+
+void tmp_drain(fgi_graph* g) {
+    for (auto& e : g->tmp_cache) hipFree(e.second);
+    g->tmp_cache.clear();
+    g->tmp_cached = 0;
+}
+
 struct Tmp {
+    fgi_graph* g = nullptr;
     void* p = nullptr;
+    size_t bytes = 0;
     ~Tmp() {
-        if (p) hipFree(p);
+        if (p) tmp_release(g, p, bytes);
     }
 };
 template <class T>
 fgi_status tmalloc(fgi_graph* g, Tmp& t, T** p, size_t count) {
-    hipError_t e = hipMalloc(&t.p, (count ? count : 1) * sizeof(T));
-    if (e != hipSuccess) return hip_check(g, e, "hipMalloc(tmp)");
+    size_t want = 4096;
+    while (want < (count ? count : 1) * sizeof(T)) want <<= 1;
+    t.g = g;
+    for (size_t i = 0; i < g->tmp_cache.size(); ++i) {
+        if (g->tmp_cache[i].first == want) {
+            t.p = g->tmp_cache[i].second;
+            t.bytes = want;
+            g->tmp_cache[i] = g->tmp_cache.back();
+            g->tmp_cache.pop_back();
+            g->tmp_cached -= want;
+            *p = reinterpret_cast<T*>(t.p);
+            return FGI_OK;
+        }
+    }
+    hipError_t e = hipMalloc(&t.p, want);
+    if (e != hipSuccess && !g->tmp_cache.empty()) {   // give the cache back and retry once
+        hipStreamSynchronize(g->stream);
+        tmp_drain(g);
+        e = hipMalloc(&t.p, want);
+    }
+    if (e != hipSuccess) {
+        t.p = nullptr;
+        return hip_check(g, e, "hipMalloc(tmp)");
+    }
+    t.bytes = want;
     *p = reinterpret_cast<T*>(t.p);
     return FGI_OK;
 }
@@ -856,6 +902,7 @@ fgi_status fgi_destroy(fgi_graph* g) {
     hipSetDevice(g->device);
     if (g->stream) hipStreamSynchronize(g->stream);
     fgi::part_destroy(g);
+    fgi::tmp_drain(g);
     dfree(g->node);
     dfree(g->row_off);
     dfree(g->row_len);
