@@ -199,7 +199,9 @@ fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats);
 fgi_status fgi_release(fgi_graph* g, uint32_t n, const uint32_t* handle);
 
 /* ---- bench / test support ------------------------------------------------------------------- */
-/* Save / restore node states and row lengths on the device (reset from a pristine copy). */
+/* Save / restore node states and row lengths on the device (reset from a pristine copy).
+ * fgi_restore is stream-ordered: it may return before the device copies finish; every later call
+ * on the graph runs after them. */
 fgi_status fgi_snapshot(fgi_graph* g);
 fgi_status fgi_restore(fgi_graph* g);
 /* Device-side synthetic workloads. All nodes Consistent with

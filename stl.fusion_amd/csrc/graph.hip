@@ -864,7 +864,7 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
         dmalloc(g, &g->row_cap, H) || dmalloc(g, &g->used_cnt, H) || dmalloc(g, &g->home, g->n_detached + 1) ||
         dmalloc(g, &g->inv, H) || dmalloc(g, &g->fr_off[0], H) || dmalloc(g, &g->fr_off[1], H) ||
         dmalloc(g, &g->fr_len[0], H) || dmalloc(g, &g->fr_len[1], H) || dmalloc(g, &g->escan, H) ||
-        dmalloc(g, &g->partials, 4 * kScanBlocks) || dmalloc(g, &g->ctr, 1) ||
+        dmalloc(g, &g->partials, 9 * kScanBlocks) || dmalloc(g, &g->ctr, 1) ||
         dmalloc(g, &g->blk_stats, (size_t)kStatBlocks * kStatCols) || dmalloc(g, &g->misc_dev, 16) ||
         dmalloc(g, &g->pool_top_dev, 1) || dmalloc(g, &g->uin_off, H) || dmalloc(g, &g->uin_len, H) ||
         dmalloc(g, &g->uin_head, g->n_slots + 1))
@@ -875,6 +875,7 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
         dmalloc(g, &g->front_nx, g->bm_words) || dmalloc(g, &g->cls_bm, g->bm_words) ||
         dmalloc(g, &g->uin_more, g->bm_words) || dmalloc(g, &g->tiles, g->tiles_cap))
         return fail(FGI_ENOMEM);
+    hipMemset(g->partials, 0, 9 * kScanBlocks * sizeof(unsigned long long));   // incl. completion counters
     hipMemset(g->vis_bm, 0, g->bm_words * 4);
     hipMemset(g->front_bm, 0, g->bm_words * 4);
     hipMemset(g->front_nx, 0, g->bm_words * 4);
@@ -1207,8 +1208,9 @@ fgi_status fgi_restore(fgi_graph* g) {
     if (g->v_dirty) FGI_HIP(g, hipMemsetAsync(g->vis_bm, 0, g->bm_words * 4, s));
     g->v_dirty = false;
     if (g->mut_epoch == g->snap_mut_epoch) {
-        // nothing but waves ran since the snapshot: rows and |_used| counts are unchanged
-        FGI_HIP(g, hipStreamSynchronize(s));
+        // nothing but waves ran since the snapshot: rows and |_used| counts are unchanged. The
+        // copies are stream-ordered before every later call on this graph, so no host wait here.
+        FGI_HIP(g, hipGetLastError());
         return FGI_OK;
     }
     FGI_HIP(g, hipMemcpyAsync(g->row_off, g->snap_row_off, H * 8, hipMemcpyDeviceToDevice, s));

@@ -391,7 +391,8 @@ __global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ r
 }
 
 // ---- frontier scan ----------------------------------------------------------------------------
-constexpr int kScanThreads = 512;   // threads per block of the collect / scan kernel (k_scan_apply)
+constexpr int kScanThreads = 256;   // threads per block of the collect / scan kernel (k_scan_apply): at its
+                                     // register budget (4 waves/SIMD) all kScanBlocks blocks are resident
 constexpr int kMaxWaves = kScanThreads / 64;
 
 __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, unsigned long long* s_red) {
@@ -406,15 +407,98 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, un
     return t;
 }
 
+// Called by every block of a pass-1 grid with its per-block sums v[q] (q < ncols) in thread 0: the
+// last block to finish turns src's columns into exclusive prefixes dst[q * G + k] and totals
+// dst[3 * G + q] — O(G) work, instead of every pass-2 block re-reading all G sums. The sums and the
+// counter are agent-scope atomic RMWs, performed at the coherence point shared by the XCDs (their
+// L2s are not coherent with each other); a block's counter increment is issued only after its sum
+// exchanges have returned, so the last block reads every sum. No L2 write-back fence is needed.
+constexpr int kDoneGroups = 16;
+constexpr int kDoneStride = 16;
+__device__ __forceinline__ unsigned long long coh_xchg(unsigned long long* p, unsigned long long v) {
+    return __hip_atomic_exchange(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long coh_read(unsigned long long* p) {
+    return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The completion counter is two-level (one counter word serialises near 88 atomics/us,
+// MI355X_MICROARCH.md): block b counts into group b % kDoneGroups, the last block of a group into
+// the top word done[0]; groups live kDoneStride words (128 B) apart.
+__device__ void finish_prefix(unsigned long long* src, unsigned long long* dst, int ncols, uint64_t G,
+                              unsigned long long* done, unsigned long long* s_red, const unsigned long long* v) {
+    __shared__ bool s_last;
+    if (threadIdx.x == 0) {
+        unsigned long long r = 0;
+        for (int q = 0; q < ncols; ++q) r |= coh_xchg(src + q * G + blockIdx.x, v[q]);
+        __builtin_amdgcn_s_waitcnt(0);   // the exchanges have been performed
+        const uint32_t grp = blockIdx.x % kDoneGroups;
+        const uint64_t gsize = (G - grp + kDoneGroups - 1) / kDoneGroups;
+        const unsigned long long t = __hip_atomic_fetch_add(done + (1 + grp) * kDoneStride, 1ull + (r & 0ull),
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        bool last = false;
+        if (t == gsize - 1) {
+            __builtin_amdgcn_s_waitcnt(0);
+            const uint64_t ng = G < (uint64_t)kDoneGroups ? G : (uint64_t)kDoneGroups;
+            last = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // every sum this thread needs is read in one round (G <= kScanBlocks, blockDim.x == kBlock)
+    constexpr uint32_t kPer = (kScanBlocks + kBlock - 1) / kBlock;
+    const uint64_t k0 = (uint64_t)threadIdx.x * kPer;
+    const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
+    unsigned long long xs[3][kPer];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j) xs[q][j] = (q < ncols && k0 + j < G) ? coh_read(src + q * G + k0 + j) : 0ull;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        if (q >= ncols) break;
+        unsigned long long loc = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j) loc += xs[q][j];
+        unsigned long long x = loc;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const unsigned long long y = __shfl_up(x, d, 64);
+            if (lane >= (uint32_t)d) x += y;
+        }
+        __syncthreads();
+        if (lane == 63) s_red[wid] = x;
+        __syncthreads();
+        unsigned long long run = x - loc, tot = 0;
+        for (uint32_t k = 0; k < (blockDim.x >> 6); ++k) {
+            if (k < wid) run += s_red[k];
+            tot += s_red[k];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kPer; ++j)
+            if (k0 + j < G) {
+                dst[q * G + k0 + j] = run;
+                run += xs[q][j];
+            }
+        if (threadIdx.x == 0) dst[3 * G + q] = tot;
+    }
+    if (threadIdx.x <= (uint32_t)kDoneGroups) coh_xchg(done + threadIdx.x * kDoneStride, 0ull);
+}
+
 __device__ __forceinline__ void scan_partial(uint64_t F, const uint32_t* __restrict__ fr_len,
-                                             unsigned long long* __restrict__ partials, unsigned long long* s_red) {
+                                             unsigned long long* __restrict__ partials, unsigned long long* s_red,
+                                             unsigned long long* done) {
     const uint64_t b = blockIdx.x, G = gridDim.x;
     const uint64_t lo = F * b / G, hi = F * (b + 1) / G;
     unsigned long long s = 0;
     for (uint64_t i = lo + threadIdx.x; i < hi; i += blockDim.x) s += fr_len[i];
     s = block_sum(s, s_red);
-    if (threadIdx.x == 0) partials[b] = s;
+    const unsigned long long v[1] = {s};
+    finish_prefix(partials, partials + 4 * G, 1, G, done, s_red, v);   // prefixes for k_scan_apply
 }
+
+__device__ __forceinline__ void probe_at(unsigned long long* pr, int k);
 
 // ---- collect: a pull level's winners bitmap -> invalidated list (+ next frontier) -------------
 // The pull level counted its winners per tile (kPullTile slots; tile t = iteration * pgrid + block,
@@ -437,6 +521,9 @@ struct CollectArgs {
     uint32_t* cstart;
     unsigned long long* part3;   // [3][G] pass-1 sums: winners, expandable winners, row lengths
     uint64_t stay_pull_f;        // a pull level is followed by another while the frontier exceeds this
+    unsigned long long* probe;   // measurement only (FGI_PROBE): phase stamps of collect pass 2
+    unsigned long long* pre3;    // [3][G] exclusive prefixes of part3's columns, then the 3 totals
+    unsigned long long* done;    // pass-1 blocks finished (the last one scans part3; zero between uses)
 };
 
 __device__ __forceinline__ void collect_pass1(const CollectArgs& c, unsigned long long* s_red) {
@@ -452,11 +539,8 @@ __device__ __forceinline__ void collect_pass1(const CollectArgs& c, unsigned lon
     w = block_sum(w, s_red);
     e = block_sum(e, s_red);
     l = block_sum(l, s_red);
-    if (threadIdx.x == 0) {
-        c.part3[b] = w;
-        c.part3[G + b] = e;
-        c.part3[2 * G + b] = l;
-    }
+    const unsigned long long v[3] = {w, e, l};
+    finish_prefix(c.part3, c.pre3, 3, G, c.done, s_red, v);
 }
 
 // One tile by one wave: lane l owns the 16 slots s0 + 16l .. s0 + 16l + 15 (one 16-bit chunk of the
@@ -464,17 +548,18 @@ __device__ __forceinline__ void collect_pass1(const CollectArgs& c, unsigned lon
 // row lengths); the entries are staged in the wave's LDS buffer and stored coalesced, in slot order,
 // at bw (inv) and be / bl (frontier index / edge offset). write_fr: also the frontier entries, their
 // scan and the chunk map.
-__device__ __forceinline__ void collect_tile(const CollectArgs& c, uint64_t t, uint64_t bw, uint64_t be, uint64_t bl,
-                                             bool write_fr, uint32_t* __restrict__ stage) {
+// The lane's 16-bit chunk of tile t's winners bitmap (loaded ahead of the tile's collect).
+__device__ __forceinline__ uint32_t collect_bits(const CollectArgs& c, uint64_t t) {
+    const uint64_t base = t * kPullTile + 16ull * lane_id();
+    return base < c.n_slots ? (uint32_t)reinterpret_cast<const uint16_t*>(c.fb)[base / 16] : 0u;
+}
+
+__device__ __forceinline__ void collect_tile(const CollectArgs& c, uint64_t t, uint32_t m, uint64_t bw, uint64_t be,
+                                             uint64_t bl, bool write_fr, uint32_t* __restrict__ stage) {
     const uint32_t lane = lane_id();
     const uint64_t s0 = t * kPullTile;   // tile t = it * pgrid + block covers slots [t * kPullTile, +kPullTile)
     const uint64_t base = s0 + 16ull * lane;
-    uint16_t* fb16 = reinterpret_cast<uint16_t*>(c.fb);
-    uint32_t m = 0;
-    if (base < c.n_slots) {
-        m = fb16[base / 16];
-        if (c.clear_fb && m) fb16[base / 16] = 0;
-    }
+    if (c.clear_fb && m) reinterpret_cast<uint16_t*>(c.fb)[base / 16] = 0;
     uint32_t rl[16];
     uint32_t em = 0, len = 0;
 #pragma unroll
@@ -563,28 +648,17 @@ __device__ __forceinline__ void collect_tile(const CollectArgs& c, uint64_t t, u
 __device__ __forceinline__ void collect_pass2(const CollectArgs& c, LevelCtr& lc, WaveCtr* ctr, bool single,
                                               int direction, uint64_t pull_threshold, uint32_t* fb_nxt,
                                               uint64_t slot_words, unsigned long long* s_red) {
-    __shared__ unsigned long long s_w[kMaxWaves], s_e[kMaxWaves], s_l[kMaxWaves];
+    __shared__ uint32_t s_ow[64], s_oe[64], s_nz[64];
+    __shared__ unsigned long long s_ol[64], s_tot[3];
     __shared__ uint32_t s_stage[kMaxWaves][kPullTile];   // per-wave staging of one tile's entries
+    if (c.probe && threadIdx.x == 0 && blockIdx.x < kProbeBlocks)
+        c.probe[blockIdx.x * kProbePhases] = __builtin_amdgcn_s_memrealtime();
     const uint64_t b = blockIdx.x, G = gridDim.x;
-    unsigned long long bw = 0, be = 0, bl = 0, tw = 0, te = 0, tl = 0;
-    for (uint64_t k = threadIdx.x; k < G; k += blockDim.x) {
-        const unsigned long long w = c.part3[k], e = c.part3[G + k], l = c.part3[2 * G + k];
-        tw += w;
-        te += e;
-        tl += l;
-        if (k < b) {
-            bw += w;
-            be += e;
-            bl += l;
-        }
-    }
-    bw = block_sum(bw, s_red);
-    be = block_sum(be, s_red);
-    bl = block_sum(bl, s_red);
-    tw = block_sum(tw, s_red);
-    te = block_sum(te, s_red);
-    tl = block_sum(tl, s_red);
+    // the block's offsets (sums over blocks < b) and the level totals: every pass-1 sum is loaded
+    // at once (kScanBlocks / kScanThreads per thread, independent loads), one fused reduction
     const uint64_t inv_base = lc.mark_lo;   // set by pass 1's kernel
+    const unsigned long long bw = c.pre3[b], be = c.pre3[G + b], bl = c.pre3[2 * G + b];
+    const unsigned long long tw = c.pre3[3 * G], te = c.pre3[3 * G + 1], tl = c.pre3[3 * G + 2];
     // Beamer's two rules: pull when the frontier's edges exceed E / alpha; after a pull, keep pulling
     // while the frontier holds more than n / beta nodes (a large frontier of short rows is cheaper
     // to pull than to expand edge by edge)
@@ -606,36 +680,55 @@ __device__ __forceinline__ void collect_pass2(const CollectArgs& c, LevelCtr& lc
         const uint64_t nthr = G * blockDim.x;
         for (uint64_t w = b * blockDim.x + threadIdx.x; w < slot_words; w += nthr) fb_nxt[w] = 0u;
     }
+    probe_at(c.probe, 2);
     const uint64_t lo = c.n_tiles * b / G, hi = c.n_tiles * (b + 1) / G;
-    const uint32_t W = blockDim.x >> 6, wid = threadIdx.x >> 6;
+    const uint32_t W = blockDim.x >> 6, wid = threadIdx.x >> 6, lane = lane_id();
     uint64_t rw = inv_base + bw, re = be, rl = bl;
-    for (uint64_t base = lo; base < hi; base += W) {   // block-uniform
-        const uint64_t t = base + wid;
-        PullTile x{0, 0, 0ull};
-        if (t < hi) x = c.tiles[t];
-        if (lane_id() == 0) {
-            s_w[wid] = x.w;
-            s_e[wid] = x.e;
-            s_l[wid] = x.len;
-        }
-        __syncthreads();
-        uint64_t ow = 0, oe = 0, ol = 0, aw = 0, ae = 0, al = 0;
-        for (uint32_t k = 0; k < W; ++k) {
-            if (k < wid) {
-                ow += s_w[k];
-                oe += s_e[k];
-                ol += s_l[k];
+    // chunks of up to 64 tiles: wave 0 loads their counts and scans them (offsets within the
+    // chunk into LDS), then the waves take the chunk's tiles round-robin with no further barrier
+    for (uint64_t cb = lo; cb < hi; cb += 64) {   // block-uniform
+        const uint32_t nt = (uint32_t)std::min<uint64_t>(64, hi - cb);
+        if (wid == 0) {
+            PullTile x{0, 0, 0ull};
+            if (lane < nt) x = c.tiles[cb + lane];
+            uint32_t tw_, te_;
+            const uint32_t ow = wave_excl_scan(x.w, tw_), oe = wave_excl_scan(x.e, te_);
+            unsigned long long il = x.len;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const unsigned long long y = __shfl_up(il, d, 64);
+                if (lane >= (uint32_t)d) il += y;
             }
-            aw += s_w[k];
-            ae += s_e[k];
-            al += s_l[k];
+            s_ow[lane] = ow;
+            s_oe[lane] = oe;
+            s_ol[lane] = il - x.len;
+            s_nz[lane] = x.w;
+            if (lane == 63) {
+                s_tot[0] = tw_;
+                s_tot[1] = te_;
+                s_tot[2] = il;
+            }
         }
         __syncthreads();
-        if (t < hi && x.w != 0) collect_tile(c, t, rw + ow, re + oe, rl + ol, write_fr, s_stage[wid]);
-        rw += aw;
-        re += ae;
-        rl += al;
+        // the next tile's bitmap chunk is loaded while the current one is collected
+        uint32_t j = wid;
+        while (j < nt && !s_nz[j]) j += W;
+        uint32_t m = j < nt ? collect_bits(c, cb + j) : 0u;
+        while (j < nt) {
+            uint32_t jn = j + W;
+            while (jn < nt && !s_nz[jn]) jn += W;
+            const uint32_t mn = jn < nt ? collect_bits(c, cb + jn) : 0u;
+            collect_tile(c, cb + j, m, rw + s_ow[j], re + s_oe[j], rl + s_ol[j], write_fr, s_stage[wid]);
+            j = jn;
+            m = mn;
+        }
+        rw += s_tot[0];
+        re += s_tot[1];
+        rl += s_tot[2];
+        if (cb == lo) probe_at(c.probe, 3);
+        __syncthreads();   // the next chunk overwrites the offsets
     }
+    probe_at(c.probe, 10);
 }
 
 // multi-GPU levels: partial sums of the frontier's row lengths, or collect pass 1 after a pull
@@ -648,7 +741,7 @@ __global__ __launch_bounds__(kBlock) void k_scan_reduce(int L, const uint32_t* _
         collect_pass1(ca, s_red);
         return;
     }
-    scan_partial(ctr->lvl[L % kRing].F, fr_len, partials, s_red);
+    scan_partial(ctr->lvl[L % kRing].F, fr_len, partials, s_red, ca.done);
 }
 
 // Single-GPU level prologue (one launch, grid kScanBlocks):
@@ -693,7 +786,7 @@ __global__ __launch_bounds__(kBlock) void k_level_begin(int L, WaveCtr* ctr, con
     // a pull at level L stores every slot word of fb_nxt; the words past the slots (detached
     // handles) are never winners of a pull and must read as zero
     for (uint64_t w = (pull ? slot_words : 0ull) + tid; w < bm_words; w += nthr) fb_nxt[w] = 0u;
-    if (!pull && F) scan_partial(F, fr_len, partials, s_red);
+    if (!pull && F) scan_partial(F, fr_len, partials, s_red, ca.done);
 }
 
 // Exclusive scan of fr_len into escan; records for every chunk of kChunk edges the frontier
@@ -715,14 +808,8 @@ __global__ __launch_bounds__(kScanThreads, 4) void k_scan_apply(int L, const uin
     const uint64_t F = lc.F;
     if (!decide && (lc.pull || F == 0)) return;
     const uint64_t b = blockIdx.x, G = gridDim.x;
-    unsigned long long before = 0, all = 0;
-    for (uint64_t k = threadIdx.x; k < G; k += blockDim.x) {
-        const unsigned long long p = partials[k];
-        all += p;
-        if (k < b) before += p;
-    }
-    before = block_sum(before, s_red);
-    all = block_sum(all, s_red);
+    // exclusive prefix and total of the per-block sums (the last pass-1 block wrote them)
+    const unsigned long long before = partials[4 * G + b], all = partials[7 * G];
     if (decide && b == 0 && threadIdx.x == 0) {
         lc.T = all;
         lc.nchunks = (all + kChunk - 1) / kChunk;
@@ -1007,11 +1094,24 @@ __device__ __forceinline__ void pull_flush(const PullArgs& p, const unsigned lon
     const uint64_t stride = (uint64_t)gridDim.x * kPullTile;
     const uint32_t lane = lane_id(), sub = lane & 7, grp = threadIdx.x >> 3;
     __syncthreads();
-    // queued slots: 8 lanes per slot, entries 2.. of its list
-    for (uint32_t e = grp; e < nq; e += blockDim.x / 8) {
-        const uint32_t d = q[e];
-        const uint32_t len = p.uin_len[d];
-        const uint64_t off = p.uin_off[d];
+    // queued slots: 8 lanes per slot, entries 2.. of its list; the next slot's list length and
+    // offset are loaded while the current list is scanned
+    const uint32_t G8 = blockDim.x / 8;
+    uint32_t d_n = 0, len_n = 0;
+    uint64_t off_n = 0;
+    if (grp < nq) {
+        d_n = q[grp];
+        len_n = p.uin_len[d_n];
+        off_n = p.uin_off[d_n];
+    }
+    for (uint32_t e = grp; e < nq; e += G8) {
+        const uint32_t d = d_n, len = len_n;
+        const uint64_t off = off_n;
+        if (e + G8 < nq) {
+            d_n = q[e + G8];
+            len_n = p.uin_len[d_n];
+            off_n = p.uin_off[d_n];
+        }
         bool found = false;
         for (uint32_t r = 2; r < len && !found; r += 8) {   // group-uniform
             const uint32_t i = r + sub;
@@ -1262,6 +1362,22 @@ __global__ __launch_bounds__(kBlock) void k_apply_recv(int L, uint64_t n, const 
 // Folds the per-block statistics into the wave counters: one block per column (coalesced sweeps).
 // Block kStats: if level L_next follows a pull level, its F and T from the pull's tiles (the host
 // reads them to decide termination before k_level_begin(L_next) has run).
+// Wave prologue in one launch (instead of three fills): the counter ring, the per-block
+// statistics and the first frontier bitmap start at zero.
+__global__ __launch_bounds__(kBlock) void k_wave_init(WaveCtr* ctr, unsigned long long* blk, uint32_t* fb0,
+                                                      uint64_t fb_words, unsigned long long* done) {
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    // finish_prefix's completion counters (normally left at zero by their last user)
+    if (tid <= (uint64_t)kDoneGroups) coh_xchg(done + tid * kDoneStride, 0ull);
+    unsigned long long* c = reinterpret_cast<unsigned long long*>(ctr);
+    for (uint64_t i = tid; i < sizeof(WaveCtr) / 8; i += nthr) c[i] = 0ull;
+    for (uint64_t i = tid; i < (uint64_t)kStatBlocks * kStatCols; i += nthr) blk[i] = 0ull;
+    uint4* f4 = reinterpret_cast<uint4*>(fb0);
+    for (uint64_t i = tid; i < fb_words / 4; i += nthr) f4[i] = make_uint4(0u, 0u, 0u, 0u);
+    for (uint64_t i = fb_words / 4 * 4 + tid; i < fb_words; i += nthr) fb0[i] = 0u;
+}
+
 __global__ __launch_bounds__(kBlock) void k_stats_reduce(const unsigned long long* __restrict__ blk, WaveCtr* ctr,
                                                          int L_next, const PullTile* __restrict__ tiles,
                                                          uint64_t n_tiles) {
@@ -1348,7 +1464,7 @@ static unsigned event_flags() {
 }
 
 // FGI_PROBE (measurement only): median per-phase offsets (us) of a push level's stamped blocks
-static fgi_status probe_report(fgi_graph* g, int L, uint32_t grid) {
+static fgi_status probe_report(fgi_graph* g, int L, uint32_t grid, const char* what = "level") {
     std::vector<unsigned long long> h((size_t)kProbeBlocks * kProbePhases);
     FGI_HIP(g, hipStreamSynchronize(g->stream));
     FGI_HIP(g, hipMemcpy(h.data(), g->probe, h.size() * 8, hipMemcpyDeviceToHost));
@@ -1359,7 +1475,7 @@ static fgi_status probe_report(fgi_graph* g, int L, uint32_t grid) {
             t0 = std::min(t0, h[(size_t)b * kProbePhases]);
             t_end = std::max(t_end, h[(size_t)b * kProbePhases + 10]);
         }
-    fprintf(stderr, "[probe] level %d span %.2f us; median phase stamps (us after first block start):", L,
+    fprintf(stderr, "[probe] %s %d span %.2f us; median phase stamps (us after first block start):", what, L,
             t0 == ~0ull ? 0.0 : (t_end - t0) / 100.0);
     for (int k = 0; k <= 10; ++k) {
         std::vector<double> v;
@@ -1394,6 +1510,9 @@ static CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, uint32_t pgrid, 
     c.escan = g->escan;
     c.cstart = g->cstart;
     c.part3 = g->partials + kScanBlocks;
+    c.pre3 = g->partials + 4 * kScanBlocks;
+    c.done = g->partials + 8 * kScanBlocks;   // (kDoneGroups + 1) counters, kDoneStride apart
+    c.probe = nullptr;
     return c;
 }
 
@@ -1422,9 +1541,9 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     if (direction == 2 && n_roots) FGI_TRY(ensure_in_lists(g));
     bool allow_pull = direction != 1 && g->uin_src && g->uin_epoch == g->mut_epoch;
     uint32_t* fb[2] = {g->front_bm, g->front_nx};
-    FGI_HIP(g, hipMemsetAsync(g->ctr, 0, sizeof(WaveCtr), s));
-    FGI_HIP(g, hipMemsetAsync(g->blk_stats, 0, sizeof(unsigned long long) * kStatBlocks * kStatCols, s));
-    FGI_HIP(g, hipMemsetAsync(fb[0], 0, g->bm_words * 4, s));
+    static_assert(sizeof(WaveCtr) % 8 == 0, "WaveCtr is cleared as 64-bit words");
+    hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, fb[0], (uint64_t)g->bm_words,
+                       g->partials + 8 * kScanBlocks);
     if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
     Out o{g->row_off, g->row_len, g->inv, g->fr_off[0], g->fr_len[0], &g->ctr->inv, &g->ctr->lvl[0]};
     if (n_roots) {
@@ -1456,12 +1575,17 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         const int dir_eff = allow_pull ? direction : 1;
         for (int k = 0; k < group; ++k, ++L) {
             const int buf = L & 1;
-            const CollectArgs ca = collect_args(g, g->n_slots, level_grid, fb[buf], 0, buf);
+            CollectArgs ca = collect_args(g, g->n_slots, level_grid, fb[buf], 0, buf);
             hipLaunchKernelGGL(k_level_begin, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->ctr, g->inv, fb[buf],
                                fb[buf ^ 1], g->bm_words, slot_words, g->fr_len[buf], g->partials, dir_eff,
                                pull_threshold, ca);
+            if (probe) {
+                FGI_HIP(g, hipMemsetAsync(g->probe, 0, sizeof(unsigned long long) * kProbeBlocks * kProbePhases, s));
+                ca.probe = g->probe;
+            }
             hipLaunchKernelGGL(k_scan_apply, dim3(kScanBlocks), dim3(kScanThreads), 0, s, L, g->fr_len[buf], g->partials,
                                g->escan, g->cstart, g->ctr, 0, ca, dir_eff, pull_threshold, fb[buf ^ 1], slot_words);
+            if (probe && L > 0) FGI_TRY(probe_report(g, L, kScanBlocks, "collect"));
             if (timing) {
                 while (g->ev.size() < 2 * (size_t)(L + 1) + 2) {
                     hipEvent_t e;
