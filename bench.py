@@ -283,6 +283,19 @@ def main():
                             "gbs": (st_k.pull_bytes / (st_k.pull_ms * 1e-3) / 1e9) if st_k.pull_ms > 0 else 0.0},
         },
     }
+    # SURVEY.md §8(d)'s layout-A formula B = 28 V_exp + 24 E_trav + 4 E_match + 4 R counts every
+    # edge of every expanded node, as a push-only traversal would read them. Pull levels read
+    # dependency-list heads instead of those edges, so B / t is a push-equivalent rate that can exceed
+    # the HBM peak; it is reported for recomputation, while `roofline` uses the bytes the kernels
+    # actually have to move. Without stale edges every traversed edge matches (E_match = E_trav).
+    per_wave = lambda x: x / args.steps
+    e_match = e_trav if not cfg.get("stale_pct") else st.e_match * world
+    b_formula = 28 * v_inv + 24 * e_trav + 4 * e_match + 4 * len(roots) * args.steps
+    result["survey_formula"] = {
+        "layout": "A", "V_exp": per_wave(v_inv), "E_trav": per_wave(e_trav), "E_match": per_wave(e_match),
+        "R": len(roots), "bytes_per_wave": per_wave(b_formula),
+        "push_equivalent_gbs": b_formula / elapsed / 1e9,
+        "note": "push-equivalent: pull levels do not read these edges; see roofline for the bytes moved"}
     if rank == 0 and world == 1 and not args.no_cpu:
         threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
         try:
