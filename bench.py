@@ -208,14 +208,14 @@ def main():
     torch.cuda.synchronize()
     instrumented_ms = (time.perf_counter() - t_k) / args.steps * 1e3
 
-    v_inv, e_trav = st.v_inv, st.e_trav
+    v_inv, e_trav, e_match_all = st.v_inv, st.e_trav, st.e_match
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        c = torch.tensor([v_inv, e_trav], dtype=torch.float64, device=f"cuda:{local_rank}")
+        c = torch.tensor([v_inv, e_trav, e_match_all], dtype=torch.float64, device=f"cuda:{local_rank}")
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        v_inv, e_trav = int(c[0].item()), int(c[1].item())
+        v_inv, e_trav, e_match_all = int(c[0].item()), int(c[1].item()), int(c[2].item())
 
     value = v_inv / elapsed
     gteps = e_trav / elapsed / 1e9
@@ -289,7 +289,7 @@ def main():
     # the HBM peak; it is reported for recomputation, while `roofline` uses the bytes the kernels
     # actually have to move. Without stale edges every traversed edge matches (E_match = E_trav).
     per_wave = lambda x: x / args.steps
-    e_match = e_trav if not cfg.get("stale_pct") else st.e_match * world
+    e_match = e_trav if not cfg.get("stale_pct") else e_match_all
     b_formula = 28 * v_inv + 24 * e_trav + 4 * e_match + 4 * len(roots) * args.steps
     result["survey_formula"] = {
         "layout": "A", "V_exp": per_wave(v_inv), "E_trav": per_wave(e_trav), "E_match": per_wave(e_match),
