@@ -304,7 +304,8 @@ bool part_view(fgi_graph* g, PartView* v);
 // Returns the number of target ids received (concatenated at recv_buf) and sent.
 fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent);
 // Sum of a device u64 over all ranks (RCCL all-reduce), returned on the host.
-fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out);
+fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out,
+                              uint32_t count = 1);
 // Partitioned wave over global root ids (wave.hip), and its phases.
 fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                          fgi_wave_stats* stats);
@@ -317,7 +318,8 @@ fgi_status part_level_work(fgi_graph* g, int L, bool pull);
 fgi_status part_level_apply(fgi_graph* g, int L, uint64_t n_recv, uint64_t n_sent);
 // all-gather every rank's local frontier words into front_global (part.hip)
 fgi_status part_allgather_front(fgi_graph* g);
-fgi_status part_level_account(fgi_graph* g, int L);
+fgi_status part_level_fetch(fgi_graph* g);
+fgi_status part_level_account(fgi_graph* g, int L, bool fetched = false);
 fgi_status part_wave_end(fgi_graph* g, fgi_wave_stats* stats);
 // Append (used, dependant slot, tag) entries to rows (set semantics, no state checks).
 fgi_status append_edges(fgi_graph* g, uint64_t m, const uint32_t* used_dev, const uint32_t* dep_dev,

@@ -105,13 +105,14 @@ fgi_status part_allgather_front(fgi_graph* g) {
     return FGI_OK;
 }
 
-fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out) {
+fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out, uint32_t count) {
     PartState* p = ps(g);
     hipStream_t s = g->stream;
-    FGI_NCCL(g, ncclAllReduce(dev_val, p->scalar, 1, ncclUint64, ncclSum, p->comm, s));
-    FGI_HIP(g, hipMemcpyAsync(p->scalar_host, p->scalar, 8, hipMemcpyDeviceToHost, s));
+    if (count < 1 || count > 2) return set_err(g, FGI_EINVAL, "part_allreduce_sum: count %u", count);
+    FGI_NCCL(g, ncclAllReduce(dev_val, p->scalar, count, ncclUint64, ncclSum, p->comm, s));
+    FGI_HIP(g, hipMemcpyAsync(p->scalar_host, p->scalar, 8 * count, hipMemcpyDeviceToHost, s));
     FGI_HIP(g, hipStreamSynchronize(s));
-    *out = *p->scalar_host;
+    for (uint32_t i = 0; i < count; ++i) out[i] = p->scalar_host[i];
     return FGI_OK;
 }
 
@@ -335,13 +336,13 @@ static fgi_status part_alloc(fgi_graph* g, uint32_t n_global) {
     if (hipMalloc(&p->v.recv_buf, (size_t)W * block * 4) != hipSuccess) return fail("recv buffer");
     if (hipMalloc(&p->v.send_cnt, (size_t)W * 8) != hipSuccess) return fail("counts");
     if (hipMalloc(&p->all_cnt, (size_t)W * W * 8) != hipSuccess) return fail("counts");
-    if (hipMalloc(&p->scalar, 8) != hipSuccess) return fail("scalar");
+    if (hipMalloc(&p->scalar, 16) != hipSuccess) return fail("scalar");
     p->v.front_words_global = (uint64_t)n_global / 32 + 2;
     if (hipMalloc(&p->v.front_global, p->v.front_words_global * 4) != hipSuccess) return fail("frontier bitmap");
     if (hipMemset(p->v.front_global, 0, p->v.front_words_global * 4) != hipSuccess) return fail("frontier bitmap");
-    if (hipMalloc(&p->v.scratch_u64, 8) != hipSuccess) return fail("scratch");
+    if (hipMalloc(&p->v.scratch_u64, 16) != hipSuccess) return fail("scratch");
     if (hipHostMalloc(reinterpret_cast<void**>(&p->all_cnt_host), (size_t)W * W * 8) != hipSuccess) return fail("host");
-    if (hipHostMalloc(reinterpret_cast<void**>(&p->scalar_host), 8) != hipSuccess) return fail("host");
+    if (hipHostMalloc(reinterpret_cast<void**>(&p->scalar_host), 16) != hipSuccess) return fail("host");
     return FGI_OK;
 }
 

@@ -1787,9 +1787,10 @@ fgi_status part_level_mark(fgi_graph* g, int L, bool pull) {
     hipStream_t s = g->stream;
     int n_cu = 256;
     hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device);
-    static const unsigned long long one = 1;
+    // the flag's high word is zero (the ring slot was cleared two levels ago or at wave start), so a
+    // 32-bit device-side set of the low word is the whole store, with no pageable host copy
     if (pull)
-        FGI_HIP(g, hipMemcpyAsync(&g->ctr->lvl[L % kRing].pull, &one, 8, hipMemcpyHostToDevice, s));
+        FGI_HIP(g, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&g->ctr->lvl[L % kRing].pull), 1, 1, s));
     hipLaunchKernelGGL(k_mark, dim3((uint32_t)n_cu * 2), dim3(kBlock), 0, s, L, g->inv, g->front_bm, g->ctr);
     FGI_HIP(g, hipGetLastError());
     return FGI_OK;
@@ -1839,10 +1840,19 @@ fgi_status part_level_apply(fgi_graph* g, int L, uint64_t n_recv, uint64_t n_sen
     return FGI_OK;
 }
 
-// after the level's frontier total is known (the stream has been synchronised by then)
-fgi_status part_level_account(fgi_graph* g, int L) {
+// after the level's frontier total is known (the stream has been synchronised by then).
+// fetched: the caller already enqueued the counter copy (part_level_fetch) ahead of the
+// synchronisation it waited on, so the copy needs no sync of its own.
+fgi_status part_level_fetch(fgi_graph* g) {
     FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, g->stream));
-    FGI_HIP(g, hipStreamSynchronize(g->stream));
+    return FGI_OK;
+}
+
+fgi_status part_level_account(fgi_graph* g, int L, bool fetched) {
+    if (!fetched) {
+        FGI_TRY(part_level_fetch(g));
+        FGI_HIP(g, hipStreamSynchronize(g->stream));
+    }
     const LevelCtr& lc = g->ctr_host->lvl[L % kRing];
     g->pw.levels++;
     g->pw.e_trav += lc.T;
@@ -1908,10 +1918,15 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     FGI_TRY(part_wave_begin(g, n_roots, roots_dev, imm_dev));
     const bool allow_pull = g->opt_direction != 1 && g->uin_src && g->uin_epoch == g->mut_epoch;
     uint64_t e_global = 0, f_global = 0, t_global = 0;
-    FGI_HIP(g, hipMemcpy(pv.scratch_u64, &g->pool_top, 8, hipMemcpyHostToDevice));
-    FGI_TRY(part_allreduce_sum(g, pv.scratch_u64, &e_global));
+    // one all-reduce of {local edges, level-0 frontier} (pull threshold and the loop condition)
+    uint64_t sums[2] = {0, 0};
+    FGI_HIP(g, hipMemcpyAsync(pv.scratch_u64, &g->pool_top, 8, hipMemcpyHostToDevice, g->stream));
+    FGI_HIP(g, hipMemcpyAsync(pv.scratch_u64 + 1, part_level_frontier_dev(g, 0), 8, hipMemcpyDeviceToDevice,
+                              g->stream));
+    FGI_TRY(part_allreduce_sum(g, pv.scratch_u64, sums, 2));
+    e_global = sums[0];
+    f_global = sums[1];
     const uint64_t threshold = e_global / (uint64_t)(g->opt_pull_alpha > 0 ? g->opt_pull_alpha : 1);
-    FGI_TRY(part_allreduce_sum(g, part_level_frontier_dev(g, 0), &f_global));
     int L = 0;
     bool last_pull = false;
     for (; f_global != 0; ++L) {
@@ -1924,8 +1939,10 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
         uint64_t n_recv = 0, n_sent = 0;
         if (!pull) FGI_TRY(part_exchange(g, &n_recv, &n_sent));
         FGI_TRY(part_level_apply(g, L, n_recv, n_sent));
+        // the counter copy rides on the all-reduce's stream synchronisation (one sync per level less)
+        FGI_TRY(part_level_fetch(g));
         FGI_TRY(part_allreduce_sum(g, part_level_frontier_dev(g, L + 1), &f_global));
-        FGI_TRY(part_level_account(g, L));
+        FGI_TRY(part_level_account(g, L, true));
         last_pull = pull;
     }
     // the last level's pull winners (without rows) are collected into the invalidated list
