@@ -312,8 +312,8 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
 fgi_status part_wave_begin(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev);
 const unsigned long long* part_level_frontier_dev(fgi_graph* g, int L);
 const unsigned long long* part_level_edges_dev(fgi_graph* g, int L);
-fgi_status part_level_scan(fgi_graph* g, int L);
-fgi_status part_level_mark(fgi_graph* g, int L, bool pull);
+fgi_status part_level_scan(fgi_graph* g, int L, bool keep_fb = false);
+fgi_status part_level_mark(fgi_graph* g, int L, bool pull, bool prev_pull = false);
 fgi_status part_level_work(fgi_graph* g, int L, bool pull);
 fgi_status part_level_apply(fgi_graph* g, int L, uint64_t n_recv, uint64_t n_sent);
 // all-gather every rank's local frontier words into front_global (part.hip)

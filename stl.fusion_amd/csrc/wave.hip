@@ -852,14 +852,14 @@ __global__ __launch_bounds__(kScanThreads, 4) void k_scan_apply(int L, const uin
 // The previous level's winners (pushed, received or collected after a pull: the range [marked,
 // inv)) become the frontier bitmap of a pull level.
 __global__ __launch_bounds__(kBlock) void k_mark(int L, const uint32_t* __restrict__ inv, uint32_t* front_bm,
-                                                 WaveCtr* ctr) {
+                                                 WaveCtr* ctr, int copied) {
     LevelCtr& lc = ctr->lvl[L % kRing];
     const uint64_t lo = ctr->marked, hi = ctr->inv;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         lc.mark_lo = lo;
         lc.mark_hi = hi;
     }
-    if (!lc.pull) return;
+    if (!lc.pull || copied) return;   // copied: the previous pull's winners bitmap was copied in whole
     for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint32_t h = inv[i];
@@ -1767,12 +1767,14 @@ const unsigned long long* part_level_edges_dev(fgi_graph* g, int L) { return &g-
 
 // scan of the local frontier (its edge total T decides push vs pull for every rank); after a pull
 // level, the local winners bitmap becomes the invalidated-list tail and the frontier list first
-fgi_status part_level_scan(fgi_graph* g, int L) {
+// keep_fb: the previous level pulled; its winners bitmap (front_nx) is kept for part_level_mark to
+// copy (the next pull overwrites every word, so stale bits are never read)
+fgi_status part_level_scan(fgi_graph* g, int L, bool keep_fb) {
     PartView pv;
     part_view(g, &pv);
     hipStream_t s = g->stream;
     const int buf = L & 1;
-    const CollectArgs ca = collect_args(g, pv.n_local, part_grid(g), g->front_nx, 1, buf);
+    const CollectArgs ca = collect_args(g, pv.n_local, part_grid(g), g->front_nx, keep_fb ? 0 : 1, buf);
     FGI_HIP(g, hipMemsetAsync(pv.send_cnt, 0, (size_t)pv.world * 8, s));
     hipLaunchKernelGGL(k_scan_reduce, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->fr_len[buf], g->partials, g->ctr, ca);
     hipLaunchKernelGGL(k_scan_apply, dim3(kScanBlocks), dim3(kScanThreads), 0, s, L, g->fr_len[buf], g->partials, g->escan,
@@ -1783,7 +1785,9 @@ fgi_status part_level_scan(fgi_graph* g, int L) {
 
 // marks the previous level's winners into the local frontier bitmap on a pull level; the local
 // frontier words front_bm[0, block/32) are then all-gathered into pv.front_global
-fgi_status part_level_mark(fgi_graph* g, int L, bool pull) {
+// prev_pull (with part_level_scan(keep_fb)): the previous pull level's winners bitmap is exactly
+// the set [marked, inv) just collected, so it is copied whole instead of one atomic per winner
+fgi_status part_level_mark(fgi_graph* g, int L, bool pull, bool prev_pull) {
     hipStream_t s = g->stream;
     int n_cu = 256;
     hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device);
@@ -1791,7 +1795,10 @@ fgi_status part_level_mark(fgi_graph* g, int L, bool pull) {
     // 32-bit device-side set of the low word is the whole store, with no pageable host copy
     if (pull)
         FGI_HIP(g, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&g->ctr->lvl[L % kRing].pull), 1, 1, s));
-    hipLaunchKernelGGL(k_mark, dim3((uint32_t)n_cu * 2), dim3(kBlock), 0, s, L, g->inv, g->front_bm, g->ctr);
+    const bool copy = pull && prev_pull;
+    if (copy) FGI_HIP(g, hipMemcpyAsync(g->front_bm, g->front_nx, g->bm_words * 4, hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(k_mark, dim3((uint32_t)n_cu * 2), dim3(kBlock), 0, s, L, g->inv, g->front_bm, g->ctr,
+                       copy ? 1 : 0);
     FGI_HIP(g, hipGetLastError());
     return FGI_OK;
 }
@@ -1930,10 +1937,10 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     int L = 0;
     bool last_pull = false;
     for (; f_global != 0; ++L) {
-        FGI_TRY(part_level_scan(g, L));
+        FGI_TRY(part_level_scan(g, L, last_pull));
         FGI_TRY(part_allreduce_sum(g, part_level_edges_dev(g, L), &t_global));
         const bool pull = allow_pull && (g->opt_direction == 2 || t_global > threshold);
-        FGI_TRY(part_level_mark(g, L, pull));
+        FGI_TRY(part_level_mark(g, L, pull, last_pull));
         if (pull) FGI_TRY(part_allgather_front(g));
         FGI_TRY(part_level_work(g, L, pull));
         uint64_t n_recv = 0, n_sent = 0;
