@@ -889,13 +889,14 @@ __device__ __forceinline__ void tile_totals(const PullTile* __restrict__ tiles, 
 
 __global__ __launch_bounds__(kBlock) void k_clear_front(int L, const uint32_t* __restrict__ inv, uint32_t* front_bm,
                                                         WaveCtr* ctr, const PullTile* __restrict__ tiles,
-                                                        uint64_t n_tiles) {
+                                                        uint64_t n_tiles, int wiped) {
     __shared__ unsigned long long s_red[kBlock / 64];
     LevelCtr& lc = ctr->lvl[L % kRing];
     const uint64_t lo = lc.mark_lo, hi = lc.mark_hi;
     if (blockIdx.x == 0 && threadIdx.x == 0) ctr->marked = hi;
     if (!lc.pull) return;
     if (blockIdx.x == 0) tile_totals(tiles, n_tiles, ctr->lvl[(L + 1) % kRing], s_red);
+    if (wiped) return;   // the host cleared the whole bitmap (one memset instead of a store per winner)
     for (uint64_t i = lo + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < hi;
          i += (uint64_t)gridDim.x * blockDim.x)
         front_bm[inv[i] >> 5] = 0u;   // every set bit of the word belongs to this level's frontier
@@ -1840,8 +1841,12 @@ fgi_status part_level_apply(fgi_graph* g, int L, uint64_t n_recv, uint64_t n_sen
                                nullptr},
                            g->ctr, g->blk_stats);
     const uint64_t n_tiles = pull_iters(pv.n_local, part_grid(g)) * part_grid(g);
+    // after a pull level every set bit of the frontier bitmap is this level's (it is all-zero
+    // otherwise), so one memset replaces the per-winner clears
+    const bool wipe = g->pw.pulled;
+    if (wipe) FGI_HIP(g, hipMemsetAsync(g->front_bm, 0, g->bm_words * 4, s));
     hipLaunchKernelGGL(k_clear_front, dim3((uint32_t)n_cu * 2), dim3(kBlock), 0, s, L, g->inv, g->front_bm, g->ctr,
-                       g->tiles, n_tiles);
+                       g->tiles, n_tiles, wipe ? 1 : 0);
     FGI_HIP(g, hipGetLastError());
     g->pw.sent += n_sent;
     return FGI_OK;
