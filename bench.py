@@ -32,40 +32,78 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(threads: int, scale: int = 20, edge_factor: int = 16, roots: int = 256, runs: int = 3):
-    """Time the oracle (reference-faithful CPU cascade) on R-MAT scale `scale` (same generator and
-    seeds as config 2, 1/16 of its nodes at scale 20) with `roots` roots, parallel over roots."""
+def host_cpu_info():
+    """What the CPU baseline runs on: nproc (honours the box's OMP_NUM_THREADS share), the cgroup
+    CPU quota, the affinity mask size and the lscpu model name."""
+    import subprocess
+    info = {"affinity": len(os.sched_getaffinity(0))}
+    try:
+        info["nproc"] = int(subprocess.run(["nproc"], capture_output=True, text=True).stdout.strip())
+    except (OSError, ValueError):
+        info["nproc"] = info["affinity"]
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        info["cgroup_cpus"] = None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        info["cgroup_cpus"] = None
+    try:
+        for line in subprocess.run(["lscpu"], capture_output=True, text=True).stdout.splitlines():
+            if line.startswith("Model name:"):
+                info["model"] = line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return info
+
+
+def peak_rss_gb():
+    try:
+        for line in open("/proc/self/status"):
+            if line.startswith("VmHWM:"):
+                return int(line.split()[1]) / 2**20
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(threads: int, cfg: dict, scale: int, gpu_roots=None):
+    """Time the oracle (reference-faithful CPU cascade: per-node mutex, HashSetSlim3 `_usedBy`,
+    hash registry; oracle/fgo.cpp restating Computed.cs:162-230) parallel over roots. At the
+    workload's own scale it builds the IDENTICAL graph and root batch (same generator and seeds;
+    the roots are checked equal to the GPU's); a smaller --cpu-scale gives a labelled sample.
+    One timed wave at T = `threads`, then (after a restore) one at T = 1."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import fgo  # test infrastructure: the CPU restatement, used here only as the baseline
-    seed = 0x5EED0024
+    fgo.set_threads(threads)
+    seed = cfg["seed"]
     n = 1 << scale
     t0 = time.time()
-    s, d = fgo.gen_rmat(scale, edge_factor, seed)
-    tags = fgo.gen_tags(s, d, seed)
+    s, d = fgo.gen_rmat(scale, cfg["edge_factor"], seed)
+    tags = fgo.gen_tags(s, d, seed, cfg.get("stale_pct", 0), cfg.get("stale_seed", 0))
     o = fgo.Oracle(n)
     o.load_graph(fgo.version_of(seed, np.arange(n)), None, s, d, tags)
-    deg = np.bincount(s, minlength=n)
-    r = fgo.gen_roots(roots, n, 0x5EED1024, deg)
+    n_roots = cfg["roots"] if scale == cfg["scale"] else max(64, cfg["roots"] >> (cfg["scale"] - scale))
+    r = fgo.gen_roots(n_roots, n, cfg["roots_seed"], np.bincount(s, minlength=n))
+    m = len(s)
+    del s, d, tags
+    identical_roots = gpu_roots is not None and scale == cfg["scale"] and np.array_equal(r, gpu_roots)
     o.snapshot()
     build_s = time.time() - t0
 
     def timed(th):
-        o.restore()
         st = fgo.Stats()
         t = time.perf_counter()
         o.invalidate_slots(r, None, threads=th, stats=st)
         return time.perf_counter() - t, st
 
     out = {}
-    for th in sorted({1, threads}):
-        timed(th)  # warm-up
-        res = [timed(th) for _ in range(runs)]
-        t_med = statistics.median([x[0] for x in res])
-        st = res[0][1]
-        out[th] = dict(s=t_med, v_inv=st.v_inv, e_trav=st.e_trav)
-    o.restore()
+    for k, th in enumerate(sorted({threads, 1}, reverse=True)):
+        if k:
+            o.restore()
+        dt, st = timed(th)
+        out[th] = dict(s=dt, v_inv=st.v_inv, e_trav=st.e_trav)
+        log(f"cpu baseline T={th}: {dt:.2f} s, {st.v_inv} nodes, {st.e_trav} edges")
     o.close()
-    return out, build_s, len(s)
+    return out, build_s, m, len(r), identical_roots
 
 
 def profiled_traffic(kname, config_scale, live_avg_ms):
@@ -104,7 +142,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="rmat24")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-scale", type=int, default=20)
+    ap.add_argument("--cpu-scale", type=int, default=0,
+                    help="R-MAT scale of the CPU baseline (default: the workload's own, i.e. the identical graph)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host roots -> host ids) leg")
     ap.add_argument("--partition", action="store_true",
                     help="use the partitioned RCCL engine even at N=1 (it is always used for N>1)")
     args = ap.parse_args()
@@ -208,6 +248,30 @@ def main():
     torch.cuda.synchronize()
     instrumented_ms = (time.perf_counter() - t_k) / args.steps * 1e3
 
+    # end-to-end leg (SURVEY.md §8(d)'s t: root H2D -> wave -> V_inv D2H complete): fgi_invalidate
+    # with the roots in host memory and the invalidated ids copied into a pinned host buffer
+    e2e = None
+    if not partitioned and not args.no_e2e:
+        out_host = torch.empty(g.n_handles, dtype=torch.int32).pin_memory()
+        g.set_option(pkg.fgi.OPT_LEVEL_TIMING, 0)
+        for _ in range(max(1, args.warmup)):
+            g.restore()
+            g.invalidate_into(roots, out_host.data_ptr(), g.n_handles)
+        st_e = pkg.WaveStats()
+        torch.cuda.synchronize()
+        t_e = time.perf_counter()
+        n_out = 0
+        for _ in range(args.steps):
+            g.restore()
+            n_out = g.invalidate_into(roots, out_host.data_ptr(), g.n_handles, st_e)
+        torch.cuda.synchronize()
+        e2e_s = time.perf_counter() - t_e
+        g.set_option(pkg.fgi.OPT_LEVEL_TIMING, 1)
+        e2e = {"ms_per_step": e2e_s / args.steps * 1e3, "value": st_e.v_inv / e2e_s,
+               "ids_copied_per_step": n_out, "d2h_bytes_per_step": 4 * n_out,
+               "note": "restore + fgi_invalidate(host roots -> pinned host ids); PCIe-inclusive, never `value`"}
+        del out_host
+
     v_inv, e_trav, e_match_all = st.v_inv, st.e_trav, st.e_match
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
@@ -296,24 +360,48 @@ def main():
         "R": len(roots), "bytes_per_wave": per_wave(b_formula),
         "push_equivalent_gbs": b_formula / elapsed / 1e9,
         "note": "push-equivalent: pull levels do not read these edges; see roofline for the bytes moved"}
-    if rank == 0 and world == 1 and not args.no_cpu:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, len(os.sched_getaffinity(0)))
+    if e2e:
+        result["e2e_ms_per_step"] = e2e["ms_per_step"]
+        result["e2e"] = e2e
+    try:
+        rv, rpath = pkg.fgi.rccl_info()
+        result["rccl"] = {"version": rv, "path": rpath}
+        log(f"[rank {rank}] libfgi RCCL: ncclGetVersion {rv} from {rpath}")
+    except Exception as e:  # informational only
+        result["rccl"] = {"error": repr(e)}
+    if rank == 0 and world == 1 and not args.no_cpu and cfg["kind"] == "rmat":
+        info = host_cpu_info()
+        threads = info["nproc"]
+        cscale = args.cpu_scale or cfg["scale"]
         try:
-            cpu, cbuild, cm = cpu_baseline(threads, scale=args.cpu_scale)
+            cpu, cbuild, cm, cr, same_roots = cpu_baseline(threads, cfg, cscale, roots)
             best = cpu[threads]
+            same = cscale == cfg["scale"]
             result["cpu_baseline"] = {
                 "value": best["v_inv"] / best["s"],
                 "unit": "invalidated nodes/s",
                 "cores": threads,
                 "kind": "port",
-                "sample": (f"oracle (C++ restatement of Computed.Invalidate cascade, per-node mutex, "
-                           f"HashSetSlim3 usedBy, hash registry) on R-MAT scale {args.cpu_scale} "
-                           f"(same generator/seed as configs[1], {cm} edges), 256 roots, parallel over roots; "
-                           f"median of 3 after 1 warm-up; {best['v_inv']} nodes / {best['e_trav']} edges per wave"),
+                "sample": (f"oracle (C++ restatement of the Computed.Invalidate cascade: per-node mutex, HashSetSlim3 "
+                           f"usedBy, hash registry, RemoveUsedBy) on "
+                           + (f"the identical {args.config} graph and {cr}-root batch (BASELINE.json configs[1]: R-MAT "
+                              f"scale {cscale}, {cm} edges; roots equal to the GPU's: {same_roots})" if same else
+                              f"a labelled sample: R-MAT scale {cscale} ({cm} edges), {cr} roots")
+                           + f", parallel over roots at T = nproc = {threads}; one timed wave per thread count, "
+                             f"{best['v_inv']} nodes / {best['e_trav']} edges per wave"),
                 "gteps": best["e_trav"] / best["s"] / 1e9,
+                "wave_s": best["s"],
                 "single_thread_value": cpu[1]["v_inv"] / cpu[1]["s"],
+                "single_thread_wave_s": cpu[1]["s"],
+                "same_result_as_gpu": bool(same and best["v_inv"] == st.v_inv // args.steps
+                                           and best["e_trav"] == st.e_trav // args.steps),
+                "host": info,
+                "build_s": cbuild,
+                "peak_rss_gb": peak_rss_gb(),
             }
-            log(f"cpu baseline: {cpu} (build {cbuild:.1f}s)")
+            if same:
+                result["cpu_baseline"]["gpu_speedup"] = value / result["cpu_baseline"]["value"]
+            log(f"cpu baseline: {cpu} (build {cbuild:.1f}s, host {info})")
         except Exception as e:  # the CPU leg must not hide the GPU number
             result["cpu_baseline"] = {"value": None, "error": repr(e)}
     if rank == 0:

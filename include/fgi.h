@@ -248,11 +248,16 @@ fgi_status fgi_part_invalidate(fgi_graph* g, uint32_t n_roots, const uint32_t* r
                                const uint8_t* immediately_dev, uint64_t* out_n, fgi_wave_stats* stats);
 fgi_status fgi_part_export_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n);
 /* In-process partition group: `p` graphs (created with rank = i, world = p) emulate p ranks in
- * one process — on one device or several — and exchange frontier targets by device copies.
- * Same kernels as the RCCL path; used to test and rehearse the multi-GPU engine on one GPU. */
+ * one process — on one device or several. fgi_part_local_invalidate runs the RCCL path's own level
+ * loop on every rank (one host thread per rank); only the collectives differ (device copies
+ * between the group's buffers instead of RCCL). Used to test and rehearse the multi-GPU engine on
+ * one GPU. */
 fgi_status fgi_part_init_local(fgi_graph* const* gs, uint32_t p, uint32_t n_global);
 fgi_status fgi_part_local_invalidate(fgi_graph* const* gs, uint32_t p, uint32_t n_roots, const uint32_t* roots,
                                      const uint8_t* immediately /*nullable*/, fgi_wave_stats* stats /*p entries*/);
+/* ncclGetVersion of the RCCL the engine's collectives are bound to, and the file it was loaded
+ * from (a process that already loaded another librccl with the same soname shares that one). */
+fgi_status fgi_rccl_info(int* version, char* path /*nullable*/, uint64_t cap);
 
 #ifdef __cplusplus
 }

@@ -213,6 +213,21 @@ struct Registry {
     }
 };
 
+// Worker threads for bulk work (graph import, snapshot/restore, generators); 1 = serial. Results
+// do not depend on it: each thread owns a disjoint set of nodes and visits the edges in input order.
+uint32_t g_threads = 1;
+
+template <class F>
+void parallel_for_threads(uint32_t T, F&& f) {
+    if (T <= 1) {
+        f(0u, 1u);
+        return;
+    }
+    std::vector<std::thread> ts;
+    for (uint32_t t = 0; t < T; ++t) ts.emplace_back([&, t]() { f(t, T); });
+    for (auto& t : ts) t.join();
+}
+
 struct Ctx {                     // per-thread cascade state
     std::vector<UsedByEntry> stack;
     std::vector<uint32_t> log;
@@ -410,15 +425,25 @@ int fgo_load_graph(fgo* o, uint32_t n, const uint64_t* version, const uint32_t* 
             o->reg.vals[i].store(nd);
         }
     }
-    for (uint64_t e = 0; e < m; ++e) {
-        Node* s = src[e] < n ? o->last[src[e]] : nullptr;
-        if (!s || dst[e] >= o->n_slots) return 1;
-        s->used_by.add(UsedByEntry{dst[e], tag[e]});
-        Node* d = o->last[dst[e]];
-        if (d && d->version == tag[e]) d->used.add(s);
-    }
+    for (uint64_t e = 0; e < m; ++e)
+        if (src[e] >= n || !o->last[src[e]] || dst[e] >= o->n_slots) return 1;
+    // thread t owns the sets of the nodes whose slot is t mod T; every thread walks the edges in
+    // input order, so each set sees the same insertion sequence as a serial import
+    parallel_for_threads(g_threads, [&](uint32_t t, uint32_t T) {
+        for (uint64_t e = 0; e < m; ++e) {
+            Node* s = o->last[src[e]];
+            if (src[e] % T == t) s->used_by.add(UsedByEntry{dst[e], tag[e]});
+            if (dst[e] % T == t) {
+                Node* d = o->last[dst[e]];
+                if (d && d->version == tag[e]) d->used.add(s);
+            }
+        }
+    });
     return 0;
 }
+
+void fgo_set_threads(uint32_t n) { g_threads = n ? n : 1; }
+uint32_t fgo_get_threads(void) { return g_threads; }
 
 uint32_t fgo_current(const fgo* o, uint32_t slot) {
     if (slot >= o->n_slots) return FGO_NONE;
@@ -649,14 +674,17 @@ int fgo_snapshot(fgo* o) {
     o->saved_node_count = o->nodes.size();
     o->saved.clear();
     o->saved.resize(o->nodes.size());
-    for (size_t i = 0; i < o->nodes.size(); ++i) {
-        Node& n = o->nodes[i];
-        SavedNode& s = o->saved[i];
-        s.state = n.state.load();
-        s.flags = n.flags;
-        s.used.copy_from(n.used);
-        s.used_by.copy_from(n.used_by);
-    }
+    const size_t N = o->nodes.size();
+    parallel_for_threads(g_threads, [&](uint32_t t, uint32_t T) {
+        for (size_t i = t; i < N; i += T) {
+            Node& n = o->nodes[i];
+            SavedNode& s = o->saved[i];
+            s.state = n.state.load();
+            s.flags = n.flags;
+            s.used.copy_from(n.used);
+            s.used_by.copy_from(n.used_by);
+        }
+    });
     o->saved_reg.resize(o->reg.mask + 1);
     for (uint64_t i = 0; i <= o->reg.mask; ++i) o->saved_reg[i] = o->reg.vals[i].load();
     return 0;
@@ -664,14 +692,17 @@ int fgo_snapshot(fgo* o) {
 
 int fgo_restore(fgo* o) {
     if (o->saved.empty() || o->nodes.size() != o->saved_node_count) return 1;
-    for (size_t i = 0; i < o->nodes.size(); ++i) {
-        Node& n = o->nodes[i];
-        SavedNode& s = o->saved[i];
-        n.state.store(s.state);
-        n.flags = s.flags;
-        n.used.copy_from(s.used);
-        n.used_by.copy_from(s.used_by);
-    }
+    const size_t N = o->nodes.size();
+    parallel_for_threads(g_threads, [&](uint32_t t, uint32_t T) {
+        for (size_t i = t; i < N; i += T) {
+            Node& n = o->nodes[i];
+            SavedNode& s = o->saved[i];
+            n.state.store(s.state);
+            n.flags = s.flags;
+            n.used.copy_from(s.used);
+            n.used_by.copy_from(s.used_by);
+        }
+    });
     for (uint64_t i = 0; i <= o->reg.mask; ++i) o->reg.vals[i].store(o->saved_reg[i]);
     o->log.clear();
     return 0;

@@ -69,6 +69,11 @@ void fgo_destroy(fgo* o);
 int fgo_load_graph(fgo* o, uint32_t n, const uint64_t* version, const uint32_t* state_flags,
                    uint64_t m, const uint32_t* src, const uint32_t* dst, const uint64_t* tag);
 
+/* Worker threads for the bulk operations (fgo_load_graph, snapshot/restore, fgo_gen_rmat,
+ * fgo_gen_tags); default 1. Results are identical for any value. */
+void fgo_set_threads(uint32_t n);
+uint32_t fgo_get_threads(void);
+
 uint32_t fgo_current(const fgo* o, uint32_t slot);   /* registry Get (ComputedRegistry.cs:57-70) */
 uint32_t fgo_last(const fgo* o, uint32_t slot);      /* most recently created node of the slot */
 uint32_t fgo_node_count(const fgo* o);

@@ -60,6 +60,8 @@ _SIG = {
     "fgo_gen_rmat": ([C.c_uint32, C.c_uint32, C.c_uint64, _u32p, _u32p], C.c_uint64),
     "fgo_gen_tags": ([C.c_uint64, _u32p, _u32p, C.c_uint64, C.c_uint32, C.c_uint64, _u64p], None),
     "fgo_gen_roots": ([C.c_uint32, C.c_uint32, C.c_uint64, _u32p, _u32p], C.c_uint32),
+    "fgo_set_threads": ([C.c_uint32], None),
+    "fgo_get_threads": ([], C.c_uint32),
 }
 _lib = None
 
@@ -88,6 +90,12 @@ def u32(a):
 
 def u64(a):
     return np.ascontiguousarray(np.asarray(a, dtype=np.uint64))
+
+
+def set_threads(n: int):
+    """Worker threads of the bulk operations (import, snapshot/restore, generators); results do not
+    depend on it."""
+    lib().fgo_set_threads(int(n))
 
 
 # ---- workload generators (CPU definitions) ----

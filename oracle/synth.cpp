@@ -4,6 +4,8 @@
 #include "fgo.h"
 
 #include <algorithm>
+#include <atomic>
+#include <thread>
 #include <vector>
 
 namespace {
@@ -32,6 +34,17 @@ inline uint32_t scramble(uint64_t x, uint32_t scale, uint64_t seed) {
     return (uint32_t)x;
 }
 
+template <class F>
+void par(uint32_t T, F&& f) {
+    if (T <= 1) {
+        f(0u, 1u);
+        return;
+    }
+    std::vector<std::thread> ts;
+    for (uint32_t t = 0; t < T; ++t) ts.emplace_back([&, t]() { f(t, T); });
+    for (auto& t : ts) t.join();
+}
+
 uint64_t finish(std::vector<uint64_t>& keys, uint32_t* src, uint32_t* dst) {
     std::sort(keys.begin(), keys.end());
     keys.erase(std::unique(keys.begin(), keys.end()), keys.end());
@@ -43,7 +56,63 @@ uint64_t finish(std::vector<uint64_t>& keys, uint32_t* src, uint32_t* dst) {
     }
     return keys.size();
 }
+
+// Sorted, deduplicated (src, dst) of `keys` (src < 2^scale in the high word) with T threads:
+// bucket by the top bits of src, sort and deduplicate the buckets independently (equal keys share
+// a bucket), concatenate. Same output as finish().
+uint64_t finish_parallel(std::vector<uint64_t>& keys, uint32_t scale, uint32_t T, uint32_t* src, uint32_t* dst) {
+    const uint32_t bb = scale < 10 ? scale : 10;
+    const uint32_t NB = 1u << bb;
+    const uint32_t shift = 32 + scale - bb;
+    const uint64_t m = keys.size();
+    std::vector<uint64_t> cnt((size_t)T * NB, 0);
+    par(T, [&](uint32_t t, uint32_t TT) {
+        const uint64_t lo = m * t / TT, hi = m * (t + 1) / TT;
+        for (uint64_t i = lo; i < hi; ++i) cnt[(size_t)t * NB + (keys[i] >> shift)]++;
+    });
+    std::vector<uint64_t> boff(NB + 1, 0), pos((size_t)T * NB);
+    uint64_t run = 0;
+    for (uint32_t b = 0; b < NB; ++b) {
+        boff[b] = run;
+        for (uint32_t t = 0; t < T; ++t) {
+            pos[(size_t)t * NB + b] = run;
+            run += cnt[(size_t)t * NB + b];
+        }
+    }
+    boff[NB] = run;
+    std::vector<uint64_t> out(m);
+    par(T, [&](uint32_t t, uint32_t TT) {
+        const uint64_t lo = m * t / TT, hi = m * (t + 1) / TT;
+        uint64_t* p = &pos[(size_t)t * NB];
+        for (uint64_t i = lo; i < hi; ++i) out[p[keys[i] >> shift]++] = keys[i];
+    });
+    std::vector<uint64_t>().swap(keys);
+    std::vector<uint64_t> ulen(NB, 0);
+    std::atomic<uint32_t> next{0};
+    par(T, [&](uint32_t, uint32_t) {
+        for (uint32_t b; (b = next.fetch_add(1)) < NB;) {
+            auto first = out.begin() + (ptrdiff_t)boff[b], last = out.begin() + (ptrdiff_t)boff[b + 1];
+            std::sort(first, last);
+            ulen[b] = (uint64_t)(std::unique(first, last) - first);
+        }
+    });
+    std::vector<uint64_t> uoff(NB + 1, 0);
+    for (uint32_t b = 0; b < NB; ++b) uoff[b + 1] = uoff[b] + ulen[b];
+    if (src && dst) {
+        par(T, [&](uint32_t t, uint32_t TT) {
+            for (uint32_t b = t; b < NB; b += TT)
+                for (uint64_t i = 0; i < ulen[b]; ++i) {
+                    const uint64_t k = out[boff[b] + i];
+                    src[uoff[b] + i] = (uint32_t)(k >> 32);
+                    dst[uoff[b] + i] = (uint32_t)k;
+                }
+        });
+    }
+    return uoff[NB];
+}
 }  // namespace
+
+extern "C" uint32_t fgo_get_threads(void);
 
 extern "C" {
 
@@ -86,9 +155,10 @@ uint64_t fgo_gen_rmat(uint32_t scale, uint32_t edge_factor, uint64_t seed, uint3
     const uint64_t one = 1ull << 53;
     const uint64_t tA = one / 100 * 57, tAB = one / 100 * 76, tABC = one / 100 * 95;
     const uint64_t ks = sm64(seed);
-    std::vector<uint64_t> keys;
-    keys.reserve(m);
-    for (uint64_t i = 0; i < m; ++i) {
+    const uint32_t T = fgo_get_threads();
+    std::vector<uint64_t> keys(m);
+    par(T, [&](uint32_t t, uint32_t TT) {
+    for (uint64_t i = m * t / TT; i < m * (t + 1) / TT; ++i) {
         uint64_t s = 0, d = 0;
         for (uint32_t l = 0; l < scale; ++l) {
             const uint64_t u = sm64(ks ^ ((i << 6) | l)) >> 11;
@@ -104,22 +174,24 @@ uint64_t fgo_gen_rmat(uint32_t scale, uint32_t edge_factor, uint64_t seed, uint3
             }
         }
         const uint64_t ps = scramble(s, scale, seed), pd = scramble(d, scale, seed);
-        keys.push_back((ps << 32) | pd);
+        keys[i] = (ps << 32) | pd;
     }
-    uint64_t n = finish(keys, src, dst);
-    return n;
+    });
+    return T > 1 ? finish_parallel(keys, scale, T, src, dst) : finish(keys, src, dst);
 }
 
 void fgo_gen_tags(uint64_t m, const uint32_t* src, const uint32_t* dst, uint64_t ver_seed,
                   uint32_t stale_pct, uint64_t stale_seed, uint64_t* tag) {
-    for (uint64_t e = 0; e < m; ++e) {
-        uint64_t v = fgo_version_of(ver_seed, dst[e]);
-        if (stale_pct) {
-            const uint64_t h = sm64(stale_seed ^ sm64(((uint64_t)src[e] << 32) | dst[e]));
-            if (h % 100 < stale_pct) v += 1;
+    par(fgo_get_threads(), [&](uint32_t t, uint32_t T) {
+        for (uint64_t e = m * t / T; e < m * (t + 1) / T; ++e) {
+            uint64_t v = fgo_version_of(ver_seed, dst[e]);
+            if (stale_pct) {
+                const uint64_t h = sm64(stale_seed ^ sm64(((uint64_t)src[e] << 32) | dst[e]));
+                if (h % 100 < stale_pct) v += 1;
+            }
+            tag[e] = v;
         }
-        tag[e] = v;
-    }
+    });
 }
 
 uint32_t fgo_gen_roots(uint32_t n_roots, uint32_t range, uint64_t seed, const uint32_t* out_degree,

@@ -138,6 +138,7 @@ struct DevBuf {
 
 struct fgi_graph {
     int device = 0;
+    int n_cu = 256;                    // compute units of the device (queried once at create)
     hipStream_t stream = nullptr;
     uint32_t n_slots = 0, n_detached = 0, n_handles = 0;
     int rank = 0, world = 1;
@@ -312,7 +313,7 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
 fgi_status part_wave_begin(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev);
 const unsigned long long* part_level_frontier_dev(fgi_graph* g, int L);
 const unsigned long long* part_level_edges_dev(fgi_graph* g, int L);
-fgi_status part_level_scan(fgi_graph* g, int L, bool keep_fb = false);
+fgi_status part_level_scan(fgi_graph* g, int L, bool prev_pull, bool write_fr);
 fgi_status part_level_mark(fgi_graph* g, int L, bool pull, bool prev_pull = false);
 fgi_status part_level_work(fgi_graph* g, int L, bool pull);
 fgi_status part_level_apply(fgi_graph* g, int L, uint64_t n_recv, uint64_t n_sent);

@@ -859,6 +859,8 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
     };
     if (hipSetDevice(g->device) != hipSuccess) return fail(FGI_EDEVICE);
     if (hipStreamCreateWithFlags(&g->stream, hipStreamNonBlocking) != hipSuccess) return fail(FGI_EDEVICE);
+    if (hipDeviceGetAttribute(&g->n_cu, hipDeviceAttributeMultiprocessorCount, g->device) != hipSuccess || g->n_cu <= 0)
+        g->n_cu = 256;
     const size_t H = g->n_handles;
     if (dmalloc(g, &g->node, H) || dmalloc(g, &g->row_off, H) || dmalloc(g, &g->row_len, H) ||
         dmalloc(g, &g->row_cap, H) || dmalloc(g, &g->used_cnt, H) || dmalloc(g, &g->home, g->n_detached + 1) ||
@@ -1244,6 +1246,11 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
 }
 
 // ---- invalidation entry points ----------------------------------------------------------------
+// The single-device wave and mutation entry points address rows whose entries are local handles; a
+// partitioned graph's rows hold global dependant ids (part.hip), so they must go through fgi_part_*.
+static fgi_status single_only(fgi_graph* g, const char* what) {
+    return g->part ? set_err(g, FGI_ESTATE, "%s: partitioned graph, use the fgi_part_* entry points", what) : FGI_OK;
+}
 static fgi_status stage_roots(fgi_graph* g, uint64_t n) {
     if (g->roots_cap >= n && g->roots_buf) return FGI_OK;
     dfree(g->roots_buf);
@@ -1266,6 +1273,7 @@ static fgi_status copy_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64
 fgi_status fgi_invalidate(fgi_graph* g, uint32_t n_roots, const uint32_t* roots, const uint8_t* immediately,
                           uint32_t* out_ids, uint64_t cap, uint64_t* out_n, fgi_wave_stats* stats) {
     if (!g || (n_roots && !roots)) return FGI_EINVAL;
+    FGI_TRY(single_only(g, "fgi_invalidate"));
     hipSetDevice(g->device);
     FGI_TRY(stage_roots(g, n_roots));
     FGI_TRY(h2d(g, g->roots_buf, roots, n_roots));
@@ -1277,6 +1285,7 @@ fgi_status fgi_invalidate(fgi_graph* g, uint32_t n_roots, const uint32_t* roots,
 fgi_status fgi_invalidate_dev(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                               uint32_t* out_ids_dev, uint64_t* out_n, fgi_wave_stats* stats) {
     if (!g || (n_roots && !roots_dev)) return FGI_EINVAL;
+    FGI_TRY(single_only(g, "fgi_invalidate_dev"));
     hipSetDevice(g->device);
     FGI_TRY(run_wave(g, n_roots, roots_dev, imm_dev, stats));
     if (out_n) *out_n = g->last_wave_n;
@@ -1302,6 +1311,7 @@ fgi_status fgi_last_wave_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint
 
 fgi_status fgi_invalidate_all(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n, fgi_wave_stats* stats) {
     if (!g) return FGI_EINVAL;
+    FGI_TRY(single_only(g, "fgi_invalidate_all"));
     hipSetDevice(g->device);
     FGI_TRY(stage_roots(g, g->n_slots));
     FGI_TRY(fold(g));
@@ -1336,6 +1346,7 @@ fgi_status fgi_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, con
         for (uint32_t j = 0; j < i; ++j) seen[slot[j] >> 6] = 0;
         if (why) return set_err(g, FGI_EINVAL, "%s (%u)", why, bad);
     }
+    FGI_TRY(single_only(g, "fgi_begin_compute"));
     hipSetDevice(g->device);
     hipStream_t st = g->stream;
     Tmp ts, tv, td, tc, tr, tf, to;
@@ -1389,6 +1400,7 @@ fgi_status fgi_add_used(fgi_graph* g, uint32_t n, const uint32_t* dependant, con
         if (dependant[i] >= g->n_handles || used[i] >= g->n_handles)
             return set_err(g, FGI_EINVAL, "handle out of range at %u", i);
     if (n == 0) return FGI_OK;
+    FGI_TRY(single_only(g, "fgi_add_used"));
     hipSetDevice(g->device);
     hipStream_t st = g->stream;
     uint64_t hcap = 64;
@@ -1447,6 +1459,7 @@ fgi_status fgi_set_output(fgi_graph* g, uint32_t n, const uint32_t* handle, uint
     if (!g || (n && !handle)) return FGI_EINVAL;
     if (out_n) *out_n = 0;
     if (n == 0) return FGI_OK;
+    FGI_TRY(single_only(g, "fgi_set_output"));
     hipSetDevice(g->device);
     hipStream_t st = g->stream;
     Tmp th, ts, tr;
@@ -1471,6 +1484,7 @@ fgi_status fgi_set_output(fgi_graph* g, uint32_t n, const uint32_t* handle, uint
 
 fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats) {
     if (!g) return FGI_EINVAL;
+    FGI_TRY(single_only(g, "fgi_prune"));
     hipSetDevice(g->device);
     const auto t0 = std::chrono::steady_clock::now();
     FGI_TRY(fold(g));

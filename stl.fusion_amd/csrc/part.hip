@@ -9,14 +9,25 @@
 // in a wave is the only one that can change it (Computed.cs:164-191 — later visits find it
 // Invalidated, or the flag already set), so dropping the repeats is exact.
 //
-// Per level: local push (k_level<true>) -> counts all-gather (ncclAllGather) -> payload by
-// grouped ncclSend/ncclRecv -> owners apply the received targets (k_apply_recv) -> global
-// frontier size by ncclAllReduce (termination).
+// Per level (run_part_wave, wave.hip): all-reduce of the level's frontier and its edges (push vs
+// pull, termination); a push level expands locally (k_level<true>), all-gathers the per-owner
+// counts, moves the targets by grouped send/recv and the owners apply them (k_apply_recv); a pull
+// level all-gathers the frontier bitmap and every rank pulls its own slots.
+//
+// The collectives sit behind PartComm: RcclComm (one process per GPU, RCCL over xGMI) or
+// LocalComm (an in-process group of P graphs driven by P host threads, device copies between their
+// buffers). Both run the same run_part_wave, so the in-process tests execute exactly the level
+// sequence a multi-GPU run does.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <dlfcn.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstring>
+#include <memory>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -26,9 +37,22 @@
 
 namespace fgi {
 
+// Collectives of a partitioned wave (every rank calls them in the same order).
+struct PartComm {
+    virtual ~PartComm() {}
+    // sum of `count` device u64 over all ranks, returned on the host (synchronises the stream)
+    virtual fgi_status allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out, uint32_t count) = 0;
+    // this level's forwarded targets: send_buf[q] (send_cnt[q] entries) to owner q; the targets
+    // received from every other rank are concatenated at recv_buf
+    virtual fgi_status exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent) = 0;
+    // every rank's local frontier words front_bm[0, block/32) into front_global
+    virtual fgi_status allgather_front(fgi_graph* g) = 0;
+};
+
 struct PartState {
     PartView v{};
     ncclComm_t comm = nullptr;
+    std::unique_ptr<PartComm> ops;
     unsigned long long* all_cnt = nullptr;     // [world * world] device
     unsigned long long* all_cnt_host = nullptr;
     unsigned long long* scalar = nullptr;      // device scratch for all-reduce
@@ -40,6 +64,7 @@ static PartState* ps(fgi_graph* g) { return reinterpret_cast<PartState*>(g->part
 fgi_status part_destroy(fgi_graph* g) {
     PartState* p = ps(g);
     if (!p) return FGI_OK;
+    p->ops.reset();
     if (p->comm) ncclCommDestroy(p->comm);
     hipFree(p->v.ver_all);
     hipFree(p->v.sent_bm);
@@ -74,46 +99,165 @@ static fgi_status nccl_check(fgi_graph* g, ncclResult_t r, const char* what) {
         if (_r != ncclSuccess) return nccl_check((g), _r, #call);          \
     } while (0)
 
-fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent) {
-    PartState* p = ps(g);
-    const uint32_t W = p->v.world, R = p->v.rank;
-    hipStream_t s = g->stream;
-    FGI_NCCL(g, ncclAllGather(p->v.send_cnt, p->all_cnt, W, ncclUint64, p->comm, s));
-    FGI_HIP(g, hipMemcpyAsync(p->all_cnt_host, p->all_cnt, (size_t)W * W * 8, hipMemcpyDeviceToHost, s));
-    FGI_HIP(g, hipStreamSynchronize(s));
-    const unsigned long long* c = p->all_cnt_host;   // c[q * W + r]: sent by q to r
-    uint64_t recv = 0, sent = 0;
-    FGI_NCCL(g, ncclGroupStart());
-    for (uint32_t q = 0; q < W; ++q) {
-        if (q == R) continue;
-        const uint64_t to_q = c[R * W + q], from_q = c[q * W + R];
-        if (to_q)
-            FGI_NCCL(g, ncclSend(p->v.send_buf + (uint64_t)q * p->v.block, to_q, ncclUint32, (int)q, p->comm, s));
-        if (from_q) FGI_NCCL(g, ncclRecv(p->v.recv_buf + recv, from_q, ncclUint32, (int)q, p->comm, s));
-        recv += from_q;
-        sent += to_q;
+// ---- RCCL (one process per GPU) ----------------------------------------------------------------
+struct RcclComm final : PartComm {
+    fgi_status allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out, uint32_t count) override {
+        PartState* p = ps(g);
+        hipStream_t s = g->stream;
+        FGI_NCCL(g, ncclAllReduce(dev_val, p->scalar, count, ncclUint64, ncclSum, p->comm, s));
+        FGI_HIP(g, hipMemcpyAsync(p->scalar_host, p->scalar, 8 * count, hipMemcpyDeviceToHost, s));
+        FGI_HIP(g, hipStreamSynchronize(s));
+        for (uint32_t i = 0; i < count; ++i) out[i] = p->scalar_host[i];
+        return FGI_OK;
     }
-    FGI_NCCL(g, ncclGroupEnd());
-    *n_recv = recv;
-    *n_sent = sent;
-    return FGI_OK;
+    fgi_status exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent) override {
+        PartState* p = ps(g);
+        const uint32_t W = p->v.world, R = p->v.rank;
+        hipStream_t s = g->stream;
+        FGI_NCCL(g, ncclAllGather(p->v.send_cnt, p->all_cnt, W, ncclUint64, p->comm, s));
+        FGI_HIP(g, hipMemcpyAsync(p->all_cnt_host, p->all_cnt, (size_t)W * W * 8, hipMemcpyDeviceToHost, s));
+        FGI_HIP(g, hipStreamSynchronize(s));
+        const unsigned long long* c = p->all_cnt_host;   // c[q * W + r]: sent by q to r
+        uint64_t recv = 0, sent = 0;
+        FGI_NCCL(g, ncclGroupStart());
+        for (uint32_t q = 0; q < W; ++q) {
+            if (q == R) continue;
+            const uint64_t to_q = c[R * W + q], from_q = c[q * W + R];
+            if (to_q)
+                FGI_NCCL(g, ncclSend(p->v.send_buf + (uint64_t)q * p->v.block, to_q, ncclUint32, (int)q, p->comm, s));
+            if (from_q) FGI_NCCL(g, ncclRecv(p->v.recv_buf + recv, from_q, ncclUint32, (int)q, p->comm, s));
+            recv += from_q;
+            sent += to_q;
+        }
+        FGI_NCCL(g, ncclGroupEnd());
+        *n_recv = recv;
+        *n_sent = sent;
+        return FGI_OK;
+    }
+    fgi_status allgather_front(fgi_graph* g) override {
+        PartState* p = ps(g);
+        FGI_NCCL(g, ncclAllGather(g->front_bm, p->v.front_global, p->v.block / 32, ncclUint32, p->comm, g->stream));
+        return FGI_OK;
+    }
+};
+
+// ---- in-process group (P graphs, one host thread per rank) ---------------------------------------
+// The ranks meet at a generation barrier; a rank that fails marks the group failed and releases
+// the others, whose collectives then return FGI_EDEVICE instead of waiting forever.
+struct LocalGroup {
+    std::vector<fgi_graph*> gs;
+    std::mutex mu;
+    std::condition_variable cv;
+    uint32_t arrived = 0;
+    uint64_t gen = 0;
+    bool failed = false;
+    std::vector<uint64_t> vals;   // [P][4] all-reduce contributions
+    std::vector<uint64_t> cnt;    // [P][P] targets rank r forwards to owner q
+
+    explicit LocalGroup(std::vector<fgi_graph*> g) : gs(std::move(g)) {
+        vals.assign(gs.size() * 4, 0);
+        cnt.assign(gs.size() * gs.size(), 0);
+    }
+    bool arrive() {
+        std::unique_lock<std::mutex> lk(mu);
+        if (failed) return false;
+        const uint64_t my = gen;
+        if (++arrived == gs.size()) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+            return true;
+        }
+        cv.wait(lk, [&] { return gen != my || failed; });
+        return !failed;
+    }
+    void fail() {
+        std::lock_guard<std::mutex> lk(mu);
+        failed = true;
+        cv.notify_all();
+    }
+    void reset() {
+        std::lock_guard<std::mutex> lk(mu);
+        failed = false;
+        arrived = 0;
+    }
+};
+
+struct LocalComm final : PartComm {
+    std::shared_ptr<LocalGroup> grp;
+    uint32_t rank;
+    LocalComm(std::shared_ptr<LocalGroup> g, uint32_t r) : grp(std::move(g)), rank(r) {}
+
+    fgi_status peer_failed(fgi_graph* g) { return set_err(g, FGI_EDEVICE, "another rank of the in-process group failed"); }
+
+    fgi_status allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out, uint32_t count) override {
+        PartState* p = ps(g);
+        FGI_HIP(g, hipMemcpyAsync(p->scalar_host, dev_val, 8 * count, hipMemcpyDeviceToHost, g->stream));
+        FGI_HIP(g, hipStreamSynchronize(g->stream));
+        {
+            std::lock_guard<std::mutex> lk(grp->mu);
+            for (uint32_t i = 0; i < count; ++i) grp->vals[(size_t)rank * 4 + i] = p->scalar_host[i];
+        }
+        if (!grp->arrive()) return peer_failed(g);
+        for (uint32_t i = 0; i < count; ++i) {
+            uint64_t t = 0;
+            for (size_t r = 0; r < grp->gs.size(); ++r) t += grp->vals[r * 4 + i];
+            out[i] = t;
+        }
+        if (!grp->arrive()) return peer_failed(g);   // nobody overwrites vals before all have read them
+        return FGI_OK;
+    }
+    fgi_status exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent) override {
+        PartState* p = ps(g);
+        const uint32_t W = p->v.world, R = rank;
+        FGI_HIP(g, hipMemcpyAsync(p->all_cnt_host, p->v.send_cnt, (size_t)W * 8, hipMemcpyDeviceToHost, g->stream));
+        FGI_HIP(g, hipStreamSynchronize(g->stream));   // also: this rank's send buffers are complete
+        {
+            std::lock_guard<std::mutex> lk(grp->mu);
+            for (uint32_t q = 0; q < W; ++q) grp->cnt[(size_t)R * W + q] = p->all_cnt_host[q];
+        }
+        if (!grp->arrive()) return peer_failed(g);
+        uint64_t recv = 0, sent = 0;
+        for (uint32_t q = 0; q < W; ++q) {
+            if (q == R) continue;
+            const uint64_t from_q = grp->cnt[(size_t)q * W + R];
+            if (from_q) {
+                PartState* pq = ps(grp->gs[q]);
+                FGI_HIP(g, hipMemcpyAsync(p->v.recv_buf + recv, pq->v.send_buf + (uint64_t)R * pq->v.block, from_q * 4,
+                                          hipMemcpyDefault, g->stream));
+            }
+            recv += from_q;
+            sent += grp->cnt[(size_t)R * W + q];
+        }
+        // the senders refill their buffers only after the level's closing all-reduce, which every
+        // rank enters after synchronising its stream (these copies included)
+        *n_recv = recv;
+        *n_sent = sent;
+        return FGI_OK;
+    }
+    fgi_status allgather_front(fgi_graph* g) override {
+        PartState* p = ps(g);
+        FGI_HIP(g, hipStreamSynchronize(g->stream));   // this rank's frontier words are final
+        if (!grp->arrive()) return peer_failed(g);
+        const uint64_t words = p->v.block / 32;
+        for (size_t q = 0; q < grp->gs.size(); ++q)
+            FGI_HIP(g, hipMemcpyAsync(p->v.front_global + q * words, grp->gs[q]->front_bm, words * 4, hipMemcpyDefault,
+                                      g->stream));
+        FGI_HIP(g, hipStreamSynchronize(g->stream));
+        if (!grp->arrive()) return peer_failed(g);     // the sources stay untouched until all copies are done
+        return FGI_OK;
+    }
+};
+
+fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent) {
+    return ps(g)->ops->exchange(g, n_recv, n_sent);
 }
 
-fgi_status part_allgather_front(fgi_graph* g) {
-    PartState* p = ps(g);
-    FGI_NCCL(g, ncclAllGather(g->front_bm, p->v.front_global, p->v.block / 32, ncclUint32, p->comm, g->stream));
-    return FGI_OK;
-}
+fgi_status part_allgather_front(fgi_graph* g) { return ps(g)->ops->allgather_front(g); }
 
 fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out, uint32_t count) {
-    PartState* p = ps(g);
-    hipStream_t s = g->stream;
-    if (count < 1 || count > 2) return set_err(g, FGI_EINVAL, "part_allreduce_sum: count %u", count);
-    FGI_NCCL(g, ncclAllReduce(dev_val, p->scalar, count, ncclUint64, ncclSum, p->comm, s));
-    FGI_HIP(g, hipMemcpyAsync(p->scalar_host, p->scalar, 8 * count, hipMemcpyDeviceToHost, s));
-    FGI_HIP(g, hipStreamSynchronize(s));
-    for (uint32_t i = 0; i < count; ++i) out[i] = p->scalar_host[i];
-    return FGI_OK;
+    if (count < 1 || count > 4) return set_err(g, FGI_EINVAL, "part_allreduce_sum: count %u", count);
+    return ps(g)->ops->allreduce_sum(g, dev_val, out, count);
 }
 
 namespace {
@@ -306,6 +450,7 @@ fgi_status fgi_part_init(fgi_graph* g, uint32_t n_global, const uint8_t* id128) 
         part_destroy(g);
         return set_err(g, FGI_EDEVICE, "ncclCommInitRank: %s", ncclGetErrorString(r));
     }
+    p->ops.reset(new RcclComm());
     return FGI_OK;
 }
 
@@ -336,13 +481,13 @@ static fgi_status part_alloc(fgi_graph* g, uint32_t n_global) {
     if (hipMalloc(&p->v.recv_buf, (size_t)W * block * 4) != hipSuccess) return fail("recv buffer");
     if (hipMalloc(&p->v.send_cnt, (size_t)W * 8) != hipSuccess) return fail("counts");
     if (hipMalloc(&p->all_cnt, (size_t)W * W * 8) != hipSuccess) return fail("counts");
-    if (hipMalloc(&p->scalar, 16) != hipSuccess) return fail("scalar");
+    if (hipMalloc(&p->scalar, 32) != hipSuccess) return fail("scalar");
     p->v.front_words_global = (uint64_t)n_global / 32 + 2;
     if (hipMalloc(&p->v.front_global, p->v.front_words_global * 4) != hipSuccess) return fail("frontier bitmap");
     if (hipMemset(p->v.front_global, 0, p->v.front_words_global * 4) != hipSuccess) return fail("frontier bitmap");
-    if (hipMalloc(&p->v.scratch_u64, 16) != hipSuccess) return fail("scratch");
+    if (hipMalloc(&p->v.scratch_u64, 32) != hipSuccess) return fail("scratch");
     if (hipHostMalloc(reinterpret_cast<void**>(&p->all_cnt_host), (size_t)W * W * 8) != hipSuccess) return fail("host");
-    if (hipHostMalloc(reinterpret_cast<void**>(&p->scalar_host), 16) != hipSuccess) return fail("host");
+    if (hipHostMalloc(reinterpret_cast<void**>(&p->scalar_host), 32) != hipSuccess) return fail("host");
     return FGI_OK;
 }
 
@@ -352,151 +497,68 @@ fgi_status fgi_part_init_local(fgi_graph* const* gs, uint32_t P, uint32_t n_glob
         if (!gs[r] || gs[r]->rank != (int)r || gs[r]->world != (int)P) return FGI_EINVAL;
         FGI_TRY(part_alloc(gs[r], n_global));
     }
+    auto grp = std::make_shared<LocalGroup>(std::vector<fgi_graph*>(gs, gs + P));
+    for (uint32_t r = 0; r < P; ++r) ps(gs[r])->ops.reset(new LocalComm(grp, r));
     return FGI_OK;
 }
 
-// In-process driver: the same phases as run_part_wave, the exchange done by device copies.
+// In-process driver: run_part_wave on every rank, one host thread per rank; the collectives meet
+// in the group's LocalComm (exactly the level sequence of the RCCL path).
 fgi_status fgi_part_local_invalidate(fgi_graph* const* gs, uint32_t P, uint32_t n_roots, const uint32_t* roots,
                                      const uint8_t* immediately, fgi_wave_stats* stats) {
     if (!gs || P == 0 || (n_roots && !roots)) return FGI_EINVAL;
-    for (uint32_t r = 0; r < P; ++r)
-        if (!gs[r] || !gs[r]->part || ps(gs[r])->v.world != P) return FGI_EINVAL;
-    std::vector<uint32_t*> rd(P, nullptr);
-    std::vector<uint8_t*> id(P, nullptr);
-    auto cleanup = [&]() {
-        for (uint32_t r = 0; r < P; ++r) {
-            hipSetDevice(gs[r]->device);
-            hipFree(rd[r]);
-            hipFree(id[r]);
-        }
-    };
-    fgi_status st = FGI_OK;
-    for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
-        fgi_graph* g = gs[r];
-        hipSetDevice(g->device);
-        if (n_roots) {
-            if (hipMalloc(&rd[r], n_roots * 4) != hipSuccess ||
-                (immediately && hipMalloc(&id[r], n_roots) != hipSuccess)) {
-                st = FGI_ENOMEM;
-                break;
-            }
-            hipMemcpy(rd[r], roots, n_roots * 4, hipMemcpyHostToDevice);
-            if (immediately) hipMemcpy(id[r], immediately, n_roots, hipMemcpyHostToDevice);
-        }
-        st = part_wave_begin(g, n_roots, rd[r], id[r]);
-    }
-    auto frontier_total = [&](int L, uint64_t* out) -> fgi_status {
-        uint64_t t = 0;
-        for (uint32_t r = 0; r < P; ++r) {
-            unsigned long long f = 0;
-            hipSetDevice(gs[r]->device);
-            FGI_HIP(gs[r], hipMemcpyAsync(&f, part_level_frontier_dev(gs[r], L), 8, hipMemcpyDeviceToHost, gs[r]->stream));
-            FGI_HIP(gs[r], hipStreamSynchronize(gs[r]->stream));
-            t += f;
-        }
-        *out = t;
-        return FGI_OK;
-    };
-    uint64_t f_global = 0;
-    if (st == FGI_OK) st = frontier_total(0, &f_global);   // level 0 frontier (the roots' winners)
-    std::vector<unsigned long long> cnt((size_t)P * P);
-    auto level_total = [&](const unsigned long long* (*field)(fgi_graph*, int), int L, uint64_t* out) -> fgi_status {
-        uint64_t t = 0;
-        for (uint32_t r = 0; r < P; ++r) {
-            unsigned long long f = 0;
-            hipSetDevice(gs[r]->device);
-            FGI_HIP(gs[r], hipMemcpyAsync(&f, field(gs[r], L), 8, hipMemcpyDeviceToHost, gs[r]->stream));
-            FGI_HIP(gs[r], hipStreamSynchronize(gs[r]->stream));
-            t += f;
-        }
-        *out = t;
-        return FGI_OK;
-    };
-    bool allow_pull = true;
-    uint64_t e_global = 0;
+    LocalComm* c0 = nullptr;
     for (uint32_t r = 0; r < P; ++r) {
-        allow_pull &= gs[r]->opt_direction != 1 && gs[r]->uin_src && gs[r]->uin_epoch == gs[r]->mut_epoch;
-        e_global += gs[r]->pool_top;
+        if (!gs[r] || !gs[r]->part || ps(gs[r])->v.world != P) return FGI_EINVAL;
+        LocalComm* c = dynamic_cast<LocalComm*>(ps(gs[r])->ops.get());
+        if (!c || c->rank != r) return set_err(gs[r], FGI_EINVAL, "graph is not rank %u of an in-process group", r);
+        if (c0 && c->grp != c0->grp) return set_err(gs[r], FGI_EINVAL, "graphs of different in-process groups");
+        c0 = c;
     }
-    const int direction = gs[0]->opt_direction;
-    const uint64_t threshold = e_global / (uint64_t)(gs[0]->opt_pull_alpha > 0 ? gs[0]->opt_pull_alpha : 1);
-    int L = 0;
-    bool last_pull = false;
-    for (; st == FGI_OK && f_global != 0; ++L) {
-        uint64_t t_global = 0;
-        for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
-            hipSetDevice(gs[r]->device);
-            st = part_level_scan(gs[r], L);
-        }
-        if (st == FGI_OK) st = level_total(part_level_edges_dev, L, &t_global);
-        const bool pull = allow_pull && (direction == 2 || t_global > threshold);
-        for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
-            hipSetDevice(gs[r]->device);
-            st = part_level_mark(gs[r], L, pull);
-            if (st == FGI_OK) st = hipStreamSynchronize(gs[r]->stream) == hipSuccess ? FGI_OK : FGI_EDEVICE;
-        }
-        if (pull) {   // all-gather of the local frontier words into every rank's global bitmap
-            for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
-                hipSetDevice(gs[r]->device);
-                for (uint32_t q = 0; q < P && st == FGI_OK; ++q) {
-                    const uint32_t words = ps(gs[q])->v.block / 32;
-                    if (hipMemcpyAsync(ps(gs[r])->v.front_global + (uint64_t)q * words, gs[q]->front_bm, words * 4,
-                                       hipMemcpyDefault, gs[r]->stream) != hipSuccess)
-                        st = set_err(gs[r], FGI_EDEVICE, "frontier gather");
-                }
+    c0->grp->reset();
+    std::vector<fgi_status> st(P, FGI_OK);
+    std::vector<std::thread> ts;
+    for (uint32_t r = 0; r < P; ++r) {
+        ts.emplace_back([&, r]() {
+            fgi_graph* g = gs[r];
+            hipSetDevice(g->device);
+            uint32_t* rd = nullptr;
+            uint8_t* id = nullptr;
+            fgi_status s = FGI_OK;
+            if (n_roots && (hipMalloc(&rd, n_roots * 4) != hipSuccess ||
+                            (immediately && hipMalloc(&id, n_roots) != hipSuccess)))
+                s = set_err(g, FGI_ENOMEM, "root buffers");
+            if (s == FGI_OK && n_roots) {
+                if (hipMemcpy(rd, roots, n_roots * 4, hipMemcpyHostToDevice) != hipSuccess ||
+                    (immediately && hipMemcpy(id, immediately, n_roots, hipMemcpyHostToDevice) != hipSuccess))
+                    s = set_err(g, FGI_EDEVICE, "root copy");
             }
-        }
-        for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
-            hipSetDevice(gs[r]->device);
-            st = part_level_work(gs[r], L, pull);
-        }
-        if (!pull) {
-            // counts: cnt[r * P + q] = targets rank r forwards to owner q
-            for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
-                hipSetDevice(gs[r]->device);
-                if (hipMemcpyAsync(&cnt[(size_t)r * P], ps(gs[r])->v.send_cnt, P * 8, hipMemcpyDeviceToHost,
-                                   gs[r]->stream) != hipSuccess ||
-                    hipStreamSynchronize(gs[r]->stream) != hipSuccess)
-                    st = set_err(gs[r], FGI_EDEVICE, "count readback");
-            }
-        } else {
-            std::fill(cnt.begin(), cnt.end(), 0ull);
-            for (uint32_t r = 0; r < P; ++r) hipStreamSynchronize(gs[r]->stream);
-        }
-        for (uint32_t q = 0; q < P && st == FGI_OK; ++q) {
-            fgi_graph* gq = gs[q];
-            hipSetDevice(gq->device);
-            uint64_t off = 0, sent = 0;
-            for (uint32_t r = 0; r < P; ++r) {
-                if (r == q) continue;
-                const uint64_t c = cnt[(size_t)r * P + q];
-                if (c && hipMemcpyAsync(ps(gq)->v.recv_buf + off, ps(gs[r])->v.send_buf + (uint64_t)q * ps(gs[r])->v.block,
-                                        c * 4, hipMemcpyDefault, gq->stream) != hipSuccess)
-                    st = set_err(gq, FGI_EDEVICE, "exchange copy");
-                off += c;
-            }
-            for (uint32_t x = 0; x < P; ++x)
-                if (x != q) sent += cnt[(size_t)q * P + x];
-            if (st == FGI_OK) st = part_level_apply(gq, L, off, sent);
-        }
-        if (st == FGI_OK) st = level_total(part_level_frontier_dev, L + 1, &f_global);
-        for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
-            hipSetDevice(gs[r]->device);
-            st = part_level_account(gs[r], L);
-        }
-        last_pull = pull;
+            if (s == FGI_OK) s = run_part_wave(g, n_roots, rd, id, stats ? stats + r : nullptr);
+            if (s != FGI_OK) c0->grp->fail();
+            hipFree(rd);
+            hipFree(id);
+            st[r] = s;
+        });
     }
-    // the last level's pull winners (without rows) are collected into the invalidated list
-    for (uint32_t r = 0; r < P && st == FGI_OK && last_pull; ++r) {
-        hipSetDevice(gs[r]->device);
-        st = part_level_scan(gs[r], L);
+    for (auto& t : ts) t.join();
+    for (uint32_t r = 0; r < P; ++r)
+        if (st[r] != FGI_OK) return st[r];
+    return FGI_OK;
+}
+
+// The RCCL library the engine's collectives bound to (libfgi links librccl; a process that has
+// already loaded another RCCL with the same soname, e.g. torch's, shares that one).
+fgi_status fgi_rccl_info(int* version, char* path, uint64_t cap) {
+    int v = 0;
+    if (ncclGetVersion(&v) != ncclSuccess) return FGI_EDEVICE;
+    if (version) *version = v;
+    if (path && cap) {
+        Dl_info info{};
+        const char* f = (dladdr(reinterpret_cast<void*>(&ncclGetVersion), &info) && info.dli_fname) ? info.dli_fname : "";
+        std::strncpy(path, f, cap - 1);
+        path[cap - 1] = 0;
     }
-    for (uint32_t r = 0; r < P && st == FGI_OK; ++r) {
-        hipSetDevice(gs[r]->device);
-        st = part_wave_end(gs[r], stats ? stats + r : nullptr);
-    }
-    cleanup();
-    return st;
+    return FGI_OK;
 }
 
 fgi_status fgi_part_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_factor, uint64_t seed, uint32_t stale_pct,

@@ -511,7 +511,7 @@ struct CollectArgs {
     uint32_t pgrid, n_slots;
     uint32_t* fb;                // winners bitmap of the pull level
     uint32_t n_handles;          // rows: row_len has n_handles entries
-    int clear_fb;                // multi-GPU: the words are scratch, cleared after reading
+    int fr_multi;                // multi-GPU collects: also write the frontier list (the next level pushes)
     const uint32_t* __restrict__ row_len;
     uint32_t* inv;
     const uint64_t* __restrict__ row_off;
@@ -559,7 +559,6 @@ __device__ __forceinline__ void collect_tile(const CollectArgs& c, uint64_t t, u
     const uint32_t lane = lane_id();
     const uint64_t s0 = t * kPullTile;   // tile t = it * pgrid + block covers slots [t * kPullTile, +kPullTile)
     const uint64_t base = s0 + 16ull * lane;
-    if (c.clear_fb && m) reinterpret_cast<uint16_t*>(c.fb)[base / 16] = 0;
     uint32_t rl[16];
     uint32_t em = 0, len = 0;
 #pragma unroll
@@ -664,7 +663,7 @@ __device__ __forceinline__ void collect_pass2(const CollectArgs& c, LevelCtr& lc
     // to pull than to expand edge by edge)
     const bool pull = single && te != 0 &&
                       (direction == 2 || (direction == 0 && (tl > pull_threshold || te > c.stay_pull_f)));
-    const bool write_fr = !pull;
+    const bool write_fr = single ? !pull : c.fr_multi != 0;
     __syncthreads();   // block 0's threads have all read lc.mark_lo before thread 0 writes lc
     if (b == 0 && threadIdx.x == 0) {
         lc.F = te;
@@ -1493,7 +1492,7 @@ static fgi_status probe_report(fgi_graph* g, int L, uint32_t grid, const char* w
     return FGI_OK;
 }
 
-static CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, uint32_t pgrid, uint32_t* fb, int clear, int buf) {
+static CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, uint32_t pgrid, uint32_t* fb, int fr_multi, int buf) {
     CollectArgs c;
     c.tiles = g->tiles;
     c.n_tiles = pull_iters(n_slots, pgrid) * pgrid;
@@ -1502,7 +1501,7 @@ static CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, uint32_t pgrid, 
     c.fb = fb;
     c.n_handles = g->n_handles;
     c.stay_pull_f = g->opt_pull_beta > 0 ? n_slots / (uint64_t)g->opt_pull_beta : ~0ull;
-    c.clear_fb = clear;
+    c.fr_multi = fr_multi;
     c.row_len = g->row_len;
     c.inv = g->inv;
     c.row_off = g->row_off;
@@ -1518,9 +1517,7 @@ static CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, uint32_t pgrid, 
 }
 
 static uint32_t level_grid_for(fgi_graph* g, uint32_t per_cu) {
-    int n_cu = 256;
-    hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device);
-    return std::min<uint32_t>((uint32_t)n_cu * per_cu, kStatBlocks);
+    return std::min<uint32_t>((uint32_t)g->n_cu * per_cu, kStatBlocks);
 }
 
 fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
@@ -1766,17 +1763,18 @@ fgi_status part_wave_begin(fgi_graph* g, uint32_t n_roots, const uint32_t* roots
 const unsigned long long* part_level_frontier_dev(fgi_graph* g, int L) { return &g->ctr->lvl[L % kRing].F; }
 const unsigned long long* part_level_edges_dev(fgi_graph* g, int L) { return &g->ctr->lvl[L % kRing].T; }
 
-// scan of the local frontier (its edge total T decides push vs pull for every rank); after a pull
-// level, the local winners bitmap becomes the invalidated-list tail and the frontier list first
-// keep_fb: the previous level pulled; its winners bitmap (front_nx) is kept for part_level_mark to
-// copy (the next pull overwrites every word, so stale bits are never read)
-fgi_status part_level_scan(fgi_graph* g, int L, bool keep_fb) {
+// Level L's list work before its traversal. After a pull level (prev_pull): collect its winners
+// bitmap (front_nx) into the invalidated list, and into the frontier list if level L pushes
+// (write_fr). After a push level, a push level L needs the exclusive scan of its frontier's row
+// lengths (escan) and the chunk map; a pull level L needs neither (part_level_mark marks its frontier).
+fgi_status part_level_scan(fgi_graph* g, int L, bool prev_pull, bool write_fr) {
     PartView pv;
     part_view(g, &pv);
     hipStream_t s = g->stream;
     const int buf = L & 1;
-    const CollectArgs ca = collect_args(g, pv.n_local, part_grid(g), g->front_nx, keep_fb ? 0 : 1, buf);
+    const CollectArgs ca = collect_args(g, pv.n_local, part_grid(g), g->front_nx, write_fr ? 1 : 0, buf);
     FGI_HIP(g, hipMemsetAsync(pv.send_cnt, 0, (size_t)pv.world * 8, s));
+    if (!prev_pull && !write_fr) return FGI_OK;
     hipLaunchKernelGGL(k_scan_reduce, dim3(kScanBlocks), dim3(kBlock), 0, s, L, g->fr_len[buf], g->partials, g->ctr, ca);
     hipLaunchKernelGGL(k_scan_apply, dim3(kScanBlocks), dim3(kScanThreads), 0, s, L, g->fr_len[buf], g->partials, g->escan,
                        g->cstart, g->ctr, 1, ca, 1, ~0ull, g->front_nx, (uint64_t)0);
@@ -1784,20 +1782,21 @@ fgi_status part_level_scan(fgi_graph* g, int L, bool keep_fb) {
     return FGI_OK;
 }
 
-// marks the previous level's winners into the local frontier bitmap on a pull level; the local
-// frontier words front_bm[0, block/32) are then all-gathered into pv.front_global
-// prev_pull (with part_level_scan(keep_fb)): the previous pull level's winners bitmap is exactly
-// the set [marked, inv) just collected, so it is copied whole instead of one atomic per winner
+// Marks the previous level's winners into the local frontier bitmap on a pull level; the local
+// frontier words front_bm[0, block/32) are then all-gathered into pv.front_global. After a pull
+// level (prev_pull) its winners bitmap front_nx is exactly the set [marked, inv) just collected:
+// a pull level L copies it whole instead of one atomic per winner; either way front_nx is cleared
+// here, so no later level or wave reads a stale winner.
 fgi_status part_level_mark(fgi_graph* g, int L, bool pull, bool prev_pull) {
     hipStream_t s = g->stream;
-    int n_cu = 256;
-    hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device);
+    const int n_cu = g->n_cu;
     // the flag's high word is zero (the ring slot was cleared two levels ago or at wave start), so a
     // 32-bit device-side set of the low word is the whole store, with no pageable host copy
     if (pull)
         FGI_HIP(g, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&g->ctr->lvl[L % kRing].pull), 1, 1, s));
     const bool copy = pull && prev_pull;
     if (copy) FGI_HIP(g, hipMemcpyAsync(g->front_bm, g->front_nx, g->bm_words * 4, hipMemcpyDeviceToDevice, s));
+    if (prev_pull) FGI_HIP(g, hipMemsetAsync(g->front_nx, 0, g->bm_words * 4, s));
     hipLaunchKernelGGL(k_mark, dim3((uint32_t)n_cu * 2), dim3(kBlock), 0, s, L, g->inv, g->front_bm, g->ctr,
                        copy ? 1 : 0);
     FGI_HIP(g, hipGetLastError());
@@ -1830,8 +1829,7 @@ fgi_status part_level_apply(fgi_graph* g, int L, uint64_t n_recv, uint64_t n_sen
     PartView pv;
     part_view(g, &pv);
     hipStream_t s = g->stream;
-    int n_cu = 256;
-    hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, g->device);
+    const int n_cu = g->n_cu;
     const int buf = L & 1;
     if (n_recv)
         hipLaunchKernelGGL(k_apply_recv, dim3(std::min<uint64_t>((n_recv + kBlock - 1) / kBlock, (uint64_t)n_cu * 8)),
@@ -1922,43 +1920,58 @@ fgi_status part_wave_end(fgi_graph* g, fgi_wave_stats* stats) {
     return FGI_OK;
 }
 
-// One process per GPU: levels in lockstep over RCCL.
+// The partitioned wave, one call per rank: levels in lockstep, collectives through the rank's
+// PartComm (RCCL over xGMI with one process per GPU, or device copies between the graphs of an
+// in-process group, one host thread per rank — the same level sequence either way). Per level one
+// all-reduce of {frontier, frontier edges} decides push vs pull (Beamer's alpha / beta rules, as
+// run_wave) and termination; push levels add the exchange (counts all-gather, then payloads).
 fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                          fgi_wave_stats* stats) {
     PartView pv;
     part_view(g, &pv);
     FGI_TRY(part_wave_begin(g, n_roots, roots_dev, imm_dev));
-    const bool allow_pull = g->opt_direction != 1 && g->uin_src && g->uin_epoch == g->mut_epoch;
-    uint64_t e_global = 0, f_global = 0, t_global = 0;
-    // one all-reduce of {local edges, level-0 frontier} (pull threshold and the loop condition)
-    uint64_t sums[2] = {0, 0};
-    FGI_HIP(g, hipMemcpyAsync(pv.scratch_u64, &g->pool_top, 8, hipMemcpyHostToDevice, g->stream));
-    FGI_HIP(g, hipMemcpyAsync(pv.scratch_u64 + 1, part_level_frontier_dev(g, 0), 8, hipMemcpyDeviceToDevice,
-                              g->stream));
-    FGI_TRY(part_allreduce_sum(g, pv.scratch_u64, sums, 2));
-    e_global = sums[0];
-    f_global = sums[1];
-    const uint64_t threshold = e_global / (uint64_t)(g->opt_pull_alpha > 0 ? g->opt_pull_alpha : 1);
+    hipStream_t s = g->stream;
+    // one all-reduce of {local edges, level-0 frontier, its edges, ranks without pull lists}
+    const bool can_pull = g->opt_direction != 1 && g->uin_src && g->uin_epoch == g->mut_epoch;
+    const uint64_t head[2] = {g->pool_top, 0};
+    const uint64_t tail[2] = {0, can_pull ? 0ull : 1ull};
+    FGI_HIP(g, hipMemcpyAsync(pv.scratch_u64, head, 8, hipMemcpyHostToDevice, s));
+    FGI_HIP(g, hipMemcpyAsync(pv.scratch_u64 + 1, part_level_frontier_dev(g, 0), 16, hipMemcpyDeviceToDevice, s));
+    FGI_HIP(g, hipMemcpyAsync(pv.scratch_u64 + 3, tail + 1, 8, hipMemcpyHostToDevice, s));
+    uint64_t sums[4] = {0, 0, 0, 0};
+    FGI_TRY(part_allreduce_sum(g, pv.scratch_u64, sums, 4));
+    const uint64_t threshold = sums[0] / (uint64_t)(g->opt_pull_alpha > 0 ? g->opt_pull_alpha : 1);
+    const uint64_t stay_pull_f = g->opt_pull_beta > 0 ? pv.n_global / (uint64_t)g->opt_pull_beta : ~0ull;
+    const bool allow_pull = sums[3] == 0;
+    const int direction = g->opt_direction;
+    uint64_t f_global = sums[1], t_global = sums[2];
     int L = 0;
     bool last_pull = false;
     for (; f_global != 0; ++L) {
-        FGI_TRY(part_level_scan(g, L, last_pull));
-        FGI_TRY(part_allreduce_sum(g, part_level_edges_dev(g, L), &t_global));
-        const bool pull = allow_pull && (g->opt_direction == 2 || t_global > threshold);
+        const bool pull = allow_pull && t_global != 0 &&
+                          (direction == 2 || (direction == 0 && (t_global > threshold ||
+                                                                 (last_pull && f_global > stay_pull_f))));
+        FGI_TRY(part_level_scan(g, L, last_pull, !pull));
         FGI_TRY(part_level_mark(g, L, pull, last_pull));
         if (pull) FGI_TRY(part_allgather_front(g));
         FGI_TRY(part_level_work(g, L, pull));
         uint64_t n_recv = 0, n_sent = 0;
         if (!pull) FGI_TRY(part_exchange(g, &n_recv, &n_sent));
         FGI_TRY(part_level_apply(g, L, n_recv, n_sent));
-        // the counter copy rides on the all-reduce's stream synchronisation (one sync per level less)
+        // the counter copy rides on the all-reduce's stream synchronisation
         FGI_TRY(part_level_fetch(g));
-        FGI_TRY(part_allreduce_sum(g, part_level_frontier_dev(g, L + 1), &f_global));
+        uint64_t ft[2] = {0, 0};
+        FGI_TRY(part_allreduce_sum(g, part_level_frontier_dev(g, L + 1), ft, 2));
+        f_global = ft[0];
+        t_global = ft[1];
         FGI_TRY(part_level_account(g, L, true));
         last_pull = pull;
     }
-    // the last level's pull winners (without rows) are collected into the invalidated list
-    if (last_pull) FGI_TRY(part_level_scan(g, L));
+    // the last pull level's winners (without rows) are collected into the invalidated list
+    if (last_pull) {
+        FGI_TRY(part_level_scan(g, L, true, false));
+        FGI_HIP(g, hipMemsetAsync(g->front_nx, 0, g->bm_words * 4, s));
+    }
     return part_wave_end(g, stats);
 }
 

@@ -101,6 +101,7 @@ SIGNATURES = {
     "fgi_part_export_ids": [_G, _u32p, C.c_uint64, _u64p],
     "fgi_part_init_local": [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32],
     "fgi_part_local_invalidate": [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32, _u32p, _u8p, C.POINTER(WaveStats)],
+    "fgi_rccl_info": [C.POINTER(C.c_int), C.c_char_p, C.c_uint64],
 }
 
 _lib = None
@@ -284,6 +285,16 @@ class Graph:
                                             C.byref(stats) if stats is not None else None), "invalidate")
         return ids[:n.value].copy()
 
+    def invalidate_into(self, roots, out_ptr: int, cap: int, stats: Optional[WaveStats] = None) -> int:
+        """fgi_invalidate with a caller-owned host output buffer (e.g. pinned memory at out_ptr,
+        `cap` entries): root H2D -> wave -> invalidated-slot D2H. Returns the count."""
+        r = _u32(roots)
+        n = C.c_uint64()
+        self._check(self.lib.fgi_invalidate(self.h, len(r), _ptr(r, C.c_uint32), None,
+                                            C.cast(C.c_void_p(out_ptr), _u32p), cap, C.byref(n),
+                                            C.byref(stats) if stats is not None else None), "invalidate")
+        return n.value
+
     def invalidate_dev(self, n_roots: int, roots_ptr: int, imm_ptr: int = 0,
                        stats: Optional[WaveStats] = None) -> int:
         n = C.c_uint64()
@@ -365,6 +376,17 @@ def part_unique_id() -> bytes:
     if st != OK:
         raise FgiError(st, "fgi_part_unique_id")
     return bytes(buf)
+
+
+def rccl_info():
+    """(ncclGetVersion, library path) of the RCCL the engine's collectives are bound to."""
+    lib = load_library()
+    v = C.c_int()
+    buf = C.create_string_buffer(4096)
+    st = lib.fgi_rccl_info(C.byref(v), buf, len(buf))
+    if st != OK:
+        raise FgiError(st, "fgi_rccl_info")
+    return v.value, buf.value.decode(errors="replace")
 
 
 def part_init_local(graphs, n_global: int):

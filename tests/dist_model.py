@@ -10,7 +10,8 @@ engine runs over RCCL. Same decomposition as part.hip:
   (ncclAllGather + ncclSend/Recv on the GPU; all_gather here), owners apply them;
 - pull level: the frontier bitmap is all-gathered and every rank pulls its own unvisited slots
   over their dependency lists (global parent ids), stopping at the first parent in the frontier;
-- termination: all_reduce(sum) of the next frontier size.
+- per level one all_reduce(sum) of {frontier size, frontier edges}: termination and the push/pull
+  choice (Beamer's alpha and beta rules, as the engine's run_part_wave).
 
 Visits follow SURVEY.md §8(a) R0 (Computed.cs:162-230): Invalidated -> no-op; Computing -> flag
 InvalidateOnSetOutput; Consistent without delay -> Invalidated + expand; Consistent with delay ->
@@ -77,7 +78,7 @@ class RankModel:
     def _matches(self, slot, tag):
         return self.ver_all[slot] == tag   # replicated versions; the owner checks the state
 
-    def wave(self, roots, immediately=None, direction="push", alpha=14):
+    def wave(self, roots, immediately=None, direction="push", alpha=14, beta=24):
         self.sent[:] = False
         visited = set()
         front = []
@@ -91,14 +92,19 @@ class RankModel:
         e_total = torch.tensor([sum(len(v) for v in self.rows.values())], dtype=torch.int64)
         dist.all_reduce(e_total)
         levels = 0
+        last_pull = False
         while True:
-            n_front = torch.tensor([len(front)], dtype=torch.int64)
-            dist.all_reduce(n_front)                       # termination (ncclAllReduce)
-            if int(n_front) == 0:
+            # one all-reduce per level of {frontier, its edges} (run_part_wave): termination and
+            # Beamer's rules — pull when the edges exceed E / alpha, keep pulling after a pull while
+            # the frontier holds more than N / beta nodes
+            ft = torch.tensor([len(front), sum(len(self.rows.get(u, ())) for u in front)], dtype=torch.int64)
+            dist.all_reduce(ft)
+            n_front, edges = int(ft[0]), int(ft[1])
+            if n_front == 0:
                 break
-            edges = torch.tensor([sum(len(self.rows.get(u, ())) for u in front)], dtype=torch.int64)
-            dist.all_reduce(edges)
-            pull = direction == "pull" or (direction == "auto" and int(edges) > int(e_total) // alpha)
+            pull = direction == "pull" or (direction == "auto" and (edges > int(e_total) // alpha or
+                                                                    (last_pull and n_front > self.n // beta)))
+            last_pull = pull
             nxt = []
             if pull:
                 bm = np.zeros(self.n, bool)

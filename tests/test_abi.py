@@ -62,3 +62,10 @@ def test_bad_config_rejected(pkg):
     cfg = pkg.fgi.Config(0, 0, 16, 0, 0, 0, 1)   # struct_size 0
     h = ctypes.c_void_p()
     assert lib.fgi_create(ctypes.byref(cfg), ctypes.byref(h)) == pkg.fgi.EINVAL
+
+
+def test_rccl_info_reports_the_bound_library(pkg):
+    """fgi_rccl_info names the RCCL the engine's collectives bind to (two RCCLs can be present in
+    one process: torch's and /opt/rocm's; they share a soname, so the first one loaded wins)."""
+    v, path = pkg.fgi.rccl_info()
+    assert v >= 22000 and "rccl" in os.path.basename(path)

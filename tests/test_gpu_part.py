@@ -1,6 +1,8 @@
 """Multi-GPU partition path, exercised on one GPU: P partitions of one R-MAT graph run in one
-process (fgi_part_init_local: same kernels as the RCCL path, exchange by device copies) and must
-produce exactly the single-device wave's invalidated set and final node states."""
+process (fgi_part_init_local). fgi_part_local_invalidate runs the RCCL path's own level loop
+(run_part_wave) on every rank in its own host thread; only the collectives are device copies
+instead of RCCL. Results must be exactly the oracle's invalidated set and final node states,
+including consecutive pull levels (direction 2: the pull->pull frontier-bitmap copy)."""
 import numpy as np
 import pytest
 
@@ -69,3 +71,32 @@ def test_partition_owns_rows_of_its_slots(pkg, gpu_available):
     want = np.stack([s.astype(np.uint64), d, O.gen_tags(s, d, seed)], 1)
     key = lambda a: a[np.lexsort((a[:, 2], a[:, 1], a[:, 0]))]
     assert np.array_equal(key(got), key(want))
+
+
+def test_single_engine_calls_refuse_a_partitioned_graph(pkg, gpu_available):
+    """A partition's rows hold global dependant ids: the single-device wave and mutation entry
+    points must refuse it (FGI_ESTATE) instead of indexing past the partition's arrays."""
+    scale, ef, seed, P = 10, 8, 7, 2
+    n = 1 << scale
+    gs = [pkg.Graph(n // P, rank=r, world=P) for r in range(P)]
+    pkg.fgi.part_init_local(gs, n)
+    for g in gs:
+        g.part_synth_rmat(scale, ef, seed)
+    g = gs[1]
+    calls = [lambda: g.invalidate(np.array([1], np.uint32)), lambda: g.invalidate_all(), lambda: g.prune(),
+             lambda: g.begin_compute(np.array([1], np.uint32), np.array([3], np.uint64)),
+             lambda: g.add_used(np.array([1], np.uint32), np.array([2], np.uint32)),
+             lambda: g.set_output(np.array([1], np.uint32))]
+    for c in calls:
+        with pytest.raises(pkg.FgiError) as e:
+            c()
+        assert e.value.status == pkg.fgi.ESTATE
+    # the partitioned wave still works afterwards
+    s, d = O.gen_rmat(scale, ef, seed)
+    o = O.Oracle(n)
+    o.load_graph(O.version_of(seed, np.arange(n)), None, s, d, O.gen_tags(s, d, seed))
+    roots = O.gen_roots(8, n, 5, np.bincount(s, minlength=n))
+    o.invalidate_slots(roots)
+    pkg.fgi.part_local_invalidate(gs, roots)
+    ids = np.concatenate([x.part_export_ids() for x in gs])
+    assert np.array_equal(np.sort(ids), np.sort(o.inv_log()))

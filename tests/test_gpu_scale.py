@@ -1,0 +1,130 @@
+"""Parity at the benchmarked sizes (BASELINE.json configs[1] / configs[3]).
+
+(a) configs[1]'s generator at R-MAT scale 20 (1M slots, 16M edges, 4,096 roots): the engine's wave
+    against the oracle, bit-exact — invalidated set, V_inv, E_trav and every final node word —
+    on the push, pull and automatic paths, with 0% and 50% stale edges.
+(b) the full configs[1] wave that bench.py times (R-MAT scale 24, 16.8M slots, 263M edges, 4,096
+    roots): the oracle's object graph would take minutes here, so the result is checked through
+    size-independent properties over the engine's exported edge set (fgi_export_edges):
+      closure  — every version-matching `_usedBy` entry of an invalidated node leads to an
+                 invalidated node (Computed.cs:212-216 recurses into it);
+      witness  — every invalidated non-root has an invalidated parent holding a matching entry;
+      and, exactly, the least closure computed by an independent level-synchronous numpy BFS.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import fgo as O
+from harness import CONSISTENT, INVALIDATED
+
+pytestmark = pytest.mark.gpu
+
+THREADS = max(1, min(16, len(os.sched_getaffinity(0))))
+SEED, ROOT_SEED, STALE_SEED = 0x5EED0024, 0x5EED1024, 0x5EED00C0
+PATHS = {"push": 1, "pull": 2, "auto": 0}
+
+
+@pytest.mark.parametrize("stale", [0, 50])
+def test_configs1_generator_scale20_bit_exact(pkg, gpu_available, stale):
+    scale, ef = 20, 16
+    n = 1 << scale
+    O.set_threads(THREADS)
+    s, d = O.gen_rmat(scale, ef, SEED)
+    tags = O.gen_tags(s, d, SEED, stale, STALE_SEED)
+    o = O.Oracle(n)
+    o.load_graph(O.version_of(SEED, np.arange(n)), None, s, d, tags)
+    roots = O.gen_roots(4096, n, ROOT_SEED, np.bincount(s, minlength=n))
+    assert len(roots) == 4096
+    st = o.invalidate_slots(roots, threads=THREADS)
+    want = np.sort(o.inv_log())
+    ov, of = o.dump_states()
+    o.close()
+    del s, d, tags
+
+    g = pkg.Graph(n)
+    g.synth_rmat(scale, ef, SEED, stale, STALE_SEED)
+    g.snapshot()
+    for name, direction in PATHS.items():
+        g.restore()
+        g.set_option(pkg.fgi.OPT_DIRECTION, direction)
+        ws = pkg.WaveStats()
+        ids = g.invalidate(roots, stats=ws)
+        assert len(np.unique(ids)) == len(ids), name
+        assert np.array_equal(np.sort(ids), want), (name, len(ids), len(want))
+        assert (ws.v_inv, ws.e_trav) == (st.v_inv, st.e_trav), (name, ws.v_inv, st.v_inv, ws.e_trav, st.e_trav)
+        if name == "pull":
+            assert ws.pull_levels == ws.levels
+        v, f = g.dump_states()
+        assert np.array_equal(v[:n], ov), name
+        bad = np.nonzero(f[:n] != of)[0]
+        assert len(bad) == 0, (name, bad[:8])
+    g.close()
+
+
+def closure_bfs(n, u, d, t, ver, roots):
+    """Least set containing the roots and closed under version-matching entries, by a level-
+    synchronous BFS over (u -> d) in numpy (all nodes Consistent, no delays: a visit invalidates)."""
+    deg = np.bincount(u, minlength=n).astype(np.int64)
+    indptr = np.zeros(n + 1, np.int64)
+    np.cumsum(deg, out=indptr[1:])
+    live = t == ver[d]
+    seen = np.zeros(n, bool)
+    front = np.unique(roots).astype(np.int64)
+    seen[front] = True
+    while len(front):
+        cnt = deg[front]
+        tot = int(cnt.sum())
+        if tot == 0:
+            break
+        starts = indptr[front]
+        off = np.repeat(starts - (np.cumsum(cnt) - cnt), cnt) + np.arange(tot, dtype=np.int64)
+        off = off[live[off]]
+        nxt = d[off]
+        nxt = np.unique(nxt[~seen[nxt]]).astype(np.int64)
+        seen[nxt] = True
+        front = nxt
+    return seen
+
+
+def test_configs1_full_scale24_wave_properties(pkg, gpu_available):
+    from stl_fusion_amd import workloads as W
+    cfg = W.CONFIGS["rmat24"]
+    n = W.n_slots(cfg)
+    g = pkg.Graph(n)
+    W.build(g, cfg)
+    roots = W.roots_for(g, cfg)
+    assert len(roots) == 4096
+    # the edge set before the wave (an invalidated node's `_usedBy` is cleared, Computed.cs:217)
+    u, d, t = g.export_edges()
+    ws = pkg.WaveStats()
+    ids = g.invalidate(roots, stats=ws)
+    assert len(ids) == ws.v_inv and len(np.unique(ids)) == len(ids)
+    _, f = g.dump_states()
+    g.close()
+    assert len(u) == 263_432_932
+    ver = O.version_of(cfg["seed"], np.arange(n))
+    inv = np.zeros(n, bool)
+    inv[ids] = True
+    # node states: exactly the returned set is Invalidated, everything else still Consistent
+    assert np.array_equal((f[:n] & 3) == INVALIDATED, inv)
+    assert np.all((f[:n] & 3)[~inv] == CONSISTENT)
+    # roots (all Consistent, no delay) are invalidated
+    assert inv[roots].all()
+    # closure: every matching entry of an invalidated node reaches an invalidated node
+    m = inv[u] & (t == ver[d])
+    assert inv[d[m]].all(), "an invalidated node has a matching dependant the wave did not invalidate"
+    # witness: every invalidated non-root has an invalidated parent with a matching entry
+    has_parent = np.zeros(n, bool)
+    has_parent[d[m]] = True
+    is_root = np.zeros(n, bool)
+    is_root[roots] = True
+    assert not np.any(inv & ~is_root & ~has_parent), "an invalidated node has no invalidated parent"
+    # E_trav: sum of |_usedBy| over the invalidated nodes
+    assert ws.e_trav == int(np.bincount(u, minlength=n)[inv].astype(np.int64).sum())
+    del m, has_parent
+    # exactly the least closure (an independent BFS)
+    want = closure_bfs(n, u, d, t, ver, roots)
+    assert np.array_equal(want, inv), (int(want.sum()), int(inv.sum()))
+    assert ws.v_inv == 7_370_581 and ws.e_trav == 261_303_996
