@@ -171,8 +171,8 @@ fgi_status fgi_set_output(fgi_graph* g, uint32_t n, const uint32_t* handle, uint
 /* One batched cascade: for each root handle, `existing.Invalidate(immediately[i])`
  * (Computed.Invalidate() scope -> ComputedExt.TryUseExisting -> Computed.cs:162-230, recursing
  * through every `_usedBy` entry whose version still matches, 212-216). immediately may be NULL
- * (all false — what the scope does). The invalidated set is written to out_ids (slots, in BFS
- * level order); if cap is too small, FGI_ECAPACITY is returned with *out_n = required size (the
+ * (all false — what the scope does). The invalidated set is written to out_ids (handles, in
+ * ascending order); if cap is too small, FGI_ECAPACITY is returned with *out_n = required size (the
  * wave itself has completed). out_ids may be NULL to skip the copy. */
 fgi_status fgi_invalidate(fgi_graph* g, uint32_t n_roots, const uint32_t* roots, const uint8_t* immediately,
                           uint32_t* out_ids, uint64_t cap, uint64_t* out_n, fgi_wave_stats* stats);

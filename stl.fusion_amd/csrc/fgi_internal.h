@@ -74,24 +74,30 @@ __host__ __device__ inline uint64_t synth_version(uint64_t seed, uint32_t slot) 
 
 // ---- wave bookkeeping -------------------------------------------------------------------------
 constexpr int kRing = 64;               // per-level counters live in a ring (deep waves roll over)
-constexpr int kScanBlocks = 1024;       // fixed grid of the two-pass frontier scan
 constexpr int kBlock = 256;             // threads per block for the traversal kernels
-constexpr int kEPT = 8;                 // edges per thread per chunk
-constexpr int kChunk = kBlock * kEPT;   // edges per expand chunk
+constexpr int kEPT = 8;                 // edges per thread per chunk (largest chunk)
+constexpr int kChunk = kBlock * kEPT;   // edges per expand chunk (largest chunk)
+constexpr int kFine = 256;              // edges per fine chunk of the chunk map (cstart granularity);
+                                        // a push level expands chunks of 1..kEPT fine chunks
 constexpr uint32_t kStatBlocks = 4096;  // per-block statistics rows (grid limit of the hot kernels)
 constexpr int kStatCols = 8;
+constexpr int kPullTile = 1024;         // slots per pull tile (one block iteration of a pull level)
+constexpr int kDoneGroups = 16;         // two-level completion counters (last-block epilogues)
+constexpr int kDoneStride = 16;         // 128 B apart
+constexpr uint32_t kFinalBlocks = 1024; // grid of the final collect (invalidated bitmap -> list)
 
-constexpr int kProbeBlocks = 2048;     // FGI_PROBE (measurement only): blocks and phases stamped
-constexpr int kProbePhases = 16;
-constexpr int kPullTile = 1024;        // slots per pull tile (one block iteration of a pull level)
-
+// Per-level counters. The producers of level L's frontier (roots, push emits, received targets)
+// reserve list space with ONE packed 64-bit atomic on `ft` (frontier entries << 32 | edges): the
+// returned value is both the entry index and the exclusive edge offset (escan) of the reserving
+// batch, so the frontier list comes out already scanned. The last block of each producer kernel
+// unpacks ft into F / T (a pull level sums its per-block counts instead).
 struct LevelCtr {
     unsigned long long F;       // frontier entries (expandable = invalidated with |row| > 0)
     unsigned long long T;       // edges of the frontier (sum of row lengths)
-    unsigned long long nchunks; // ceil(T / kChunk)
+    unsigned long long ft;      // packed reservation counter (F << 32 | T)
     unsigned long long pull;    // 1 if this level runs bottom-up (pull)
-    unsigned long long mark_lo; // inv[] range of the previous level's winners (marked into the
-    unsigned long long mark_hi; //   frontier bitmap before a pull; appended here after a pull)
+    unsigned long long w;       // pull level L-1: its winners (the frontier count before rows)
+    unsigned long long mult;    // push: fine chunks per expand chunk
     unsigned long long pad0;
     unsigned long long pad1;
 };
@@ -103,11 +109,10 @@ struct PullTile {
 };
 
 struct WaveCtr {
-    unsigned long long inv;         // invalidated nodes appended so far (V_inv)
+    unsigned long long inv;         // invalidated handles of the wave (V_inv; the final collect)
     unsigned long long e_match;
     unsigned long long n_flagged;
     unsigned long long root_inv;    // winners of the roots kernel
-    unsigned long long marked;      // inv[] entries already marked in the dead bitmap
     unsigned long long pull_cand;   // pull: slots whose dependency list was scanned
     unsigned long long pull_edges;  // pull: dependency entries examined
     unsigned long long pull_live;   // pull: slots not yet dead when scanned
@@ -115,7 +120,7 @@ struct WaveCtr {
     unsigned long long pull_scan;   // pull: slots scanned (bitmap reads), summed over pull levels
     unsigned long long pull_tail;   // pull: candidates whose head dependency missed (list scanned)
     unsigned long long root_flagged;  // flag-only visits of the roots kernel
-    unsigned long long pad[4];
+    unsigned long long pad[5];
     LevelCtr lvl[kRing];
 };
 
@@ -166,14 +171,14 @@ struct fgi_graph {
     uint64_t pool_epoch = 0;           // bumped on compaction (invalidates snapshots)
 
     // wave workspace
-    unsigned long long* probe = nullptr;   // FGI_PROBE: [kProbeBlocks][kProbePhases] timestamps
-    uint32_t* inv = nullptr;           // [n_handles] invalidated handles of the last wave
+    uint32_t* inv = nullptr;           // [n_handles] invalidated handles of the last wave (ascending)
     uint32_t* fr_off[2] = {nullptr, nullptr};  // frontier lists: row offsets (pool positions < 2^32)
     uint32_t* fr_len[2] = {nullptr, nullptr};
-    uint64_t* escan = nullptr;         // [n_handles]
-    uint32_t* cstart = nullptr;        // [cstart_cap]
+    uint64_t* escan[2] = {nullptr, nullptr};   // exclusive edge offset of every frontier entry
+    uint32_t* cstart[2] = {nullptr, nullptr};  // fine chunk -> frontier entry holding its first edge
     uint64_t cstart_cap = 0;
-    unsigned long long* partials = nullptr;  // [kScanBlocks]
+    unsigned long long* bsum = nullptr;  // [8][kStatBlocks] per-block sums / prefixes of the epilogues
+    unsigned long long* done = nullptr;  // completion counters of the last-block epilogues
     fgi::WaveCtr* ctr = nullptr;
     unsigned long long* blk_stats = nullptr;   // [kStatBlocks][kStatCols] per-block wave statistics
     fgi::WaveCtr* ctr_host = nullptr;  // pinned
@@ -196,9 +201,12 @@ struct fgi_graph {
     bool words_dirty = true;           // node words changed since the snapshot
     fgi::PullTile* tiles = nullptr;    // per pull tile counts of the last pull level
     uint64_t tiles_cap = 0;
-    uint32_t* front_bm = nullptr;      // frontier bitmap (pull levels); multi-GPU: the local words
-    uint32_t* front_nx = nullptr;      // second frontier bitmap: pull level L reads fb[L&1] and
-                                       // writes its winners into fb[(L+1)&1]
+    // Invalidated bitmap: bit h set = node h was invalidated by this wave. It is the frontier of a
+    // pull level: every node invalidated before the previous level already had all its dependants
+    // visited, so "an invalidated parent" and "a parent in the previous level's frontier" select
+    // the same unvisited slots. Multi-GPU: all-gathered into front_global.
+    uint32_t* inv_bm = nullptr;
+    uint32_t* lw_bm = nullptr;         // the last pull level's winners (collected if the next level pushes)
     uint64_t bm_words = 0;             // words per bitmap (even: pull levels store 64-bit words)
 
     // dependency-list cache for pull levels: for slot d, the handles whose `_usedBy` row holds
@@ -296,7 +304,7 @@ struct PartView {
     uint32_t* send_buf;         // [world][block] outgoing target ids per owner
     uint32_t* recv_buf;         // [world * block] incoming, concatenated
     unsigned long long* send_cnt;   // [world] device counters
-    uint32_t* front_global;     // [n_global bits] all-gathered frontier bitmap (pull levels)
+    uint32_t* front_global;     // [n_global bits] all-gathered invalidated bitmap (pull levels)
     uint64_t front_words_global;
     unsigned long long* scratch_u64;
 };
@@ -304,24 +312,14 @@ bool part_view(fgi_graph* g, PartView* v);
 // Exchange this level's messages: counts by all-gather, payload by grouped send/recv over RCCL.
 // Returns the number of target ids received (concatenated at recv_buf) and sent.
 fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent);
-// Sum of a device u64 over all ranks (RCCL all-reduce), returned on the host.
+// Sum of count (1..4) device u64 over all ranks, returned on the host.
 fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out,
                               uint32_t count = 1);
-// Partitioned wave over global root ids (wave.hip), and its phases.
+// all-gather every rank's local invalidated-bitmap words into front_global (part.hip)
+fgi_status part_allgather_front(fgi_graph* g);
+// Partitioned wave over global root ids (wave.hip): run_part_wave drives the phases below.
 fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                          fgi_wave_stats* stats);
-fgi_status part_wave_begin(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev);
-const unsigned long long* part_level_frontier_dev(fgi_graph* g, int L);
-const unsigned long long* part_level_edges_dev(fgi_graph* g, int L);
-fgi_status part_level_scan(fgi_graph* g, int L, bool prev_pull, bool write_fr);
-fgi_status part_level_mark(fgi_graph* g, int L, bool pull, bool prev_pull = false);
-fgi_status part_level_work(fgi_graph* g, int L, bool pull);
-fgi_status part_level_apply(fgi_graph* g, int L, uint64_t n_recv, uint64_t n_sent);
-// all-gather every rank's local frontier words into front_global (part.hip)
-fgi_status part_allgather_front(fgi_graph* g);
-fgi_status part_level_fetch(fgi_graph* g);
-fgi_status part_level_account(fgi_graph* g, int L, bool fetched = false);
-fgi_status part_wave_end(fgi_graph* g, fgi_wave_stats* stats);
 // Append (used, dependant slot, tag) entries to rows (set semantics, no state checks).
 fgi_status append_edges(fgi_graph* g, uint64_t m, const uint32_t* used_dev, const uint32_t* dep_dev,
                         const uint64_t* tag_dev, const uint32_t* dep_handle_dev);

@@ -642,12 +642,15 @@ fgi_status gather_live(fgi_graph* g, Tmp& tk, Tmp& tt, uint64_t** keys, uint64_t
 
 }  // namespace
 
+// the chunk maps of the two frontier lists: one entry per kFine edges of a level's frontier
 fgi_status ensure_cstart(fgi_graph* g, uint64_t total_edges) {
-    const uint64_t need = total_edges / kChunk + 4;
+    const uint64_t need = total_edges / kFine + 4;
     if (g->cstart_cap >= need) return FGI_OK;
-    dfree(g->cstart);
+    dfree(g->cstart[0]);
+    dfree(g->cstart[1]);
     const uint64_t cap = std::max<uint64_t>(need, g->cstart_cap * 3 / 2);
-    FGI_TRY(dmalloc(g, &g->cstart, cap));
+    FGI_TRY(dmalloc(g, &g->cstart[0], cap));
+    FGI_TRY(dmalloc(g, &g->cstart[1], cap));
     g->cstart_cap = cap;
     return FGI_OK;
 }
@@ -865,22 +868,24 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
     if (dmalloc(g, &g->node, H) || dmalloc(g, &g->row_off, H) || dmalloc(g, &g->row_len, H) ||
         dmalloc(g, &g->row_cap, H) || dmalloc(g, &g->used_cnt, H) || dmalloc(g, &g->home, g->n_detached + 1) ||
         dmalloc(g, &g->inv, H) || dmalloc(g, &g->fr_off[0], H) || dmalloc(g, &g->fr_off[1], H) ||
-        dmalloc(g, &g->fr_len[0], H) || dmalloc(g, &g->fr_len[1], H) || dmalloc(g, &g->escan, H) ||
-        dmalloc(g, &g->partials, 9 * kScanBlocks) || dmalloc(g, &g->ctr, 1) ||
+        dmalloc(g, &g->fr_len[0], H) || dmalloc(g, &g->fr_len[1], H) || dmalloc(g, &g->escan[0], H) ||
+        dmalloc(g, &g->escan[1], H) || dmalloc(g, &g->bsum, 8ull * kStatBlocks) ||
+        dmalloc(g, &g->done, (size_t)(kDoneGroups + 1) * kDoneStride) || dmalloc(g, &g->ctr, 1) ||
         dmalloc(g, &g->blk_stats, (size_t)kStatBlocks * kStatCols) || dmalloc(g, &g->misc_dev, 16) ||
         dmalloc(g, &g->pool_top_dev, 1) || dmalloc(g, &g->uin_off, H) || dmalloc(g, &g->uin_len, H) ||
         dmalloc(g, &g->uin_head, g->n_slots + 1))
         return fail(FGI_ENOMEM);
     g->bm_words = (H + 63) / 64 * 2 + 2;
     g->tiles_cap = (uint64_t)H / kPullTile + kStatBlocks + 1;
-    if (dmalloc(g, &g->vis_bm, g->bm_words) || dmalloc(g, &g->front_bm, g->bm_words) ||
-        dmalloc(g, &g->front_nx, g->bm_words) || dmalloc(g, &g->cls_bm, g->bm_words) ||
+    if (dmalloc(g, &g->vis_bm, g->bm_words) || dmalloc(g, &g->inv_bm, g->bm_words) ||
+        dmalloc(g, &g->lw_bm, g->bm_words) || dmalloc(g, &g->cls_bm, g->bm_words) ||
         dmalloc(g, &g->uin_more, g->bm_words) || dmalloc(g, &g->tiles, g->tiles_cap))
         return fail(FGI_ENOMEM);
-    hipMemset(g->partials, 0, 9 * kScanBlocks * sizeof(unsigned long long));   // incl. completion counters
+    hipMemset(g->done, 0, (size_t)(kDoneGroups + 1) * kDoneStride * sizeof(unsigned long long));
+    hipMemset(g->bsum, 0, 8ull * kStatBlocks * sizeof(unsigned long long));
     hipMemset(g->vis_bm, 0, g->bm_words * 4);
-    hipMemset(g->front_bm, 0, g->bm_words * 4);
-    hipMemset(g->front_nx, 0, g->bm_words * 4);
+    hipMemset(g->inv_bm, 0, g->bm_words * 4);
+    hipMemset(g->lw_bm, 0, g->bm_words * 4);
     hipMemset(g->uin_more, 0, g->bm_words * 4);
     if (hipHostMalloc(reinterpret_cast<void**>(&g->ctr_host), sizeof(WaveCtr)) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&g->misc_host), 16 * sizeof(unsigned long long)) != hipSuccess)
@@ -916,13 +921,14 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->pool_tag);
     dfree(g->pool_top_dev);
     dfree(g->inv);
-    dfree(g->probe);
     for (int i = 0; i < 2; ++i) {
         dfree(g->fr_off[i]);
         dfree(g->fr_len[i]);
     }
-    dfree(g->escan);
-    dfree(g->cstart);
+    for (int i = 0; i < 2; ++i) {
+        dfree(g->escan[i]);
+        dfree(g->cstart[i]);
+    }
     dfree(g->uin_off);
     dfree(g->uin_len);
     dfree(g->uin_src);
@@ -931,9 +937,10 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->cls_bm);
     dfree(g->uin_more);
     dfree(g->tiles);
-    dfree(g->front_bm);
-    dfree(g->front_nx);
-    dfree(g->partials);
+    dfree(g->inv_bm);
+    dfree(g->lw_bm);
+    dfree(g->bsum);
+    dfree(g->done);
     dfree(g->ctr);
     dfree(g->blk_stats);
     dfree(g->roots_buf);

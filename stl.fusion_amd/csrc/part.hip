@@ -45,7 +45,7 @@ struct PartComm {
     // this level's forwarded targets: send_buf[q] (send_cnt[q] entries) to owner q; the targets
     // received from every other rank are concatenated at recv_buf
     virtual fgi_status exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent) = 0;
-    // every rank's local frontier words front_bm[0, block/32) into front_global
+    // every rank's local invalidated-bitmap words inv_bm[0, block/32) into front_global
     virtual fgi_status allgather_front(fgi_graph* g) = 0;
 };
 
@@ -136,7 +136,7 @@ struct RcclComm final : PartComm {
     }
     fgi_status allgather_front(fgi_graph* g) override {
         PartState* p = ps(g);
-        FGI_NCCL(g, ncclAllGather(g->front_bm, p->v.front_global, p->v.block / 32, ncclUint32, p->comm, g->stream));
+        FGI_NCCL(g, ncclAllGather(g->inv_bm, p->v.front_global, p->v.block / 32, ncclUint32, p->comm, g->stream));
         return FGI_OK;
     }
 };
@@ -237,11 +237,11 @@ struct LocalComm final : PartComm {
     }
     fgi_status allgather_front(fgi_graph* g) override {
         PartState* p = ps(g);
-        FGI_HIP(g, hipStreamSynchronize(g->stream));   // this rank's frontier words are final
+        FGI_HIP(g, hipStreamSynchronize(g->stream));   // this rank's invalidated words are final
         if (!grp->arrive()) return peer_failed(g);
         const uint64_t words = p->v.block / 32;
         for (size_t q = 0; q < grp->gs.size(); ++q)
-            FGI_HIP(g, hipMemcpyAsync(p->v.front_global + q * words, grp->gs[q]->front_bm, words * 4, hipMemcpyDefault,
+            FGI_HIP(g, hipMemcpyAsync(p->v.front_global + q * words, grp->gs[q]->inv_bm, words * 4, hipMemcpyDefault,
                                       g->stream));
         FGI_HIP(g, hipStreamSynchronize(g->stream));
         if (!grp->arrive()) return peer_failed(g);     // the sources stay untouched until all copies are done
