@@ -16,7 +16,8 @@ import os
 import shutil
 
 WAVE_KERNELS = ("k_roots", "k_level_begin", "k_scan_reduce", "k_scan_apply", "k_mark", "k_expand", "k_pull",
-                "k_pull_long", "k_clear_front", "k_level")
+                "k_pull_long", "k_clear_front", "k_level", "k_collect", "k_wave_init",
+                "k_final_count", "k_final_write", "k_final")
 
 
 def base_name(n):

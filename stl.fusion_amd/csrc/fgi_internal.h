@@ -85,6 +85,8 @@ constexpr int kPullTile = 1024;         // slots per pull tile (one block iterat
 constexpr int kDoneGroups = 16;         // two-level completion counters (last-block epilogues)
 constexpr int kDoneStride = 16;         // 128 B apart
 constexpr uint32_t kFinalBlocks = 1024; // grid of the final collect (invalidated bitmap -> list)
+constexpr uint32_t kHot = 65536;        // hot list heads (pull probes through an 8 KB snapshot)
+constexpr uint32_t kHotFlag = 0x80000000u;
 
 // Per-level counters. The producers of level L's frontier (roots, push emits, received targets)
 // reserve list space with ONE packed 64-bit atomic on `ft` (frontier entries << 32 | edges): the
@@ -98,7 +100,7 @@ struct LevelCtr {
     unsigned long long pull;    // 1 if this level runs bottom-up (pull)
     unsigned long long w;       // pull level L-1: its winners (the frontier count before rows)
     unsigned long long mult;    // push: fine chunks per expand chunk
-    unsigned long long pad0;
+    unsigned long long npull;   // pull levels of the wave before this one (which candidate list to read)
     unsigned long long pad1;
 };
 
@@ -113,7 +115,7 @@ struct WaveCtr {
     unsigned long long e_match;
     unsigned long long n_flagged;
     unsigned long long root_inv;    // winners of the roots kernel
-    unsigned long long pull_cand;   // pull: slots whose dependency list was scanned
+    unsigned long long pull_surv;   // pull: candidates still unvisited after their level (written forward)
     unsigned long long pull_edges;  // pull: dependency entries examined
     unsigned long long pull_live;   // pull: slots not yet dead when scanned
     unsigned long long pull_win;    // pull: nodes invalidated by pull levels
@@ -219,6 +221,25 @@ struct fgi_graph {
                                        // dependencies of each entry, the ones a wave reaches earliest
     uint32_t* uin_more = nullptr;      // bitmap: the list has more than two entries
     uint64_t uin_cap = 0;
+    // Pull candidates: the slots with a non-empty dependency list, grouped by the
+    // pull block owning their tile range (segment [cand_seg[b], cand_seg[b + 1]), slot order), as
+    // (slot, list heads, row length | more-than-two-entries bit << 31). A pull level reads the
+    // static list (first pull of a wave) or the survivors of the previous pull level, and writes its
+    // own survivors (still unvisited) into the other survivor buffer at the same segment bases.
+    // One 16-byte entry per candidate: {slot, row length | more << 31, head 0, head 1}.
+    uint4* cand = nullptr;
+    uint32_t* cand_seg = nullptr;      // [pull grid + 1]
+    // Hot heads: the (at most kHot) handles that head the most lists get a rank; candidate entries
+    // name them as kHotFlag | rank, and a pull level probes them in hot_bm, a snapshot of their
+    // invalidated bits taken before the level (8 KB: L1-resident) instead of the whole bitmap.
+    uint32_t* hot_id = nullptr;        // [kHot] rank -> handle (FGI_NONE past n_hot)
+    uint32_t* hot_bm = nullptr;        // [kHot / 32]
+    uint32_t n_hot = 0;
+    uint32_t final_epoch = 0;          // launch epoch of k_final's status words
+    uint4* sv[2] = {nullptr, nullptr};
+    uint32_t* sv_cnt[2] = {nullptr, nullptr};   // [pull grid] survivors per block
+    uint64_t cand_cap = 0;
+    uint32_t cand_grid = 0;            // pull grid the segments were built for (0 = none)
     uint64_t uin_epoch = 0;            // mut_epoch the cache was built at (0 = never)
     uint64_t mut_epoch = 1;            // changes on every mutation of rows or versions
     uint64_t epoch_counter = 1;
@@ -276,8 +297,13 @@ fgi_status build_rows_from_keys(fgi_graph* g, uint64_t m, uint64_t* keys, uint64
                                 uint32_t src_base = 0, uint32_t dst_base = 0);
 // Build the pull dependency-list cache if the graph changed since it was built.
 fgi_status ensure_in_lists(fgi_graph* g);
-// Copy the first two entries of every slot's list into uin_head.
+// Copy the first two entries of every slot's list into uin_head, then (re)build the pull
+// candidate segments (wave.hip).
 fgi_status build_in_heads(fgi_graph* g);
+fgi_status build_candidates(fgi_graph* g);
+// Pull geometry of a graph: blocks of a pull level and the tiles each owns (0 blocks: the graph is
+// too large to pull on one device; its waves push).
+void pull_geometry(const fgi_graph* g, uint32_t* grid, uint32_t* tpb);
 // Record a mutation of rows or versions (invalidates the dependency-list cache).
 inline void touch(fgi_graph* g) { g->mut_epoch = ++g->epoch_counter; }
 // Record a change of node words (class bitmap rebuilt before the next wave; restore copies words).

@@ -586,6 +586,69 @@ __global__ void k_in_ends(uint32_t n, const uint64_t* __restrict__ off, const ui
     if (d < n) end[d] = off[d] + len[d];
 }
 
+// pull candidates: slots with a non-empty dependency list, in slot order
+__global__ void k_cand_flag(uint32_t n, const uint32_t* __restrict__ uin_len, uint32_t* flag) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d < n) flag[d] = uin_len[d] ? 1u : 0u;
+}
+
+// how often each handle heads a candidate's list (first or second entry)
+__global__ void k_head_count(uint32_t n, const uint32_t* __restrict__ flag, const uint64_t* __restrict__ uin_head,
+                             uint32_t* cnt) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= n || !flag[d]) return;
+    const uint64_t h = uin_head[d];
+    const uint32_t h0 = (uint32_t)h, h1 = (uint32_t)(h >> 32);
+    if (h0 != FGI_NONE) atomicAdd(cnt + h0, 1u);
+    if (h1 != FGI_NONE) atomicAdd(cnt + h1, 1u);
+}
+
+__global__ void k_head_keys(uint32_t n, const uint32_t* __restrict__ cnt, uint64_t* keys) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u < n) keys[u] = ((uint64_t)cnt[u] << 32) | u;
+}
+
+// ranks 0..kHot-1 to the most frequent heads (keys sorted by count, descending)
+__global__ void k_hot_pick(uint32_t k_max, const uint64_t* __restrict__ sorted, uint32_t* hot_id, uint32_t* hot_rank) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= kHot) return;
+    const uint64_t key = k < k_max ? sorted[k] : 0ull;
+    if ((key >> 32) == 0) {
+        hot_id[k] = FGI_NONE;
+        return;
+    }
+    hot_id[k] = (uint32_t)key;
+    hot_rank[(uint32_t)key] = k;
+}
+
+__device__ __forceinline__ uint32_t head_code(uint32_t h, const uint32_t* hot_rank) {
+    if (h == FGI_NONE || !hot_rank) return h;
+    const uint32_t r = hot_rank[h];
+    return r != FGI_NONE ? (kHotFlag | r) : h;
+}
+
+__global__ void k_cand_fill(uint32_t n, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos,
+                            const uint64_t* __restrict__ uin_head, const uint32_t* __restrict__ uin_len,
+                            const uint32_t* __restrict__ row_len, const uint32_t* __restrict__ hot_rank, uint4* cand,
+                            unsigned long long* too_long) {
+    const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
+    if (d >= n || !flag[d]) return;
+    const uint32_t p = pos[d], rl = row_len[d];
+    if (rl >> 31) atomicAdd(too_long, 1ull);
+    const uint64_t h = uin_head[d];
+    cand[p] = make_uint4(d, (rl & 0x7FFFFFFFu) | (uin_len[d] > 2 ? 0x80000000u : 0u), head_code((uint32_t)h, hot_rank),
+                         head_code((uint32_t)(h >> 32), hot_rank));
+}
+
+// segment base of pull block b: the candidates before its first slot b * tpb * kPullTile
+__global__ void k_cand_seg(uint32_t G, uint64_t span, uint32_t n, const uint32_t* __restrict__ pos, uint32_t total,
+                           uint32_t* seg) {
+    const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+    if (b > G) return;
+    const uint64_t s0 = (uint64_t)b * span;
+    seg[b] = s0 < n ? pos[s0] : total;
+}
+
 __global__ void k_invalidate_all_roots(uint32_t n_slots, const unsigned long long* node, uint32_t* roots,
                                        unsigned long long* cnt) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
@@ -767,6 +830,85 @@ fgi_status build_in_heads(fgi_graph* g) {
     hipLaunchKernelGGL(k_in_head, dim3(nblk(N)), dim3(256), 0, g->stream, N, g->uin_off, g->uin_len, g->uin_src,
                        g->uin_head, reinterpret_cast<unsigned long long*>(g->uin_more));
     FGI_HIP(g, hipGetLastError());
+    return build_candidates(g);
+}
+
+// The pull candidate segments for the graph's pull geometry (see fgi_internal.h). A graph too large
+// to pull on one device, or with a row of 2^31 entries or more, gets none (its waves push).
+fgi_status build_candidates(fgi_graph* g) {
+    g->cand_grid = 0;
+    uint32_t G = 0, tpb = 0;
+    pull_geometry(g, &G, &tpb);
+    if (G == 0) return FGI_OK;
+    hipStream_t s = g->stream;
+    const uint32_t N = g->n_slots;
+    if (g->cand_cap < N || !g->cand) {
+        dfree(g->cand);
+        for (int k = 0; k < 2; ++k) dfree(g->sv[k]);
+        g->cand_cap = 0;
+        FGI_TRY(dmalloc(g, &g->cand, N));
+        for (int k = 0; k < 2; ++k) FGI_TRY(dmalloc(g, &g->sv[k], N));
+        g->cand_cap = N;
+    }
+    if (!g->cand_seg) {   // sized for the largest pull grid
+        FGI_TRY(dmalloc(g, &g->cand_seg, (size_t)kStatBlocks + 1));
+        FGI_TRY(dmalloc(g, &g->sv_cnt[0], kStatBlocks));
+        FGI_TRY(dmalloc(g, &g->sv_cnt[1], kStatBlocks));
+    }
+    Tmp tf, tp, ts;
+    uint32_t *flag, *pos;
+    FGI_TRY(tmalloc(g, tf, &flag, N));
+    FGI_TRY(tmalloc(g, tp, &pos, N));
+    hipLaunchKernelGGL(k_cand_flag, dim3(nblk(N)), dim3(256), 0, s, N, g->uin_len, flag);
+    size_t tb = 0;
+    FGI_HIP(g, rocprim::exclusive_scan(nullptr, tb, flag, pos, 0u, (size_t)N, rocprim::plus<uint32_t>(), s));
+    char* tmp;
+    FGI_TRY(tmalloc(g, ts, &tmp, tb));
+    FGI_HIP(g, rocprim::exclusive_scan(tmp, tb, flag, pos, 0u, (size_t)N, rocprim::plus<uint32_t>(), s));
+    uint32_t lp = 0, lf = 0;
+    FGI_TRY(d2h(g, &lp, pos + N - 1, 1));
+    FGI_TRY(d2h(g, &lf, flag + N - 1, 1));
+    const uint32_t total = lp + lf;
+    // hot heads (single-device graphs; a partition's heads are global ids)
+    Tmp th;
+    uint32_t* hot_rank = nullptr;
+    g->n_hot = 0;
+    if (!g->part && g->n_handles < kHotFlag) {
+        if (!g->hot_id) {
+            FGI_TRY(dmalloc(g, &g->hot_id, kHot));
+            FGI_TRY(dmalloc(g, &g->hot_bm, kHot / 32));
+        }
+        const uint32_t NH = g->n_handles;
+        Tmp tc, tk0, tk1, tt;
+        uint32_t* cnt;
+        uint64_t *k0, *k1;
+        FGI_TRY(tmalloc(g, tc, &cnt, NH));
+        FGI_TRY(tmalloc(g, th, &hot_rank, NH));
+        FGI_TRY(tmalloc(g, tk0, &k0, NH));
+        FGI_TRY(tmalloc(g, tk1, &k1, NH));
+        FGI_HIP(g, hipMemsetAsync(cnt, 0, (size_t)NH * 4, s));
+        FGI_HIP(g, hipMemsetAsync(hot_rank, 0xFF, (size_t)NH * 4, s));
+        hipLaunchKernelGGL(k_head_count, dim3(nblk(N)), dim3(256), 0, s, N, flag, g->uin_head, cnt);
+        hipLaunchKernelGGL(k_head_keys, dim3(nblk(NH)), dim3(256), 0, s, NH, cnt, k0);
+        size_t sb = 0;
+        FGI_HIP(g, rocprim::radix_sort_keys_desc(nullptr, sb, k0, k1, (size_t)NH, 0, 64, s));
+        char* st;
+        FGI_TRY(tmalloc(g, tt, &st, sb));
+        FGI_HIP(g, rocprim::radix_sort_keys_desc(st, sb, k0, k1, (size_t)NH, 0, 64, s));
+        hipLaunchKernelGGL(k_hot_pick, dim3(kHot / 256), dim3(256), 0, s, NH, k1, g->hot_id, hot_rank);
+        FGI_HIP(g, hipGetLastError());
+        FGI_HIP(g, hipStreamSynchronize(s));
+        g->n_hot = kHot;
+    }
+    FGI_HIP(g, hipMemsetAsync(g->misc_dev + 15, 0, sizeof(unsigned long long), s));
+    hipLaunchKernelGGL(k_cand_fill, dim3(nblk(N)), dim3(256), 0, s, N, flag, pos, g->uin_head, g->uin_len, g->row_len,
+                       hot_rank, g->cand, g->misc_dev + 15);
+    hipLaunchKernelGGL(k_cand_seg, dim3(nblk(G + 1)), dim3(256), 0, s, G, (uint64_t)tpb * kPullTile, N, pos, total,
+                       g->cand_seg);
+    FGI_HIP(g, hipGetLastError());
+    unsigned long long too_long = 0;
+    FGI_TRY(d2h(g, &too_long, g->misc_dev + 15, 1));
+    if (too_long == 0) g->cand_grid = G;
     return FGI_OK;
 }
 
@@ -933,6 +1075,14 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->uin_len);
     dfree(g->uin_src);
     dfree(g->uin_head);
+    dfree(g->cand);
+    dfree(g->cand_seg);
+    dfree(g->hot_id);
+    dfree(g->hot_bm);
+    for (int k = 0; k < 2; ++k) {
+        dfree(g->sv[k]);
+        dfree(g->sv_cnt[k]);
+    }
     dfree(g->vis_bm);
     dfree(g->cls_bm);
     dfree(g->uin_more);

@@ -628,6 +628,8 @@ fgi_status fgi_part_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_facto
         hipFree(keys);
         keys = nullptr;
         st = build_rows_from_keys(g, mo, own, nullptr, seed, stale_pct, stale_seed, p->v.base, p->v.base);
+        // the pull candidates carry row lengths: (re)built once the rows exist
+        if (st == FGI_OK && p->v.block % 32 == 0) st = build_candidates(g);
         g->uin_epoch = (p->v.block % 32 == 0) ? g->mut_epoch : 0;   // rows and lists of one edge set
     } while (0);
     cleanup();

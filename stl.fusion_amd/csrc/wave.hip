@@ -24,7 +24,7 @@
 //                                    probes its dependency list (the reference's `_used`) for an
 //                                    invalidated parent (Beamer's bottom-up step); its last block
 //                                    publishes level L+1's frontier size
-//   k_final_count, k_final_write   — the invalidated bitmap -> the invalidated list (ascending)
+//   k_final                        — the invalidated bitmap -> the invalidated list (ascending)
 // The push/pull choice of a level is a pure function of device counters that every block of the
 // level's kernels evaluates the same way; the host synchronises once per group of levels.
 #include <hip/hip_runtime.h>
@@ -37,10 +37,38 @@
 
 #include "fgi_internal.h"
 
+#ifndef FGI_PULL_PREFETCH
+#define FGI_PULL_PREFETCH 1
+#endif
+// measurement-only builds (make variant-exp EXP=<mask>): parts of a pull level skipped to attribute
+// its time (results are wrong): 1 tail scans, 2 survivor writes, 4 head probes, 8 visit/class gathers
+#ifndef FGI_EXP
+#define FGI_EXP 0
+#endif
+// measurement-only build (make variant-probe): k_level stamps per-block phase times (100 MHz wall
+// clock) into d_probe; run_wave prints per-level medians with FGI_TRACE=1
+#ifndef FGI_PROBE
+#define FGI_PROBE 0
+#endif
+
 namespace fgi {
 namespace {
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+
+constexpr int kProbeLevels = 8, kProbePts = 8, kProbeBlocks = 2048;
+#if FGI_PROBE
+__device__ unsigned long long d_probe[kProbeLevels][kProbeBlocks][kProbePts];
+#define PROBE(L, k)                                                                    \
+    do {                                                                               \
+        if (threadIdx.x == 0 && (L) < kProbeLevels && blockIdx.x < (uint32_t)kProbeBlocks) \
+            d_probe[(L)][blockIdx.x][(k)] = wall_clock64();                            \
+    } while (0)
+#else
+#define PROBE(L, k) \
+    do {            \
+    } while (0)
+#endif
 
 __device__ __forceinline__ bool bit_of(const uint32_t* __restrict__ bm, uint32_t h) {
     return (bm[h >> 5] >> (h & 31)) & 1u;
@@ -111,12 +139,6 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-__device__ __forceinline__ unsigned long long wave_sum64(unsigned long long v) {
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v;
-}
-
 __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 
 __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, unsigned long long* s_red) {
@@ -134,7 +156,7 @@ __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, un
 // Per-block statistics: hot kernels keep their counters per block (plain read-modify-write of the
 // block's own column entry by one thread, launches of a wave are stream-ordered) instead of per-wave
 // atomics on a few words: a single device-scope word saturates near 88 atomics/us. Column-major
-// ([column][block]) so k_stats_reduce sweeps each column coalesced.
+// ([column][block]) so k_final sweeps each column coalesced.
 enum : int { kStEMatch, kStFlagged, kStPullCand, kStPullEdges, kStPullLive, kStPullWin, kStPullTail, kStPullScan, kStats };
 static_assert(kStats == kStatCols, "statistics columns");
 
@@ -168,16 +190,16 @@ __device__ __forceinline__ unsigned long long coh_read(unsigned long long* p) {
     return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Block-uniform: true in the block that arrives last at this launch's completion counter. The
-// counter is two-level (one word serialises near 88 atomics/us, MI355X_MICROARCH.md "dequeue"):
-// block b counts into group b % kDoneGroups, the last block of a group into the top word; the last
-// block resets every word for the next launch.
-__device__ bool last_block(unsigned long long* done) {
+// Block-uniform: true in the block that arrives last at this launch's completion counter, over the
+// blocks [0, G) taking part (G = the grid unless the level leaves blocks idle). The counter is
+// two-level (one word serialises near 88 atomics/us, MI355X_MICROARCH.md "dequeue"): block b counts
+// into group b % kDoneGroups, the last block of a group into the top word; the last block resets
+// every word for the next launch.
+__device__ bool last_block(unsigned long long* done, uint64_t G) {
     __shared__ bool s_last;
     __syncthreads();
     if (threadIdx.x == 0) {
         __builtin_amdgcn_s_waitcnt(0);
-        const uint64_t G = gridDim.x;
         const uint32_t grp = blockIdx.x % kDoneGroups;
         const uint64_t gsize = (G - grp + kDoneGroups - 1) / kDoneGroups;
         const unsigned long long t = __hip_atomic_fetch_add(done + (1 + grp) * kDoneStride, 1ull, __ATOMIC_RELAXED,
@@ -195,30 +217,44 @@ __device__ bool last_block(unsigned long long* done) {
     return last;
 }
 
-// Called by the last block: exclusive prefixes over blocks of `ncols` columns src[q * G + k] into
-// dst[q * G + k], column totals into tot[q]. Chunks of blockDim.x blocks, one block scan each.
+// Called by the last block: exclusive prefixes over blocks of `ncols` (<= 3) columns
+// src[q * G + k] into dst[q * G + k], column totals into tot[q]. Every value is read in ONE round
+// (thread t holds blocks [t * kPer, t * kPer + kPer) of every column: the reads are agent-scope
+// atomics, performed at the coherence point, each a round trip), then one block scan per column.
+constexpr uint32_t kEpiloguePer = 8;    // G <= kBlock * kEpiloguePer (kLevelGridMax)
 __device__ void prefix_columns(unsigned long long* src, unsigned long long* dst, int ncols, uint64_t G,
                                unsigned long long* tot, unsigned long long* s_red) {
     const uint32_t lane = lane_id(), wid = threadIdx.x >> 6, W = blockDim.x >> 6;
-    for (int q = 0; q < ncols; ++q) {
-        unsigned long long run = 0;
-        for (uint64_t base = 0; base < G; base += blockDim.x) {
-            const uint64_t k = base + threadIdx.x;
-            const unsigned long long v = k < G ? coh_read(src + q * G + k) : 0ull;
-            unsigned long long t;
-            const unsigned long long x = wave_excl_scan64(v, t);
-            __syncthreads();
-            if (lane == 63) s_red[wid] = x + v;
-            __syncthreads();
-            unsigned long long woff = 0, all = 0;
-            for (uint32_t j = 0; j < W; ++j) {
-                if (j < wid) woff += s_red[j];
-                all += s_red[j];
-            }
-            if (k < G) dst[q * G + k] = run + woff + x;
-            run += all;
+    const uint64_t k0 = (uint64_t)threadIdx.x * kEpiloguePer;
+    unsigned long long xs[3][kEpiloguePer];
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+#pragma unroll
+        for (uint32_t j = 0; j < kEpiloguePer; ++j)
+            xs[q][j] = (q < ncols && k0 + j < G) ? coh_read(src + q * G + k0 + j) : 0ull;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        if (q >= ncols) break;
+        unsigned long long loc = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < kEpiloguePer; ++j) loc += xs[q][j];
+        unsigned long long t;
+        const unsigned long long x = wave_excl_scan64(loc, t);
+        __syncthreads();
+        if (lane == 0) s_red[wid] = t;
+        __syncthreads();
+        unsigned long long run = x, all = 0;
+        for (uint32_t j = 0; j < W; ++j) {
+            if (j < wid) run += s_red[j];
+            all += s_red[j];
         }
-        if (threadIdx.x == 0) tot[q] = run;
+#pragma unroll
+        for (uint32_t j = 0; j < kEpiloguePer; ++j)
+            if (k0 + j < G) {
+                dst[q * G + k0 + j] = run;
+                run += xs[q][j];
+            }
+        if (threadIdx.x == 0) tot[q] = all;
     }
 }
 
@@ -366,8 +402,8 @@ __device__ __forceinline__ void emit_flush(Emit& e, uint32_t* buf, uint32_t at, 
 
 // Last block of a producer kernel (roots, push level, received targets): level L+1's F and T from
 // the packed counter.
-__device__ __forceinline__ void publish_ft(LevelCtr* ln, unsigned long long* done) {
-    if (last_block(done) && threadIdx.x == 0) {
+__device__ __forceinline__ void publish_ft(LevelCtr* ln, unsigned long long* done, uint64_t G) {
+    if (last_block(done, G) && threadIdx.x == 0) {
         const unsigned long long ft = coh_read(&ln->ft);
         ln->F = ft >> 32;
         ln->T = ft & 0xFFFFFFFFull;
@@ -479,7 +515,7 @@ __global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ r
     const uint32_t fs = wave_sum(flagged), ws = wave_sum(win);
     if (lane_id() == 0 && fs) atomicAdd(&ctr->root_flagged, (unsigned long long)fs);
     if (lane_id() == 0 && ws) atomicAdd(&ctr->root_inv, (unsigned long long)ws);
-    publish_ft(o.ln, done);
+    publish_ft(o.ln, done, gridDim.x);
 }
 
 // ---- the level's direction ------------------------------------------------------------------------
@@ -526,6 +562,11 @@ struct CollectArgs {
     uint32_t* fr_len;
     uint64_t* escan;
     uint32_t* cstart;
+    // hot heads: before a pull level, hot_bm = the invalidated bits of hot_id[0 .. n_hot)
+    const uint32_t* __restrict__ hot_id;
+    uint32_t* hot_bm;
+    uint32_t n_hot;
+    const uint32_t* inv;
 };
 
 constexpr int kCollectThreads = 256;
@@ -614,11 +655,22 @@ __global__ __launch_bounds__(kCollectThreads) void k_collect(int L, WaveCtr* ctr
     __shared__ unsigned long long s_ol[64], s_tot[2];
     __shared__ uint32_t s_nz[64];
     __shared__ uint32_t s_stage[kMaxWaves][kPullTile];
+    if (ctr->lvl[L % kRing].F == 0) return;
+    if (level_pulls(ctr, L, wp)) {   // the hot heads' snapshot for this pull level
+        // one entry per lane, 64 bits per wave (n_hot and the grid stride are multiples of 64)
+        unsigned long long* hot64 = reinterpret_cast<unsigned long long*>(c.hot_bm);
+        for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < c.n_hot; k += gridDim.x * blockDim.x) {
+            const uint32_t u = c.hot_id[k];
+            const unsigned long long m = __ballot(u != FGI_NONE && bit_of(c.inv, u));
+            if (lane_id() == 0) hot64[k >> 6] = m;
+        }
+        return;
+    }
     if (L == 0 || !ctr->lvl[(L + kRing - 1) % kRing].pull) return;
-    if (ctr->lvl[L % kRing].F == 0 || level_pulls(ctr, L, wp)) return;
-    const uint64_t b = blockIdx.x, G = gridDim.x;
-    const uint64_t lo = b * wp.tpb, hi = std::min<uint64_t>(wp.n_tiles, lo + wp.tpb);
+    const uint64_t G = wp.grid;   // the pull grid; this grid is smaller (a no-op launch stays cheap)
     const uint32_t W = blockDim.x >> 6, wid = threadIdx.x >> 6, lane = lane_id();
+    for (uint64_t b = blockIdx.x; b < G; b += gridDim.x) {
+    const uint64_t lo = b * wp.tpb, hi = std::min<uint64_t>(wp.n_tiles, lo + wp.tpb);
     uint64_t re = c.pre[G + b], rl = c.pre[2 * G + b];
     for (uint64_t cb = lo; cb < hi; cb += 64) {   // block-uniform
         const uint32_t nt = (uint32_t)std::min<uint64_t>(64, hi - cb);
@@ -643,6 +695,7 @@ __global__ __launch_bounds__(kCollectThreads) void k_collect(int L, WaveCtr* ctr
         re += s_tot[0];
         rl += s_tot[1];
         __syncthreads();   // the next chunk overwrites the offsets
+    }
     }
 }
 
@@ -782,256 +835,339 @@ __device__ __forceinline__ void expand_level(uint64_t F, uint64_t T, uint32_t mu
     block_stats_add(blk, s_st, v);
 }
 
-// ---- pull: every live slot looks for an invalidated parent -------------------------------------
+// ---- pull: every live candidate looks for an invalidated parent --------------------------------
 // uin_* is the dependency-list cache: for slot d, the handles u whose `_usedBy` row holds
 // (d, version(d)) — the reference's d._used (Computed.cs:36, 365-366). An invalidated parent means
 // the push step would visit d from it (in this level or already in the previous one).
+// Only slots with a non-empty list can ever be reached bottom-up (R-MAT 24: about half of them), and
+// each pull level leaves fewer unvisited: a level reads the candidate list of its block (the static
+// list on the wave's first pull, the previous pull's survivors after that) and writes its own
+// survivors forward.
 struct PullArgs {
     uint32_t n_slots;
     const uint64_t* __restrict__ uin_off;
     const uint32_t* __restrict__ uin_len;
     const uint32_t* __restrict__ uin_src;
-    const uint64_t* __restrict__ uin_head;   // first two list entries (lo | hi << 32)
-    const uint32_t* __restrict__ uin_more;   // bitmap: the list has more than two entries
     const uint32_t* front_rd;                // invalidated bitmap (multi-GPU: all-gathered, global ids)
     uint32_t* inv_bm;                        // this device's invalidated bitmap (owned words |= winners)
-    uint32_t* lw_bm;                         // this level's winners, stored whole per tile
+    uint32_t* lw_bm;                         // this level's winners, stored whole per owned word
     const uint32_t* __restrict__ cls;        // expandable-class bitmap
-    const uint32_t* __restrict__ row_len;
+    const uint32_t* hot_bm;                  // the hot heads' invalidated bits (kHotFlag | rank)
     PullTile* tiles;
     unsigned long long* bsum;                // [3][grid] per-block sums, then [3][grid] prefixes
+    const uint32_t* __restrict__ cand_seg;   // [grid + 1] segment bases
+    const uint4* c[3];                       // [0] the static candidates, [1 + k] survivors buffer k
+    uint4* sv[2];
+    uint32_t* sv_cnt[2];                     // [grid] survivors per block
 };
 
-// A block owns the consecutive tiles [b * tpb, (b + 1) * tpb): kPullTile slots each, kPS per lane
-// (64 apart), so a lane issues kPS independent loads of each kind. Per slot: the visit, class and
-// "more" bitmap words (one 64-bit word per 64 slots), the two list heads, all unconditional and
-// coalesced; then the invalidated bits of the heads (L2); a hit is a visit. The wave's visits and
-// wins go to LDS as 64-bit ballot words; slots whose heads missed but whose list goes on are
-// queued in LDS and scanned at the flush by 8-lane groups (8 entries per probe step, early exit).
-// The flush (every kMaxIter tiles and at the end) writes the owned visit / invalidated / winners
-// words and the per-tile counts (row lengths gathered for winners only) — no global atomics.
-constexpr uint32_t kPS = kPullTile / kBlock;
-constexpr uint32_t kMaxIter = 16;           // tiles buffered in LDS between flushes
-constexpr uint32_t kTailCap = kChunk;       // queued slots
+// A block owns the tiles [b * tpb, (b + 1) * tpb) (tpb <= kMaxIter): their visit, class and winners
+// words live in LDS for the whole level (loaded once, coalesced) and the visit / winners words are
+// written back once (owned words, plain stores), so a pull level does no global atomics and a
+// candidate's only global gathers are the invalidated bits of its two list heads (L2). Candidates
+// are read 4 per lane per batch (one 16-byte entry each, streamed); a hit is a visit. Candidates
+// whose heads missed but whose list goes on are queued in LDS and scanned at the flush by 8-lane
+// groups (8 entries per probe step, early exit). Candidates neither hit nor queued, and queued ones
+// whose scan found nothing, are this level's survivors.
+constexpr uint32_t kMaxIter = 16;           // tiles per pull block (kMaxIter * kPullTile slots)
+constexpr uint32_t kTailCap = kChunk;       // queued candidates
 constexpr uint32_t kTileWords = kPullTile / 64;
-static_assert(kPS == 4 && kTileWords == 16, "pull geometry");
+constexpr uint32_t kOwnWords = 2 * kMaxIter * kTileWords;   // owned 32-bit bitmap words
+constexpr uint32_t kCandBatch = 4 * kBlock; // candidates per block step (4 per lane)
+constexpr uint32_t kWaveBatch = 4 * 64;     // a wave's run per step
+constexpr uint32_t kWaveTailCap = kTailCap / (kBlock / 64);   // queued candidates per wave
 
+// visits / winners / classes of the owned tiles in LDS: 32-bit words (two lanes of a wave that
+// share a word serialise their atomics; narrower words halve how many do)
 struct PullLds {
-    unsigned long long vm[kMaxIter * kTileWords];   // visits, per 64-slot word of the buffered tiles
-    unsigned long long wm[kMaxIter * kTileWords];   // winners
+    uint32_t vm[kOwnWords];                         // visits: the level's start, | this level's
+    uint32_t wm[kOwnWords];                         // winners
+    uint32_t cs[kOwnWords];                         // expandable class (read only)
     unsigned long long cl[kMaxIter];                // per tile: row lengths of the winners
     uint32_t cw[kMaxIter], ce[kMaxIter];            // per tile: winners, expandable winners
-    uint32_t qn;                                    // queued slots
+    uint32_t sn;                                    // survivors written
 };
 
-__device__ __forceinline__ void pull_flush(const PullArgs& p, const unsigned long long* node, uint32_t* vis,
-                                           uint64_t t0, uint32_t nbuf, const uint32_t* q, uint32_t nq, PullLds& s,
-                                           uint32_t& flagged, uint32_t& examined, uint32_t& tails,
-                                           unsigned long long (&bs)[3]) {
-    const uint32_t lane = lane_id(), sub = lane & 7, grp = threadIdx.x >> 3;
-    __syncthreads();
-    // queued slots: 8 lanes per slot, entries 2.. of its list; the next slot's list length and
-    // offset are loaded while the current list is scanned
-    const uint32_t G8 = blockDim.x / 8;
-    uint32_t d_n = 0, len_n = 0;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// the bitmap word holding a list head's invalidated bit: a hot head's in the snapshot (the bit
+// index is the rank, whose low 5 bits the code keeps), any other in the invalidated bitmap
+__device__ __forceinline__ const uint32_t* head_word(const PullArgs& p, uint32_t h) {
+    return (h & kHotFlag) ? p.hot_bm + ((h & ~kHotFlag) >> 5) : p.front_rd + (h >> 5);
+}
+
+// an entry past the list reads as a dead candidate at the block's first slot
+__device__ __forceinline__ uint4 load_cand(const uint4* p, bool in, uint32_t s_lo) {
+    if (!in) return make_uint4(s_lo, 0u, FGI_NONE, FGI_NONE);
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+__device__ __forceinline__ void pull_hit(PullLds& s, uint64_t s_lo, uint32_t d, bool win, uint32_t aux) {
+    const uint32_t rel = (uint32_t)(d - s_lo), k = rel / kPullTile;
+    const uint32_t bit = 1u << (d & 31);
+    atomicOr(&s.vm[rel >> 5], bit);
+    if (win) {
+        atomicOr(&s.wm[rel >> 5], bit);
+        const uint32_t rl = aux & 0x7FFFFFFFu;
+        atomicAdd(&s.cw[k], 1u);
+        if (rl) {
+            atomicAdd(&s.ce[k], 1u);
+            atomicAdd(&s.cl[k], (unsigned long long)rl);
+        }
+    }
+}
+
+// A thread's winners in increasing slot order (its candidates are): it accumulates the tile counts
+// in registers and adds them to the tile's LDS counters when the tile changes — a wave's lanes share
+// one tile almost always, and 64 lanes adding to one LDS word serialise.
+struct TileAcc {
+    uint32_t tile = 0xFFFFFFFFu, w = 0, e = 0;
+    unsigned long long l = 0;
+    __device__ __forceinline__ void flush(PullLds& s) {
+        if (w) {
+            atomicAdd(&s.cw[tile], w);
+            if (e) atomicAdd(&s.ce[tile], e);
+            if (l) atomicAdd(&s.cl[tile], l);
+        }
+        w = e = 0;
+        l = 0;
+    }
+    __device__ __forceinline__ void add(PullLds& s, uint32_t k, uint32_t rl) {
+        if (k != tile) {
+            flush(s);
+            tile = k;
+        }
+        ++w;
+        e += rl ? 1u : 0u;
+        l += rl;
+    }
+};
+
+// A wave's queued candidates: 8 lanes per candidate, entries 2.. of its list; the next candidate's
+// list length and offset are loaded while the current list is scanned.
+__device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, int dst, const unsigned long long* node,
+                                           uint64_t s_lo, uint64_t seg, const uint32_t* q, uint32_t nq, PullLds& s,
+                                           uint32_t& flagged, uint32_t& examined, uint32_t& tails) {
+    const uint32_t lane = lane_id(), sub = lane & 7, grp = lane >> 3;
+    constexpr uint32_t G8 = 8;
+    uint4 c_n = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t len_n = 0;
     uint64_t off_n = 0;
     if (grp < nq) {
-        d_n = q[grp];
-        len_n = p.uin_len[d_n];
-        off_n = p.uin_off[d_n];
+        c_n = src[seg + q[grp]];
+        len_n = p.uin_len[c_n.x];
+        off_n = p.uin_off[c_n.x];
     }
-    const uint64_t s_base = t0 * kPullTile;
     for (uint32_t e = grp; e < nq; e += G8) {
-        const uint32_t d = d_n, len = len_n;
+        const uint4 c = c_n;
+        const uint32_t len = len_n;
         const uint64_t off = off_n;
         if (e + G8 < nq) {
-            d_n = q[e + G8];
-            len_n = p.uin_len[d_n];
-            off_n = p.uin_off[d_n];
+            c_n = src[seg + q[e + G8]];
+            len_n = p.uin_len[c_n.x];
+            off_n = p.uin_off[c_n.x];
         }
         bool found = false;
         for (uint32_t r = 2; r < len && !found; r += 8) {   // group-uniform
-            const uint32_t i = r + sub;
-            const bool x = i < len && bit_of(p.front_rd, p.uin_src[off + i]);
-            examined += (i < len) ? 1u : 0u;
+            const uint32_t k = r + sub;
+            const bool x = k < len && bit_of(p.front_rd, p.uin_src[off + k]);
+            examined += (k < len) ? 1u : 0u;
             found = ((__ballot(x) >> (lane & ~7u)) & 0xFFull) != 0;
         }
-        if (found && sub == 0) {
-            const uint32_t rel = (uint32_t)(d - s_base), k = rel / kPullTile;
-            const unsigned long long bit = 1ull << (d & 63);
-            atomicOr(&s.vm[rel >> 6], bit);
-            if (bit_of(p.cls, d)) {
-                atomicOr(&s.wm[rel >> 6], bit);
-                const uint32_t rl = p.row_len[d];
-                atomicAdd(&s.cw[k], 1u);
-                if (rl) {
-                    atomicAdd(&s.ce[k], 1u);
-                    atomicAdd(&s.cl[k], (unsigned long long)rl);
-                }
+        if (sub == 0) {
+            const uint32_t d = c.x;
+            if (found) {
+                const uint32_t rel = (uint32_t)(d - s_lo);
+                const bool win = (s.cs[rel >> 5] >> (d & 31)) & 1u;
+                pull_hit(s, s_lo, d, win, c.y);
+                if (!win) flagged += first_visit(node[d]) == 2 ? 1u : 0u;
             } else {
-                flagged += first_visit(node[d]) == 2 ? 1u : 0u;
+                p.sv[dst][seg + atomicAdd(&s.sn, 1u)] = c;
             }
-        }
-        tails += sub == 0 ? 1u : 0u;
-    }
-    __syncthreads();
-    // the owned words (the block owns them during the level: plain read-modify-write)
-    unsigned long long* vis64 = reinterpret_cast<unsigned long long*>(vis);
-    unsigned long long* inv64 = reinterpret_cast<unsigned long long*>(p.inv_bm);
-    unsigned long long* lw64 = reinterpret_cast<unsigned long long*>(p.lw_bm);
-    for (uint32_t i = threadIdx.x; i < nbuf * kTileWords; i += blockDim.x) {
-        const uint64_t sl = t0 * kPullTile + (uint64_t)i * 64;
-        if (sl < p.n_slots) {
-            const unsigned long long vm = s.vm[i], wm = s.wm[i];
-            if (vm) vis64[sl >> 6] |= vm;
-            if (wm) inv64[sl >> 6] |= wm;
-            lw64[sl >> 6] = wm;
+            ++tails;
         }
     }
-    for (uint32_t k = threadIdx.x; k < nbuf; k += blockDim.x) {
-        p.tiles[t0 + k] = PullTile{s.cw[k], s.ce[k], s.cl[k]};
-        bs[0] += s.cw[k];
-        bs[1] += s.ce[k];
-        bs[2] += s.cl[k];
-        s.cw[k] = 0;
-        s.ce[k] = 0;
-        s.cl[k] = 0;
-    }
-    __syncthreads();
 }
 
-// One tile's per-slot words of a wave (kPS slots per lane, 64 apart): visit, class and "more"
-// bitmap words (the 32-bit word holding the lane's bit), the two list heads and the row length.
-struct PullSlots {
-    uint32_t vw[kPS], cw[kPS], mw[kPS], rl[kPS];
-    uint64_t hd[kPS];
-};
-
-__device__ __forceinline__ void pull_load(const PullArgs& p, const uint32_t* vis, uint64_t d0, uint32_t lane, bool valid,
-                                          PullSlots& x) {
+__device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveParams& wp, uint64_t npull,
+                                           const unsigned long long* node, uint32_t* vis, uint32_t* lds_q, PullLds& s,
+                                           unsigned long long* blk, unsigned long long (*s_st)[kStats],
+                                           unsigned long long (&bs)[3]) {
+    uint32_t flagged = 0, examined = 0, live = 0, tails = 0, examined_tail = 0;
+    const uint32_t lane = lane_id();
+    const uint32_t b = blockIdx.x;
+    const uint64_t s_lo = (uint64_t)b * wp.tpb * kPullTile;
+    const uint64_t seg = p.cand_seg[b];
+    const int sid = npull == 0 ? 0 : 1 + (int)((npull - 1) & 1);
+    const int dst = (int)(npull & 1);
+    const uint4* src = p.c[sid];
+    const uint32_t cnt = npull == 0 ? p.cand_seg[b + 1] - p.cand_seg[b] : p.sv_cnt[sid - 1][b];
+    // the first batch's entries are requested before the owned words are staged
+    // (FGI_PULL_PREFETCH=0 builds the variant without the look-ahead, for measurement)
+    uint4 c[4];
 #pragma unroll
-    for (int j = 0; j < (int)kPS; ++j) {
-        const uint64_t d = d0 + j * 64 + lane;
-        const bool in = valid && d < p.n_slots;
-        x.vw[j] = in ? vis[d >> 5] : ~0u;
-        x.cw[j] = in ? p.cls[d >> 5] : 0u;
-        x.mw[j] = in ? p.uin_more[d >> 5] : 0u;
-        x.hd[j] = in ? __builtin_nontemporal_load(p.uin_head + d) : ~0ull;
-        x.rl[j] = in ? p.row_len[d] : 0u;
+    for (int j = 0; j < 4; ++j) {
+        const uint32_t i = (threadIdx.x >> 6) * kWaveBatch + j * 64 + lane;
+        c[j] = load_cand(src + seg + i, i < cnt, (uint32_t)s_lo);
     }
-}
-
-__device__ __forceinline__ void pull_level(const PullArgs& p, const WaveParams& wp, const unsigned long long* node,
-                                           uint32_t* vis, uint32_t* lds_q, PullLds& s, unsigned long long* blk,
-                                           unsigned long long (*s_st)[kStats], unsigned long long (&bs)[3]) {
-    uint32_t flagged = 0, cand = 0, examined = 0, live = 0, tails = 0, examined_tail = 0;
-    const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
-    const uint64_t t_lo = (uint64_t)blockIdx.x * wp.tpb;
-    const uint64_t t_hi = std::min<uint64_t>(wp.n_tiles, t_lo + wp.tpb);
+    {
+        const uint64_t w_lo = s_lo >> 5, w_end = ((uint64_t)p.n_slots + 31) >> 5;
+        for (uint32_t i = threadIdx.x; i < 2 * wp.tpb * kTileWords; i += blockDim.x) {
+            const bool in = w_lo + i < w_end;
+            s.vm[i] = in ? vis[w_lo + i] : ~0u;
+            s.cs[i] = in ? p.cls[w_lo + i] : 0u;
+            s.wm[i] = 0;
+        }
+    }
     if (threadIdx.x < kMaxIter) {
         s.cw[threadIdx.x] = 0;
         s.ce[threadIdx.x] = 0;
         s.cl[threadIdx.x] = 0;
     }
-    if (threadIdx.x == 0) s.qn = 0;
+    if (threadIdx.x == 0) s.sn = 0;
     __syncthreads();
-    uint64_t t_base = t_lo;
-    // the slot words of tile t + 1 are loaded while tile t waits for its parents' bits
-    PullSlots cur;
-    pull_load(p, vis, t_lo * kPullTile + wid * (64 * kPS), lane, t_lo < t_hi, cur);
-    for (uint64_t t = t_lo; t < t_hi; ++t) {
-        const uint32_t k = (uint32_t)(t - t_base);
-        const uint64_t d0 = t * kPullTile + wid * (64 * kPS);
-        bool c[kPS];
-        uint32_t f0[kPS], f1[kPS];
+    PROBE(L, 1);
+    TileAcc acc;
+    // every wave streams its own 256-candidate runs (4 entries per lane) and scans its own tail
+    // queue: no block barrier until the write-back
+    const uint32_t wid = threadIdx.x >> 6;
+    uint32_t* wq = lds_q + wid * kWaveTailCap;
+    uint32_t qn = 0;
+    for (uint32_t base = wid * kWaveBatch; base < cnt; base += kCandBatch) {   // wave-uniform
+        bool lv[4];
+        uint32_t f0[4], f1[4];
 #pragma unroll
-        for (int j = 0; j < (int)kPS; ++j) {
-            const uint64_t d = d0 + j * 64 + lane;
-            const bool lv = d < p.n_slots && !((cur.vw[j] >> (lane & 31)) & 1u);
-            const uint32_t h0 = (uint32_t)cur.hd[j], h1 = (uint32_t)(cur.hd[j] >> 32);
-            c[j] = lv && h0 != FGI_NONE;
-            f0[j] = c[j] ? p.front_rd[h0 >> 5] : 0u;
-            f1[j] = (c[j] && h1 != FGI_NONE) ? p.front_rd[h1 >> 5] : 0u;
-            live += (uint32_t)__popcll(__ballot(lv));
+        for (int j = 0; j < 4; ++j) {
+            const bool in = base + j * 64 + lane < cnt;
+            const uint32_t rel = c[j].x - (uint32_t)s_lo;
+#if FGI_EXP & 8
+            lv[j] = in;
+#else
+            lv[j] = in && !((s.vm[rel >> 5] >> (c[j].x & 31)) & 1u);
+#endif
+#if FGI_EXP & 4
+            f0[j] = (lv[j] && (c[j].z & 1)) ? ~0u : 0u;
+            f1[j] = 0u;
+#else
+            f0[j] = lv[j] ? *head_word(p, c[j].z) : 0u;
+            f1[j] = (lv[j] && c[j].w != FGI_NONE) ? *head_word(p, c[j].w) : 0u;
+#endif
         }
-        PullSlots nxt;
-        pull_load(p, vis, d0 + kPullTile, lane, t + 1 < t_hi, nxt);
-        bool hit[kPS], tail[kPS];
+        uint4 cn[4];
 #pragma unroll
-        for (int j = 0; j < (int)kPS; ++j) {
-            const uint32_t h0 = (uint32_t)cur.hd[j], h1 = (uint32_t)(cur.hd[j] >> 32);
-            const bool b0 = c[j] && ((f0[j] >> (h0 & 31)) & 1u);
-            const bool b1 = c[j] && h1 != FGI_NONE && ((f1[j] >> (h1 & 31)) & 1u);
-            // statistics as wave-uniform counts (scalar registers), reported by lane 0
-            cand += (uint32_t)__popcll(__ballot(c[j]));
-            examined += (uint32_t)__popcll(__ballot(c[j])) + (uint32_t)__popcll(__ballot(c[j] && h1 != FGI_NONE && !b0));
-            hit[j] = b0 || b1;
-            tail[j] = c[j] && !hit[j] && ((cur.mw[j] >> (lane & 31)) & 1u);
+        for (int j = 0; j < 4; ++j) {
+#if FGI_PULL_PREFETCH
+            const uint32_t i = base + kCandBatch + j * 64 + lane;
+#else
+            const uint32_t i = cnt;
+#endif
+            cn[j] = load_cand(src + seg + i, i < cnt, (uint32_t)s_lo);
         }
-        uint32_t q_end = 0, nw = 0, ne = 0;
-        unsigned long long nl = 0;
 #pragma unroll
-        for (int j = 0; j < (int)kPS; ++j) {
-            const uint64_t d = d0 + j * 64 + lane;
-            const bool win = hit[j] && ((cur.cw[j] >> (lane & 31)) & 1u);
-            if (hit[j] && !win) flagged += first_visit(node[d]) == 2 ? 1u : 0u;
-            const unsigned long long vm = __ballot(hit[j]), wm = __ballot(win);
-            if (lane == 0) {
-                s.vm[k * kTileWords + wid * kPS + j] = vm;
-                s.wm[k * kTileWords + wid * kPS + j] = wm;
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t i = base + j * 64 + lane;
+            const uint32_t d = c[j].x, h0 = c[j].z, h1 = c[j].w, aux = c[j].y;
+            const bool b0 = lv[j] && ((f0[j] >> (h0 & 31)) & 1u);
+            const bool b1 = lv[j] && h1 != FGI_NONE && ((f1[j] >> (h1 & 31)) & 1u);
+            const bool hit = b0 || b1;
+            const bool tail = lv[j] && !hit && (aux >> 31);
+            const bool surv = lv[j] && !hit && !tail;
+            live += lv[j] ? 1u : 0u;
+            examined += (lv[j] ? 1u : 0u) + ((lv[j] && h1 != FGI_NONE && !b0) ? 1u : 0u);
+            if (hit) {
+                const uint32_t rel = d - (uint32_t)s_lo;
+                const uint32_t bit = 1u << (d & 31);
+                const bool win = (s.cs[rel >> 5] & bit) != 0;
+                atomicOr(&s.vm[rel >> 5], bit);
+                if (win) {
+                    atomicOr(&s.wm[rel >> 5], bit);
+                    acc.add(s, rel / kPullTile, aux & 0x7FFFFFFFu);
+                } else {
+                    flagged += first_visit(node[d]) == 2 ? 1u : 0u;
+                }
             }
-            nw += (uint32_t)__popcll(wm);
-            ne += (uint32_t)__popcll(__ballot(win && cur.rl[j]));
-            nl += win ? cur.rl[j] : 0u;
-            const unsigned long long tm = __ballot(tail[j]);
-            if (tm) {
-                uint32_t qb = 0;
-                if (lane == 0) qb = atomicAdd(&s.qn, (uint32_t)__popcll(tm));
-                qb = __shfl(qb, 0, 64);
-                if (tail[j]) lds_q[qb + __popcll(tm & lanemask_lt())] = (uint32_t)d;
-                q_end = qb + (uint32_t)__popcll(tm);
+            const unsigned long long tm = __ballot(tail);
+            if (tail) wq[qn + __popcll(tm & lanemask_lt())] = i;
+            qn += (uint32_t)__popcll(tm);
+            const unsigned long long sm = __ballot(surv);
+            if (sm) {
+                uint32_t sb = 0;
+                if (lane == 0) sb = atomicAdd(&s.sn, (uint32_t)__popcll(sm));
+                sb = __shfl(sb, 0, 64);
+#if !(FGI_EXP & 2)
+                if (surv) p.sv[dst][seg + sb + (uint32_t)__popcll(sm & lanemask_lt())] = c[j];
+#endif
             }
         }
-        nl = wave_sum64(nl);
-        if (lane == 0) {
-            if (nw) atomicAdd(&s.cw[k], nw);
-            if (ne) atomicAdd(&s.ce[k], ne);
-            if (nl) atomicAdd(&s.cl[k], nl);
+        // scan the queued tails when the queue could overflow next batch, or at the wave's end
+        if (base + kCandBatch >= cnt) PROBE(L, 7);
+        if (qn > kWaveTailCap - kWaveBatch || base + kCandBatch >= cnt) {
+            __builtin_amdgcn_wave_barrier();
+            pull_tails(p, src, dst, node, s_lo, seg, wq, (FGI_EXP & 1) ? 0u : qn, s, flagged, examined_tail, tails);
+            __builtin_amdgcn_wave_barrier();
+            qn = 0;
         }
-        // flush when the LDS buffers are full, the queue could overflow next time, or at the end
-        const bool full = k + 1 == kMaxIter || t + 1 == t_hi;
-        if (__syncthreads_or(full || q_end > kTailCap - kPullTile)) {
-            const uint32_t nq = s.qn;
-            pull_flush(p, node, vis, t_base, k + 1, lds_q, nq, s, flagged, examined_tail, tails, bs);
-            if (threadIdx.x == 0) s.qn = 0;
-            __syncthreads();
-            t_base = t + 1;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#if FGI_PULL_PREFETCH
+            c[j] = cn[j];
+#else
+            const uint32_t i = base + kCandBatch + j * 64 + lane;
+            c[j] = load_cand(src + seg + i, i < cnt, (uint32_t)s_lo);
+#endif
         }
-        cur = nxt;
     }
-    const uint32_t scan = (blockIdx.x == 0 && threadIdx.x == 0) ? p.n_slots : 0u;
-    // cand, live and the head probes of `examined` are wave-uniform counts; the tail probes and
-    // flag counts are per lane; the winners are the flushes' per-thread tile sums (bs[0])
-    const bool l0 = lane == 0;
-    const uint32_t v[kStats] = {0, flagged, l0 ? cand : 0u, examined_tail + (l0 ? examined : 0u), l0 ? live : 0u,
-                                (uint32_t)bs[0], tails, scan};
+    PROBE(L, 2);
+    acc.flush(s);
+    __syncthreads();
+    PROBE(L, 3);
+    // write back the owned words (visits before this level | this level's) and the per-tile counts
+    unsigned long long* vis64 = reinterpret_cast<unsigned long long*>(vis);
+    unsigned long long* inv64 = reinterpret_cast<unsigned long long*>(p.inv_bm);
+    unsigned long long* lw64 = reinterpret_cast<unsigned long long*>(p.lw_bm);
+    for (uint32_t i = threadIdx.x; i < wp.tpb * kTileWords; i += blockDim.x) {
+        const uint64_t sl = s_lo + (uint64_t)i * 64;
+        if (sl < p.n_slots) {
+            const unsigned long long wm = s.wm[2 * i] | ((unsigned long long)s.wm[2 * i + 1] << 32);
+            vis64[sl >> 6] = s.vm[2 * i] | ((unsigned long long)s.vm[2 * i + 1] << 32);
+            if (wm) inv64[sl >> 6] |= wm;
+            lw64[sl >> 6] = wm;
+        }
+    }
+    for (uint32_t k = threadIdx.x; k < wp.tpb; k += blockDim.x) {
+        const uint64_t t = (uint64_t)b * wp.tpb + k;
+        if (t < wp.n_tiles) p.tiles[t] = PullTile{s.cw[k], s.ce[k], s.cl[k]};
+        bs[0] += s.cw[k];
+        bs[1] += s.ce[k];
+        bs[2] += s.cl[k];
+    }
+    if (threadIdx.x == 0) p.sv_cnt[dst][b] = s.sn;
+    // the tail probes, flag counts, live and head probes are per lane; the winners are the per-thread
+    // tile sums (bs[0]); the scanned count is the block's list length
+    const uint32_t v[kStats] = {0, flagged, threadIdx.x == 0 ? s.sn : 0u, examined_tail + examined,
+                                live, (uint32_t)bs[0], tails, threadIdx.x == 0 ? cnt : 0u};
     block_stats_add(blk, s_st, v);
 }
 
 // The last block of a pull level: prefixes of the per-block (winners, expandable winners, row
 // lengths) for a possible collect, and level L+1's frontier totals.
-__device__ __forceinline__ void pull_epilogue(const PullArgs& p, LevelCtr* ln, unsigned long long* done,
+__device__ __forceinline__ void pull_epilogue(int L, const PullArgs& p, LevelCtr* ln, unsigned long long* done,
                                               const unsigned long long (&bs)[3], unsigned long long* s_red) {
     __shared__ unsigned long long s_tot[3];
     const uint64_t G = gridDim.x;
-    // per-wave partial sums -> the block's sums
+    // per-thread partial sums -> the block's sums
     const unsigned long long b0 = block_sum(bs[0], s_red), b1 = block_sum(bs[1], s_red), b2 = block_sum(bs[2], s_red);
     if (threadIdx.x == 0) {
         coh_xchg(p.bsum + blockIdx.x, b0);
         coh_xchg(p.bsum + G + blockIdx.x, b1);
         coh_xchg(p.bsum + 2 * G + blockIdx.x, b2);
     }
-    if (!last_block(done)) return;
+    PROBE(L, 5);
+    if (!last_block(done, gridDim.x)) {
+        PROBE(L, 6);
+        return;
+    }
     prefix_columns(p.bsum, p.bsum + 3 * G, 3, G, s_tot, s_red);
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1039,6 +1175,7 @@ __device__ __forceinline__ void pull_epilogue(const PullArgs& p, LevelCtr* ln, u
         ln->F = s_tot[1];
         ln->T = s_tot[2];
     }
+    PROBE(L, 6);
 }
 
 // One level's traversal: push (expand) or pull, as decided for the level on the device.
@@ -1054,27 +1191,40 @@ __global__ __launch_bounds__(kBlock, 5) void k_level(int L, WaveParams wp, Expan
     __shared__ MsgEmit<PART> me;
     __shared__ unsigned long long s_st[kBlock / 64][kStats];
     __shared__ unsigned long long s_red[kBlock / 64];
-    static_assert(sizeof(PullLds) <= (kChunk + 2) * 4, "pull LDS");
+    static_assert(sizeof(PullLds) <= (kChunk + 2) * 4 && kTailCap <= kChunk, "pull LDS");
+    PROBE(L, 0);
     LevelCtr& lc = ctr->lvl[L % kRing];
     o.ln = &ctr->lvl[(L + 1) % kRing];
     if (blockIdx.x == 0 && threadIdx.x < sizeof(LevelCtr) / 8)
         reinterpret_cast<unsigned long long*>(&ctr->lvl[(L + 2) % kRing])[threadIdx.x] = 0ull;
     const bool pull = level_pulls(ctr, L, wp);
-    if (!PART && blockIdx.x == 0 && threadIdx.x == 0) lc.pull = pull ? 1ull : 0ull;
+    const uint64_t npull = lc.npull;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        if (!PART) lc.pull = pull ? 1ull : 0ull;
+        o.ln->npull = npull + (pull ? 1 : 0);
+    }
     // multi-GPU pull levels run on every rank (parents may be remote); otherwise no frontier, no work
     if (pull) {
         unsigned long long bs[3] = {0, 0, 0};
-        pull_level(p, wp, node, vis, s_rel, *reinterpret_cast<PullLds*>(s_base), blk, s_st, bs);
-        pull_epilogue(p, o.ln, done, bs, s_red);
+        pull_level(L, p, wp, npull, node, vis, s_rel, *reinterpret_cast<PullLds*>(s_base), blk, s_st, bs);
+        PROBE(L, 4);
+        pull_epilogue(L, p, o.ln, done, bs, s_red);
         return;
     }
     const uint64_t F = lc.F, T = lc.T;
     if (F == 0) return;
     const uint32_t mult = level_mult(T, gridDim.x);
     if (blockIdx.x == 0 && threadIdx.x == 0) lc.mult = mult;
+    // blocks without a chunk leave at once and are not counted (a small level costs its chunks only)
+    const uint64_t nch = ((T + kFine - 1) / kFine + mult - 1) / mult;
+    const uint64_t active = nch < gridDim.x ? nch : gridDim.x;
+    if (blockIdx.x >= active) return;
     emit_init(em);
+    PROBE(L, 1);
     expand_level<PART>(F, T, mult, x, node, vis, o, em, s_x, me, s_rel, s_base, blk, s_st, ra);
-    publish_ft(o.ln, done);
+    PROBE(L, 2);
+    publish_ft(o.ln, done, active);
+    PROBE(L, 3);
 }
 
 // multi-GPU: apply the targets other ranks forwarded (their versions were checked by the sender)
@@ -1108,41 +1258,89 @@ __global__ __launch_bounds__(kBlock) void k_apply_recv(int L, uint64_t n, const 
     emit_flush<kEmitCap>(em, eb, 1, o);
     const uint32_t v[kStats] = {0, flagged, 0, 0, 0, 0, 0, 0};
     block_stats_add(blk, s_st, v);
-    publish_ft(o.ln, done);
+    publish_ft(o.ln, done, gridDim.x);
 }
 
 // ---- final collect: the invalidated bitmap -> the invalidated list -----------------------------
-// Block b owns 64-bit words [b * wpb, (b + 1) * wpb) of the bitmap. Pass 1 counts, the last block
-// turns the counts into offsets and the total (V_inv); pass 2 writes every set bit's handle, in
-// ascending order.
-__global__ __launch_bounds__(kBlock) void k_final_count(const unsigned long long* __restrict__ inv64, uint64_t words,
-                                                        uint64_t wpb, unsigned long long* bsum, unsigned long long* done,
-                                                        WaveCtr* ctr) {
+// One pass with a decoupled look-back: a block takes a ticket (its place in the order — a lower
+// ticket belongs to a block that is already running), counts the set bits of its 64-bit words
+// [t * wpb, (t + 1) * wpb), publishes the count, then adds up its predecessors' counts or, at the
+// first one that has it, their inclusive prefix (one wave, 64 predecessors per step), publishes its
+// own inclusive prefix and writes every set bit's handle at that offset, in ascending order: one
+// 1,024-handle tile per wave, 16 handles per lane, staged in LDS and stored coalesced. Status words
+// carry the launch's epoch (bits 48-63) and a flag (bit 46 count, bit 47 prefix), so they need no
+// reset; the last ticket resets the ticket counter. Tickets 0..kStats-1 also fold the per-block
+// statistics into the wave counters (one column each, coalesced sweeps).
+constexpr unsigned long long kStAgg = 1ull << 46, kStInc = 1ull << 47, kStVal = kStAgg - 1;
+
+__global__ __launch_bounds__(kBlock) void k_final(const unsigned long long* __restrict__ inv64, uint64_t words,
+                                                  uint64_t wpb, unsigned long long* status, unsigned long long* ticket,
+                                                  uint32_t epoch, WaveCtr* ctr, const unsigned long long* __restrict__ blk,
+                                                  uint32_t* out) {
     __shared__ unsigned long long s_red[kBlock / 64];
-    __shared__ unsigned long long s_tot[1];
-    const uint64_t lo = blockIdx.x * wpb, hi = std::min<uint64_t>(words, lo + wpb);
+    __shared__ unsigned long long s_excl;
+    __shared__ uint32_t s_t;
+    __shared__ uint32_t s_w[kBlock / 64];
+    __shared__ uint32_t s_stage[kBlock / 64][kPullTile];
+    if (threadIdx.x == 0)
+        s_t = (uint32_t)__hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const uint32_t t = s_t;
+    const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
+    if (t < (uint32_t)kStats) {
+        const int k = t;
+        unsigned long long* dst[kStats] = {&ctr->e_match,   &ctr->n_flagged, &ctr->pull_surv, &ctr->pull_edges,
+                                           &ctr->pull_live, &ctr->pull_win,  &ctr->pull_tail, &ctr->pull_scan};
+        const unsigned long long* col = blk + (uint64_t)k * kStatBlocks;
+        unsigned long long x = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kStatBlocks / kBlock; ++q) x += col[q * kBlock + threadIdx.x];
+        x = block_sum(x, s_red);
+        if (threadIdx.x == 0) *dst[k] = x + (k == kStFlagged ? ctr->root_flagged : 0ull);
+    }
+    const uint64_t lo = t * wpb, hi = std::min<uint64_t>(words, lo + wpb);
     unsigned long long c = 0;
     for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x) c += (unsigned long long)__popcll(inv64[w]);
     c = block_sum(c, s_red);
-    if (threadIdx.x == 0) coh_xchg(bsum + blockIdx.x, c);
-    if (!last_block(done)) return;
-    prefix_columns(bsum, bsum + gridDim.x, 1, gridDim.x, s_tot, s_red);
+    const unsigned long long ep = (unsigned long long)epoch << 48;
+    if (threadIdx.x == 0) coh_xchg(status + t, ep | (t == 0 ? kStInc : kStAgg) | c);
+    if (wid == 0) {
+        unsigned long long excl = 0;
+        for (int64_t j = (int64_t)t - 1; j >= 0; j -= 64) {   // wave-uniform
+            const int64_t k = j - (int64_t)lane;               // lane 0: the nearest predecessor
+            unsigned long long v = kStInc | ep;                // below ticket 0: an empty prefix
+            if (k >= 0) {
+                do {
+                    v = coh_read(status + k);
+                } while ((v & ~((1ull << 48) - 1)) != ep || !(v & (kStAgg | kStInc)));
+            }
+            const unsigned long long inc = __ballot((v & kStInc) != 0);
+            const uint32_t upto = inc ? (uint32_t)__ffsll((long long)inc) - 1 : 63u;
+            unsigned long long x = (lane <= upto) ? (v & kStVal) : 0ull;
+#pragma unroll
+            for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
+            excl += x;
+            if (inc) break;
+        }
+        if (lane == 0) {
+            s_excl = excl;
+            if (t > 0) coh_xchg(status + t, ep | kStInc | (excl + c));
+            if (t == gridDim.x - 1) {
+                ctr->inv = excl + c;
+                coh_xchg(ticket, 0ull);   // every ticket is taken
+            }
+        }
+    }
     __syncthreads();
-    if (threadIdx.x == 0) ctr->inv = s_tot[0];
-}
-
-__global__ __launch_bounds__(kBlock) void k_final_write(const unsigned long long* __restrict__ inv64, uint64_t words,
-                                                        uint64_t wpb, const unsigned long long* __restrict__ pre,
-                                                        uint32_t* out) {
-    __shared__ uint32_t s_w[kBlock / 64];
-    const uint64_t lo = blockIdx.x * wpb, hi = std::min<uint64_t>(words, lo + wpb);
-    const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
-    uint64_t run = pre[blockIdx.x];
-    for (uint64_t b = lo; b < hi; b += blockDim.x) {   // block-uniform
-        const uint64_t w = b + threadIdx.x;
-        unsigned long long x = w < hi ? inv64[w] : 0ull;
+    const uint16_t* bits16 = reinterpret_cast<const uint16_t*>(inv64);
+    uint64_t run = s_excl;
+    // rounds of one 16-word tile per wave
+    for (uint64_t w0 = lo; w0 < hi; w0 += (uint64_t)(blockDim.x >> 6) * kTileWords) {   // block-uniform
+        const uint64_t tw = w0 + (uint64_t)wid * kTileWords;                            // the wave's first word
+        const uint64_t q = tw * 4 + lane;                                                // the lane's 16-bit chunk
+        const uint32_t m = (tw + lane / 4 < hi) ? (uint32_t)bits16[q] : 0u;
         uint32_t tot;
-        const uint32_t ex = wave_excl_scan((uint32_t)__popcll(x), tot);
+        const uint32_t ex = wave_excl_scan((uint32_t)__popc(m), tot);
         __syncthreads();
         if (lane == 0) s_w[wid] = tot;
         __syncthreads();
@@ -1151,28 +1349,15 @@ __global__ __launch_bounds__(kBlock) void k_final_write(const unsigned long long
             if (k < wid) before += s_w[k];
             all += s_w[k];
         }
-        uint64_t o = run + before + ex;
-        for (; x; x &= x - 1) out[o++] = (uint32_t)(w * 64 + (uint64_t)(__ffsll((long long)x) - 1));
+        uint32_t o = ex;
+        for (uint32_t mm = m; mm; mm &= mm - 1) s_stage[wid][o++] = (uint32_t)(q * 16 + (uint32_t)(__ffs(mm) - 1));
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i = lane; i < tot; i += 64) out[run + before + i] = s_stage[wid][i];
+        __builtin_amdgcn_wave_barrier();
         run += all;
     }
 }
 
-// Folds the per-block statistics into the wave counters: one block per column (coalesced sweeps).
-__global__ __launch_bounds__(kBlock) void k_stats_reduce(const unsigned long long* __restrict__ blk, WaveCtr* ctr) {
-    __shared__ unsigned long long s_red[kBlock / 64];
-    const int k = blockIdx.x;
-    unsigned long long* dst[kStats] = {&ctr->e_match,   &ctr->n_flagged, &ctr->pull_cand, &ctr->pull_edges,
-                                       &ctr->pull_live, &ctr->pull_win,  &ctr->pull_tail, &ctr->pull_scan};
-    const unsigned long long* col = blk + (uint64_t)k * kStatBlocks;
-    unsigned long long t = 0;
-#pragma unroll
-    for (uint32_t b = 0; b < kStatBlocks / kBlock; ++b) t += col[b * kBlock + threadIdx.x];
-    t = block_sum(t, s_red);
-    if (threadIdx.x == 0) *dst[k] = t + (k == kStFlagged ? ctr->root_flagged : 0ull);
-}
-
-// Wave prologue in one launch: the counter ring, the per-block statistics and the invalidated bitmap
-// start at zero.
 __global__ __launch_bounds__(kBlock) void k_wave_init(WaveCtr* ctr, unsigned long long* blk, uint32_t* inv_bm,
                                                       uint64_t bm_words) {
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1234,14 +1419,15 @@ fgi_status ensure_cls(fgi_graph* g) {
 
 namespace {
 
-// Algorithmic bytes of the pull levels of a wave (k_level on pull levels): per slot scanned its
-// two list heads (8 B) and the visit / class / "more" words (3/8 B); per queued slot its list
-// offset and length (12 B) and 4 B per further dependency examined; per winner its row length
-// (4 B). The invalidated-bitmap probes hit L2 and are not counted.
+// Algorithmic bytes of the pull levels of a wave (k_level on pull levels): per candidate scanned
+// its entry (slot 4, heads 8, row length 4) and the visit / class words (1/4 B); per survivor its
+// entry written forward (16 B); per queued candidate its list offset and length (12 B) and entry
+// re-read (4 B), and 4 B per further dependency examined. The invalidated-bitmap probes hit L2 and
+// are not counted.
 uint64_t pull_level_bytes(const WaveCtr& c) {
-    const uint64_t head_probes = c.pull_cand;   // >= 1 examined per candidate in the head step
+    const uint64_t head_probes = c.pull_live;   // >= 1 examined per live candidate in the head step
     const uint64_t tail_deps = c.pull_edges > head_probes ? c.pull_edges - head_probes : 0;
-    return c.pull_scan * 8 + c.pull_scan * 3 / 8 + 12 * c.pull_tail + 4 * tail_deps + 4 * c.pull_win;
+    return 16 * c.pull_scan + c.pull_scan / 4 + 16 * c.pull_surv + 16 * c.pull_tail + 4 * tail_deps;
 }
 
 // Flags of the per-level timing events (FGI_EVENT_FLAGS overrides, for measurement). Without the
@@ -1252,20 +1438,46 @@ unsigned event_flags() {
     return f;
 }
 
-uint32_t level_grid_for(fgi_graph* g, uint32_t per_cu) {
-    return std::min<uint32_t>((uint32_t)g->n_cu * per_cu, kStatBlocks);
+// the last-block epilogues read every block's sums in one round (kEpiloguePer per thread)
+constexpr uint32_t kLevelGridMax = kBlock * kEpiloguePer;
+static_assert(kLevelGridMax <= kStatBlocks && kFinalBlocks <= kLevelGridMax, "epilogue geometry");
+
+}  // namespace
+
+// 5 resident blocks per CU (k_level launch bounds); a pull block owns at most kMaxIter tiles, so a
+// larger graph gets more blocks, up to kLevelGridMax (67M slots per device); beyond that, no pull.
+void pull_geometry(const fgi_graph* g, uint32_t* grid, uint32_t* tpb) {
+    const uint64_t n_tiles = ((uint64_t)g->n_slots + kPullTile - 1) / kPullTile;
+    uint64_t G = std::min<uint64_t>((uint64_t)g->n_cu * 5, kLevelGridMax);
+    uint64_t t = (n_tiles + G - 1) / G;
+    if (t > kMaxIter) {
+        t = kMaxIter;
+        G = (n_tiles + t - 1) / t;
+    }
+    *grid = G <= kLevelGridMax ? (uint32_t)G : 0u;
+    *tpb = (uint32_t)std::max<uint64_t>(t, 1);
 }
 
-WaveParams wave_params(fgi_graph* g, uint32_t n_slots, int multi, int direction, uint64_t total_edges) {
+namespace {
+
+WaveParams wave_params(fgi_graph* g, int multi, int direction, uint64_t total_edges, uint64_t n_beta) {
     WaveParams wp;
     wp.multi = multi;
     wp.direction = direction;
     wp.pull_threshold = total_edges / (uint64_t)(g->opt_pull_alpha > 0 ? g->opt_pull_alpha : 1);
-    wp.stay_pull_f = g->opt_pull_beta > 0 ? n_slots / (uint64_t)g->opt_pull_beta : ~0ull;
-    wp.grid = level_grid_for(g, 5);   // 5 resident blocks per CU (k_level launch bounds)
-    wp.n_tiles = ((uint64_t)n_slots + kPullTile - 1) / kPullTile;
-    wp.tpb = (uint32_t)((wp.n_tiles + wp.grid - 1) / wp.grid);
+    wp.stay_pull_f = g->opt_pull_beta > 0 ? n_beta / (uint64_t)g->opt_pull_beta : ~0ull;
+    pull_geometry(g, &wp.grid, &wp.tpb);
+    if (wp.grid == 0) {   // no pull levels: the traversal grid of a push level
+        wp.grid = std::min<uint32_t>((uint32_t)g->n_cu * 5, kLevelGridMax);
+        wp.tpb = 0;
+        if (wp.direction != 1) wp.direction = 1;
+    }
+    wp.n_tiles = ((uint64_t)g->n_slots + kPullTile - 1) / kPullTile;
     return wp;
+}
+
+bool pull_ready(const fgi_graph* g, const WaveParams& wp) {
+    return wp.tpb != 0 && g->uin_src && g->uin_epoch == g->mut_epoch && g->cand_grid == wp.grid;
 }
 
 Out out_for(fgi_graph* g, int buf, LevelCtr* ln) {
@@ -1285,12 +1497,41 @@ CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, const WaveParams& wp, i
     c.fr_len = g->fr_len[buf];
     c.escan = g->escan[buf];
     c.cstart = g->cstart[buf];
+    c.hot_id = g->hot_id;
+    c.hot_bm = g->hot_bm;
+    c.n_hot = g->n_hot;
+    c.inv = g->inv_bm;
     return c;
 }
 
+// k_collect walks the pull grid's blocks in a grid-stride loop: two blocks per CU keep the (usual)
+// no-op launch cheap
+uint32_t collect_grid(const fgi_graph* g, const WaveParams& wp) {
+    const uint32_t cap = 2 * std::max<uint32_t>(g->n_cu, 1);
+    return std::max<uint32_t>(1, std::min<uint32_t>(wp.grid, cap));
+}
+
 PullArgs pull_args(fgi_graph* g, uint32_t n_slots, const uint32_t* front_rd) {
-    return PullArgs{n_slots,  g->uin_off, g->uin_len, g->uin_src,  g->uin_head, g->uin_more, front_rd,
-                    g->inv_bm, g->lw_bm,   g->cls_bm,  g->row_len, g->tiles,    g->bsum};
+    PullArgs p;
+    p.n_slots = n_slots;
+    p.uin_off = g->uin_off;
+    p.uin_len = g->uin_len;
+    p.uin_src = g->uin_src;
+    p.front_rd = front_rd;
+    p.inv_bm = g->inv_bm;
+    p.lw_bm = g->lw_bm;
+    p.cls = g->cls_bm;
+    p.hot_bm = g->hot_bm;
+    p.tiles = g->tiles;
+    p.bsum = g->bsum;
+    p.cand_seg = g->cand_seg;
+    p.c[0] = g->cand;
+    for (int k = 0; k < 2; ++k) {
+        p.c[1 + k] = g->sv[k];
+        p.sv[k] = g->sv[k];
+        p.sv_cnt[k] = g->sv_cnt[k];
+    }
+    return p;
 }
 
 ExpandArgs expand_args(fgi_graph* g, int buf) {
@@ -1300,12 +1541,15 @@ ExpandArgs expand_args(fgi_graph* g, int buf) {
 // the invalidated bitmap -> the invalidated list and V_inv (ctr->inv)
 void launch_final(fgi_graph* g, uint32_t n_handles) {
     const uint64_t words = ((uint64_t)n_handles + 63) / 64;
-    const uint32_t G = (uint32_t)std::min<uint64_t>(kFinalBlocks, std::max<uint64_t>(1, (words + 255) / 256));
+    const uint32_t G = (uint32_t)std::min<uint64_t>(kFinalBlocks, std::max<uint64_t>(kStats, (words + 255) / 256));
     const uint64_t wpb = (words + G - 1) / G;
     const auto* inv64 = reinterpret_cast<const unsigned long long*>(g->inv_bm);
-    unsigned long long* fs = g->bsum + 6ull * kStatBlocks;   // apart from the pull prefixes a collect may still read
-    hipLaunchKernelGGL(k_final_count, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb, fs, g->done, g->ctr);
-    hipLaunchKernelGGL(k_final_write, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb, fs + G, g->inv);
+    // status words and the ticket apart from the pull prefixes a collect may still read
+    unsigned long long* st = g->bsum + 6ull * kStatBlocks;
+    g->final_epoch = (g->final_epoch + 1) & 0xFFFFu;
+    if (g->final_epoch == 0) g->final_epoch = 1;
+    hipLaunchKernelGGL(k_final, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb, st, st + kStatBlocks,
+                       g->final_epoch, g->ctr, g->blk_stats, g->inv);
 }
 
 void launch_roots(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev, uint32_t base,
@@ -1322,6 +1566,45 @@ void launch_roots(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, con
 
 }  // namespace
 
+#if FGI_PROBE
+// per level: kernel span, dispatch skew, and per-phase medians / maxima over the blocks (us)
+void print_probe(fgi_graph* g, int L0, int L1) {
+    static unsigned long long h[kProbeLevels][kProbeBlocks][kProbePts];
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(d_probe), sizeof(h)) != hipSuccess) return;
+    for (int l = L0; l < L1 && l < kProbeLevels; ++l) {
+        const bool pull = g->ctr_host->lvl[l % kRing].pull != 0;
+        // phase boundaries in order: pull 0 entry, 1 staged, 7 last batch (wave 0), 2 loop done
+        // (wave 0), 3 all waves, 4 write-back + stats, 5 sums published, 6 exit; push 0 entry,
+        // 1 set up, 2 expanded, 3 published
+        const int pull_pts[] = {0, 1, 7, 2, 3, 4, 5, 6};
+        const int push_pts[] = {0, 1, 2, 3};
+        const int* pts = pull ? pull_pts : push_pts;
+        const int np = pull ? 8 : 4;
+        unsigned long long t_lo = ~0ull, t_hi = 0, s_hi = 0;
+        std::vector<std::vector<double>> d(np);
+        for (int b = 0; b < kProbeBlocks; ++b) {
+            const unsigned long long* t = h[l][b];
+            if (!t[0]) continue;
+            t_lo = std::min(t_lo, t[0]);
+            s_hi = std::max(s_hi, t[0]);
+            for (int k = 0; k < np; ++k) t_hi = std::max(t_hi, t[pts[k]]);
+            for (int k = 1; k < np; ++k)
+                if (t[pts[k]] && t[pts[k - 1]]) d[k].push_back((double)(t[pts[k]] - t[pts[k - 1]]) / 100.0);
+        }
+        if (t_lo == ~0ull) continue;
+        fprintf(stderr, "[probe] level %d %s: span %.1f us, start skew %.1f us; phases (median/max us):", l,
+                pull ? "pull" : "push", (t_hi - t_lo) / 100.0, (s_hi - t_lo) / 100.0);
+        for (int k = 1; k < np; ++k) {
+            auto& v = d[k];
+            if (v.empty()) continue;
+            std::sort(v.begin(), v.end());
+            fprintf(stderr, " %d:%.1f/%.1f", k, v[v.size() / 2], v.back());
+        }
+        fprintf(stderr, "\n");
+    }
+}
+#endif
+
 fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                     fgi_wave_stats* stats) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -1335,10 +1618,17 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     // run push-only; once a level group shows a frontier heavy enough to pull, the cache is
     // (re)built and later groups may pull. Small waves (streaming mixes) never pay for it.
     const int direction = g->opt_direction;
-    if (direction == 2 && n_roots) FGI_TRY(ensure_in_lists(g));
-    bool allow_pull = direction != 1 && g->uin_src && g->uin_epoch == g->mut_epoch;
+    const WaveParams wp0 = wave_params(g, 0, direction, g->pool_top, g->n_slots);
+    if (wp0.direction == 2 && n_roots) FGI_TRY(ensure_in_lists(g));
+    bool allow_pull = wp0.direction != 1 && pull_ready(g, wp0);
     static_assert(sizeof(WaveCtr) % 8 == 0, "WaveCtr is cleared as 64-bit words");
     hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm, (uint64_t)g->bm_words);
+#if FGI_PROBE
+    {
+        void* pp = nullptr;
+        if (hipGetSymbolAddress(&pp, HIP_SYMBOL(d_probe)) == hipSuccess) (void)hipMemsetAsync(pp, 0, sizeof(d_probe), s);
+    }
+#endif
     if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
     if (n_roots) {
         g->v_dirty = true;
@@ -1358,10 +1648,11 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     bool final_done = false;
     while (!done) {
         const int L0 = L;
-        const WaveParams wp = wave_params(g, g->n_slots, 0, allow_pull ? direction : 1, g->pool_top);
+        WaveParams wp = wp0;
+        if (!allow_pull) wp.direction = 1;
         for (int k = 0; k < group; ++k, ++L) {
             const int buf = L & 1;
-            hipLaunchKernelGGL(k_collect, dim3(wp.grid), dim3(kCollectThreads), 0, s, L, g->ctr, wp,
+            hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp,
                                collect_args(g, g->n_slots, wp, buf));
             if (timing) {
                 while (g->ev.size() < 2 * (size_t)(L + 1) + 2) {
@@ -1378,7 +1669,6 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         }
         launch_final(g, g->n_handles);   // idempotent: repeated if the wave goes on
         final_done = true;
-        hipLaunchKernelGGL(k_stats_reduce, dim3(kStats), dim3(kBlock), 0, s, g->blk_stats, g->ctr);
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
         FGI_HIP(g, hipStreamSynchronize(s));
@@ -1413,22 +1703,24 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                         lc.pull ? "pull" : "push", (unsigned long long)lc.F, (unsigned long long)lc.T,
                         (unsigned long long)lc.mult, ms);
         }
+#if FGI_PROBE
+        if (trace) print_probe(g, L0, L);
+#endif
         done = g->ctr_host->lvl[L % kRing].F == 0;
         group = 4;
         // also when the wave is already done (its level groups are sized from the previous wave's
         // depth, so a repeated wave after a mutation finishes in one group): the next wave pulls
-        if (!allow_pull && direction == 0) {
+        if (!allow_pull && wp0.direction == 0) {
             bool heavy = false;
             for (int l = L0; l <= L; ++l) heavy |= g->ctr_host->lvl[l % kRing].T > wp.pull_threshold;
             if (heavy) {
                 FGI_TRY(ensure_in_lists(g));
-                allow_pull = true;
+                allow_pull = pull_ready(g, wp0);
             }
         }
     }
     if (!final_done) {   // no roots
         launch_final(g, g->n_handles);
-        hipLaunchKernelGGL(k_stats_reduce, dim3(kStats), dim3(kBlock), 0, s, g->blk_stats, g->ctr);
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
         FGI_HIP(g, hipStreamSynchronize(s));
@@ -1443,9 +1735,9 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     const WaveCtr& c = *g->ctr_host;
     if (trace)
         fprintf(stderr,
-                "[fgi] wave: %llu invalidated; pull: live %llu, candidates %llu, queued %llu, dependencies "
+                "[fgi] wave: %llu invalidated; pull: live %llu, survivors %llu, queued %llu, dependencies "
                 "examined %llu, winners %llu\n",
-                (unsigned long long)c.inv, (unsigned long long)c.pull_live, (unsigned long long)c.pull_cand,
+                (unsigned long long)c.inv, (unsigned long long)c.pull_live, (unsigned long long)c.pull_surv,
                 (unsigned long long)c.pull_tail, (unsigned long long)c.pull_edges, (unsigned long long)c.pull_win);
     if (stats) {
         const uint64_t v = c.inv;
@@ -1508,17 +1800,18 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     FGI_HIP(g, hipGetLastError());
     const auto* node = reinterpret_cast<const unsigned long long*>(g->node);
     // one all-reduce of {local edges, level-0 frontier, its edges, ranks without pull lists}
-    const bool can_pull = g->opt_direction != 1 && g->uin_src && g->uin_epoch == g->mut_epoch;
+    const WaveParams wp0 = wave_params(g, 1, g->opt_direction, g->pool_top, pv.n_global);
+    const bool can_pull = wp0.direction != 1 && pull_ready(g, wp0);
     const uint64_t head = g->pool_top, tail = can_pull ? 0ull : 1ull;
     FGI_HIP(g, hipMemcpyAsync(pv.scratch_u64, &head, 8, hipMemcpyHostToDevice, s));
     FGI_HIP(g, hipMemcpyAsync(pv.scratch_u64 + 1, &g->ctr->lvl[0].F, 16, hipMemcpyDeviceToDevice, s));
     FGI_HIP(g, hipMemcpyAsync(pv.scratch_u64 + 3, &tail, 8, hipMemcpyHostToDevice, s));
     uint64_t sums[4] = {0, 0, 0, 0};
     FGI_TRY(part_allreduce_sum(g, pv.scratch_u64, sums, 4));
-    const WaveParams wp = wave_params(g, pv.n_local, 1, g->opt_direction, sums[0]);
-    const uint64_t stay_pull_f = g->opt_pull_beta > 0 ? pv.n_global / (uint64_t)g->opt_pull_beta : ~0ull;
+    const WaveParams wp = wave_params(g, 1, g->opt_direction, sums[0], pv.n_global);
+    const uint64_t stay_pull_f = wp.stay_pull_f;
     const bool allow_pull = sums[3] == 0;
-    const int direction = g->opt_direction;
+    const int direction = wp.direction;
     const RemoteArgs ra{pv.base, pv.n_local, pv.block, pv.world, pv.ver_all, pv.sent_bm, pv.send_buf, pv.send_cnt};
     uint64_t f_global = sums[1], t_global = sums[2];
     uint64_t levels = 0, e_trav = 0, f_total = 0, sent_total = 0, push_edges = 0, push_f = 0;
@@ -1538,11 +1831,11 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
             FGI_HIP(g, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&g->ctr->lvl[L % kRing].pull), 1, 1, s));
             FGI_TRY(part_allgather_front(g));
         }
-        hipLaunchKernelGGL(k_collect, dim3(wp.grid), dim3(kCollectThreads), 0, s, L, g->ctr, wp,
+        hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp,
                            collect_args(g, pv.n_local, wp, buf));
         if (g->opt_level_timing) FGI_HIP(g, hipEventRecord(g->ev[0], s));
         hipLaunchKernelGGL(k_level<true>, dim3(wp.grid), dim3(kBlock), 0, s, L, wp, expand_args(g, buf),
-                           pull_args(g, pv.n_local, pv.front_global), node, g->vis_bm, out_for(g, buf ^ 1, nullptr),
+                           pull_args(g, g->n_slots, pv.front_global), node, g->vis_bm, out_for(g, buf ^ 1, nullptr),
                            g->ctr, g->blk_stats, g->done, ra);
         if (g->opt_level_timing) FGI_HIP(g, hipEventRecord(g->ev[1], s));
         FGI_HIP(g, hipGetLastError());
@@ -1579,7 +1872,6 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
         last_pull = pull;
     }
     launch_final(g, pv.n_local);
-    hipLaunchKernelGGL(k_stats_reduce, dim3(kStats), dim3(kBlock), 0, s, g->blk_stats, g->ctr);
     FGI_HIP(g, hipGetLastError());
     FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
     FGI_HIP(g, hipEventRecord(g->ev_w1, s));

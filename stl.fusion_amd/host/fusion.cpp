@@ -2,9 +2,57 @@
 #include "fusion.hpp"
 
 #include <algorithm>
+#include <chrono>
+#include <thread>
 
 namespace fusion {
 
+namespace {
+constexpr uint32_t kNone = 0xFFFFFFFFu;
+constexpr uint64_t kParallelMin = 1u << 16;   // ids below this fan out on the dispatcher thread
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+}  // namespace
+
+// ---- InvalidatedHandlerSet ------------------------------------------------------------------------
+void InvalidatedHandlerSet::Add(const InvalidatedHandler& h) {
+    if (!h) return;
+    if (set_) {
+        set_->insert(h);
+        return;
+    }
+    for (const auto& x : list_)
+        if (x == h) return;
+    if (list_.size() < ListSize) {
+        list_.push_back(h);
+        return;
+    }
+    set_ = std::make_unique<std::unordered_set<InvalidatedHandler>>(list_.begin(), list_.end());
+    set_->insert(h);
+    list_.clear();
+}
+
+void InvalidatedHandlerSet::Remove(const InvalidatedHandler& h) {
+    if (!h) return;
+    if (set_) {
+        set_->erase(h);
+        return;
+    }
+    auto it = std::find(list_.begin(), list_.end(), h);
+    if (it != list_.end()) list_.erase(it);
+}
+
+void InvalidatedHandlerSet::Invoke(Computed& c) const {
+    if (set_) {
+        for (const auto& h : *set_) (*h)(c);
+        return;
+    }
+    for (const auto& h : list_) (*h)(c);
+}
+
+// ---- registry -------------------------------------------------------------------------------------
 ComputedRegistry::ComputedRegistry(uint32_t n_slots, uint32_t n_detached, int device) : n_slots_(n_slots) {
     fgi_config cfg{};
     cfg.struct_size = sizeof(cfg);
@@ -14,7 +62,9 @@ ComputedRegistry::ComputedRegistry(uint32_t n_slots, uint32_t n_detached, int de
     cfg.world = 1;
     fgi_status s = fgi_create(&cfg, &g_);
     if (s != FGI_OK) throw FgiError(s, "fgi_create failed (no GPU?)");
+    n_handles_ = n_slots + n_detached;
     current_.resize(n_slots);
+    has_obj_.assign(n_handles_, 0);
 }
 
 ComputedRegistry::~ComputedRegistry() { fgi_destroy(g_); }
@@ -41,12 +91,28 @@ LTag ComputedRegistry::NextVersion(LTag current) {
     return ltag_;
 }
 
+uint32_t* ComputedRegistry::IdsBuffer(uint64_t need) {
+    if (need > ids_cap_) {
+        const uint64_t cap = std::max<uint64_t>(need, ids_cap_ + ids_cap_ / 2);
+        ids_.reset(new uint32_t[cap]);   // default-initialised: no zero-fill
+        ids_cap_ = cap;
+    }
+    return ids_.get();
+}
+
 std::shared_ptr<Computed> ComputedRegistry::Get(const std::string& input) {
     const uint32_t s = SlotOf(input, false);
     if (s == FGI_NONE || !current_[s]) return nullptr;
     const ConsistencyState st = current_[s]->State();
     if (st == ConsistencyState::Invalidated) return nullptr;   // unregistered on invalidation
     return current_[s];
+}
+
+void ComputedRegistry::MoveSubs(uint32_t from, uint32_t to) {
+    if (from >= sub_head_.size() || sub_head_[from] == kNone) return;
+    if (to >= sub_head_.size()) sub_head_.resize(n_handles_, kNone);
+    sub_head_[to] = sub_head_[from];
+    sub_head_[from] = kNone;
 }
 
 std::shared_ptr<Computed> ComputedRegistry::BeginCompute(const std::string& input, bool has_delay) {
@@ -62,21 +128,24 @@ std::shared_ptr<Computed> ComputedRegistry::BeginCompute(const std::string& inpu
     fgi_wave_stats ws{};
     Check(fgi_begin_compute(g_, 1, &s, &c->version_, &hd, &detached, &ws), "fgi_begin_compute");
     auto old = current_[s];
-    if (old) {
-        if (detached != FGI_NONE) {
-            old->handle_ = detached;       // displaced but alive (Computing / delayed)
+    if (detached != FGI_NONE) {   // displaced but alive (Computing / delayed): its handle moves
+        if (old) {
+            old->handle_ = detached;
             detached_[detached] = old;
+            has_obj_[detached] = 1;
         }
+        MoveSubs(s, detached);   // the replicas follow the old node
     }
     // the displacement cascade's invalidated nodes (the old node among them) get their handlers
     if (ws.v_inv) {
-        std::vector<uint32_t> ids(ws.v_inv);
         uint64_t n = 0;
-        Check(fgi_last_wave_ids(g_, ids.data(), ids.size(), &n), "fgi_last_wave_ids");
-        Dispatch(ids.data(), n);
+        uint32_t* ids = IdsBuffer(ws.v_inv);
+        Check(fgi_last_wave_ids(g_, ids, ws.v_inv, &n), "fgi_last_wave_ids");
         last_ = ws;
+        Dispatch(ids, n);
     }
     current_[s] = c;
+    has_obj_[s] = 1;
     if (OnRegister) OnRegister(*c);
     return c;
 }
@@ -91,49 +160,169 @@ uint32_t ComputedRegistry::AddUsed(Computed& dependant, Computed& used) {
 bool ComputedRegistry::SetOutput(Computed& c) {
     uint8_t set = 0;
     const uint32_t h = c.handle_;
-    std::vector<uint32_t> ids(n_slots_ + 1024);
     uint64_t n = 0;
-    Check(fgi_set_output(g_, 1, &h, &set, ids.data(), ids.size(), &n, &last_), "fgi_set_output");
-    Dispatch(ids.data(), n);
+    uint32_t* ids = IdsBuffer(1024);
+    fgi_status s = fgi_set_output(g_, 1, &h, &set, ids, ids_cap_, &n, &last_);
+    if (s == FGI_ECAPACITY) {   // the cascade completed; fetch its ids with the right size
+        ids = IdsBuffer(n);
+        s = fgi_last_wave_ids(g_, ids, n, &n);
+    }
+    Check(s, "fgi_set_output");
+    Dispatch(ids, n);
     return set != 0;
 }
 
-void ComputedRegistry::RunWave(const std::vector<uint32_t>& roots, const std::vector<uint8_t>& imm) {
-    std::vector<uint32_t> ids(n_slots_ + detached_.size() + 1);
+void ComputedRegistry::RunWave(const uint32_t* roots, size_t n_roots, const uint8_t* imm) {
     uint64_t n = 0;
     last_ = fgi_wave_stats{};
-    fgi_status s = fgi_invalidate(g_, (uint32_t)roots.size(), roots.data(), imm.empty() ? nullptr : imm.data(),
-                                  ids.data(), ids.size(), &n, &last_);
+    uint32_t* ids = IdsBuffer(1024);
+    fgi_status s = fgi_invalidate(g_, (uint32_t)n_roots, roots, imm, ids, ids_cap_, &n, &last_);
     if (s == FGI_ECAPACITY) {   // the wave itself completed; fetch the ids with the right size
-        ids.resize(n);
-        s = fgi_last_wave_ids(g_, ids.data(), ids.size(), &n);
+        ids = IdsBuffer(n);
+        s = fgi_last_wave_ids(g_, ids, n, &n);
     }
     Check(s, "fgi_invalidate");
-    Dispatch(ids.data(), n);
+    Dispatch(ids, n);
 }
 
-// Invalidated handlers: once per node, after the wave (InvalidatedHandlerSet.Invoke, :100-127);
-// OnUnregister for registry nodes (ComputeMethodComputed.OnInvalidated -> Unregister).
+// The post-wave fan-out (fusion.hpp, "Threading"). Reference: InvalidatedHandlerSet.Invoke
+// (Internal/InvalidatedHandlerSet.cs:100-127) per node; one `$sys-c.Invalidate` per replica call
+// (Client/Internal/RpcInboundComputeCall.cs:53-62, 102-106), batched per peer here.
 void ComputedRegistry::Dispatch(const uint32_t* ids, uint64_t n) {
-    for (uint64_t i = 0; i < n; ++i) {
-        const uint32_t h = ids[i];
-        std::shared_ptr<Computed> c;
-        if (h < n_slots_) {
-            c = current_[h];
-        } else {
-            auto it = detached_.find(h);
-            if (it != detached_.end()) {
-                c = it->second;
-                detached_.erase(it);
-                fgi_release(g_, 1, &h);
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t P = (uint32_t)peers_.size();
+    fan_.ids = n;
+    fan_.objects = fan_.calls = fan_.batches = 0;
+    fan_.peers_hit = 0;
+    fan_.peer_calls.assign(P, 0);
+    fan_.peer_batches.assign(P, 0);
+    // 1. parallel gather: per thread, per peer call ids (ids ascending -> handle order), freed
+    //    subscription entries, and the ids that have host objects
+    uint32_t T = 1;
+    if (n >= kParallelMin) {
+        T = FanoutThreads ? FanoutThreads : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+        T = (uint32_t)std::min<uint64_t>(T, (n + kParallelMin - 1) / kParallelMin * 4);
+    }
+    fan_.threads = T;
+    struct Part {
+        std::vector<std::vector<uint64_t>> calls;
+        std::vector<uint32_t> freed, objs;
+    };
+    std::vector<Part> parts(T);
+    const bool any_subs = !subs_.empty() && !sub_head_.empty();
+    auto gather = [&](uint32_t t) {
+        Part& pt = parts[t];
+        pt.calls.resize(P);
+        const uint64_t lo = n * t / T, hi = n * (t + 1) / T;
+        for (uint64_t i = lo; i < hi; ++i) {
+            const uint32_t h = ids[i];
+            if (h >= n_handles_) continue;
+            if (has_obj_[h]) pt.objs.push_back(h);
+            if (!any_subs || h >= sub_head_.size()) continue;
+            uint32_t e = sub_head_[h];
+            if (e == kNone) continue;
+            sub_head_[h] = kNone;   // a call completes once (each handle is in one range only)
+            while (e != kNone) {
+                const Sub& sb = subs_[e];
+                pt.calls[sb.peer].push_back(sb.call_id);
+                pt.freed.push_back(e);
+                e = sb.next;
             }
         }
-        if (!c || c->fired_) continue;
-        c->fired_ = true;
-        if (h < n_slots_ && OnUnregister) OnUnregister(*c);
-        auto hs = std::move(c->handlers_);
-        c->handlers_.clear();
-        for (auto& f : hs) f(*c);
+    };
+    if (T == 1) {
+        gather(0);
+    } else {
+        std::vector<std::thread> th;
+        th.reserve(T - 1);
+        for (uint32_t t = 1; t < T; ++t) th.emplace_back(gather, t);
+        gather(0);
+        for (auto& x : th) x.join();
+    }
+    fan_.gather_ms = ms_since(t0);
+    // 2. per peer: its call ids in handle order, PeerBatch per sink call
+    std::vector<uint64_t> buf;
+    for (uint32_t q = 0; q < P; ++q) {
+        uint64_t tot = 0;
+        for (auto& pt : parts) tot += pt.calls[q].size();
+        if (!tot) continue;
+        const uint64_t* data;
+        if (T == 1) {
+            data = parts[0].calls[q].data();
+        } else {
+            buf.clear();
+            buf.reserve(tot);
+            for (auto& pt : parts) buf.insert(buf.end(), pt.calls[q].begin(), pt.calls[q].end());
+            data = buf.data();
+        }
+        const size_t B = std::max<size_t>(1, PeerBatch);
+        for (uint64_t o = 0; o < tot; o += B) {
+            const size_t k = (size_t)std::min<uint64_t>(B, tot - o);
+            if (peers_[q]) peers_[q](q, data + o, k);
+            ++fan_.peer_batches[q];
+        }
+        fan_.peer_calls[q] = tot;
+        fan_.calls += tot;
+        fan_.batches += fan_.peer_batches[q];
+        ++fan_.peers_hit;
+    }
+    for (auto& pt : parts) sub_free_.insert(sub_free_.end(), pt.freed.begin(), pt.freed.end());
+    // 3. the registry-level handler class, over the whole list
+    if (OnInvalidatedBatch) {
+        const size_t C = std::max<size_t>(1, BatchChunk);
+        for (uint64_t o = 0; o < n; o += C) OnInvalidatedBatch(ids + o, (size_t)std::min<uint64_t>(C, n - o));
+    }
+    // 4. host objects: OnUnregister, then each node's handler set, exactly once
+    for (auto& pt : parts) {
+        for (const uint32_t h : pt.objs) {
+            std::shared_ptr<Computed> c;
+            if (h < n_slots_) {
+                c = current_[h];
+            } else {
+                auto it = detached_.find(h);
+                if (it != detached_.end()) {
+                    c = it->second;
+                    detached_.erase(it);
+                    has_obj_[h] = 0;
+                    fgi_release(g_, 1, &h);
+                }
+            }
+            if (!c || c->fired_) continue;
+            ++fan_.objects;
+            c->fired_ = true;
+            if (h < n_slots_ && OnUnregister) OnUnregister(*c);
+            InvalidatedHandlerSet hs = std::move(c->handlers_);
+            c->handlers_.Clear();
+            hs.Invoke(*c);
+        }
+    }
+    fan_.dispatch_ms = ms_since(t0);
+}
+
+uint32_t ComputedRegistry::AddPeer(PeerSink sink) {
+    peers_.push_back(std::move(sink));
+    return (uint32_t)peers_.size() - 1;
+}
+
+void ComputedRegistry::Subscribe(uint32_t handle, uint32_t peer, uint64_t call_id) {
+    Subscribe(1, &handle, &peer, &call_id);
+}
+
+void ComputedRegistry::Subscribe(size_t n, const uint32_t* handles, const uint32_t* peers, const uint64_t* call_ids) {
+    if (sub_head_.empty()) sub_head_.assign(n_handles_, kNone);   // once, on the first subscription
+    for (size_t i = 0; i < n; ++i) {
+        const uint32_t h = handles[i];
+        if (h >= n_handles_ || peers[i] >= peers_.size()) throw FgiError(FGI_EINVAL, "Subscribe: bad handle or peer");
+        uint32_t e;
+        if (!sub_free_.empty()) {
+            e = sub_free_.back();
+            sub_free_.pop_back();
+        } else {
+            e = (uint32_t)subs_.size();
+            subs_.push_back({});
+        }
+        subs_[e] = Sub{call_ids[i], peers[i], sub_head_[h]};
+        sub_head_[h] = e;
     }
 }
 
@@ -144,7 +333,16 @@ void ComputedRegistry::InvalidateInput(const std::string& input) {
         scope_roots_.push_back(s);
         scope_imm_.push_back(0);
     } else {
-        RunWave({s}, {});
+        RunWave(&s, 1, nullptr);
+    }
+}
+
+void ComputedRegistry::InvalidateSlots(const std::vector<uint32_t>& slots) {
+    if (IsInvalidating()) {
+        scope_roots_.insert(scope_roots_.end(), slots.begin(), slots.end());
+        scope_imm_.insert(scope_imm_.end(), slots.size(), 0);
+    } else {
+        RunWave(slots.data(), slots.size(), nullptr);
     }
 }
 
@@ -154,15 +352,20 @@ void ComputedRegistry::FlushScope() {
     std::vector<uint8_t> imm;
     roots.swap(scope_roots_);
     imm.swap(scope_imm_);
-    RunWave(roots, imm);
+    RunWave(roots.data(), roots.size(), imm.data());
 }
 
 void ComputedRegistry::InvalidateEverything() {
-    std::vector<uint32_t> ids(n_slots_ + detached_.size() + 1);
     uint64_t n = 0;
     last_ = fgi_wave_stats{};
-    Check(fgi_invalidate_all(g_, ids.data(), ids.size(), &n, &last_), "fgi_invalidate_all");
-    Dispatch(ids.data(), n);
+    uint32_t* ids = IdsBuffer(1024);
+    fgi_status s = fgi_invalidate_all(g_, ids, ids_cap_, &n, &last_);
+    if (s == FGI_ECAPACITY) {
+        ids = IdsBuffer(n);
+        s = fgi_last_wave_ids(g_, ids, n, &n);
+    }
+    Check(s, "fgi_invalidate_all");
+    Dispatch(ids, n);
 }
 
 std::pair<uint64_t, uint64_t> ComputedRegistry::Prune() {
@@ -171,6 +374,7 @@ std::pair<uint64_t, uint64_t> ComputedRegistry::Prune() {
     return {ps.old_edges, ps.new_edges};
 }
 
+// ---- Computed --------------------------------------------------------------------------------------
 ConsistencyState Computed::State() const { return (ConsistencyState)(Flags() & FGI_STATE_MASK); }
 
 uint32_t Computed::Flags() const {
@@ -186,17 +390,26 @@ void Computed::Invalidate(bool immediately) {
         reg_->scope_roots_.push_back(handle_);
         reg_->scope_imm_.push_back(immediately ? 1 : 0);
     } else {
-        reg_->RunWave({handle_}, {static_cast<uint8_t>(immediately ? 1 : 0)});
+        const uint8_t imm = immediately ? 1 : 0;
+        reg_->RunWave(&handle_, 1, &imm);
     }
 }
 
-void Computed::OnInvalidated(std::function<void(Computed&)> handler) {
-    if (fired_ || IsInvalidated()) {
-        handler(*this);
+InvalidatedHandler Computed::OnInvalidated(std::function<void(Computed&)> handler) {
+    auto h = std::make_shared<const std::function<void(Computed&)>>(std::move(handler));
+    OnInvalidated(h);
+    return h;
+}
+
+void Computed::OnInvalidated(const InvalidatedHandler& handler) {
+    if (fired_ || IsInvalidated()) {   // Computed.cs:84-97: added after invalidation -> fires now
+        (*handler)(*this);
         return;
     }
-    handlers_.push_back(std::move(handler));
+    handlers_.Add(handler);
 }
+
+void Computed::RemoveOnInvalidated(const InvalidatedHandler& handler) { handlers_.Remove(handler); }
 
 std::vector<std::pair<uint32_t, LTag>> Computed::UsedBy() const {
     uint64_t n = 0;

@@ -6,14 +6,25 @@
 //   Computed.Invalidate() scope, Computed.IsInvalidating()   (Computed.Static.cs:41-47)
 //   IComputed.Invalidate(immediately), ConsistencyState, Version, event Invalidated
 //                                                   (Computed.cs:11-26, 84-105, 162)
+//   InvalidatedHandlerSet                            (Internal/InvalidatedHandlerSet.cs:3-128)
 //   ComputeMethodFunctionBase.Compute -> new Computing node (ComputeMethodFunctionBase.cs:19-27)
 //   IComputedImpl.AddUsed, TrySetOutput, UsedBy      (Computed.cs:141-160, 327-385)
 //   ComputedGraphPruner pass                         (Internal/ComputedGraphPruner.cs:79-94)
+//   RPC replica invalidation: an inbound compute call waits for its computed's invalidation and
+//   then sends `$sys-c.Invalidate(callId)` to its peer (Client/Internal/RpcInboundComputeCall.cs:
+//   53-62, 102-106) — here a subscription (handle -> peer, call id), delivered per peer in batches
+//   after the wave.
 // The C# host this stands in for is sketched in INTEGRATION.md ([LibraryImport] stubs); no .NET
 // SDK exists in this image, so the mirror is C++ and is exercised by host/test_fusion.cpp.
 //
-// Threading: one registry = one dispatcher thread (the ABI is externally synchronised). Invalidated
-// handlers run on that thread after each wave, each exactly once (InvalidatedHandlerSet.cs:100-127).
+// Threading: one registry = one dispatcher thread (the ABI is externally synchronised). After each
+// wave the dispatcher fans the returned ids out (Dispatch):
+//   1. in parallel over contiguous id ranges (ids come in ascending order): per-peer call-id lists
+//      (subscriptions are consumed: a call completes once), and the ids that have host objects;
+//   2. per peer, its call ids in handle order, cut into batches of at most PeerBatch — one sink
+//      call per batch (what one `$sys-c.Invalidate` message per peer per batch would carry);
+//   3. registry-level batch handlers get the whole id list in chunks of BatchChunk;
+//   4. per host object: OnUnregister, then its InvalidatedHandlerSet, each handler exactly once.
 #pragma once
 
 #include <cstdint>
@@ -22,6 +33,7 @@
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/fgi.h"
@@ -31,12 +43,37 @@ namespace fusion {
 using LTag = uint64_t;
 enum class ConsistencyState : uint32_t { Computing = 0, Consistent = 1, Invalidated = 2 };
 
+class Computed;
 class ComputedRegistry;
 
 class FgiError : public std::runtime_error {
    public:
     FgiError(fgi_status s, const std::string& what) : std::runtime_error(what), status(s) {}
     fgi_status status;
+};
+
+// A handler's identity is its shared_ptr (the reference compares delegates).
+using InvalidatedHandler = std::shared_ptr<const std::function<void(Computed&)>>;
+
+// InvalidatedHandlerSet (Internal/InvalidatedHandlerSet.cs:3-128): empty, one handler, a list of up
+// to ListSize, then a hash set. Add of a handler already present is a no-op; Remove keeps the order
+// of the rest; Invoke calls each handler once (list order; set order unspecified, as there).
+class InvalidatedHandlerSet {
+   public:
+    static constexpr size_t ListSize = 5;
+    void Add(const InvalidatedHandler& h);
+    void Remove(const InvalidatedHandler& h);
+    void Clear() {
+        list_.clear();
+        set_.reset();
+    }
+    size_t Size() const { return set_ ? set_->size() : list_.size(); }
+    bool Spilled() const { return (bool)set_; }
+    void Invoke(Computed& c) const;
+
+   private:
+    std::vector<InvalidatedHandler> list_;                         // <= ListSize entries
+    std::unique_ptr<std::unordered_set<InvalidatedHandler>> set_;  // after the list overflows
 };
 
 // One Computed instance (a node). Holds the engine handle: the input's slot while it is the
@@ -53,8 +90,11 @@ class Computed {
     // IComputed.Invalidate(immediately): inside a Computed.Invalidate() scope the node joins the
     // scope's batch; otherwise one wave runs now.
     void Invalidate(bool immediately = false);
-    // event Invalidated: fires once; added after invalidation it fires at once (Computed.cs:84-97)
-    void OnInvalidated(std::function<void(Computed&)> handler);
+    // event Invalidated += / -= (Computed.cs:84-105): fires once; added after invalidation it fires
+    // at once. Returns the handler's identity for RemoveOnInvalidated.
+    InvalidatedHandler OnInvalidated(std::function<void(Computed&)> handler);
+    void OnInvalidated(const InvalidatedHandler& handler);
+    void RemoveOnInvalidated(const InvalidatedHandler& handler);
     std::vector<std::pair<uint32_t, LTag>> UsedBy() const;   // IComputedImpl.UsedBy
     uint32_t UsedCount() const;                               // IComputedImpl.Used.Length
 
@@ -65,7 +105,20 @@ class Computed {
     uint32_t slot_ = 0, handle_ = 0;
     LTag version_ = 0;
     bool fired_ = false;
-    std::vector<std::function<void(Computed&)>> handlers_;
+    InvalidatedHandlerSet handlers_;
+};
+
+// Per-wave fan-out statistics (the last Dispatch).
+struct FanoutStats {
+    uint64_t ids = 0;            // invalidated handles dispatched
+    uint64_t objects = 0;        // of which had host objects (handlers / OnUnregister ran)
+    uint64_t calls = 0;          // peer call ids delivered
+    uint64_t batches = 0;        // peer sink invocations
+    uint32_t peers_hit = 0;      // peers that received at least one batch
+    uint32_t threads = 0;        // threads of the parallel phase
+    double dispatch_ms = 0;      // whole Dispatch
+    double gather_ms = 0;        // parallel phase (subscriptions -> per-peer lists)
+    std::vector<uint64_t> peer_calls, peer_batches;   // per peer id
 };
 
 class ComputedRegistry {
@@ -105,30 +158,63 @@ class ComputedRegistry {
     bool IsInvalidating() const { return scope_depth_ > 0; }
     // `_ = svc.Get(input)` inside a scope: TryUseExisting's Invalidate branch (ComputedExt.cs:29-35)
     void InvalidateInput(const std::string& input);
+    // Slot-level roots (inputs already resolved by the host, e.g. bulk-registered nodes)
+    void InvalidateSlots(const std::vector<uint32_t>& slots);
+
+    // ---- RPC replica fan-out -----------------------------------------------------------------
+    // A peer's sink receives its invalidated call ids, in handle order, PeerBatch at most per call.
+    using PeerSink = std::function<void(uint32_t peer, const uint64_t* call_ids, size_t n)>;
+    uint32_t AddPeer(PeerSink sink);
+    // An inbound compute call of `peer` (call id) now waits for the node `handle`'s invalidation.
+    void Subscribe(uint32_t handle, uint32_t peer, uint64_t call_id);
+    void Subscribe(size_t n, const uint32_t* handles, const uint32_t* peers, const uint64_t* call_ids);
+    size_t PeerBatch = 4096;
+    uint32_t FanoutThreads = 0;   // 0: hardware concurrency, capped at 16
 
     std::function<void(Computed&)> OnRegister, OnUnregister;
+    // registry-level handler class: the wave's invalidated handles, BatchChunk at a time
+    std::function<void(const uint32_t* ids, size_t n)> OnInvalidatedBatch;
+    size_t BatchChunk = 65536;
+
     fgi_graph* Graph() const { return g_; }
     const fgi_wave_stats& LastWave() const { return last_; }
+    const FanoutStats& LastFanout() const { return fan_; }
 
    private:
     friend class Computed;
+    struct Sub {
+        uint64_t call_id;
+        uint32_t peer, next;
+    };
     void Check(fgi_status s, const char* what) const;
     uint32_t SlotOf(const std::string& input, bool create);
-    void RunWave(const std::vector<uint32_t>& roots, const std::vector<uint8_t>& imm);
+    void RunWave(const uint32_t* roots, size_t n, const uint8_t* imm);
+    // the engine's ids of the last call into ids_ (grown without zero-fill, reused across waves)
+    uint32_t* IdsBuffer(uint64_t need);
     void Dispatch(const uint32_t* ids, uint64_t n);
     void FlushScope();
     LTag NextVersion(LTag current);
+    void MoveSubs(uint32_t from, uint32_t to);
 
     fgi_graph* g_ = nullptr;
-    uint32_t n_slots_ = 0;
+    uint32_t n_slots_ = 0, n_handles_ = 0;
     std::unordered_map<std::string, uint32_t> slots_;
     std::vector<std::shared_ptr<Computed>> current_;                 // slot -> newest node
     std::unordered_map<uint32_t, std::shared_ptr<Computed>> detached_;  // detached handle -> node
+    std::vector<uint8_t> has_obj_;                                   // handle -> host object exists
     std::vector<uint32_t> scope_roots_;
     std::vector<uint8_t> scope_imm_;
     int scope_depth_ = 0;
     LTag ltag_ = 0x100000;
     fgi_wave_stats last_{};
+    FanoutStats fan_;
+    std::unique_ptr<uint32_t[]> ids_;
+    uint64_t ids_cap_ = 0;
+    // subscriptions: per handle a singly-linked list in one pool (kNone-terminated), free list
+    std::vector<PeerSink> peers_;
+    std::vector<uint32_t> sub_head_;
+    std::vector<Sub> subs_;
+    std::vector<uint32_t> sub_free_;
 };
 
 }  // namespace fusion

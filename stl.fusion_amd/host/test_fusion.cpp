@@ -2,9 +2,12 @@
 // mirror (fusion.hpp) over the fgi engine. Needs a GPU; run by tests/test_gpu_host.py.
 // Each case names the reference test it restates; tests/test_oracle_scenarios.py holds the same
 // cases against the CPU oracle.
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
+#include <vector>
 
 #include "fusion.hpp"
 
@@ -202,7 +205,119 @@ static void prune() {
     CHECK(pr.first == 2 && pr.second == 1 && a->UsedBy().size() == 1);
 }
 
-int main() {
+// TodoApp-style replica fan-out at BASELINE.json configs[4]'s size (DESIGN.md §Host fan-out):
+// 10,000 hubs x 1,000 leaves = 10M leaves (1% with an invalidation delay), every leaf computed
+// held by one RPC client (peer = leaf % 100, call id = leaf), as RpcInboundComputeCall keeps the
+// computed it served (Client/Internal/RpcInboundComputeCall.cs:53-62). One scope invalidates all
+// hubs: the wave invalidates 10k hubs + 9.9M undelayed leaves; every undelayed leaf's call id
+// must reach its peer exactly once, in handle order, in batches of PeerBatch. Runs the dispatch
+// with 16 threads and with 1 and prints one JSON line.
+static void fanout_10m() {
+    const uint32_t H = 10000, Lh = 1000, P = 100;
+    const uint32_t N = H + H * Lh;
+    ComputedRegistry r(N, 64);
+    std::vector<uint32_t> slot(N), flags(N);
+    std::vector<uint64_t> ver(N);
+    for (uint32_t s = 0; s < N; ++s) {
+        slot[s] = s;
+        uint64_t x = (uint64_t)s * 0x9E3779B97F4A7C15ull + 0x5EED00E0;
+        x ^= x >> 31;
+        ver[s] = ((x * 0xBF58476D1CE4E5B9ull) & ((1ull << 54) - 1)) | 1ull;
+        const bool delayed = s >= H && (x % 100) == 0;
+        flags[s] = FGI_CONSISTENT | (delayed ? 16u : 0u);
+    }
+    if (fgi_register_nodes(r.Graph(), N, slot.data(), ver.data(), flags.data()) != FGI_OK) throw FgiError(FGI_EDEVICE, "register");
+    std::vector<uint32_t> hub(N - H), leaf(N - H);
+    std::vector<uint64_t> tag(N - H);
+    uint64_t undelayed = 0;
+    for (uint32_t k = 0; k < N - H; ++k) {
+        leaf[k] = H + k;
+        hub[k] = k / Lh;
+        tag[k] = ver[H + k];
+        undelayed += (flags[H + k] & 16u) ? 0 : 1;
+    }
+    if (fgi_load_edges(r.Graph(), N - H, hub.data(), leaf.data(), tag.data()) != FGI_OK) throw FgiError(FGI_EDEVICE, "load");
+    if (fgi_snapshot(r.Graph()) != FGI_OK) throw FgiError(FGI_EDEVICE, "snapshot");
+    // peers: count calls and check order per peer
+    std::vector<uint64_t> got(P, 0), last(P, 0), sum(P, 0);
+    uint64_t order_bad = 0;
+    for (uint32_t q = 0; q < P; ++q)
+        r.AddPeer([&](uint32_t peer, const uint64_t* ids, size_t n) {
+            for (size_t i = 0; i < n; ++i) {
+                order_bad += (ids[i] <= last[peer] && got[peer]) ? 1 : 0;
+                last[peer] = ids[i];
+                sum[peer] += ids[i];
+            }
+            got[peer] += n;
+        });
+    std::vector<uint32_t> roots(H);
+    for (uint32_t h = 0; h < H; ++h) roots[h] = h;
+    std::vector<uint32_t> sh(N - H), sp(N - H);
+    std::vector<uint64_t> sc(N - H);
+    for (uint32_t k = 0; k < N - H; ++k) {
+        sh[k] = H + k;
+        sp[k] = (H + k) % P;
+        sc[k] = H + k;
+    }
+    std::string runs;
+    for (uint32_t threads : {16u, 1u}) {
+        std::fill(got.begin(), got.end(), 0);
+        std::fill(sum.begin(), sum.end(), 0);
+        std::fill(last.begin(), last.end(), 0);
+        order_bad = 0;
+        const auto t0 = std::chrono::steady_clock::now();
+        r.Subscribe(sh.size(), sh.data(), sp.data(), sc.data());
+        const double sub_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        r.FanoutThreads = threads;
+        const auto t1 = std::chrono::steady_clock::now();
+        r.InvalidateSlots(roots);
+        const double call_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+        const FanoutStats& f = r.LastFanout();
+        const fgi_wave_stats& w = r.LastWave();
+        CHECK(w.v_inv == H + undelayed);
+        CHECK(f.ids == w.v_inv && f.calls == undelayed && order_bad == 0);
+        uint64_t min_b = ~0ull, max_b = 0, tot = 0;
+        bool sums_ok = true;
+        for (uint32_t q = 0; q < P; ++q) {
+            min_b = std::min(min_b, f.peer_batches[q]);
+            max_b = std::max(max_b, f.peer_batches[q]);
+            tot += got[q];
+            CHECK(f.peer_calls[q] == got[q]);
+            CHECK(f.peer_batches[q] == (got[q] + r.PeerBatch - 1) / r.PeerBatch);
+        }
+        // expected per-peer sums of the undelayed leaves' call ids
+        std::vector<uint64_t> want(P, 0);
+        for (uint32_t k = 0; k < N - H; ++k)
+            if (!(flags[H + k] & 16u)) want[(H + k) % P] += H + k;
+        for (uint32_t q = 0; q < P; ++q) sums_ok &= want[q] == sum[q];
+        CHECK(tot == undelayed && sums_ok);
+        char line[768];
+        std::snprintf(line, sizeof line,
+                      "%s{\"threads\": %u, \"v_inv\": %llu, \"wave_kernel_ms\": %.3f, \"wave_call_ms\": %.3f, "
+                      "\"invalidate_call_ms\": %.3f, \"dispatch_ms\": %.3f, \"gather_ms\": %.3f, \"subscribe_ms\": %.1f, "
+                      "\"calls\": %llu, \"batches\": %llu, \"peers\": %u, \"batches_per_peer\": [%llu, %llu], "
+                      "\"peer_batch\": %zu}",
+                      runs.empty() ? "" : ", ", f.threads, (unsigned long long)w.v_inv, w.kernel_ms, w.total_ms, call_ms,
+                      f.dispatch_ms, f.gather_ms, sub_ms, (unsigned long long)f.calls, (unsigned long long)f.batches,
+                      f.peers_hit, (unsigned long long)min_b, (unsigned long long)max_b, r.PeerBatch);
+        runs += line;
+        if (fgi_restore(r.Graph()) != FGI_OK) throw FgiError(FGI_EDEVICE, "restore");
+    }
+    std::printf("FANOUT {\"workload\": \"10000 hubs x 1000 leaves, 1%% delayed, 100 peers, all hubs in one scope\", "
+                "\"runs\": [%s]}\n", runs.c_str());
+}
+
+int main(int argc, char** argv) {
+    if (argc > 1 && std::strcmp(argv[1], "--fanout") == 0) {
+        try {
+            fanout_10m();
+        } catch (const FgiError& e) {
+            std::fprintf(stderr, "FgiError %d: %s\n", (int)e.status, e.what());
+            return 2;
+        }
+        std::printf("%d/%d checks passed\n", g_checks - g_fail, g_checks);
+        return g_fail ? 1 : 0;
+    }
     try {
         counter_basic();
         counter_long_wait();

@@ -3,6 +3,7 @@
 The binary links the in-tree engine (stl.fusion_amd/lib/libfgi.so) through the host mirror
 (host/build/libfusion.so); both are built by __graft_entry__.build() / `make -C stl.fusion_amd/host`.
 """
+import json
 import os
 import subprocess
 
@@ -21,9 +22,40 @@ def test_host_mirror_builds_and_links():
     assert "libfgi.so" in out and "libfusion.so" in out and "not found" not in out
 
 
+def test_invalidated_handler_set():
+    """CPU: InvalidatedHandlerSetTest (Internal/InvalidatedHandlerSetTest.cs:10-48) over the
+    mirror's InvalidatedHandlerSet (host/test_handlers.cpp; no engine call)."""
+    subprocess.run(["make", "-s", "-C", HOST], check=True, timeout=300)
+    r = subprocess.run([os.path.join(HOST, "build", "test_handlers")], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "checks passed" in r.stdout
+
+
 @pytest.mark.gpu
 def test_host_mirror_scenarios(gpu_available):
     subprocess.run(["make", "-s", "-C", HOST], check=True, timeout=300)
     r = subprocess.run([BIN], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "checks passed" in r.stdout
+
+
+@pytest.mark.gpu
+def test_host_fanout_10m_leaves(gpu_available):
+    """BASELINE.json configs[4]'s replica fan-out through the mirror: one wave over all 10,000 hubs
+    invalidates 9.9M leaves; each undelayed leaf's call id reaches its peer once, in handle order,
+    in PeerBatch-sized batches (host/test_fusion.cpp fanout_10m). The JSON line (dispatch time with
+    16 threads and with 1, per-peer batch counts) is kept in $FGI_FANOUT_OUT when set."""
+    subprocess.run(["make", "-s", "-C", HOST], check=True, timeout=300)
+    r = subprocess.run([BIN, "--fanout"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = [x for x in r.stdout.splitlines() if x.startswith("FANOUT ")]
+    assert line, r.stdout
+    rec = json.loads(line[0][len("FANOUT "):])
+    for run in rec["runs"]:
+        assert 9_800_000 < run["calls"] < 10_000_000   # exact counts are checked in C++
+        assert run["peers"] == 100
+    out = os.environ.get("FGI_FANOUT_OUT")
+    if out:
+        with open(out, "w") as f:
+            json.dump(rec, f, indent=1)
+    print(json.dumps(rec))

@@ -84,6 +84,254 @@ def test_counter_service_concurrent_wait(W=World):
     assert w.o.used_count(dh2) == 2
 
 
+def test_counter_service_concurrent_wait_error(W=World):
+    """CounterServiceTest.ConcurrentWaitTest case 3 (:87-97): the first dependency ("x fail")
+    completes with an error, so GetFirstNonZero returns (with that error) before "y wait" completes:
+    the error result is a recorded dependency, the late one is dropped (Used.Length == 1), and
+    invalidating the failing dependency invalidates the dependant like any other output."""
+    w = W()
+    xf = w.compute(4)                       # Get("x fail"): an error output is still an output
+    yh, _ = w.begin(5)                      # Get("y wait"): still computing
+    dh, _ = w.begin(6)                      # GetFirstNonZero("x fail", "y wait")
+    assert w.o.add_used(dh, xf) == ADDED
+    assert w.o.set_output(dh) == 1          # completes with x fail's error
+    assert w.o.set_output(yh) == 1
+    assert w.o.add_used(dh, yh) == DROPPED
+    assert w.o.used_count(dh) == 1
+    assert w.invalidate(4) == [4, 6]        # Set("x fail", 0) invalidates Get and the dependant
+    assert w.state(5) == K
+
+
+def test_anonymous_computed_basic(W=World):
+    """AnonymousComputedTest.BasicTest (AnonymousComputedTest.cs:9-36): an AnonymousComputedSource
+    has no computed until first used; Use() computes once (value 1) and keeps returning the cached
+    node while it is Consistent; ci.Computed.Invalidate() makes the next Use() compute value 2."""
+    w = W()
+    made = []
+    val = {}
+
+    def use():
+        h = w.o.current(0)
+        if h == O.NONE:
+            h = w.compute(0)
+            made.append(h)
+            val[h] = len(made)
+        return val[h]
+
+    assert w.o.last(0) == O.NONE                     # IsComputed == false
+    assert use() == 1 and use() == 1 and len(made) == 1
+    h = w.o.last(0)
+    assert w.state(0) == K
+    w.o.clear_log()
+    w.o.invalidate_nodes([h], [0])                   # ci.Computed.Invalidate()
+    assert w.o.inv_log().tolist() == [0] and w.state(0) == I
+    assert use() == 2 and use() == 2 and len(made) == 2
+
+
+def test_anonymous_computed_auto_invalidation(W=World):
+    """AnonymousComputedTest.ComputedOptionsTest (:38-60): AutoInvalidationDelay = 0.2 s. Each new
+    output schedules Invalidate(true) on the timer set (StartAutoInvalidation, Computed.cs:235-246;
+    ComputedExt.cs:10-24; Timeouts.cs:22-28); a firing invalidates the node (and anything that used
+    it) and the next Use() computes a new value. Changes().Take(3) sees three firings, after which
+    Use() returns a value > 3. A timer that fires after the node was already invalidated is a no-op."""
+    w = W()
+    val = {}
+    n = 0
+
+    def use():
+        nonlocal n
+        h = w.o.current(0)
+        if h == O.NONE:
+            n += 1
+            h = w.compute(0)
+            val[h] = n
+        return val[h]
+
+    assert use() == 1
+    reader = w.compute(1, deps=[0])                  # a computed observing the source
+    for k in range(3):                               # three timer rounds
+        h = w.o.last(0)
+        w.o.clear_log()
+        w.o.invalidate_nodes([h], [1])               # the auto-invalidation timer fires
+        assert sorted(w.o.inv_log().tolist()) == ([0, 1] if k == 0 else [0])
+        w.o.clear_log()
+        w.o.invalidate_nodes([h], [1])               # a second firing: already invalidated
+        assert w.o.inv_log().tolist() == []
+        assert use() == k + 2
+    assert use() > 3
+    assert w.o.node_info(reader)[2] == I
+
+
+def test_computed_concurrency_counter_sum(W=World, iterations=120):
+    """ConcurrencyTest.ComputedConcurrencyTest (ConcurrencyTest.cs:143-223) over CounterSumService
+    (tests/Stl.Fusion.Tests/Services/CounterSumService.cs): Sum(0, 1) = Get0(0) + Get1(1), where
+    Get1 has InvalidationDelay = 0.2 s. Readers — Computed.Capture(Sum) and an
+    AnonymousComputedSource over Sum — follow the changes while a mutator sets one counter
+    `iterations` times; the update delayer (ZeroUnsafe / Instant / 0.1 s) sets how often the readers
+    catch up, and every `delay_frequency` mutations the delay timers get to fire. After the final
+    wait (500 ms > the 0.2 s delay) every reader sees the registry's Sum node, with value
+    2 * iterations.
+
+    Slot model: counters c0, c1 are MutableStates (a set = invalidate the state's node + a new
+    node); Get0(0), Get1(1), Sum and the reader sources are compute methods. Along the way:
+    a Consistent Get0 always holds the current counter value; a Consistent Get1 without
+    DelayStarted does too; a counter change reaches Get1 only as DelayStarted (Computed.cs:186-198),
+    so Sum stays Consistent with the old value until the timer's Invalidate(true)."""
+    C0, C1, G0, G1, S = 0, 1, 2, 3, 4
+    R = 4                                         # HardwareInfo.GetProcessorCountFactor() readers
+    SRC = list(range(5, 5 + R))
+    deps = {G0: [C0], G1: [C1], S: [G0, G1], **{r: [S] for r in SRC}}
+    for delayer, readers_every in (("zero", 1), ("instant", 2), ("0.1s", 7)):
+        for delay_frequency in (50, 1000):
+            w = W(32)
+            val, cv = {}, [0, 0]
+            pending = set()
+            fired = [0]
+
+            def set_counter(i, v):
+                if w.o.last(i) != O.NONE:
+                    w.invalidate(i)
+                h = w.compute(i)
+                val[h] = v
+                cv[i] = v
+                track_timers()
+
+            def track_timers():
+                h = w.o.last(G1)
+                if h != O.NONE:
+                    st = w.o.node_info(h)[2]
+                    if st & 3 == K and st & DS:
+                        pending.add(h)
+
+            def fire_timers():
+                for h in sorted(pending):
+                    w.o.invalidate_nodes([h], [1])   # Timeouts: t.Invalidate(true)
+                    fired[0] += 1
+                pending.clear()
+
+            def use(slot):
+                h = w.o.current(slot)
+                if h != O.NONE and w.o.node_info(h)[2] & 3 == K:
+                    return val[h]
+                if slot in (C0, C1):
+                    return val[w.o.last(slot)]
+                vals = [use(d) for d in deps[slot]]
+                h = w.compute(slot, deps=deps[slot], delay=(slot == G1))
+                val[h] = vals[0] if slot in (G0, G1) or slot in SRC else vals[0] + vals[1]
+                return val[h]
+
+            def check_invariants():
+                for slot, ci in ((G0, 0), (G1, 1)):
+                    h = w.o.last(slot)
+                    st = w.o.node_info(h)[2]
+                    if st & 3 == K and not (st & DS):
+                        assert val[h] == cv[ci], (delayer, slot, val[h], cv[ci])
+                hs = w.o.last(S)
+                if w.o.node_info(hs)[2] & 3 == K:
+                    assert val[hs] in (cv[0] + cv[1], val[w.o.last(G0)] + val[w.o.last(G1)])
+
+            set_counter(C0, 0)
+            set_counter(C1, 0)
+            for r in SRC:
+                use(r)
+            for used in (0, 1):
+                for i in (0, 1):
+                    set_counter(i, iterations)
+                set_counter(used, 0)
+                for k in range(1, iterations + 1):          # Mutator
+                    set_counter(used, k)
+                    if k % readers_every == 0:
+                        for r in SRC:
+                            use(r)
+                        check_invariants()
+                    if k % delay_frequency == 0:            # await Task.Delay(1)
+                        fire_timers()
+                assert cv[used] == iterations
+                fire_timers()                               # await Task.Delay(500)
+                expected = 2 * iterations
+                assert use(S) == expected, delayer
+                s_node = w.o.current(S)
+                for r in SRC:                               # every reader: same Sum node, value
+                    assert use(r) == expected
+                    assert w.o.current(S) == s_node
+                check_invariants()
+            assert fired[0] >= 1, delayer                   # Get1's delay was exercised
+
+
+def test_invalidated_handler_set():
+    """InvalidatedHandlerSetTest (Internal/InvalidatedHandlerSetTest.cs:10-48) over the fan-out
+    model the host mirror implements (InvalidatedHandlerSet.cs: a single item, then a 5-slot
+    array, then a hash set; Add is idempotent per handler; Remove keeps the order of the rest):
+    for sizes 0..9 and removal probabilities (k + 1) / 200, Invoke calls every remaining handler
+    exactly once and never a removed one."""
+    rng = np.random.default_rng(0x1A5E7)
+    for iteration in range(200):
+        p = (iteration + 1.0) / 200
+        for size in range(10):
+            used = []
+            hs = HandlerSet()
+            handlers = [(lambda i: (lambda: used.append(i)))(i) for i in range(size)]
+            for h in handlers:
+                hs.add(h)
+                hs.add(h)                                   # idempotent
+            hs.invoke()
+            assert sorted(used) == list(range(size))
+            removed = {i for i in range(size) if rng.random() < p}
+            for i in removed:
+                hs.remove(handlers[i])
+            used.clear()
+            hs.invoke()
+            assert len(used) == len(set(used)) == size - len(removed)
+            assert not (set(used) & removed)
+
+
+class HandlerSet:
+    """InvalidatedHandlerSet (Internal/InvalidatedHandlerSet.cs:3-128) restated: storage is None,
+    one handler, a list of up to 5, or a set (insertion-ordered here; the reference's HashSet order
+    is unspecified and nothing depends on it)."""
+    LIST = 5
+
+    def __init__(self):
+        self.st = None
+
+    def add(self, h):
+        st = self.st
+        if st is None:
+            self.st = h
+        elif callable(st):
+            if st is not h:
+                self.st = [st, h]
+        elif isinstance(st, list):
+            if h in st:
+                return
+            if len(st) < self.LIST:
+                st.append(h)
+            else:
+                self.st = dict.fromkeys(st + [h])
+        else:
+            st[h] = None
+
+    def remove(self, h):
+        st = self.st
+        if st is None:
+            return
+        if callable(st):
+            if st is h:
+                self.st = None
+        elif isinstance(st, list):
+            if h in st:
+                st.remove(h)
+        else:
+            st.pop(h, None)
+
+    def invoke(self):
+        st = self.st
+        if st is None:
+            return
+        for h in ([st] if callable(st) else list(st)):
+            h()
+
+
 def test_simplest_provider_cascade_and_new_version(W=World):
     """SimplestProviderTest.BasicTest (SimplestProviderTest.cs:9-32) + EdgeCaseServiceTest
     (EdgeCaseServiceTest.cs:52): SetValue invalidates GetValue, which cascades to GetCharCount;
