@@ -190,6 +190,50 @@ fgi_status fgi_last_wave_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint
 fgi_status fgi_invalidate_all(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n,
                               fgi_wave_stats* stats);
 
+/* ---- streaming batches (BASELINE.json configs[4]) ------------------------------- */
+/* One step of a batch: the arguments of the matching single call. */
+#define FGI_STEP_INVALIDATE 1     /* fgi_invalidate: handles, flags = immediately (nullable) */
+#define FGI_STEP_BEGIN_COMPUTE 2  /* fgi_begin_compute: handles = slots, version, flags = has_delay (nullable) */
+#define FGI_STEP_ADD_USED 3       /* fgi_add_used: handles = dependants, used */
+#define FGI_STEP_SET_OUTPUT 4     /* fgi_set_output: handles */
+typedef struct fgi_step {
+    uint32_t kind;
+    uint32_t n;
+    const uint32_t* handles;
+    const uint32_t* used;
+    const uint64_t* version;
+    const uint8_t* flags;
+    void* out;   /* nullable: BEGIN_COMPUTE uint32_t detached[n]; ADD_USED uint32_t result[n];
+                    SET_OUTPUT uint8_t set[n] */
+} fgi_step;
+
+typedef struct fgi_batch_stats {
+    uint64_t waves;        /* cascade waves run (steps with a non-empty root set count; empty ones too) */
+    uint64_t levels;       /* BFS levels with a non-empty frontier, summed over the waves */
+    uint64_t v_inv;        /* Consistent -> Invalidated transitions, summed over the waves */
+    uint64_t e_trav;
+    uint64_t e_match;
+    uint64_t n_flagged;
+    double kernel_ms;      /* device time from the batch's first launch to its last (HIP events) */
+    double wave_ms;        /* of which the waves' cooperative launches (HIP events) */
+    double total_ms;       /* wall time of the call */
+    uint32_t host_syncs;   /* times the call waited for the device */
+    uint32_t pad;
+} fgi_batch_stats;
+
+/* A host layer's batch of compute-method work in one call: the steps are applied in order, each
+ * exactly as the matching single call would apply it (fgi_invalidate, fgi_begin_compute — its
+ * displacement cascade included —, fgi_add_used, fgi_set_output — its InvalidateOnSetOutput cascade
+ * included; Computed.cs:141-230, 347-385, ComputedRegistry.cs:83-97), but every count stays on the
+ * device and each cascade runs as one cooperative launch: the call uploads the batch once and waits
+ * for the device once (once more if an add_used step must grow the edge pool, and once more to copy
+ * out_ids). out_ids gets the handles invalidated by the batch's cascades, cascade after cascade
+ * (each in ascending order); FGI_ECAPACITY with *out_n = the count if cap is too small. If the
+ * batch runs out of detached handles, FGI_ECAPACITY names the step: the steps before it are
+ * applied, it and the later ones are not. */
+fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, uint32_t* out_ids, uint64_t cap,
+                         uint64_t* out_n, fgi_batch_stats* stats);
+
 /* ---- graph maintenance ---------------------------------------------------------------------- */
 /* One ComputedGraphPruner pass (Internal/ComputedGraphPruner.cs:79-94): PruneUsedBy on every
  * registered Consistent node (Computed.cs:400-419) — keep (slot, tag) iff the slot's current node

@@ -87,6 +87,7 @@ constexpr int kDoneStride = 16;         // 128 B apart
 constexpr uint32_t kFinalBlocks = 1024; // grid of the final collect (invalidated bitmap -> list)
 constexpr uint32_t kHot = 65536;        // hot list heads (pull probes through an 8 KB snapshot)
 constexpr uint32_t kHotFlag = 0x80000000u;
+constexpr int kAccCount = 8;            // batch accumulators (fgi_run_batch; run_wave_coop's acc)
 
 // Per-level counters. The producers of level L's frontier (roots, push emits, received targets)
 // reserve list space with ONE packed 64-bit atomic on `ft` (frontier entries << 32 | edges): the
@@ -102,12 +103,6 @@ struct LevelCtr {
     unsigned long long mult;    // push: fine chunks per expand chunk
     unsigned long long npull;   // pull levels of the wave before this one (which candidate list to read)
     unsigned long long pad1;
-};
-
-// Per pull tile (kPullTile slots): winners, expandable winners (|row| > 0), their row lengths.
-struct PullTile {
-    uint32_t w, e;
-    unsigned long long len;
 };
 
 struct WaveCtr {
@@ -201,14 +196,11 @@ struct fgi_graph {
     uint32_t* cls_bm = nullptr;
     bool cls_valid = false;
     bool words_dirty = true;           // node words changed since the snapshot
-    fgi::PullTile* tiles = nullptr;    // per pull tile counts of the last pull level
-    uint64_t tiles_cap = 0;
     // Invalidated bitmap: bit h set = node h was invalidated by this wave. It is the frontier of a
     // pull level: every node invalidated before the previous level already had all its dependants
     // visited, so "an invalidated parent" and "a parent in the previous level's frontier" select
     // the same unvisited slots. Multi-GPU: all-gathered into front_global.
     uint32_t* inv_bm = nullptr;
-    uint32_t* lw_bm = nullptr;         // the last pull level's winners (collected if the next level pushes)
     uint64_t bm_words = 0;             // words per bitmap (even: pull levels store 64-bit words)
 
     // dependency-list cache for pull levels: for slot d, the handles whose `_usedBy` row holds
@@ -229,6 +221,7 @@ struct fgi_graph {
     // One 16-byte entry per candidate: {slot, row length | more << 31, head 0, head 1}.
     uint4* cand = nullptr;
     uint32_t* cand_seg = nullptr;      // [pull grid + 1]
+    uint32_t* wl = nullptr;            // [n_slots] a pull level's expandable winners, per block at cand_seg
     // Hot heads: the (at most kHot) handles that head the most lists get a rank; candidate entries
     // name them as kHotFlag | rank, and a pull level probes them in hot_bm, a snapshot of their
     // invalidated bits taken before the level (8 KB: L1-resident) instead of the whole bitmap.
@@ -268,6 +261,12 @@ struct fgi_graph {
 
     // timing
     std::vector<hipEvent_t> ev;        // pairs around expand launches
+    // streaming batches (fgi_run_batch): pinned host staging + its device copy, the ids output
+    char* bst_h = nullptr;
+    char* bst_d = nullptr;
+    size_t bst_cap = 0;
+    uint32_t* bout = nullptr;
+    uint64_t bout_cap = 0;
     hipEvent_t ev_w0 = nullptr, ev_w1 = nullptr;
 
     // multi-GPU
@@ -314,6 +313,13 @@ inline void note_words(fgi_graph* g) {
 // Apply the visit bitmap to the node words and clear it (wave.hip). Every entry point that reads or
 // mutates node words outside a wave calls it first.
 fgi_status fold(fgi_graph* g);
+// A push-only wave in one cooperative launch, without host synchronisation (streaming batches):
+// device-resident roots (n_max, or *n_dev of them), ids appended at out[*out_n ..), totals added to
+// acc[0..6] (waves, levels, invalidated, E_trav, E_match, flagged, frontier entries); nothing
+// happens if *abort (nullable) is set when the wave starts.
+fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev, const uint8_t* imm_dev,
+                         const unsigned long long* n_dev, uint32_t* out, unsigned long long* out_n,
+                         unsigned long long* acc, const unsigned long long* abort);
 // Rebuild the expandable-class bitmap if node words changed (wave.hip).
 fgi_status ensure_cls(fgi_graph* g);
 // Pull tiles of a level over n slots with `grid` blocks.

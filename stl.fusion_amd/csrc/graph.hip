@@ -237,10 +237,8 @@ __global__ void k_gather_words(uint32_t n, const uint32_t* __restrict__ h, const
 // ---- begin_compute ---------------------------------------------------------------------------
 // class: 0 nothing current, 1 displacement root (Consistent, no delay), 2 detach (Computing, or
 // Consistent with a delay: ComputedRegistry.cs:91-96 invalidates it, which only flags it).
-__global__ void k_bc_classify(uint32_t n, const uint32_t* __restrict__ slot, const unsigned long long* node,
-                              uint8_t* cls, uint32_t* roots, unsigned long long* cnt /*[0]=roots,[1]=detach*/) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+__device__ __forceinline__ void bc_classify(uint32_t i, const uint32_t* __restrict__ slot, const unsigned long long* node,
+                                            uint8_t* cls, uint32_t* roots, unsigned long long* cnt) {
     const unsigned long long w = node[slot[i]];
     uint8_t c = 0;
     if (word_is_current(w)) {
@@ -252,13 +250,44 @@ __global__ void k_bc_classify(uint32_t n, const uint32_t* __restrict__ slot, con
     if (c == 2) atomicAdd(&cnt[1], 1ull);
 }
 
-__global__ void k_bc_install(uint32_t n, const uint32_t* __restrict__ slot, const uint64_t* __restrict__ version,
-                             const uint8_t* __restrict__ has_delay, const uint8_t* __restrict__ cls,
-                             const uint32_t* __restrict__ free_h, unsigned long long* cursor, uint32_t n_slots,
-                             unsigned long long* node, uint64_t* row_off, uint32_t* row_len, uint32_t* row_cap,
-                             uint32_t* used_cnt, uint32_t* home, uint32_t* out_det) {
+__global__ void k_bc_classify(uint32_t n, const uint32_t* __restrict__ slot, const unsigned long long* node,
+                              uint8_t* cls, uint32_t* roots, unsigned long long* cnt /*[0]=roots,[1]=detach*/) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    if (i < n) bc_classify(i, slot, node, cls, roots, cnt);
+}
+
+struct InstallArgs {
+    const uint32_t* slot;
+    const uint64_t* version;
+    const uint8_t* has_delay;
+    const uint8_t* cls;
+    const uint32_t* free_h;
+    unsigned long long* cursor;
+    uint32_t n_slots;
+    unsigned long long* node;
+    uint64_t* row_off;
+    uint32_t* row_len;
+    uint32_t* row_cap;
+    uint32_t* used_cnt;
+    uint32_t* home;
+    uint32_t* out_det;
+};
+
+__device__ __forceinline__ void bc_install(uint32_t i, const InstallArgs& a) {
+    const uint32_t* slot = a.slot;
+    const uint64_t* version = a.version;
+    const uint8_t* has_delay = a.has_delay;
+    const uint8_t* cls = a.cls;
+    const uint32_t* free_h = a.free_h;
+    unsigned long long* cursor = a.cursor;
+    const uint32_t n_slots = a.n_slots;
+    unsigned long long* node = a.node;
+    uint64_t* row_off = a.row_off;
+    uint32_t* row_len = a.row_len;
+    uint32_t* row_cap = a.row_cap;
+    uint32_t* used_cnt = a.used_cnt;
+    uint32_t* home = a.home;
+    uint32_t* out_det = a.out_det;
     const uint32_t s = slot[i];
     uint32_t det = FGI_NONE;
     if (cls[i] == 2) {
@@ -283,20 +312,54 @@ __global__ void k_bc_install(uint32_t n, const uint32_t* __restrict__ slot, cons
     out_det[i] = det;
 }
 
+__global__ void k_bc_install(uint32_t n, InstallArgs a) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) bc_install(i, a);
+}
+
 // ---- add_used --------------------------------------------------------------------------------
 struct Cand {
     uint32_t used, dep_handle, dep_slot, pad;
     uint64_t tag;
 };
 
-__global__ void k_au_classify(uint32_t n, const uint32_t* __restrict__ dep, const uint32_t* __restrict__ used,
-                              uint32_t n_slots, const uint32_t* __restrict__ home, unsigned long long* node,
-                              const uint64_t* __restrict__ row_off, const uint32_t* __restrict__ row_len,
-                              const uint32_t* __restrict__ used_cnt, const uint32_t* __restrict__ pool_col,
-                              const uint64_t* __restrict__ pool_tag, unsigned long long* hset, uint64_t hmask,
-                              uint32_t* result, Cand* cand, unsigned long long* ncand) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+struct AuArgs {
+    const uint32_t* dep;
+    const uint32_t* used;
+    uint32_t n_slots;
+    const uint32_t* home;
+    unsigned long long* node;
+    uint64_t* row_off;
+    uint32_t* row_len;
+    uint32_t* row_cap;
+    uint32_t* used_cnt;
+    uint32_t* pool_col;
+    uint64_t* pool_tag;
+    unsigned long long* hset;
+    uint64_t hmask;
+    uint32_t* result;
+    Cand* cand;
+    uint32_t* pend_pos;
+    uint32_t* ovf_rows;
+    unsigned long long* cnt;   // [0] candidates [1] pending [2] overflow rows [3] entries the overflow rows need
+};
+
+__device__ __forceinline__ void au_classify(uint32_t i, const AuArgs& a) {
+    const uint32_t* dep = a.dep;
+    const uint32_t* used = a.used;
+    const uint32_t n_slots = a.n_slots;
+    const uint32_t* home = a.home;
+    unsigned long long* node = a.node;
+    const uint64_t* row_off = a.row_off;
+    const uint32_t* row_len = a.row_len;
+    const uint32_t* used_cnt = a.used_cnt;
+    const uint32_t* pool_col = a.pool_col;
+    const uint64_t* pool_tag = a.pool_tag;
+    unsigned long long* hset = a.hset;
+    const uint64_t hmask = a.hmask;
+    uint32_t* result = a.result;
+    Cand* cand = a.cand;
+    unsigned long long* ncand = a.cnt;
     const uint32_t d = dep[i], u = used[i];
     const unsigned long long wd = node[d];
     if ((wd & kVMask) == 0 || word_state(wd) != FGI_COMPUTING) {   // Computed.cs:351-364
@@ -336,13 +399,22 @@ __global__ void k_au_classify(uint32_t n, const uint32_t* __restrict__ dep, cons
     cand[c] = Cand{u, d, ds, 0, tag};
 }
 
-__global__ void k_au_reserve(uint64_t nc, const Cand* __restrict__ cand, const uint64_t* __restrict__ row_off,
-                             uint32_t* row_len, const uint32_t* __restrict__ row_cap, uint32_t* used_cnt,
-                             uint32_t* pool_col, uint64_t* pool_tag, uint32_t* pend_pos, uint32_t* ovf_rows,
-                             unsigned long long* cnt /*[0] pending, [1] overflow rows*/) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nc) return;
-    const Cand c = cand[i];
+__global__ void k_au_classify(uint32_t n, AuArgs a) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) au_classify(i, a);
+}
+
+__device__ __forceinline__ void au_reserve(uint64_t i, const AuArgs& a) {
+    const uint64_t* row_off = a.row_off;
+    uint32_t* row_len = a.row_len;
+    const uint32_t* row_cap = a.row_cap;
+    uint32_t* used_cnt = a.used_cnt;
+    uint32_t* pool_col = a.pool_col;
+    uint64_t* pool_tag = a.pool_tag;
+    uint32_t* pend_pos = a.pend_pos;
+    uint32_t* ovf_rows = a.ovf_rows;
+    unsigned long long* cnt = a.cnt + 1;
+    const Cand c = a.cand[i];
     const uint32_t pos = atomicAdd(&row_len[c.used], 1u);
     const uint32_t cap = row_cap[c.used];
     atomicAdd(&used_cnt[c.dep_handle], 1u);                          // dependant._used.Add (365-366)
@@ -357,6 +429,11 @@ __global__ void k_au_reserve(uint64_t nc, const Cand* __restrict__ cand, const u
     }
 }
 
+__global__ void k_au_reserve(uint64_t nc, AuArgs a) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nc) au_reserve(i, a);
+}
+
 __device__ __forceinline__ uint32_t grow_cap(uint32_t need) {
     const uint64_t c = (uint64_t)need + (need >> 1);
     return (uint32_t)(c < 4 ? 4 : (c > 0xFFFFFFF0ull ? 0xFFFFFFF0ull : c));
@@ -369,12 +446,10 @@ __global__ void k_au_size(uint64_t no, const uint32_t* __restrict__ ovf_rows, co
 }
 
 // one wave per overflowing row: allocate a larger run at the pool top and move the old entries
-__global__ void k_au_relocate(uint64_t no, const uint32_t* __restrict__ ovf_rows, uint64_t* row_off,
-                              const uint32_t* __restrict__ row_len, uint32_t* row_cap, uint32_t* pool_col,
-                              uint64_t* pool_tag, unsigned long long* top) {
-    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+__device__ __forceinline__ void au_relocate_row(uint64_t wave, const uint32_t* __restrict__ ovf_rows, uint64_t* row_off,
+                                                const uint32_t* __restrict__ row_len, uint32_t* row_cap,
+                                                uint32_t* pool_col, uint64_t* pool_tag, unsigned long long* top) {
     const uint32_t lane = threadIdx.x & 63;
-    if (wave >= no) return;
     const uint32_t u = ovf_rows[wave];
     const uint32_t ncap = grow_cap(row_len[u]);
     unsigned long long base = 0;
@@ -392,20 +467,31 @@ __global__ void k_au_relocate(uint64_t no, const uint32_t* __restrict__ ovf_rows
     }
 }
 
-__global__ void k_au_pending(uint64_t nc, const Cand* __restrict__ cand, const uint32_t* __restrict__ pend_pos,
-                             const uint64_t* __restrict__ row_off, uint32_t* pool_col, uint64_t* pool_tag) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nc || pend_pos[i] == FGI_NONE) return;
+__global__ void k_au_relocate(uint64_t no, const uint32_t* __restrict__ ovf_rows, uint64_t* row_off,
+                              const uint32_t* __restrict__ row_len, uint32_t* row_cap, uint32_t* pool_col,
+                              uint64_t* pool_tag, unsigned long long* top) {
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (wave < no) au_relocate_row(wave, ovf_rows, row_off, row_len, row_cap, pool_col, pool_tag, top);
+}
+
+__device__ __forceinline__ void au_pending(uint64_t i, const Cand* __restrict__ cand, const uint32_t* __restrict__ pend_pos,
+                                           const uint64_t* __restrict__ row_off, uint32_t* pool_col, uint64_t* pool_tag) {
+    if (pend_pos[i] == FGI_NONE) return;
     const Cand c = cand[i];
     pool_col[row_off[c.used] + pend_pos[i]] = c.dep_slot;
     pool_tag[row_off[c.used] + pend_pos[i]] = c.tag;
 }
 
+__global__ void k_au_pending(uint64_t nc, const Cand* __restrict__ cand, const uint32_t* __restrict__ pend_pos,
+                             const uint64_t* __restrict__ row_off, uint32_t* pool_col, uint64_t* pool_tag) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < nc) au_pending(i, cand, pend_pos, row_off, pool_col, pool_tag);
+}
+
 // ---- set_output ------------------------------------------------------------------------------
-__global__ void k_set_output(uint32_t n, const uint32_t* __restrict__ h, uint32_t n_handles, unsigned long long* node,
-                             uint8_t* out_set, uint32_t* roots, unsigned long long* nroots) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+__device__ __forceinline__ void set_output(uint32_t i, const uint32_t* __restrict__ h, uint32_t n_handles,
+                                           unsigned long long* node, uint8_t* out_set, uint32_t* roots,
+                                           unsigned long long* nroots) {
     uint8_t set = 0;
     const uint32_t x = h[i];
     if (x < n_handles) {
@@ -422,6 +508,91 @@ __global__ void k_set_output(uint32_t n, const uint32_t* __restrict__ h, uint32_
         }
     }
     out_set[i] = set;
+}
+
+__global__ void k_set_output(uint32_t n, const uint32_t* __restrict__ h, uint32_t n_handles, unsigned long long* node,
+                             uint8_t* out_set, uint32_t* roots, unsigned long long* nroots) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) set_output(i, h, n_handles, node, out_set, roots, nroots);
+}
+
+// ---- streaming batches (fgi_run_batch) ------------------------------------------------------------
+// A batch's kernels read their item counts from the device and do nothing once the batch's abort
+// word is set (a step that cannot complete here: the host finishes it, or reports it, after its one
+// synchronisation). Abort word: reason << 32 | (step + 1).
+constexpr unsigned long long kAbortDetach = 1, kAbortPool = 2;
+
+__device__ __forceinline__ bool batch_aborted(const unsigned long long* ab) {
+    return __hip_atomic_load(ab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+}
+
+__device__ __forceinline__ uint64_t grid_tid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
+__device__ __forceinline__ uint64_t grid_threads() { return (uint64_t)gridDim.x * blockDim.x; }
+
+__global__ void kb_bc_classify(const unsigned long long* ab, uint32_t n, const uint32_t* __restrict__ slot,
+                               const unsigned long long* node, uint8_t* cls, uint32_t* roots, unsigned long long* cnt) {
+    if (batch_aborted(ab)) return;
+    const uint64_t i = grid_tid();
+    if (i < n) bc_classify((uint32_t)i, slot, node, cls, roots, cnt);
+}
+
+// the displaced nodes that survive (cnt[1]) need detached handles: the batch's list has n_take
+__global__ void kb_bc_check(unsigned long long* ab, const unsigned long long* cnt, const unsigned long long* cursor,
+                            uint64_t n_take, uint32_t step) {
+    if (threadIdx.x || blockIdx.x || batch_aborted(ab)) return;
+    if (*cursor + cnt[1] > n_take) *ab = (kAbortDetach << 32) | (step + 1ull);
+}
+
+__global__ void kb_bc_install(const unsigned long long* ab, uint32_t n, InstallArgs a) {
+    if (batch_aborted(ab)) return;
+    const uint64_t i = grid_tid();
+    if (i < n) bc_install((uint32_t)i, a);
+}
+
+__global__ void kb_au_classify(const unsigned long long* ab, uint32_t n, AuArgs a) {
+    if (batch_aborted(ab)) return;
+    const uint64_t i = grid_tid();
+    if (i < n) au_classify((uint32_t)i, a);
+}
+
+__global__ void kb_au_reserve(const unsigned long long* ab, AuArgs a) {
+    if (batch_aborted(ab)) return;
+    const uint64_t nc = a.cnt[0];
+    for (uint64_t i = grid_tid(); i < nc; i += grid_threads()) au_reserve(i, a);
+}
+
+__global__ void kb_au_size(const unsigned long long* ab, AuArgs a) {
+    if (batch_aborted(ab)) return;
+    const uint64_t no = a.cnt[2];
+    for (uint64_t i = grid_tid(); i < no; i += grid_threads())
+        atomicAdd(&a.cnt[3], (unsigned long long)grow_cap(a.row_len[a.ovf_rows[i]]));
+}
+
+// the overflowing rows fit in the pool? (otherwise the host grows it and finishes the step)
+__global__ void kb_au_check(unsigned long long* ab, const unsigned long long* cnt, const unsigned long long* top,
+                            uint64_t cap, uint32_t step) {
+    if (threadIdx.x || blockIdx.x || batch_aborted(ab)) return;
+    if (cnt[2] && *top + cnt[3] > cap) *ab = (kAbortPool << 32) | (step + 1ull);
+}
+
+__global__ void kb_au_relocate(const unsigned long long* ab, AuArgs a, unsigned long long* top) {
+    if (batch_aborted(ab)) return;
+    const uint64_t no = a.cnt[2];
+    for (uint64_t w = grid_tid() >> 6; w < no; w += grid_threads() >> 6)   // wave-uniform
+        au_relocate_row(w, a.ovf_rows, a.row_off, a.row_len, a.row_cap, a.pool_col, a.pool_tag, top);
+}
+
+__global__ void kb_au_pending(const unsigned long long* ab, AuArgs a) {
+    if (batch_aborted(ab)) return;
+    const uint64_t nc = a.cnt[0];
+    for (uint64_t i = grid_tid(); i < nc; i += grid_threads()) au_pending(i, a.cand, a.pend_pos, a.row_off, a.pool_col, a.pool_tag);
+}
+
+__global__ void kb_set_output(const unsigned long long* ab, uint32_t n, const uint32_t* __restrict__ h, uint32_t n_handles,
+                              unsigned long long* node, uint8_t* out_set, uint32_t* roots, unsigned long long* nroots) {
+    if (batch_aborted(ab)) return;
+    const uint64_t i = grid_tid();
+    if (i < n) set_output((uint32_t)i, h, n_handles, node, out_set, roots, nroots);
 }
 
 // ---- prune -----------------------------------------------------------------------------------
@@ -844,9 +1015,11 @@ fgi_status build_candidates(fgi_graph* g) {
     const uint32_t N = g->n_slots;
     if (g->cand_cap < N || !g->cand) {
         dfree(g->cand);
+        dfree(g->wl);
         for (int k = 0; k < 2; ++k) dfree(g->sv[k]);
         g->cand_cap = 0;
         FGI_TRY(dmalloc(g, &g->cand, N));
+        FGI_TRY(dmalloc(g, &g->wl, N));
         for (int k = 0; k < 2; ++k) FGI_TRY(dmalloc(g, &g->sv[k], N));
         g->cand_cap = N;
     }
@@ -1018,16 +1191,13 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
         dmalloc(g, &g->uin_head, g->n_slots + 1))
         return fail(FGI_ENOMEM);
     g->bm_words = (H + 63) / 64 * 2 + 2;
-    g->tiles_cap = (uint64_t)H / kPullTile + kStatBlocks + 1;
     if (dmalloc(g, &g->vis_bm, g->bm_words) || dmalloc(g, &g->inv_bm, g->bm_words) ||
-        dmalloc(g, &g->lw_bm, g->bm_words) || dmalloc(g, &g->cls_bm, g->bm_words) ||
-        dmalloc(g, &g->uin_more, g->bm_words) || dmalloc(g, &g->tiles, g->tiles_cap))
+        dmalloc(g, &g->cls_bm, g->bm_words) || dmalloc(g, &g->uin_more, g->bm_words))
         return fail(FGI_ENOMEM);
     hipMemset(g->done, 0, (size_t)(kDoneGroups + 1) * kDoneStride * sizeof(unsigned long long));
     hipMemset(g->bsum, 0, 8ull * kStatBlocks * sizeof(unsigned long long));
     hipMemset(g->vis_bm, 0, g->bm_words * 4);
     hipMemset(g->inv_bm, 0, g->bm_words * 4);
-    hipMemset(g->lw_bm, 0, g->bm_words * 4);
     hipMemset(g->uin_more, 0, g->bm_words * 4);
     if (hipHostMalloc(reinterpret_cast<void**>(&g->ctr_host), sizeof(WaveCtr)) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&g->misc_host), 16 * sizeof(unsigned long long)) != hipSuccess)
@@ -1076,6 +1246,7 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->uin_src);
     dfree(g->uin_head);
     dfree(g->cand);
+    dfree(g->wl);
     dfree(g->cand_seg);
     dfree(g->hot_id);
     dfree(g->hot_bm);
@@ -1086,9 +1257,7 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->vis_bm);
     dfree(g->cls_bm);
     dfree(g->uin_more);
-    dfree(g->tiles);
     dfree(g->inv_bm);
-    dfree(g->lw_bm);
     dfree(g->bsum);
     dfree(g->done);
     dfree(g->ctr);
@@ -1105,6 +1274,9 @@ fgi_status fgi_destroy(fgi_graph* g) {
     if (g->ctr_host) hipHostFree(g->ctr_host);
     if (g->misc_host) hipHostFree(g->misc_host);
     for (hipEvent_t e : g->ev) hipEventDestroy(e);
+    if (g->bst_h) hipHostFree(g->bst_h);
+    dfree(g->bst_d);
+    dfree(g->bout);
     if (g->ev_w0) hipEventDestroy(g->ev_w0);
     if (g->ev_w1) hipEventDestroy(g->ev_w1);
     if (g->stream) hipStreamDestroy(g->stream);
@@ -1540,9 +1712,10 @@ fgi_status fgi_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, con
     FGI_HIP(g, hipMemsetAsync(g->misc_dev + 2, 0, sizeof(unsigned long long), st));
     touch(g);
     note_words(g);
-    hipLaunchKernelGGL(k_bc_install, dim3(nblk(n)), dim3(256), 0, st, n, ds, dv, dd, dcls, dfree_h, g->misc_dev + 2,
-                       g->n_slots, reinterpret_cast<unsigned long long*>(g->node), g->row_off, g->row_len, g->row_cap,
-                       g->used_cnt, g->home, dout);
+    const InstallArgs ia{ds,          dv,          dd,         dcls,       dfree_h, g->misc_dev + 2, g->n_slots,
+                         reinterpret_cast<unsigned long long*>(g->node), g->row_off, g->row_len, g->row_cap,
+                         g->used_cnt, g->home, dout};
+    hipLaunchKernelGGL(k_bc_install, dim3(nblk(n)), dim3(256), 0, st, n, ia);
     FGI_HIP(g, hipGetLastError());
     std::vector<uint32_t> od(n);
     FGI_TRY(d2h(g, od.data(), dout, n));
@@ -1579,15 +1752,16 @@ fgi_status fgi_add_used(fgi_graph* g, uint32_t n, const uint32_t* dependant, con
     note_words(g);   // may set InvalidateOnSetOutput (Computed.cs:376-378)
     FGI_HIP(g, hipMemsetAsync(dhash, 0xFF, hcap * sizeof(unsigned long long), st));
     FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, 8 * sizeof(unsigned long long), st));
-    hipLaunchKernelGGL(k_au_classify, dim3(nblk(n)), dim3(256), 0, st, n, ddep, duse, g->n_slots, g->home,
-                       reinterpret_cast<unsigned long long*>(g->node), g->row_off, g->row_len, g->used_cnt, g->pool_col,
-                       g->pool_tag, dhash, hcap - 1, dres, dcand, g->misc_dev);
+    const AuArgs aa{ddep,        duse,       g->n_slots,   g->home,     reinterpret_cast<unsigned long long*>(g->node),
+                    g->row_off,  g->row_len, g->row_cap,   g->used_cnt, g->pool_col,
+                    g->pool_tag, dhash,      hcap - 1,     dres,        dcand,
+                    dpend,       dovf,       g->misc_dev};
+    hipLaunchKernelGGL(k_au_classify, dim3(nblk(n)), dim3(256), 0, st, n, aa);
     unsigned long long nc = 0;
     FGI_TRY(d2h(g, &nc, g->misc_dev, 1));
     if (nc) {
         touch(g);
-        hipLaunchKernelGGL(k_au_reserve, dim3(nblk(nc)), dim3(256), 0, st, (uint64_t)nc, dcand, g->row_off, g->row_len,
-                           g->row_cap, g->used_cnt, g->pool_col, g->pool_tag, dpend, dovf, g->misc_dev + 1);
+        hipLaunchKernelGGL(k_au_reserve, dim3(nblk(nc)), dim3(256), 0, st, (uint64_t)nc, aa);
         unsigned long long c2[2];
         FGI_TRY(d2h(g, c2, g->misc_dev + 1, 2));
         if (c2[1]) {   // some rows outgrew their capacity: relocate them to the pool top
@@ -1637,6 +1811,363 @@ fgi_status fgi_set_output(fgi_graph* g, uint32_t n, const uint32_t* handle, uint
     g->last_wave_n = 0;
     if (nr) FGI_TRY(run_wave(g, (uint32_t)nr, droots, nullptr, stats));   // Invalidate() (Computed.cs:153-156)
     return copy_ids(g, out_ids, cap, out_n);
+}
+
+// ---- streaming batches ---------------------------------------------------------------------------
+namespace {
+
+constexpr size_t kStageAlign = 256;
+inline size_t stage_round(size_t b) { return (b + kStageAlign - 1) / kStageAlign * kStageAlign; }
+
+// Per-step device state of a batch (kept until the call returns: a pool growth resumes a step).
+struct BatchStep {
+    const uint32_t* h = nullptr;     // staged inputs (device)
+    const uint32_t* used = nullptr;
+    const uint64_t* ver = nullptr;
+    const uint8_t* flags = nullptr;
+    uint8_t* cls = nullptr;          // begin_compute
+    uint32_t* roots = nullptr;       // begin_compute / set_output cascade roots
+    uint32_t* out32 = nullptr;       // detached handles / add_used results
+    uint8_t* out8 = nullptr;         // set_output flags
+    unsigned long long* hash = nullptr;
+    uint64_t hcap = 0;
+    Cand* cand = nullptr;
+    uint32_t* pend = nullptr;
+    uint32_t* ovf = nullptr;
+    unsigned long long* cnt = nullptr;   // 4 counters
+    size_t out_off = 0;              // where its output lands in the pinned staging
+    std::vector<Tmp> tmp;
+};
+
+}  // namespace
+
+// Launches steps [from, n) of a batch; returns with the work queued (no synchronisation).
+static fgi_status batch_launch(fgi_graph* g, uint32_t from, uint32_t n_steps, const fgi_step* steps,
+                               std::vector<BatchStep>& bs, unsigned long long* scr, const uint32_t* take,
+                               uint64_t n_take, std::vector<std::pair<hipEvent_t, hipEvent_t>>& wave_ev) {
+    hipStream_t st = g->stream;
+    unsigned long long* abort = scr;
+    unsigned long long* out_n = scr + 1;
+    unsigned long long* cursor = scr + 2;
+    unsigned long long* acc = scr + 3;
+    auto* node = reinterpret_cast<unsigned long long*>(g->node);
+    auto wave = [&](uint32_t n_max, const uint32_t* roots, const uint8_t* imm, const unsigned long long* n_dev) -> fgi_status {
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
+            wave_ev.emplace_back(e0, e1);
+            hipEventRecord(e0, st);
+        }
+        FGI_TRY(run_wave_coop(g, n_max, roots, imm, n_dev, g->bout, out_n, acc, abort));
+        if (e1) hipEventRecord(e1, st);
+        return fold(g);
+    };
+    for (uint32_t k = from; k < n_steps; ++k) {
+        const fgi_step& sp = steps[k];
+        BatchStep& b = bs[k];
+        const uint32_t n = sp.n;
+        if (n == 0) continue;
+        const uint32_t grid = (uint32_t)std::min<uint64_t>(nblk(n), 8192);
+        switch (sp.kind) {
+            case FGI_STEP_INVALIDATE:
+                FGI_TRY(fold(g));
+                FGI_TRY(wave(n, b.h, b.flags, nullptr));
+                break;
+            case FGI_STEP_BEGIN_COMPUTE: {
+                FGI_TRY(fold(g));
+                hipLaunchKernelGGL(kb_bc_classify, dim3(nblk(n)), dim3(256), 0, st, abort, n, b.h, node, b.cls, b.roots,
+                                   b.cnt);
+                hipLaunchKernelGGL(kb_bc_check, dim3(1), dim3(64), 0, st, abort, b.cnt, cursor, n_take, k);
+                FGI_TRY(wave(n, b.roots, nullptr, b.cnt));   // displacement cascade (ComputedRegistry.cs:91-94)
+                touch(g);
+                note_words(g);
+                const InstallArgs ia{b.h,        b.ver,      b.flags,    b.cls,       take, cursor, g->n_slots, node,
+                                     g->row_off, g->row_len, g->row_cap, g->used_cnt, g->home, b.out32};
+                hipLaunchKernelGGL(kb_bc_install, dim3(nblk(n)), dim3(256), 0, st, abort, n, ia);
+                break;
+            }
+            case FGI_STEP_ADD_USED: {
+                FGI_TRY(fold(g));
+                note_words(g);
+                touch(g);
+                const AuArgs aa{b.h,        b.used,     g->n_slots, g->home,     node,        g->row_off,
+                                g->row_len, g->row_cap, g->used_cnt, g->pool_col, g->pool_tag, b.hash,
+                                b.hcap - 1, b.out32,    b.cand,     b.pend,      b.ovf,       b.cnt};
+                if (from == k && b.hcap == 0) {   // resumed after a pool growth: relocate and finish
+                    hipLaunchKernelGGL(kb_au_relocate, dim3(grid), dim3(256), 0, st, abort, aa, g->pool_top_dev);
+                    hipLaunchKernelGGL(kb_au_pending, dim3(grid), dim3(256), 0, st, abort, aa);
+                    break;
+                }
+                FGI_HIP(g, hipMemsetAsync(b.hash, 0xFF, b.hcap * sizeof(unsigned long long), st));
+                hipLaunchKernelGGL(kb_au_classify, dim3(nblk(n)), dim3(256), 0, st, abort, n, aa);
+                hipLaunchKernelGGL(kb_au_reserve, dim3(grid), dim3(256), 0, st, abort, aa);
+                hipLaunchKernelGGL(kb_au_size, dim3(grid), dim3(256), 0, st, abort, aa);
+                hipLaunchKernelGGL(kb_au_check, dim3(1), dim3(64), 0, st, abort, b.cnt, g->pool_top_dev, g->pool_cap, k);
+                hipLaunchKernelGGL(kb_au_relocate, dim3(grid), dim3(256), 0, st, abort, aa, g->pool_top_dev);
+                hipLaunchKernelGGL(kb_au_pending, dim3(grid), dim3(256), 0, st, abort, aa);
+                break;
+            }
+            case FGI_STEP_SET_OUTPUT:
+                FGI_TRY(fold(g));
+                note_words(g);
+                hipLaunchKernelGGL(kb_set_output, dim3(nblk(n)), dim3(256), 0, st, abort, n, b.h, g->n_handles, node,
+                                   b.out8, b.roots, b.cnt);
+                FGI_TRY(wave(n, b.roots, nullptr, b.cnt));   // Invalidate() of InvalidateOnSetOutput nodes (153-156)
+                break;
+            default:
+                break;
+        }
+    }
+    FGI_HIP(g, hipGetLastError());
+    return FGI_OK;
+}
+
+fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, uint32_t* out_ids, uint64_t cap,
+                         uint64_t* out_n, fgi_batch_stats* stats) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!g || (n_steps && !steps)) return FGI_EINVAL;
+    if (out_n) *out_n = 0;
+    uint64_t n_waves = 0, n_begin = 0, n_add = 0;
+    for (uint32_t k = 0; k < n_steps; ++k) {   // the single calls' argument checks
+        const fgi_step& sp = steps[k];
+        if (sp.n && !sp.handles) return set_err(g, FGI_EINVAL, "step %u: no handles", k);
+        switch (sp.kind) {
+            case FGI_STEP_INVALIDATE:
+            case FGI_STEP_SET_OUTPUT:
+                ++n_waves;
+                break;
+            case FGI_STEP_BEGIN_COMPUTE: {
+                if (sp.n && !sp.version) return set_err(g, FGI_EINVAL, "step %u: no versions", k);
+                std::vector<uint64_t>& seen = g->seen_bits;
+                if (seen.size() < ((size_t)g->n_slots + 63) / 64) seen.assign(((size_t)g->n_slots + 63) / 64, 0);
+                const char* why = nullptr;
+                uint32_t i = 0, bad = 0;
+                for (; i < sp.n; ++i) {
+                    const uint32_t x = sp.handles[i];
+                    if (x >= g->n_slots) { why = "slot out of range"; bad = x; break; }
+                    if (sp.version[i] == 0 || sp.version[i] > kVMask) { why = "bad version"; bad = i; break; }
+                    const uint64_t m = 1ull << (x & 63);
+                    if (seen[x >> 6] & m) { why = "slot repeated in one step"; bad = x; break; }
+                    seen[x >> 6] |= m;
+                }
+                for (uint32_t j = 0; j < i; ++j) seen[sp.handles[j] >> 6] = 0;
+                if (why) return set_err(g, FGI_EINVAL, "step %u: %s (%u)", k, why, bad);
+                ++n_waves;
+                n_begin += sp.n;
+                break;
+            }
+            case FGI_STEP_ADD_USED:
+                if (sp.n && !sp.used) return set_err(g, FGI_EINVAL, "step %u: no used handles", k);
+                for (uint32_t i = 0; i < sp.n; ++i)
+                    if (sp.handles[i] >= g->n_handles || sp.used[i] >= g->n_handles)
+                        return set_err(g, FGI_EINVAL, "step %u: handle out of range at %u", k, i);
+                n_add += sp.n;
+                break;
+            default:
+                return set_err(g, FGI_EINVAL, "step %u: unknown kind %u", k, sp.kind);
+        }
+    }
+    FGI_TRY(single_only(g, "fgi_run_batch"));
+    hipSetDevice(g->device);
+    hipStream_t st = g->stream;
+    // capacities, before anything is queued: the ids of every cascade, pool headroom for the rows
+    // the add_used steps may relocate (an add_used step that needs more resumes after a growth)
+    const uint64_t need_out = std::max<uint64_t>(1, n_waves) * g->n_handles;
+    if (g->bout_cap < need_out) {
+        dfree(g->bout);
+        g->bout_cap = 0;
+        FGI_TRY(dmalloc(g, &g->bout, need_out));
+        g->bout_cap = need_out;
+    }
+    if (n_add) FGI_TRY(ensure_pool(g, g->pool_top + std::max<uint64_t>(1ull << 20, 4 * n_add)));
+    FGI_TRY(ensure_cstart(g, std::max<uint64_t>(g->pool_top, g->pool_cap)));
+    // detached handles the begin_compute steps may take (top of the free list)
+    const uint64_t n_take = std::min<uint64_t>(n_begin, g->free_detached.size());
+    // staging: inputs (uploaded once) | the detached-handle list | outputs (downloaded once)
+    size_t in_bytes = stage_round(n_take * 4), out_bytes = 0;
+    std::vector<size_t> in_off(n_steps * 4, 0);
+    for (uint32_t k = 0; k < n_steps; ++k) {
+        const fgi_step& sp = steps[k];
+        const size_t n = sp.n;
+        in_off[4 * k] = in_bytes;
+        in_bytes += stage_round(n * 4);
+        if (sp.kind == FGI_STEP_ADD_USED) {
+            in_off[4 * k + 1] = in_bytes;
+            in_bytes += stage_round(n * 4);
+        }
+        if (sp.kind == FGI_STEP_BEGIN_COMPUTE) {
+            in_off[4 * k + 2] = in_bytes;
+            in_bytes += stage_round(n * 8);
+        }
+        if (sp.flags && (sp.kind == FGI_STEP_BEGIN_COMPUTE || sp.kind == FGI_STEP_INVALIDATE)) {
+            in_off[4 * k + 3] = in_bytes;
+            in_bytes += stage_round(n);
+        }
+    }
+    std::vector<BatchStep> bs(n_steps);
+    for (uint32_t k = 0; k < n_steps; ++k) {
+        const fgi_step& sp = steps[k];
+        bs[k].out_off = out_bytes;
+        if (sp.kind == FGI_STEP_BEGIN_COMPUTE || sp.kind == FGI_STEP_ADD_USED) out_bytes += stage_round(sp.n * 4);
+        if (sp.kind == FGI_STEP_SET_OUTPUT) out_bytes += stage_round(sp.n);
+    }
+    const size_t scr_words = 3 + kAccCount + 4 * (size_t)n_steps;
+    const size_t scr_bytes = stage_round(scr_words * 8);
+    const size_t total = in_bytes + out_bytes + scr_bytes;
+    if (g->bst_cap < total) {
+        if (g->bst_h) hipHostFree(g->bst_h);
+        dfree(g->bst_d);
+        g->bst_h = nullptr;
+        g->bst_cap = 0;
+        const size_t c = std::max(total, g->bst_cap * 2);
+        if (hipHostMalloc(reinterpret_cast<void**>(&g->bst_h), c) != hipSuccess) return set_err(g, FGI_ENOMEM, "pinned staging");
+        FGI_TRY(dmalloc(g, &g->bst_d, c));
+        g->bst_cap = c;
+    }
+    char* H = g->bst_h;
+    char* D = g->bst_d;
+    if (n_take) std::memcpy(H, g->free_detached.data() + (g->free_detached.size() - n_take), n_take * 4);
+    for (uint32_t k = 0; k < n_steps; ++k) {
+        const fgi_step& sp = steps[k];
+        const size_t n = sp.n;
+        std::memcpy(H + in_off[4 * k], sp.handles, n * 4);
+        bs[k].h = reinterpret_cast<const uint32_t*>(D + in_off[4 * k]);
+        if (sp.kind == FGI_STEP_ADD_USED) {
+            std::memcpy(H + in_off[4 * k + 1], sp.used, n * 4);
+            bs[k].used = reinterpret_cast<const uint32_t*>(D + in_off[4 * k + 1]);
+        }
+        if (sp.kind == FGI_STEP_BEGIN_COMPUTE) {
+            std::memcpy(H + in_off[4 * k + 2], sp.version, n * 8);
+            bs[k].ver = reinterpret_cast<const uint64_t*>(D + in_off[4 * k + 2]);
+        }
+        if (in_off[4 * k + 3]) {
+            std::memcpy(H + in_off[4 * k + 3], sp.flags, n);
+            bs[k].flags = reinterpret_cast<const uint8_t*>(D + in_off[4 * k + 3]);
+        }
+    }
+    unsigned long long* scr = reinterpret_cast<unsigned long long*>(D + in_bytes + out_bytes);
+    unsigned long long* scr_h = reinterpret_cast<unsigned long long*>(H + in_bytes + out_bytes);
+    std::memset(scr_h, 0, scr_words * 8);
+    hipEvent_t b0 = g->ev_w0, b1 = g->ev_w1;
+    FGI_HIP(g, hipEventRecord(b0, st));
+    FGI_HIP(g, hipMemcpyAsync(D, H, in_bytes, hipMemcpyHostToDevice, st));
+    FGI_HIP(g, hipMemcpyAsync(scr, scr_h, scr_words * 8, hipMemcpyHostToDevice, st));
+    // per-step device temporaries
+    for (uint32_t k = 0; k < n_steps; ++k) {
+        const fgi_step& sp = steps[k];
+        BatchStep& b = bs[k];
+        const uint32_t n = sp.n;
+        b.cnt = scr + 3 + kAccCount + 4 * k;
+        if (!n) continue;
+        b.tmp.resize(8);
+        switch (sp.kind) {
+            case FGI_STEP_BEGIN_COMPUTE:
+                FGI_TRY(tmalloc(g, b.tmp[0], &b.cls, n));
+                FGI_TRY(tmalloc(g, b.tmp[1], &b.roots, n));
+                FGI_TRY(tmalloc(g, b.tmp[2], &b.out32, n));
+                break;
+            case FGI_STEP_ADD_USED:
+                b.hcap = 64;
+                while (b.hcap < 2ull * n) b.hcap <<= 1;
+                FGI_TRY(tmalloc(g, b.tmp[0], &b.hash, b.hcap));
+                FGI_TRY(tmalloc(g, b.tmp[1], &b.cand, n));
+                FGI_TRY(tmalloc(g, b.tmp[2], &b.pend, n));
+                FGI_TRY(tmalloc(g, b.tmp[3], &b.ovf, n));
+                FGI_TRY(tmalloc(g, b.tmp[4], &b.out32, n));
+                break;
+            case FGI_STEP_SET_OUTPUT:
+                FGI_TRY(tmalloc(g, b.tmp[0], &b.out8, n));
+                FGI_TRY(tmalloc(g, b.tmp[1], &b.roots, n));
+                break;
+            default:
+                break;
+        }
+    }
+    const uint32_t* take = reinterpret_cast<const uint32_t*>(D);
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> wave_ev;
+    auto release_events = [&]() {
+        for (auto& e : wave_ev) {
+            hipEventDestroy(e.first);
+            hipEventDestroy(e.second);
+        }
+    };
+    uint32_t syncs = 0, from = 0;
+    g->last_wave_n = 0;
+    while (true) {
+        fgi_status s = batch_launch(g, from, n_steps, steps, bs, scr, take, n_take, wave_ev);
+        if (s != FGI_OK) {
+            release_events();
+            return s;
+        }
+        // results: counters, the pool top, every step's output, in one copy each, then one wait
+        for (uint32_t k = from; k < n_steps; ++k) {
+            const BatchStep& b = bs[k];
+            if (b.out32) FGI_HIP(g, hipMemcpyAsync(H + in_bytes + b.out_off, b.out32, steps[k].n * 4, hipMemcpyDeviceToHost, st));
+            if (b.out8) FGI_HIP(g, hipMemcpyAsync(H + in_bytes + b.out_off, b.out8, steps[k].n, hipMemcpyDeviceToHost, st));
+        }
+        FGI_HIP(g, hipMemcpyAsync(scr_h, scr, scr_words * 8, hipMemcpyDeviceToHost, st));
+        FGI_HIP(g, hipMemcpyAsync(&g->pool_top, g->pool_top_dev, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        FGI_HIP(g, hipEventRecord(b1, st));
+        FGI_HIP(g, hipStreamSynchronize(st));
+        ++syncs;
+        const unsigned long long ab = scr_h[0];
+        if (!ab) break;
+        const uint32_t k = (uint32_t)(ab & 0xFFFFFFFFull) - 1;
+        if ((ab >> 32) == kAbortPool) {   // grow the pool, then finish step k and run the rest
+            const unsigned long long need = bs[k].cnt ? scr_h[3 + kAccCount + 4 * k + 3] : 0;
+            fgi_status s2 = ensure_pool(g, g->pool_top + need + std::max<uint64_t>(1ull << 20, 4 * n_add));
+            if (s2 != FGI_OK) {
+                release_events();
+                return s2;
+            }
+            scr_h[0] = 0;
+            FGI_HIP(g, hipMemcpyAsync(scr, scr_h, 8, hipMemcpyHostToDevice, st));
+            bs[k].hcap = 0;   // marks the resumed step: relocation and pending entries only
+            from = k;
+            continue;
+        }
+        // out of detached handles at step k: steps before it are applied
+        g->free_detached.resize(g->free_detached.size() - (size_t)scr_h[2]);
+        release_events();
+        return set_err(g, FGI_ECAPACITY, "step %u: out of detached handles (%zu free)", k, g->free_detached.size());
+    }
+    // host bookkeeping: the detached handles taken, the per-step outputs
+    g->free_detached.resize(g->free_detached.size() - (size_t)scr_h[2]);
+    for (uint32_t k = 0; k < n_steps; ++k) {
+        const fgi_step& sp = steps[k];
+        if (!sp.out || !sp.n) continue;
+        const char* src = H + in_bytes + bs[k].out_off;
+        if (sp.kind == FGI_STEP_SET_OUTPUT) std::memcpy(sp.out, src, sp.n);
+        else if (sp.kind == FGI_STEP_BEGIN_COMPUTE || sp.kind == FGI_STEP_ADD_USED) std::memcpy(sp.out, src, sp.n * 4);
+    }
+    const uint64_t n_ids = scr_h[1];
+    if (out_n) *out_n = n_ids;
+    fgi_status ret = FGI_OK;
+    if (out_ids) {
+        if (n_ids > cap) {
+            ret = FGI_ECAPACITY;
+        } else if (n_ids) {
+            FGI_HIP(g, hipMemcpyAsync(out_ids, g->bout, n_ids * 4, hipMemcpyDeviceToHost, st));
+            FGI_HIP(g, hipStreamSynchronize(st));
+            ++syncs;
+        }
+    }
+    if (stats) {
+        const unsigned long long* acc = scr_h + 3;
+        stats->waves += acc[0];
+        stats->levels += acc[1];
+        stats->v_inv += acc[2];
+        stats->e_trav += acc[3];
+        stats->e_match += acc[4];
+        stats->n_flagged += acc[5];
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, b0, b1) == hipSuccess) stats->kernel_ms += ms;
+        for (auto& e : wave_ev)
+            if (hipEventElapsedTime(&ms, e.first, e.second) == hipSuccess) stats->wave_ms += ms;
+        stats->host_syncs += syncs;
+        stats->total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    release_events();
+    return ret;
 }
 
 fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats) {

@@ -27,6 +27,7 @@
 //   k_final                        — the invalidated bitmap -> the invalidated list (ascending)
 // The push/pull choice of a level is a pure function of device counters that every block of the
 // level's kernels evaluates the same way; the host synchronises once per group of levels.
+#include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -56,8 +57,8 @@ namespace {
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 
-constexpr int kProbeLevels = 8, kProbePts = 8, kProbeBlocks = 2048;
 #if FGI_PROBE
+constexpr int kProbeLevels = 8, kProbePts = 8, kProbeBlocks = 2048;
 __device__ unsigned long long d_probe[kProbeLevels][kProbeBlocks][kProbePts];
 #define PROBE(L, k)                                                                    \
     do {                                                                               \
@@ -476,11 +477,12 @@ __device__ __forceinline__ void msg_flush(MsgEmit<true>& me, uint32_t at, const 
 // IMM = 1: only the roots with immediately[i] set (Invalidate(true) ignores the delay, so it can
 // change the node word; CAS on the word with the visit bit folded in), launched before IMM = 0,
 // which visits the other roots through the visit bitmap.
+// One root per lane (i < n), every lane of the wave calls it: the visit, the frontier entry, the
+// root counters.
 template <int IMM>
-__global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ roots, const uint8_t* __restrict__ imm,
-                                                  uint32_t n, uint32_t base, uint32_t n_range, unsigned long long* node,
-                                                  uint32_t* vis, Out o, WaveCtr* ctr, unsigned long long* done) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void root_step(uint32_t i, const uint32_t* __restrict__ roots, const uint8_t* __restrict__ imm,
+                                          uint32_t n, uint32_t base, uint32_t n_range, unsigned long long* node,
+                                          uint32_t* vis, const Out& o, WaveCtr* ctr) {
     uint32_t win = 0, flagged = 0, h = 0;
     if (i < n) {
         h = roots[i] - base;
@@ -515,6 +517,13 @@ __global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ r
     const uint32_t fs = wave_sum(flagged), ws = wave_sum(win);
     if (lane_id() == 0 && fs) atomicAdd(&ctr->root_flagged, (unsigned long long)fs);
     if (lane_id() == 0 && ws) atomicAdd(&ctr->root_inv, (unsigned long long)ws);
+}
+
+template <int IMM>
+__global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ roots, const uint8_t* __restrict__ imm,
+                                                  uint32_t n, uint32_t base, uint32_t n_range, unsigned long long* node,
+                                                  uint32_t* vis, Out o, WaveCtr* ctr, unsigned long long* done) {
+    root_step<IMM>(blockIdx.x * blockDim.x + threadIdx.x, roots, imm, n, base, n_range, node, vis, o, ctr);
     publish_ft(o.ln, done, gridDim.x);
 }
 
@@ -547,14 +556,15 @@ __device__ __forceinline__ uint32_t level_mult(uint64_t T, uint32_t grid) {
     return m;
 }
 
-// ---- collect: a pull level's winners bitmap -> the next level's frontier list ----------------
-// Block b of the pull grid owns tiles [b * tpb, (b + 1) * tpb); the pull's last block left the
-// exclusive prefixes of the per-block (expandable winners, row lengths) sums in pre[]. Block b of
-// the collect walks the same tiles at those offsets: one tile by one wave, 16 slots per lane.
+// ---- collect: a pull level's winners lists -> the next level's frontier list ------------------
+// Pull block b listed its expandable winners at wl[seg[b] ..); the pull's last block left the
+// exclusive prefixes of the per-block (winners, expandable winners, row lengths) sums in pre[].
+// One wave per pull block: 64 entries per step, their row lengths and offsets gathered together,
+// a wave scan for the edge offsets, the entries written at the block's offsets (frontier order is
+// the lists' order: a push does not depend on it).
 struct CollectArgs {
-    const PullTile* __restrict__ tiles;
-    const uint32_t* __restrict__ lw;       // the pull level's winners bitmap
-    uint32_t n_slots, n_handles;
+    const uint32_t* __restrict__ wl;
+    const uint32_t* __restrict__ seg;
     const uint32_t* __restrict__ row_len;
     const uint64_t* __restrict__ row_off;
     const unsigned long long* __restrict__ pre;   // [3][grid]: winners, expandable winners, lengths
@@ -570,93 +580,13 @@ struct CollectArgs {
 };
 
 constexpr int kCollectThreads = 256;
-constexpr int kMaxWaves = kCollectThreads / 64;
 
-__device__ __forceinline__ void collect_tile(const CollectArgs& c, uint64_t t, uint64_t be, uint64_t bl,
-                                             uint32_t* __restrict__ stage) {
-    const uint32_t lane = lane_id();
-    const uint64_t base = t * kPullTile + 16ull * lane;
-    const uint32_t m = base < c.n_slots ? (uint32_t)reinterpret_cast<const uint16_t*>(c.lw)[base / 16] : 0u;
-    uint32_t rl[16];
-    uint32_t em = 0, len = 0;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) rl[k] = 0;
-    if (m) {
-        if (base + 16 <= c.n_handles) {
-            const uint4* p = reinterpret_cast<const uint4*>(c.row_len + base);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint4 v = p[q];
-                rl[4 * q] = v.x;
-                rl[4 * q + 1] = v.y;
-                rl[4 * q + 2] = v.z;
-                rl[4 * q + 3] = v.w;
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < 16; ++k) rl[k] = ((m >> k) & 1u) ? c.row_len[base + k] : 0u;
-        }
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            if (!((m >> k) & 1u)) rl[k] = 0;
-            em |= (rl[k] != 0 ? 1u : 0u) << k;
-            len += rl[k];
-        }
-    }
-    uint32_t n_e, tot_l;
-    const uint32_t pe = wave_excl_scan((uint32_t)__popc(em), n_e);
-    const uint32_t pl = wave_excl_scan(len, tot_l);
-    if (n_e == 0) return;
-    // fr_len
-    {
-        uint32_t o = pe;
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if (rl[k]) stage[o++] = rl[k];
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t i = lane; i < n_e; i += 64) c.fr_len[be + i] = stage[i];
-        __builtin_amdgcn_wave_barrier();
-    }
-    // escan (+ cstart for every fine chunk whose first edge the entry holds)
-    {
-        uint32_t o = pe, r = pl;
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-            if (!rl[k]) continue;
-            const uint64_t es = bl + r, idx = be + o;
-            const uint64_t c_lo = (es + kFine - 1) / kFine, c_hi = (es + rl[k] - 1) / kFine;
-            for (uint64_t q = c_lo; q <= c_hi; ++q) c.cstart[q] = (uint32_t)idx;
-            stage[o++] = r;
-            r += rl[k];
-        }
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t i = lane; i < n_e; i += 64) c.escan[be + i] = bl + stage[i];
-        __builtin_amdgcn_wave_barrier();
-    }
-    // row offsets of the expandable slots only (low words: pool positions are < 2^32)
-    {
-        const uint32_t* off32 = reinterpret_cast<const uint32_t*>(c.row_off);
-        uint32_t ro[16];
-#pragma unroll
-        for (int k = 0; k < 16; ++k) ro[k] = ((em >> k) & 1u) ? off32[2 * (base + k)] : 0u;
-        uint32_t o = pe;
-#pragma unroll
-        for (int k = 0; k < 16; ++k)
-            if ((em >> k) & 1u) stage[o++] = ro[k];
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t i = lane; i < n_e; i += 64) c.fr_off[be + i] = stage[i];
-        __builtin_amdgcn_wave_barrier();
-    }
-}
-
-// Level L's frontier list when level L-1 pulled and level L pushes; otherwise nothing to do.
+// Level L's frontier list when level L-1 pulled and level L pushes; before a pull level, the hot
+// heads' snapshot; otherwise nothing to do.
 __global__ __launch_bounds__(kCollectThreads) void k_collect(int L, WaveCtr* ctr, WaveParams wp, CollectArgs c) {
-    __shared__ uint32_t s_oe[64];
-    __shared__ unsigned long long s_ol[64], s_tot[2];
-    __shared__ uint32_t s_nz[64];
-    __shared__ uint32_t s_stage[kMaxWaves][kPullTile];
-    if (ctr->lvl[L % kRing].F == 0) return;
-    if (level_pulls(ctr, L, wp)) {   // the hot heads' snapshot for this pull level
+    const LevelCtr& lc = ctr->lvl[L % kRing];
+    if (lc.F == 0) return;
+    if (level_pulls(ctr, L, wp)) {
         // one entry per lane, 64 bits per wave (n_hot and the grid stride are multiples of 64)
         unsigned long long* hot64 = reinterpret_cast<unsigned long long*>(c.hot_bm);
         for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < c.n_hot; k += gridDim.x * blockDim.x) {
@@ -667,35 +597,31 @@ __global__ __launch_bounds__(kCollectThreads) void k_collect(int L, WaveCtr* ctr
         return;
     }
     if (L == 0 || !ctr->lvl[(L + kRing - 1) % kRing].pull) return;
-    const uint64_t G = wp.grid;   // the pull grid; this grid is smaller (a no-op launch stays cheap)
-    const uint32_t W = blockDim.x >> 6, wid = threadIdx.x >> 6, lane = lane_id();
-    for (uint64_t b = blockIdx.x; b < G; b += gridDim.x) {
-    const uint64_t lo = b * wp.tpb, hi = std::min<uint64_t>(wp.n_tiles, lo + wp.tpb);
-    uint64_t re = c.pre[G + b], rl = c.pre[2 * G + b];
-    for (uint64_t cb = lo; cb < hi; cb += 64) {   // block-uniform
-        const uint32_t nt = (uint32_t)std::min<uint64_t>(64, hi - cb);
-        if (wid == 0) {
-            PullTile x{0, 0, 0ull};
-            if (lane < nt) x = c.tiles[cb + lane];
-            uint32_t te;
-            const uint32_t oe = wave_excl_scan(x.e, te);
-            unsigned long long tl;
-            const unsigned long long ol = wave_excl_scan64(x.len, tl);
-            s_oe[lane] = oe;
-            s_ol[lane] = ol;
-            s_nz[lane] = x.e;
-            if (lane == 0) {
-                s_tot[0] = te;
-                s_tot[1] = tl;
+    const uint64_t G = wp.grid;   // the pull grid
+    const uint32_t lane = lane_id();
+    const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t b = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < G; b += W) {   // wave-uniform
+        const uint64_t e0 = c.pre[G + b], e1 = b + 1 < G ? c.pre[G + b + 1] : lc.F;
+        uint64_t es = c.pre[2 * G + b];
+        const uint64_t base = c.seg[b];
+        for (uint64_t i0 = 0; i0 < e1 - e0; i0 += 64) {
+            const uint64_t i = i0 + lane;
+            const bool in = i < e1 - e0;
+            const uint32_t d = in ? c.wl[base + i] : 0u;
+            const uint32_t len = in ? c.row_len[d] : 0u;
+            const uint32_t off = in ? (uint32_t)c.row_off[d] : 0u;   // pool positions are < 2^32
+            uint32_t tot;
+            const uint32_t ex = wave_excl_scan(len, tot);
+            if (in) {
+                const uint64_t idx = e0 + i, e = es + ex;
+                c.fr_off[idx] = off;
+                c.fr_len[idx] = len;
+                c.escan[idx] = e;
+                const uint64_t c_lo = (e + kFine - 1) / kFine, c_hi = (e + len - 1) / kFine;
+                for (uint64_t q = c_lo; q <= c_hi; ++q) c.cstart[q] = (uint32_t)idx;
             }
+            es += tot;
         }
-        __syncthreads();
-        for (uint32_t j = wid; j < nt; j += W)
-            if (s_nz[j]) collect_tile(c, cb + j, re + s_oe[j], rl + s_ol[j], s_stage[wid]);
-        re += s_tot[0];
-        rl += s_tot[1];
-        __syncthreads();   // the next chunk overwrites the offsets
-    }
     }
 }
 
@@ -850,10 +776,9 @@ struct PullArgs {
     const uint32_t* __restrict__ uin_src;
     const uint32_t* front_rd;                // invalidated bitmap (multi-GPU: all-gathered, global ids)
     uint32_t* inv_bm;                        // this device's invalidated bitmap (owned words |= winners)
-    uint32_t* lw_bm;                         // this level's winners, stored whole per owned word
     const uint32_t* __restrict__ cls;        // expandable-class bitmap
     const uint32_t* hot_bm;                  // the hot heads' invalidated bits (kHotFlag | rank)
-    PullTile* tiles;
+    uint32_t* wl;                            // per block (at its segment base): expandable winners
     unsigned long long* bsum;                // [3][grid] per-block sums, then [3][grid] prefixes
     const uint32_t* __restrict__ cand_seg;   // [grid + 1] segment bases
     const uint4* c[3];                       // [0] the static candidates, [1 + k] survivors buffer k
@@ -864,11 +789,13 @@ struct PullArgs {
 // A block owns the tiles [b * tpb, (b + 1) * tpb) (tpb <= kMaxIter): their visit, class and winners
 // words live in LDS for the whole level (loaded once, coalesced) and the visit / winners words are
 // written back once (owned words, plain stores), so a pull level does no global atomics and a
-// candidate's only global gathers are the invalidated bits of its two list heads (L2). Candidates
-// are read 4 per lane per batch (one 16-byte entry each, streamed); a hit is a visit. Candidates
-// whose heads missed but whose list goes on are queued in LDS and scanned at the flush by 8-lane
-// groups (8 entries per probe step, early exit). Candidates neither hit nor queued, and queued ones
-// whose scan found nothing, are this level's survivors.
+// candidate's only global gathers are the invalidated bits of its two list heads (hot heads: an
+// L1-resident snapshot). Candidates are read 4 per lane per batch (one 16-byte entry each,
+// streamed); a hit is a visit. A winner with a non-empty row is appended to the block's winners
+// list (for the collect, if the next level pushes); the block's winner / expandable / row-length
+// totals are per-thread register sums. Candidates whose heads missed but whose list goes on are
+// queued in LDS and scanned at the wave's flush (pull_tails). Candidates neither hit nor queued,
+// and queued ones whose scan found nothing, are this level's survivors.
 constexpr uint32_t kMaxIter = 16;           // tiles per pull block (kMaxIter * kPullTile slots)
 constexpr uint32_t kTailCap = kChunk;       // queued candidates
 constexpr uint32_t kTileWords = kPullTile / 64;
@@ -880,12 +807,17 @@ constexpr uint32_t kWaveTailCap = kTailCap / (kBlock / 64);   // queued candidat
 // visits / winners / classes of the owned tiles in LDS: 32-bit words (two lanes of a wave that
 // share a word serialise their atomics; narrower words halve how many do)
 struct PullLds {
-    uint32_t vm[kOwnWords];                         // visits: the level's start, | this level's
+    uint32_t vm[kOwnWords];                         // visits: the level's start, | this level's non-winners
     uint32_t wm[kOwnWords];                         // winners
     uint32_t cs[kOwnWords];                         // expandable class (read only)
-    unsigned long long cl[kMaxIter];                // per tile: row lengths of the winners
-    uint32_t cw[kMaxIter], ce[kMaxIter];            // per tile: winners, expandable winners
     uint32_t sn;                                    // survivors written
+    uint32_t wn;                                    // expandable winners listed
+};
+
+// a thread's winners: count, those with a non-empty row, their row lengths
+struct WinSum {
+    uint32_t w = 0, e = 0;
+    unsigned long long l = 0;
 };
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -903,73 +835,93 @@ __device__ __forceinline__ uint4 load_cand(const uint4* p, bool in, uint32_t s_l
     return make_uint4(v.x, v.y, v.z, v.w);
 }
 
-__device__ __forceinline__ void pull_hit(PullLds& s, uint64_t s_lo, uint32_t d, bool win, uint32_t aux) {
-    const uint32_t rel = (uint32_t)(d - s_lo), k = rel / kPullTile;
+// one lane's hit (tails): visit bits, and a winner's sums and list entry
+__device__ __forceinline__ void pull_hit(const PullArgs& p, PullLds& s, uint64_t s_lo, uint64_t seg, uint32_t d, bool win,
+                                         uint32_t aux, WinSum& ws) {
+    const uint32_t rel = (uint32_t)(d - s_lo);
     const uint32_t bit = 1u << (d & 31);
-    atomicOr(&s.vm[rel >> 5], bit);
     if (win) {
         atomicOr(&s.wm[rel >> 5], bit);
         const uint32_t rl = aux & 0x7FFFFFFFu;
-        atomicAdd(&s.cw[k], 1u);
+        ++ws.w;
         if (rl) {
-            atomicAdd(&s.ce[k], 1u);
-            atomicAdd(&s.cl[k], (unsigned long long)rl);
+            ++ws.e;
+            ws.l += rl;
+            p.wl[seg + atomicAdd(&s.wn, 1u)] = d;
         }
+    } else {
+        atomicOr(&s.vm[rel >> 5], bit);
     }
 }
 
-// A thread's winners in increasing slot order (its candidates are): it accumulates the tile counts
-// in registers and adds them to the tile's LDS counters when the tile changes — a wave's lanes share
-// one tile almost always, and 64 lanes adding to one LDS word serialise.
-struct TileAcc {
-    uint32_t tile = 0xFFFFFFFFu, w = 0, e = 0;
-    unsigned long long l = 0;
-    __device__ __forceinline__ void flush(PullLds& s) {
-        if (w) {
-            atomicAdd(&s.cw[tile], w);
-            if (e) atomicAdd(&s.ce[tile], e);
-            if (l) atomicAdd(&s.cl[tile], l);
-        }
-        w = e = 0;
-        l = 0;
-    }
-    __device__ __forceinline__ void add(PullLds& s, uint32_t k, uint32_t rl) {
-        if (k != tile) {
-            flush(s);
-            tile = k;
-        }
-        ++w;
-        e += rl ? 1u : 0u;
-        l += rl;
-    }
-};
-
-// A wave's queued candidates: 8 lanes per candidate, entries 2.. of its list; the next candidate's
-// list length and offset are loaded while the current list is scanned.
+// A wave's queued candidates (both heads missed, the list goes on). Pass 1: one lane per candidate
+// probes entries 2 and 3 (both in flight together) — most queued candidates settle here. Pass 2:
+// the ones whose list goes past entry 3 without a hit, 8 lanes per candidate over entries 4.. in
+// steps of 8 (early exit); the next candidate's list is located while the current one is scanned.
+// q (the wave's queue of candidate indices) is reused for pass 2's list.
 __device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, int dst, const unsigned long long* node,
-                                           uint64_t s_lo, uint64_t seg, const uint32_t* q, uint32_t nq, PullLds& s,
-                                           uint32_t& flagged, uint32_t& examined, uint32_t& tails) {
-    const uint32_t lane = lane_id(), sub = lane & 7, grp = lane >> 3;
+                                           uint64_t s_lo, uint64_t seg, uint32_t* q, uint32_t nq, PullLds& s,
+                                           uint32_t& flagged, uint32_t& examined, uint32_t& tails, WinSum& ws) {
+    const uint32_t lane = lane_id();
+    uint32_t nlong = 0;
+    for (uint32_t r0 = 0; r0 < nq; r0 += 64) {   // wave-uniform
+        const uint32_t e = r0 + lane;
+        const bool in = e < nq;
+        uint32_t qi = 0, len = 0;
+        uint64_t off = 0;
+        uint4 c = make_uint4(0u, 0u, 0u, 0u);
+        if (in) {
+            qi = q[e];
+            c = src[seg + qi];
+            len = p.uin_len[c.x];
+            off = p.uin_off[c.x];
+        }
+        const uint32_t u2 = (in && len > 2) ? p.uin_src[off + 2] : FGI_NONE;
+        const uint32_t u3 = (in && len > 3) ? p.uin_src[off + 3] : FGI_NONE;
+        const bool hit = (u2 != FGI_NONE && bit_of(p.front_rd, u2)) || (u3 != FGI_NONE && bit_of(p.front_rd, u3));
+        examined += (u2 != FGI_NONE ? 1u : 0u) + (u3 != FGI_NONE ? 1u : 0u);
+        const bool more = in && !hit && len > 4;
+        const unsigned long long mm = __ballot(more);
+        if (more) q[nlong + __popcll(mm & lanemask_lt())] = qi;   // below every entry still unread
+        nlong += (uint32_t)__popcll(mm);
+        if (in && hit) {
+            const uint32_t d = c.x, rel = (uint32_t)(d - s_lo);
+            const bool win = (s.cs[rel >> 5] >> (d & 31)) & 1u;
+            pull_hit(p, s, s_lo, seg, d, win, c.y, ws);
+            if (!win) flagged += first_visit(node[d]) == 2 ? 1u : 0u;
+        }
+        const bool surv = in && !hit && !more;
+        const unsigned long long sm = __ballot(surv);
+        if (sm) {
+            uint32_t sb = 0;
+            if (lane == 0) sb = atomicAdd(&s.sn, (uint32_t)__popcll(sm));
+            sb = __shfl(sb, 0, 64);
+            if (surv) p.sv[dst][seg + sb + (uint32_t)__popcll(sm & lanemask_lt())] = c;
+        }
+        tails += in ? 1u : 0u;
+    }
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t sub = lane & 7, grp = lane >> 3;
     constexpr uint32_t G8 = 8;
     uint4 c_n = make_uint4(0u, 0u, 0u, 0u);
     uint32_t len_n = 0;
     uint64_t off_n = 0;
-    if (grp < nq) {
+    if (grp < nlong) {
         c_n = src[seg + q[grp]];
         len_n = p.uin_len[c_n.x];
         off_n = p.uin_off[c_n.x];
     }
-    for (uint32_t e = grp; e < nq; e += G8) {
+    for (uint32_t e = grp; e < nlong; e += G8) {
         const uint4 c = c_n;
         const uint32_t len = len_n;
         const uint64_t off = off_n;
-        if (e + G8 < nq) {
+        if (e + G8 < nlong) {
             c_n = src[seg + q[e + G8]];
             len_n = p.uin_len[c_n.x];
             off_n = p.uin_off[c_n.x];
         }
         bool found = false;
-        for (uint32_t r = 2; r < len && !found; r += 8) {   // group-uniform
+        for (uint32_t r = 4; r < len && !found; r += 8) {   // group-uniform
             const uint32_t k = r + sub;
             const bool x = k < len && bit_of(p.front_rd, p.uin_src[off + k]);
             examined += (k < len) ? 1u : 0u;
@@ -980,12 +932,11 @@ __device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, 
             if (found) {
                 const uint32_t rel = (uint32_t)(d - s_lo);
                 const bool win = (s.cs[rel >> 5] >> (d & 31)) & 1u;
-                pull_hit(s, s_lo, d, win, c.y);
+                pull_hit(p, s, s_lo, seg, d, win, c.y, ws);
                 if (!win) flagged += first_visit(node[d]) == 2 ? 1u : 0u;
             } else {
                 p.sv[dst][seg + atomicAdd(&s.sn, 1u)] = c;
             }
-            ++tails;
         }
     }
 }
@@ -1020,15 +971,13 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
             s.wm[i] = 0;
         }
     }
-    if (threadIdx.x < kMaxIter) {
-        s.cw[threadIdx.x] = 0;
-        s.ce[threadIdx.x] = 0;
-        s.cl[threadIdx.x] = 0;
+    if (threadIdx.x == 0) {
+        s.sn = 0;
+        s.wn = 0;
     }
-    if (threadIdx.x == 0) s.sn = 0;
     __syncthreads();
     PROBE(L, 1);
-    TileAcc acc;
+    WinSum ws;
     // every wave streams its own 256-candidate runs (4 entries per lane) and scans its own tail
     // queue: no block barrier until the write-back
     const uint32_t wid = threadIdx.x >> 6;
@@ -1079,13 +1028,24 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
                 const uint32_t rel = d - (uint32_t)s_lo;
                 const uint32_t bit = 1u << (d & 31);
                 const bool win = (s.cs[rel >> 5] & bit) != 0;
-                atomicOr(&s.vm[rel >> 5], bit);
-                if (win) {
+                if (win) {   // a winner's visit bit is folded in from wm at the write-back
                     atomicOr(&s.wm[rel >> 5], bit);
-                    acc.add(s, rel / kPullTile, aux & 0x7FFFFFFFu);
+                    const uint32_t rl = aux & 0x7FFFFFFFu;
+                    ++ws.w;
+                    ws.e += rl ? 1u : 0u;
+                    ws.l += rl;
                 } else {
+                    atomicOr(&s.vm[rel >> 5], bit);
                     flagged += first_visit(node[d]) == 2 ? 1u : 0u;
                 }
+            }
+            const bool xw = hit && (aux & 0x7FFFFFFFu) && ((s.cs[(d - (uint32_t)s_lo) >> 5] >> (d & 31)) & 1u);
+            const unsigned long long xm = __ballot(xw);
+            if (xm) {
+                uint32_t xb = 0;
+                if (lane == 0) xb = atomicAdd(&s.wn, (uint32_t)__popcll(xm));
+                xb = __shfl(xb, 0, 64);
+                if (xw) p.wl[seg + xb + (uint32_t)__popcll(xm & lanemask_lt())] = d;
             }
             const unsigned long long tm = __ballot(tail);
             if (tail) wq[qn + __popcll(tm & lanemask_lt())] = i;
@@ -1104,7 +1064,7 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
         if (base + kCandBatch >= cnt) PROBE(L, 7);
         if (qn > kWaveTailCap - kWaveBatch || base + kCandBatch >= cnt) {
             __builtin_amdgcn_wave_barrier();
-            pull_tails(p, src, dst, node, s_lo, seg, wq, (FGI_EXP & 1) ? 0u : qn, s, flagged, examined_tail, tails);
+            pull_tails(p, src, dst, node, s_lo, seg, wq, (FGI_EXP & 1) ? 0u : qn, s, flagged, examined_tail, tails, ws);
             __builtin_amdgcn_wave_barrier();
             qn = 0;
         }
@@ -1119,32 +1079,25 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
         }
     }
     PROBE(L, 2);
-    acc.flush(s);
     __syncthreads();
     PROBE(L, 3);
-    // write back the owned words (visits before this level | this level's) and the per-tile counts
+    // write back the owned words (visits before this level | this level's)
     unsigned long long* vis64 = reinterpret_cast<unsigned long long*>(vis);
     unsigned long long* inv64 = reinterpret_cast<unsigned long long*>(p.inv_bm);
-    unsigned long long* lw64 = reinterpret_cast<unsigned long long*>(p.lw_bm);
     for (uint32_t i = threadIdx.x; i < wp.tpb * kTileWords; i += blockDim.x) {
         const uint64_t sl = s_lo + (uint64_t)i * 64;
         if (sl < p.n_slots) {
             const unsigned long long wm = s.wm[2 * i] | ((unsigned long long)s.wm[2 * i + 1] << 32);
-            vis64[sl >> 6] = s.vm[2 * i] | ((unsigned long long)s.vm[2 * i + 1] << 32);
+            vis64[sl >> 6] = wm | s.vm[2 * i] | ((unsigned long long)s.vm[2 * i + 1] << 32);
             if (wm) inv64[sl >> 6] |= wm;
-            lw64[sl >> 6] = wm;
         }
     }
-    for (uint32_t k = threadIdx.x; k < wp.tpb; k += blockDim.x) {
-        const uint64_t t = (uint64_t)b * wp.tpb + k;
-        if (t < wp.n_tiles) p.tiles[t] = PullTile{s.cw[k], s.ce[k], s.cl[k]};
-        bs[0] += s.cw[k];
-        bs[1] += s.ce[k];
-        bs[2] += s.cl[k];
-    }
+    bs[0] = ws.w;
+    bs[1] = ws.e;
+    bs[2] = ws.l;
     if (threadIdx.x == 0) p.sv_cnt[dst][b] = s.sn;
     // the tail probes, flag counts, live and head probes are per lane; the winners are the per-thread
-    // tile sums (bs[0]); the scanned count is the block's list length
+    // sums (bs[0]); the scanned count is the block's list length
     const uint32_t v[kStats] = {0, flagged, threadIdx.x == 0 ? s.sn : 0u, examined_tail + examined,
                                 live, (uint32_t)bs[0], tails, threadIdx.x == 0 ? cnt : 0u};
     block_stats_add(blk, s_st, v);
@@ -1262,30 +1215,26 @@ __global__ __launch_bounds__(kBlock) void k_apply_recv(int L, uint64_t n, const 
 }
 
 // ---- final collect: the invalidated bitmap -> the invalidated list -----------------------------
-// One pass with a decoupled look-back: a block takes a ticket (its place in the order — a lower
-// ticket belongs to a block that is already running), counts the set bits of its 64-bit words
-// [t * wpb, (t + 1) * wpb), publishes the count, then adds up its predecessors' counts or, at the
-// first one that has it, their inclusive prefix (one wave, 64 predecessors per step), publishes its
-// own inclusive prefix and writes every set bit's handle at that offset, in ascending order: one
-// 1,024-handle tile per wave, 16 handles per lane, staged in LDS and stored coalesced. Status words
-// carry the launch's epoch (bits 48-63) and a flag (bit 46 count, bit 47 prefix), so they need no
-// reset; the last ticket resets the ticket counter. Tickets 0..kStats-1 also fold the per-block
+// One pass, launched cooperatively (every block resident, so waiting on another block cannot
+// deadlock; a ticket counter would serialise ~1,000 atomics on one word): block t counts the set
+// bits of its 64-bit words [t * wpb, (t + 1) * wpb), publishes the count, adds up its
+// predecessors' counts (all of them at once) and writes every set bit's handle at that offset, in
+// ascending order: one 1,024-handle tile per wave, 16 handles per lane, staged in LDS and stored
+// coalesced. Status words carry the launch's epoch (bits 48-63) and a flag (bit 46), so they need
+// no reset. Tickets 0..kStats-1 also fold the per-block
 // statistics into the wave counters (one column each, coalesced sweeps).
-constexpr unsigned long long kStAgg = 1ull << 46, kStInc = 1ull << 47, kStVal = kStAgg - 1;
+constexpr unsigned long long kStAgg = 1ull << 46, kStVal = kStAgg - 1;
+constexpr uint32_t kFinalStage = 1024;   // bitmap words a block keeps in LDS (8 KB)
 
 __global__ __launch_bounds__(kBlock) void k_final(const unsigned long long* __restrict__ inv64, uint64_t words,
-                                                  uint64_t wpb, unsigned long long* status, unsigned long long* ticket,
-                                                  uint32_t epoch, WaveCtr* ctr, const unsigned long long* __restrict__ blk,
-                                                  uint32_t* out) {
+                                                  uint64_t wpb, unsigned long long* status, uint32_t epoch, WaveCtr* ctr,
+                                                  const unsigned long long* __restrict__ blk, uint32_t* out) {
     __shared__ unsigned long long s_red[kBlock / 64];
     __shared__ unsigned long long s_excl;
-    __shared__ uint32_t s_t;
     __shared__ uint32_t s_w[kBlock / 64];
     __shared__ uint32_t s_stage[kBlock / 64][kPullTile];
-    if (threadIdx.x == 0)
-        s_t = (uint32_t)__hip_atomic_fetch_add(ticket, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();
-    const uint32_t t = s_t;
+    __shared__ unsigned long long s_words[kFinalStage];   // the block's words, read once
+    const uint32_t t = blockIdx.x;
     const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
     if (t < (uint32_t)kStats) {
         const int k = t;
@@ -1300,36 +1249,28 @@ __global__ __launch_bounds__(kBlock) void k_final(const unsigned long long* __re
     }
     const uint64_t lo = t * wpb, hi = std::min<uint64_t>(words, lo + wpb);
     unsigned long long c = 0;
-    for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x) c += (unsigned long long)__popcll(inv64[w]);
-    c = block_sum(c, s_red);
+    for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x) {
+        const unsigned long long v = inv64[w];
+        if (w - lo < kFinalStage) s_words[w - lo] = v;
+        c += (unsigned long long)__popcll(v);
+    }
+    c = block_sum(c, s_red);   // (its barriers also publish s_words)
     const unsigned long long ep = (unsigned long long)epoch << 48;
-    if (threadIdx.x == 0) coh_xchg(status + t, ep | (t == 0 ? kStInc : kStAgg) | c);
-    if (wid == 0) {
-        unsigned long long excl = 0;
-        for (int64_t j = (int64_t)t - 1; j >= 0; j -= 64) {   // wave-uniform
-            const int64_t k = j - (int64_t)lane;               // lane 0: the nearest predecessor
-            unsigned long long v = kStInc | ep;                // below ticket 0: an empty prefix
-            if (k >= 0) {
-                do {
-                    v = coh_read(status + k);
-                } while ((v & ~((1ull << 48) - 1)) != ep || !(v & (kStAgg | kStInc)));
-            }
-            const unsigned long long inc = __ballot((v & kStInc) != 0);
-            const uint32_t upto = inc ? (uint32_t)__ffsll((long long)inc) - 1 : 63u;
-            unsigned long long x = (lane <= upto) ? (v & kStVal) : 0ull;
-#pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) x += __shfl_xor(x, d, 64);
-            excl += x;
-            if (inc) break;
-        }
-        if (lane == 0) {
-            s_excl = excl;
-            if (t > 0) coh_xchg(status + t, ep | kStInc | (excl + c));
-            if (t == gridDim.x - 1) {
-                ctr->inv = excl + c;
-                coh_xchg(ticket, 0ull);   // every ticket is taken
-            }
-        }
+    if (threadIdx.x == 0) coh_xchg(status + t, ep | kStAgg | c);
+    // every predecessor's count, read by all threads in one round (atomic loads at agent scope:
+    // served where the XCDs agree, without serialising like read-modify-writes on one word)
+    unsigned long long part = 0;
+    for (uint32_t k = threadIdx.x; k < t; k += blockDim.x) {
+        unsigned long long v;
+        do {
+            v = __hip_atomic_load(status + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } while ((v & ~((1ull << 48) - 1)) != ep);
+        part += v & kStVal;
+    }
+    const unsigned long long excl = block_sum(part, s_red);
+    if (threadIdx.x == 0) {
+        s_excl = excl;
+        if (t == gridDim.x - 1) ctr->inv = excl + c;
     }
     __syncthreads();
     const uint16_t* bits16 = reinterpret_cast<const uint16_t*>(inv64);
@@ -1338,7 +1279,10 @@ __global__ __launch_bounds__(kBlock) void k_final(const unsigned long long* __re
     for (uint64_t w0 = lo; w0 < hi; w0 += (uint64_t)(blockDim.x >> 6) * kTileWords) {   // block-uniform
         const uint64_t tw = w0 + (uint64_t)wid * kTileWords;                            // the wave's first word
         const uint64_t q = tw * 4 + lane;                                                // the lane's 16-bit chunk
-        const uint32_t m = (tw + lane / 4 < hi) ? (uint32_t)bits16[q] : 0u;
+        const uint64_t wl = tw - lo + lane / 4;
+        const uint32_t m = (tw + lane / 4 >= hi) ? 0u
+                           : wl < kFinalStage ? (uint32_t)(s_words[wl] >> (16 * (lane & 3))) & 0xFFFFu
+                                              : (uint32_t)bits16[q];
         uint32_t tot;
         const uint32_t ex = wave_excl_scan((uint32_t)__popc(m), tot);
         __syncthreads();
@@ -1353,6 +1297,166 @@ __global__ __launch_bounds__(kBlock) void k_final(const unsigned long long* __re
         for (uint32_t mm = m; mm; mm &= mm - 1) s_stage[wid][o++] = (uint32_t)(q * 16 + (uint32_t)(__ffs(mm) - 1));
         __builtin_amdgcn_wave_barrier();
         for (uint32_t i = lane; i < tot; i += 64) out[run + before + i] = s_stage[wid][i];
+        __builtin_amdgcn_wave_barrier();
+        run += all;
+    }
+}
+
+// ---- a whole (push-only) wave in one launch ---------------------------------------------------
+// Streaming batches (fgi_run_batch) queue mutation steps and waves back to back and synchronise once
+// at the end, so their waves cannot come back to the host between levels. A cooperative grid (every
+// block resident) runs the roots (immediate ones first), every level and the final collect, with a
+// grid barrier where run_wave has a kernel boundary. The root count may be read from the device
+// (roots produced by an earlier step). The invalidated handles are appended at out[*out_n ..) in
+// ascending order and *out_n advanced; acc accumulates the batch's totals.
+enum : int { kAccWaves, kAccLevels, kAccInv, kAccETrav, kAccEMatch, kAccFlagged, kAccFTotal, kAccN };
+static_assert(kAccN <= kAccCount, "batch accumulators");
+
+struct CoopArgs {
+    const uint32_t* roots;
+    const uint8_t* imm;
+    uint32_t n_max;
+    const unsigned long long* n_dev;   // nullable: n_max roots
+    unsigned long long* node;
+    uint32_t* vis;
+    uint32_t* inv_bm;
+    const uint64_t* row_off;
+    const uint32_t* row_len;
+    uint32_t* fr_off[2];
+    uint32_t* fr_len[2];
+    uint64_t* escan[2];
+    uint32_t* cstart[2];
+    const uint32_t* pool_col;
+    const uint64_t* pool_tag;
+    int dead_filter;
+    uint32_t n_handles;
+    WaveCtr* ctr;
+    unsigned long long* blk;
+    unsigned long long* cnt;           // [grid] final collect counts
+    uint32_t* out;
+    unsigned long long* out_n;
+    unsigned long long* acc;           // [kAccN]
+    const unsigned long long* abort;   // nullable: a batch's abort word (set: the wave does nothing)
+};
+
+__global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
+    cooperative_groups::grid_group grid = cooperative_groups::this_grid();
+    __shared__ __align__(16) uint32_t s_x[kChunkEmitCap + 8];
+    uint32_t* s_rel = s_x;
+    uint32_t* s_base = s_x + kChunk + 4;
+    __shared__ Emit em;
+    __shared__ MsgEmit<false> me;
+    __shared__ unsigned long long s_st[kBlock / 64][kStats];
+    __shared__ unsigned long long s_red[kBlock / 64];
+    __shared__ unsigned long long s_ft, s_base_out;
+    __shared__ uint32_t s_w[kBlock / 64];
+    __shared__ unsigned long long s_words[kFinalStage];
+    // uniform across the grid: the word is written before the launch and not during it
+    if (a.abort && __hip_atomic_load(a.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+    WaveCtr* ctr = a.ctr;
+    const uint32_t n = a.n_dev ? (uint32_t)std::min<unsigned long long>(*a.n_dev, a.n_max) : a.n_max;
+    const uint32_t gsize = gridDim.x * blockDim.x;
+    const Out o0{a.row_off, a.row_len, a.inv_bm, a.fr_off[0], a.fr_len[0], a.escan[0], a.cstart[0], &ctr->lvl[0]};
+    if (a.imm) {   // Invalidate(true) roots first: their CAS may change node words
+        for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gsize)
+            root_step<1>(i0 + threadIdx.x, a.roots, a.imm, n, 0u, a.n_handles, a.node, a.vis, o0, ctr);
+        grid.sync();
+    }
+    for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gsize)
+        root_step<0>(i0 + threadIdx.x, a.roots, a.imm, n, 0u, a.n_handles, a.node, a.vis, o0, ctr);
+    uint64_t levels = 0, e_trav = 0, f_total = 0;
+    for (int L = 0;; ++L) {
+        grid.sync();   // level L's frontier (and its counter) is complete
+        if (threadIdx.x == 0) s_ft = coh_read(&ctr->lvl[L % kRing].ft);
+        __syncthreads();
+        const uint64_t F = s_ft >> 32, T = s_ft & 0xFFFFFFFFull;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            ctr->lvl[L % kRing].F = F;
+            ctr->lvl[L % kRing].T = T;
+        }
+        // level L + 1's counter accumulates during this level; L + 2's is cleared for the next one
+        if (blockIdx.x == 0 && threadIdx.x < sizeof(LevelCtr) / 8)
+            reinterpret_cast<unsigned long long*>(&ctr->lvl[(L + 2) % kRing])[threadIdx.x] = 0ull;
+        if (F == 0) break;
+        ++levels;
+        e_trav += T;
+        f_total += F;
+        const int buf = L & 1;
+        const ExpandArgs x{a.fr_off[buf], a.escan[buf], a.cstart[buf], a.pool_col, a.pool_tag, a.dead_filter};
+        const Out o{a.row_off, a.row_len,        a.inv_bm, a.fr_off[buf ^ 1], a.fr_len[buf ^ 1],
+                    a.escan[buf ^ 1], a.cstart[buf ^ 1], &ctr->lvl[(L + 1) % kRing]};
+        emit_init(em);
+        expand_level<false>(F, T, level_mult(T, gridDim.x), x, a.node, a.vis, o, em, s_x, me, s_rel, s_base, a.blk,
+                            s_st, RemoteArgs{});
+    }
+    // final collect (as k_final, with a grid barrier instead of waiting on status words)
+    const uint64_t words = ((uint64_t)a.n_handles + 63) / 64;
+    const uint64_t wpb = (words + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = std::min<uint64_t>(words, blockIdx.x * wpb), hi = std::min<uint64_t>(words, lo + wpb);
+    const unsigned long long* inv64 = reinterpret_cast<const unsigned long long*>(a.inv_bm);
+    if (threadIdx.x == 0) s_base_out = *a.out_n;   // advanced only after the barrier below
+    if (blockIdx.x < (uint32_t)kStats) {
+        const int k = blockIdx.x;
+        unsigned long long* dst[kStats] = {&ctr->e_match,   &ctr->n_flagged, &ctr->pull_surv, &ctr->pull_edges,
+                                           &ctr->pull_live, &ctr->pull_win,  &ctr->pull_tail, &ctr->pull_scan};
+        const unsigned long long* col = a.blk + (uint64_t)k * kStatBlocks;
+        unsigned long long x = 0;
+        for (uint32_t q = threadIdx.x; q < kStatBlocks; q += blockDim.x) x += col[q];
+        x = block_sum(x, s_red);
+        if (threadIdx.x == 0) {
+            const unsigned long long v = x + (k == kStFlagged ? ctr->root_flagged : 0ull);
+            *dst[k] = v;
+            if (k == kStEMatch) atomicAdd(a.acc + kAccEMatch, v);
+            if (k == kStFlagged) atomicAdd(a.acc + kAccFlagged, v);
+        }
+    }
+    unsigned long long c = 0;
+    for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x) {
+        const unsigned long long v = inv64[w];
+        if (w - lo < kFinalStage) s_words[w - lo] = v;
+        c += (unsigned long long)__popcll(v);
+    }
+    c = block_sum(c, s_red);
+    if (threadIdx.x == 0) coh_xchg(a.cnt + blockIdx.x, c);
+    grid.sync();
+    unsigned long long part = 0;
+    for (uint32_t k = threadIdx.x; k < blockIdx.x; k += blockDim.x) part += coh_read(a.cnt + k);
+    const unsigned long long excl = block_sum(part, s_red);
+    if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 0) {
+        ctr->inv = excl + c;
+        *a.out_n = s_base_out + excl + c;
+        a.acc[kAccWaves] += 1;
+        a.acc[kAccLevels] += levels;
+        a.acc[kAccInv] += excl + c;
+        a.acc[kAccETrav] += e_trav;
+        a.acc[kAccFTotal] += f_total;
+    }
+    const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
+    const uint16_t* bits16 = reinterpret_cast<const uint16_t*>(inv64);
+    uint64_t run = s_base_out + excl;
+    for (uint64_t w0 = lo; w0 < hi; w0 += (uint64_t)(blockDim.x >> 6) * kTileWords) {   // block-uniform
+        const uint64_t tw = w0 + (uint64_t)wid * kTileWords;
+        const uint64_t q = tw * 4 + lane;
+        const uint64_t wl = tw - lo + lane / 4;
+        const uint32_t m = (tw + lane / 4 >= hi) ? 0u
+                           : wl < kFinalStage ? (uint32_t)(s_words[wl] >> (16 * (lane & 3))) & 0xFFFFu
+                                              : (uint32_t)bits16[q];
+        uint32_t tot;
+        const uint32_t ex = wave_excl_scan((uint32_t)__popc(m), tot);
+        __syncthreads();
+        if (lane == 0) s_w[wid] = tot;
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+        for (uint32_t k = 0; k < blockDim.x / 64; ++k) {
+            if (k < wid) before += s_w[k];
+            all += s_w[k];
+        }
+        // the chunk map's LDS is free now: one 1,024-handle tile per wave
+        uint32_t* stage = s_x + wid * kPullTile;
+        uint32_t o = ex;
+        for (uint32_t mm = m; mm; mm &= mm - 1) stage[o++] = (uint32_t)(q * 16 + (uint32_t)(__ffs(mm) - 1));
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i = lane; i < tot; i += 64) a.out[run + before + i] = stage[i];
         __builtin_amdgcn_wave_barrier();
         run += all;
     }
@@ -1486,10 +1590,9 @@ Out out_for(fgi_graph* g, int buf, LevelCtr* ln) {
 
 CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, const WaveParams& wp, int buf) {
     CollectArgs c;
-    c.tiles = g->tiles;
-    c.lw = g->lw_bm;
-    c.n_slots = n_slots;
-    c.n_handles = g->n_handles;
+    (void)n_slots;
+    c.wl = g->wl;
+    c.seg = g->cand_seg;
     c.row_len = g->row_len;
     c.row_off = g->row_off;
     c.pre = g->bsum + 3ull * wp.grid;
@@ -1504,11 +1607,11 @@ CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, const WaveParams& wp, i
     return c;
 }
 
-// k_collect walks the pull grid's blocks in a grid-stride loop: two blocks per CU keep the (usual)
-// no-op launch cheap
+// k_collect: one wave per pull block (a grid-stride loop covers any grid)
 uint32_t collect_grid(const fgi_graph* g, const WaveParams& wp) {
-    const uint32_t cap = 2 * std::max<uint32_t>(g->n_cu, 1);
-    return std::max<uint32_t>(1, std::min<uint32_t>(wp.grid, cap));
+    (void)g;
+    constexpr uint32_t W = kCollectThreads / 64;
+    return std::max<uint32_t>(1, (wp.grid + W - 1) / W);
 }
 
 PullArgs pull_args(fgi_graph* g, uint32_t n_slots, const uint32_t* front_rd) {
@@ -1519,10 +1622,9 @@ PullArgs pull_args(fgi_graph* g, uint32_t n_slots, const uint32_t* front_rd) {
     p.uin_src = g->uin_src;
     p.front_rd = front_rd;
     p.inv_bm = g->inv_bm;
-    p.lw_bm = g->lw_bm;
+    p.wl = g->wl;
     p.cls = g->cls_bm;
     p.hot_bm = g->hot_bm;
-    p.tiles = g->tiles;
     p.bsum = g->bsum;
     p.cand_seg = g->cand_seg;
     p.c[0] = g->cand;
@@ -1539,17 +1641,27 @@ ExpandArgs expand_args(fgi_graph* g, int buf) {
 }
 
 // the invalidated bitmap -> the invalidated list and V_inv (ctr->inv)
-void launch_final(fgi_graph* g, uint32_t n_handles) {
-    const uint64_t words = ((uint64_t)n_handles + 63) / 64;
-    const uint32_t G = (uint32_t)std::min<uint64_t>(kFinalBlocks, std::max<uint64_t>(kStats, (words + 255) / 256));
-    const uint64_t wpb = (words + G - 1) / G;
+hipError_t launch_final(fgi_graph* g, uint32_t n_handles) {
+    uint64_t words = ((uint64_t)n_handles + 63) / 64;
+    static int per_cu = 0;
+    if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_final, kBlock, 0) != hipSuccess || per_cu < 1))
+        per_cu = 1;
+    const uint64_t resident = (uint64_t)per_cu * (uint64_t)std::max(g->n_cu, 1);
+    uint32_t G = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(kFinalBlocks, resident),
+                                               std::max<uint64_t>(kStats, (words + 255) / 256));
+    G = std::max<uint32_t>(G, (uint32_t)kStats);
+    uint64_t wpb = (words + G - 1) / G;
     const auto* inv64 = reinterpret_cast<const unsigned long long*>(g->inv_bm);
-    // status words and the ticket apart from the pull prefixes a collect may still read
+    // status words apart from the pull prefixes a collect may still read
     unsigned long long* st = g->bsum + 6ull * kStatBlocks;
     g->final_epoch = (g->final_epoch + 1) & 0xFFFFu;
     if (g->final_epoch == 0) g->final_epoch = 1;
-    hipLaunchKernelGGL(k_final, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb, st, st + kStatBlocks,
-                       g->final_epoch, g->ctr, g->blk_stats, g->inv);
+    uint32_t ep = g->final_epoch;
+    WaveCtr* ctr = g->ctr;
+    const unsigned long long* blk = g->blk_stats;
+    uint32_t* out = g->inv;
+    void* args[] = {&inv64, &words, &wpb, &st, &ep, &ctr, &blk, &out};
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_final), dim3(G), dim3(kBlock), args, 0, g->stream);
 }
 
 void launch_roots(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev, uint32_t base,
@@ -1565,6 +1677,57 @@ void launch_roots(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, con
 }
 
 }  // namespace
+
+// One push-only wave in a single cooperative launch (k_wave_coop): no host synchronisation. The roots
+// (n_max, or *n_dev of them) are device-resident; the invalidated handles are appended at
+// out[*out_n ..). Node words are folded by the next call that needs them (v_dirty).
+fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev, const uint8_t* imm_dev,
+                         const unsigned long long* n_dev, uint32_t* out, unsigned long long* out_n,
+                         unsigned long long* acc, const unsigned long long* abort) {
+    hipStream_t s = g->stream;
+    FGI_TRY(ensure_cstart(g, std::max<uint64_t>(g->pool_top, g->pool_cap)));
+    static int per_cu = 0;
+    if (per_cu == 0 &&
+        (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wave_coop, kBlock, 0) != hipSuccess || per_cu < 1))
+        per_cu = 1;
+    // one block per CU: enough for the waves this path serves, and a cheaper grid barrier
+    const uint32_t G = std::max<uint32_t>((uint32_t)kStats, (uint32_t)std::max(g->n_cu, 1));
+    if ((uint64_t)G > (uint64_t)per_cu * (uint64_t)std::max(g->n_cu, 1))
+        return set_err(g, FGI_ENOTSUP, "cooperative wave: %u blocks cannot be resident", G);
+    hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm, (uint64_t)g->bm_words);
+    CoopArgs a{};
+    a.roots = roots_dev;
+    a.imm = imm_dev;
+    a.n_max = n_max;
+    a.n_dev = n_dev;
+    a.node = reinterpret_cast<unsigned long long*>(g->node);
+    a.vis = g->vis_bm;
+    a.inv_bm = g->inv_bm;
+    a.row_off = g->row_off;
+    a.row_len = g->row_len;
+    for (int k = 0; k < 2; ++k) {
+        a.fr_off[k] = g->fr_off[k];
+        a.fr_len[k] = g->fr_len[k];
+        a.escan[k] = g->escan[k];
+        a.cstart[k] = g->cstart[k];
+    }
+    a.pool_col = g->pool_col;
+    a.pool_tag = g->pool_tag;
+    a.dead_filter = g->opt_dead_filter;
+    a.n_handles = g->n_handles;
+    a.ctr = g->ctr;
+    a.blk = g->blk_stats;
+    a.cnt = g->bsum + 5ull * kStatBlocks;   // apart from the pull prefixes and k_final's status words
+    a.out = out;
+    a.out_n = out_n;
+    a.acc = acc;
+    a.abort = abort;
+    void* args[] = {&a};
+    FGI_HIP(g, hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_wave_coop), dim3(G), dim3(kBlock), args, 0, s));
+    g->v_dirty = true;
+    if (imm_dev) note_words(g);
+    return FGI_OK;
+}
 
 #if FGI_PROBE
 // per level: kernel span, dispatch skew, and per-phase medians / maxima over the blocks (us)
@@ -1667,7 +1830,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                                out_for(g, buf ^ 1, nullptr), g->ctr, g->blk_stats, g->done, RemoteArgs{});
             if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L + 1], s));
         }
-        launch_final(g, g->n_handles);   // idempotent: repeated if the wave goes on
+        FGI_HIP(g, launch_final(g, g->n_handles));   // idempotent: repeated if the wave goes on
         final_done = true;
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
@@ -1720,7 +1883,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         }
     }
     if (!final_done) {   // no roots
-        launch_final(g, g->n_handles);
+        FGI_HIP(g, launch_final(g, g->n_handles));
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
         FGI_HIP(g, hipStreamSynchronize(s));
@@ -1871,7 +2034,7 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
         }
         last_pull = pull;
     }
-    launch_final(g, pv.n_local);
+    FGI_HIP(g, launch_final(g, pv.n_local));
     FGI_HIP(g, hipGetLastError());
     FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
     FGI_HIP(g, hipEventRecord(g->ev_w1, s));

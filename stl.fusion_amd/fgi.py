@@ -55,6 +55,23 @@ class WaveStats(C.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class Step(C.Structure):
+    _fields_ = [("kind", C.c_uint32), ("n", C.c_uint32), ("handles", C.c_void_p), ("used", C.c_void_p),
+                ("version", C.c_void_p), ("flags", C.c_void_p), ("out", C.c_void_p)]
+
+
+class BatchStats(C.Structure):
+    _fields_ = [("waves", C.c_uint64), ("levels", C.c_uint64), ("v_inv", C.c_uint64), ("e_trav", C.c_uint64),
+                ("e_match", C.c_uint64), ("n_flagged", C.c_uint64), ("kernel_ms", C.c_double),
+                ("wave_ms", C.c_double), ("total_ms", C.c_double), ("host_syncs", C.c_uint32), ("pad", C.c_uint32)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad"}
+
+
+STEP_INVALIDATE, STEP_BEGIN_COMPUTE, STEP_ADD_USED, STEP_SET_OUTPUT = 1, 2, 3, 4
+
+
 class PruneStats(C.Structure):
     _fields_ = [("old_edges", C.c_uint64), ("new_edges", C.c_uint64), ("pool_before", C.c_uint64),
                 ("pool_after", C.c_uint64), ("kernel_ms", C.c_double)]
@@ -102,6 +119,7 @@ SIGNATURES = {
     "fgi_part_init_local": [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32],
     "fgi_part_local_invalidate": [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32, _u32p, _u8p, C.POINTER(WaveStats)],
     "fgi_rccl_info": [C.POINTER(C.c_int), C.c_char_p, C.c_uint64],
+    "fgi_run_batch": [_G, C.c_uint32, C.POINTER(Step), _u32p, C.c_uint64, _u64p, C.POINTER(BatchStats)],
 }
 
 _lib = None
@@ -284,6 +302,62 @@ class Graph:
                                             _ptr(ids, C.c_uint32), len(ids), C.byref(n),
                                             C.byref(stats) if stats is not None else None), "invalidate")
         return ids[:n.value].copy()
+
+    def run_batch(self, steps, stats: Optional[BatchStats] = None, want_ids: bool = True):
+        """fgi_run_batch. `steps`: a list of ("invalidate", handles[, immediately]),
+        ("begin_compute", slots, versions[, has_delay]), ("add_used", dependants, used),
+        ("set_output", handles). Returns (ids of every cascade of the batch, per-step outputs: detached
+        handles / add_used results / set flags, None for invalidate)."""
+        arr = (Step * len(steps))()
+        keep, outs = [], []
+        for k, sp in enumerate(steps):
+            kind = sp[0]
+            h = _u32(sp[1])
+            keep.append(h)
+            st = arr[k]
+            st.n = len(h)
+            st.handles = h.ctypes.data
+            out = None
+            if kind == "invalidate":
+                st.kind = STEP_INVALIDATE
+                if len(sp) > 2 and sp[2] is not None:
+                    f = _u8(sp[2])
+                    keep.append(f)
+                    st.flags = f.ctypes.data
+            elif kind == "begin_compute":
+                st.kind = STEP_BEGIN_COMPUTE
+                v = _u64(sp[2])
+                keep.append(v)
+                st.version = v.ctypes.data
+                if len(sp) > 3 and sp[3] is not None:
+                    f = _u8(sp[3])
+                    keep.append(f)
+                    st.flags = f.ctypes.data
+                out = np.zeros(len(h), np.uint32)
+            elif kind == "add_used":
+                st.kind = STEP_ADD_USED
+                u = _u32(sp[2])
+                keep.append(u)
+                st.used = u.ctypes.data
+                out = np.zeros(len(h), np.uint32)
+            elif kind == "set_output":
+                st.kind = STEP_SET_OUTPUT
+                out = np.zeros(len(h), np.uint8)
+            else:
+                raise ValueError(kind)
+            if out is not None:
+                st.out = out.ctypes.data
+            outs.append(out)
+        n = C.c_uint64()
+        if want_ids:
+            cap = max(1, sum(1 for sp in steps if sp[0] != "add_used")) * self.n_handles
+            ids = np.zeros(cap, np.uint32)
+            self._check(self.lib.fgi_run_batch(self.h, len(steps), arr, _ptr(ids, C.c_uint32), cap, C.byref(n),
+                                               C.byref(stats) if stats is not None else None), "run_batch")
+            return ids[:n.value].copy(), outs
+        self._check(self.lib.fgi_run_batch(self.h, len(steps), arr, None, 0, C.byref(n),
+                                           C.byref(stats) if stats is not None else None), "run_batch")
+        return n.value, outs
 
     def invalidate_into(self, roots, out_ptr: int, cap: int, stats: Optional[WaveStats] = None) -> int:
         """fgi_invalidate with a caller-owned host output buffer (e.g. pinned memory at out_ptr,

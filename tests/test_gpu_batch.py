@@ -1,0 +1,143 @@
+"""fgi_run_batch (streaming batches) against the oracle.
+
+(a) The streaming mix (BASELINE.json configs[4], workloads.StreamMix) with one batch per round:
+    timers (Invalidate(true)) -> begin_compute(hubs) -> set_output(hubs) -> begin_compute(leaves) ->
+    add_used(leaves -> hubs) -> set_output(leaves) -> the round's hub wave, checked round by round
+    (every node word, every cascade's ids) against the oracle applying the same calls one by one.
+(b) Every behaviour scenario of tests/test_oracle_scenarios.py with each engine call made as a
+    one-step batch (displacement and InvalidateOnSetOutput cascades included).
+(c) A batch whose add_used step outgrows the pool headroom (the call grows the pool and resumes).
+(d) A batch that runs out of detached handles: FGI_ECAPACITY, the steps before it applied.
+"""
+import functools
+
+import numpy as np
+import pytest
+
+import fgo as O
+import test_oracle_scenarios as S
+from harness import assert_states_equal, build_pair
+from test_gpu_scenarios import SCENARIOS, EngineOracle
+from test_gpu_stream import _mix, _oracle_round
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("hubs,leaves,k,delay_pct", [(40, 30, 4, 10), (64, 200, 8, 5), (7, 1, 7, 50)])
+def test_stream_mix_batches_match_oracle(pkg, gpu_available, hubs, leaves, k, delay_pct):
+    mix = _mix(pkg, hubs, leaves, k, delay_pct, 0x5EED00E0)
+    n = mix.n
+    used, dep, tag = mix.initial_edges()
+    g, o = build_pair(pkg, n, mix.version.copy(), mix.state_flags(), used, dep, tag)
+    prev = np.zeros(0, np.uint32)
+    for r in range(8):
+        timers, hs, ls = mix.plan(prev)
+        vh = mix.new_versions(hs).copy()
+        vl = mix.new_versions(ls).copy()
+        t_oracle = _oracle_round(o, mix, timers, hs, ls, vh, vl)
+        roots = mix.roots(r)
+        o.clear_log()
+        o.invalidate_slots(roots)
+        w_oracle = o.inv_log()
+        steps = []
+        if len(timers):
+            steps.append(("invalidate", timers, np.ones(len(timers), np.uint8)))
+        steps += [("begin_compute", hs, vh), ("set_output", hs), ("begin_compute", ls, vl, mix.has_delay[ls]),
+                  ("add_used", ls, mix.hub_of(ls)), ("set_output", ls), ("invalidate", roots)]
+        st = pkg.fgi.BatchStats()
+        ids, outs = g.run_batch(steps, stats=st)
+        assert st.host_syncs <= 2, st.as_dict()
+        res = outs[-3]
+        assert np.all(res == pkg.fgi.USED_ADDED)
+        assert np.all(outs[-2] == 1)
+        # cascades in step order: timers, (empty displacement / IOSO cascades), the hub wave
+        want = np.concatenate([np.sort(t_oracle), np.sort(w_oracle)]).astype(np.uint32)
+        assert np.array_equal(ids, want), f"round {r}"
+        assert st.v_inv == len(want)
+        assert_states_equal(g, o, n)
+        prev = roots
+    g.close()
+    o.close()
+
+
+class BatchEngineOracle(EngineOracle):
+    """EngineOracle whose engine calls are one-step batches."""
+
+    def begin_compute(self, slot, version, has_delay=False, stats=None):
+        old = self.slot_last.get(slot)
+        ids, outs = self.g.run_batch([("begin_compute", [slot], [version], [int(has_delay)])])
+        self._log(ids)
+        det = int(outs[0][0])
+        if old is not None and det != O.NONE:
+            self.nodes[old][3] = det
+            self.home[det] = slot
+        self.nodes.append([slot, version, bool(has_delay), slot])
+        nid = len(self.nodes) - 1
+        self.slot_last[slot] = nid
+        return nid, (old if old is not None else O.NONE)
+
+    def set_output(self, h, stats=None):
+        ids, outs = self.g.run_batch([("set_output", [self.nodes[h][3]])])
+        self._log(ids)
+        return int(outs[0][0])
+
+    def add_used(self, dependant_h, used_h):
+        _, outs = self.g.run_batch([("add_used", [self.nodes[dependant_h][3]], [self.nodes[used_h][3]])])
+        return int(outs[0][0])
+
+    def invalidate_slots(self, slots, immediately=None, threads=1, stats=None):
+        self._log(self.g.run_batch([("invalidate", slots, immediately)])[0])
+
+    def invalidate_nodes(self, handles, immediately=None, stats=None):
+        self._log(self.g.run_batch([("invalidate", [self.nodes[h][3] for h in handles], immediately)])[0])
+
+
+@pytest.mark.parametrize("scenario", SCENARIOS, ids=[f.__name__[5:] for f in SCENARIOS])
+def test_scenarios_as_batches(pkg, gpu_available, scenario):
+    scenario(W=functools.partial(S.World, make=lambda n: BatchEngineOracle(pkg, n)))
+
+
+def test_batch_grows_the_pool(pkg, gpu_available):
+    """Used node 0 holds 3M entries in a full row; one batch adds a dependant to it, which needs a
+    relocation larger than the call's headroom: the batch grows the pool, finishes the step and
+    the remaining steps, with the same result as the single calls."""
+    n = 3_000_010
+    ver = O.version_of(11, np.arange(n))
+    flags = np.full(n, 1, np.uint32)
+    src = np.zeros(n - 10, np.uint32)
+    dst = np.arange(10, n, dtype=np.uint32)
+    states = []
+    for use_batch in (False, True):
+        g = pkg.Graph(n, n_detached=16)
+        g.register_nodes(np.arange(n, dtype=np.uint32), ver, flags)
+        g.load_edges(src, dst, ver[dst])
+        if use_batch:
+            st = pkg.fgi.BatchStats()
+            ids, outs = g.run_batch([("begin_compute", [5], [ver[5] + 2]), ("add_used", [5], [0]),
+                                     ("set_output", [5]), ("invalidate", [0])], stats=st)
+            assert st.host_syncs >= 2
+            assert outs[1][0] == pkg.fgi.USED_ADDED
+            assert ids[0] == 5                       # the displacement cascade of step 0
+            ids = ids[1:]                            # the last step's wave
+        else:
+            g.begin_compute([5], [ver[5] + 2])
+            assert g.add_used([5], [0])[0] == pkg.fgi.USED_ADDED
+            g.set_output([5])
+            ids = g.invalidate([0])
+        states.append((np.sort(ids), g.dump_states()))
+        g.close()
+    assert np.array_equal(states[0][0], states[1][0]) and len(states[0][0]) == n - 10 + 2
+    assert np.array_equal(states[0][1][0], states[1][1][0]) and np.array_equal(states[0][1][1], states[1][1][1])
+
+
+def test_batch_out_of_detached_handles(pkg, gpu_available):
+    g = pkg.Graph(8, n_detached=1)
+    g.register_nodes(np.arange(8, dtype=np.uint32), np.arange(8, dtype=np.uint64) * 2 + 1,
+                     np.zeros(8, np.uint32))   # all Computing: a new computation detaches them
+    with pytest.raises(pkg.fgi.FgiError) as e:
+        g.run_batch([("set_output", [7]), ("begin_compute", [0, 1], [101, 103])])
+    assert e.value.status == 3
+    v, f = g.get_state([7, 0, 1])
+    assert (f[0] & 3) == 1                  # step 0 applied
+    assert (f[1] & 3) == 0 and v[1] == 1    # step 1 not
+    g.close()
