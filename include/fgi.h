@@ -108,9 +108,14 @@ typedef struct fgi_wave_stats {
 typedef struct fgi_prune_stats {
     uint64_t old_edges;        /* sum of |_usedBy| over pruned (Consistent, registered) nodes before */
     uint64_t new_edges;        /* ... and after (ComputedGraphPruner.cs:91-93) */
-    uint64_t pool_before;      /* edge-pool slots in use before compaction */
-    uint64_t pool_after;
-    double kernel_ms;
+    uint64_t pool_before;      /* edge-pool slots in use (pool top) before */
+    uint64_t pool_after;       /* ... and after (smaller only if the pass defragmented the pool) */
+    double kernel_ms;          /* device time of the pruning kernels (HIP events) */
+    double total_ms;           /* wall time of the call */
+    uint64_t live_edges;       /* entries left in the rows the call visited */
+    uint64_t dropped_edges;    /* entries of Invalidated nodes' rows dropped (their `_usedBy` was cleared) */
+    uint32_t first, count;     /* the handle range visited */
+    uint64_t stale_estimate;   /* fgi_prune_step: the estimate that triggered the batch */
 } fgi_prune_stats;
 
 /* ---- lifetime ------------------------------------------------------------------------------ */
@@ -239,6 +244,17 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
  * registered Consistent node (Computed.cs:400-419) — keep (slot, tag) iff the slot's current node
  * exists with version == tag — then compact the edge pool. */
 fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats);
+/* The same PruneUsedBy pass over the rows of handles [first, first + count) only (one batch of
+ * ComputedGraphPruner's walk, ComputedGraphPruner.cs:79-94). Rows are compacted in place: their
+ * offsets and capacities stay, the freed entries become slack the rows grow into. fgi_prune visits
+ * every row and, when holes exceed FGI_OPT_DEFRAG_PCT of the pool, copies the rows to a fresh pool
+ * (each with max(4, len / 8) slack). */
+fgi_status fgi_prune_range(fgi_graph* g, uint32_t first, uint32_t count, fgi_prune_stats* stats);
+/* Incremental pruning: the next `batch` handles after the previous step's (wrapping around), but
+ * only while the engine's estimate of stale entries exceeds stale_pct of the pool (waves add the
+ * entries they make stale: the rows of invalidated nodes and the entries pointing at them);
+ * otherwise returns at once with zero counts. */
+fgi_status fgi_prune_step(fgi_graph* g, uint32_t batch, uint32_t stale_pct, fgi_prune_stats* stats);
 /* Release a detached handle once the host no longer references the node. */
 fgi_status fgi_release(fgi_graph* g, uint32_t n, const uint32_t* handle);
 
@@ -269,12 +285,15 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *                            than n_slots / beta nodes (0: the alpha rule only)
  *   FGI_OPT_LEVEL_TIMING [1] with a stats argument, time every level's traversal launch with HIP
  *                            events (per-kernel figures for the roofline); 0 keeps only the
- *                            wave-boundary events, so measured waves carry no per-level markers */
+ *                            wave-boundary events, so measured waves carry no per-level markers
+ *   FGI_OPT_DEFRAG_PCT  [60] fgi_prune copies the rows to a fresh pool when holes exceed this % of
+ *                            it (0: never) */
 #define FGI_OPT_DEAD_FILTER 1
 #define FGI_OPT_DIRECTION 2
 #define FGI_OPT_PULL_ALPHA 3
 #define FGI_OPT_LEVEL_TIMING 4
 #define FGI_OPT_PULL_BETA 5
+#define FGI_OPT_DEFRAG_PCT 6
 fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value);
 
 /* ---- multi-GPU (1-D vertex-range partition, RCCL all-to-all frontier exchange) --------------- */

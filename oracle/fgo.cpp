@@ -615,9 +615,16 @@ int fgo_invalidate_everything(fgo* o, fgo_stats* st) {
 // ComputedGraphPruner.OnRun batch loop (Internal/ComputedGraphPruner.cs:79-94) calling
 // IComputedImpl.PruneUsedBy (Computed.cs:400-419) on every registered Consistent node.
 int fgo_prune(fgo* o, uint64_t* old_edges, uint64_t* new_edges) {
+    return fgo_prune_range(o, 0, 0xFFFFFFFFu, old_edges, new_edges);
+}
+
+// One batch of ComputedGraphPruner's walk over the registry (ComputedGraphPruner.cs:79-94): the
+// registered keys (slots) in [first, first + count).
+int fgo_prune_range(fgo* o, uint32_t first, uint32_t count, uint64_t* old_edges, uint64_t* new_edges) {
     uint64_t oe = 0, ne = 0;
+    const uint64_t last = (uint64_t)first + count;
     for (uint32_t k : o->reg.keys) {
-        if (k == FGO_NONE) continue;
+        if (k == FGO_NONE || k < first || (uint64_t)k >= last) continue;
         Node* c = o->reg.get(k);
         if (!c || c->state.load() != kConsistent) continue;
         std::lock_guard<std::mutex> g(c->lock);

@@ -106,6 +106,8 @@ int fgo_invalidate_everything(fgo* o, fgo_stats* st);
 /* ComputedGraphPruner pass: PruneUsedBy on every registered Consistent node
  * (ComputedGraphPruner.cs:79-94, Computed.cs:400-419). */
 int fgo_prune(fgo* o, uint64_t* old_edges, uint64_t* new_edges);
+/* The same over the registered slots in [first, first + count) (one batch of the pruner's walk). */
+int fgo_prune_range(fgo* o, uint32_t first, uint32_t count, uint64_t* old_edges, uint64_t* new_edges);
 
 /* Slots invalidated since the last fgo_clear_log, in transition order. */
 uint64_t fgo_inv_log(const fgo* o, uint32_t* out, uint64_t cap);

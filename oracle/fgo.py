@@ -47,6 +47,7 @@ _SIG = {
     "fgo_invalidate_nodes": ([_O, C.c_uint32, _u32p, _u8p, C.POINTER(Stats)], C.c_int),
     "fgo_invalidate_everything": ([_O, C.POINTER(Stats)], C.c_int),
     "fgo_prune": ([_O, _u64p, _u64p], C.c_int),
+    "fgo_prune_range": ([_O, C.c_uint32, C.c_uint32, _u64p, _u64p], C.c_int),
     "fgo_inv_log": ([_O, _u32p, C.c_uint64], C.c_uint64),
     "fgo_clear_log": ([_O], None),
     "fgo_used_by": ([_O, C.c_uint32, _u32p, _u64p, C.c_uint64], C.c_uint64),
@@ -216,6 +217,11 @@ class Oracle:
     def prune(self):
         a, b = C.c_uint64(), C.c_uint64()
         self.l.fgo_prune(self.o, C.byref(a), C.byref(b))
+        return a.value, b.value
+
+    def prune_range(self, first, count):
+        a, b = C.c_uint64(), C.c_uint64()
+        self.l.fgo_prune_range(self.o, first, count, C.byref(a), C.byref(b))
         return a.value, b.value
 
     def inv_log(self):

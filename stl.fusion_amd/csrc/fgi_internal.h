@@ -191,6 +191,7 @@ struct fgi_graph {
     // visitor. fold() applies the bits to the words before any mutation or state query.
     uint32_t* vis_bm = nullptr;
     bool v_dirty = false;              // vis_bm may hold set bits
+    bool coop_clean = false;           // wave counters, statistics and bitmaps clear (a cooperative wave left them so)
     // Expandable-class bitmap (Consistent, no delay: a first visit invalidates and expands), built
     // from the node words; pull levels read it instead of the words (2 MB vs 128 MB at 16M slots).
     uint32_t* cls_bm = nullptr;
@@ -240,6 +241,9 @@ struct fgi_graph {
 
     // options (fgi_set_option)
     int opt_dead_filter = 1;
+    int opt_defrag_pct = 60;
+    uint64_t stale_est = 0;            // entries waves made stale since the last prune (fgi_prune_step)
+    uint32_t prune_cursor = 0;         // next handle of fgi_prune_step's walk
     int opt_direction = 0;
     int opt_pull_alpha = 14;
     int opt_pull_beta = 24;           // after a pull, pull again while the frontier exceeds n / beta
@@ -267,6 +271,7 @@ struct fgi_graph {
     size_t bst_cap = 0;
     uint32_t* bout = nullptr;
     uint64_t bout_cap = 0;
+    uint64_t batch_ids_hint = 0;       // the previous batch's id count (sizes the copy made with the results)
     hipEvent_t ev_w0 = nullptr, ev_w1 = nullptr;
 
     // multi-GPU
@@ -313,6 +318,9 @@ inline void note_words(fgi_graph* g) {
 // Apply the visit bitmap to the node words and clear it (wave.hip). Every entry point that reads or
 // mutates node words outside a wave calls it first.
 fgi_status fold(fgi_graph* g);
+#if FGI_PROBE
+void print_coop_probe();
+#endif
 // A push-only wave in one cooperative launch, without host synchronisation (streaming batches):
 // device-resident roots (n_max, or *n_dev of them), ids appended at out[*out_n ..), totals added to
 // acc[0..6] (waves, levels, invalidated, E_trav, E_match, flagged, frontier entries); nothing

@@ -7,6 +7,7 @@
 //   Computed<T>.TrySetOutput                                 Computed.cs:141-160
 //   IComputedImpl.PruneUsedBy + ComputedGraphPruner          Computed.cs:400-419, Internal/ComputedGraphPruner.cs:79-94
 #include <hip/hip_runtime.h>
+#include <hip/hip_cooperative_groups.h>
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_reduce.hpp>
@@ -588,6 +589,11 @@ __global__ void kb_au_pending(const unsigned long long* ab, AuArgs a) {
     for (uint64_t i = grid_tid(); i < nc; i += grid_threads()) au_pending(i, a.cand, a.pend_pos, a.row_off, a.pool_col, a.pool_tag);
 }
 
+// the values the host reads after the batch, next to its counters (one copy back)
+__global__ void kb_finish(const unsigned long long* top, unsigned long long* dst) {
+    if (threadIdx.x == 0 && blockIdx.x == 0) *dst = *top;
+}
+
 __global__ void kb_set_output(const unsigned long long* ab, uint32_t n, const uint32_t* __restrict__ h, uint32_t n_handles,
                               unsigned long long* node, uint8_t* out_set, uint32_t* roots, unsigned long long* nroots) {
     if (batch_aborted(ab)) return;
@@ -603,84 +609,331 @@ __device__ __forceinline__ int prune_mode(uint32_t h, uint32_t n_slots, unsigned
     return 2;                                          // Computing, or detached (not in the registry)
 }
 
+// measurement variants of k_prune (make variant-pexp PEXP=mask; wrong results): 1 = skip long
+// rows, 2 / 8 = non-temporal pool loads / stores, 4 = no liveness gathers
+#ifndef FGI_PEXP
+#define FGI_PEXP 0
+#endif
+
 __device__ __forceinline__ bool edge_live(const unsigned long long* node, uint32_t dst, uint64_t tag) {
+#if FGI_PEXP & 4
+    return (tag ^ dst) & 1;
+#endif
     const unsigned long long w = node[dst];              // Computed.cs:412-413
     return word_is_current(w) && (w & kVMask) == tag;
 }
 
-__global__ void k_prune_count(uint32_t n, uint32_t n_slots, const unsigned long long* node,
-                              const uint64_t* __restrict__ row_off, const uint32_t* __restrict__ row_len,
-                              const uint32_t* __restrict__ pool_col, const uint64_t* __restrict__ pool_tag,
-                              uint32_t* newlen, unsigned long long* st /*[0] old,[1] new*/) {
-    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+// pool accesses of a prune (non-temporal loads in the PEXP & 2 variant, stores in PEXP & 8:
+// measured slower together, 6.6 against 5.5 ms on configs[3])
+template <class T> __device__ __forceinline__ T pr_ld(const T* p) {
+#if FGI_PEXP & 2
+    return __builtin_nontemporal_load(p);
+#else
+    return *p;
+#endif
+}
+template <class T> __device__ __forceinline__ void pr_st(T* p, T v) {
+#if FGI_PEXP & 8
+    __builtin_nontemporal_store(v, p);
+#else
+    *p = v;
+#endif
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v, uint32_t& total) {
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    unsigned long long old_e = 0, new_e = 0;
-    for (uint64_t h = wave; h < n; h += nw) {
-        const unsigned long long w = node[h];
-        const int mode = prune_mode((uint32_t)h, n_slots, w);
-        const uint32_t len = row_len[h];
-        uint32_t kept = 0;
-        if (mode == 2) {
-            kept = len;
-        } else if (mode == 1) {
-            const uint64_t o = row_off[h];
-            for (uint32_t k = lane; k < len; k += 64)
-                if (edge_live(node, pool_col[o + k], pool_tag[o + k])) ++kept;
+    uint32_t x = v;
 #pragma unroll
-            for (int d = 32; d >= 1; d >>= 1) kept += __shfl_xor(kept, d, 64);
-            old_e += len;
-            new_e += kept;
-        }
-        if (lane == 0) newlen[h] = kept;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
     }
-    if (lane == 0) {
-        if (old_e) atomicAdd(&st[0], old_e);
-        if (new_e) atomicAdd(&st[1], new_e);
+    total = __shfl(x, 63, 64);
+    return x - v;
+}
+
+// PruneUsedBy in place, rows of handles [lo, hi), one cooperative launch (k_prune): an Invalidated /
+// empty node's row is dropped (len 0), a registered Consistent node's row keeps the entries whose
+// slot's current node is at the entry's version, every other row is kept whole. Rows keep their
+// offsets and capacities (the freed entries are slack the row grows into).
+//   phase 1: waves take 64 consecutive rows and filter the rows of at most kPruneLong entries as
+//            one flattened sequence; the longer rows are listed as chunks of kChunk entries
+//            (chunk map: handle | first chunk of the row << 32), one atomic per block.
+//   grid barrier
+//   phase 2: blocks take chunks in index order. A chunk loads and checks its entries, publishes
+//            its kept count, then sums the counts of the row's earlier chunks (each published only
+//            after that chunk's loads, so no store of this chunk can pass an unread entry) and
+//            stores; the row's last chunk sets its length. Chunks wait only on lower chunk
+//            indices, every block is resident: the lowest unfinished chunk always proceeds.
+constexpr uint32_t kPruneLong = 1024;
+constexpr uint32_t kBlockLong = 64;     // long rows a block lists with one atomic
+constexpr int kChunkPer = 8;
+constexpr uint32_t kChunk = 256 * kChunkPer;
+constexpr uint32_t kChunkDone = 1u << 31;
+enum : int { kPrOld, kPrNew, kPrChunks, kPrDropped, kPrLive, kPrN };
+
+struct PruneArgs {
+    uint32_t lo, hi, n_slots;
+    const unsigned long long* node;
+    const uint64_t* row_off;
+    uint32_t* row_len;
+    uint32_t* pool_col;
+    uint64_t* pool_tag;
+    uint64_t* chunk_map;        // chunk -> handle | first chunk of its row << 32
+    uint32_t* chunk_st;         // zeroed; kChunkDone | kept entries once a chunk has loaded
+    unsigned long long* st;     // kPrN counters
+};
+
+// the chunk map entries of one long row (nch chunks from cb), by the calling threads
+__device__ __forceinline__ void prune_map_row(uint64_t* map, uint32_t h, uint32_t cb, uint32_t nch, uint32_t t,
+                                              uint32_t nt) {
+    for (uint32_t j = t; j < nch; j += nt) map[cb + j] = (uint64_t)h | ((uint64_t)cb << 32);
+}
+
+__device__ void prune_short_rows(const PruneArgs& a, uint32_t* s_lh, uint32_t* s_lc, uint32_t& s_nl,
+                                 unsigned long long* acc) {
+    __shared__ uint32_t s_pre[4][65];    // flattened start of each lane's row (+ the total)
+    __shared__ uint32_t s_kept[4][64];   // kept entries so far, per row
+    __shared__ uint64_t s_off[4][64];    // row offsets
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint64_t n_rows = a.hi - a.lo;
+    for (uint64_t r0 = (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; r0 < n_rows; r0 += nw * 64) {
+        const uint64_t h = a.lo + r0 + lane;
+        uint32_t len = 0, eff = 0;
+        uint64_t off = 0;
+        int mode = 2;
+        if (r0 + lane < n_rows) {   // one round: length, word and offset
+            len = a.row_len[h];
+            const unsigned long long w = a.node[h];
+            off = a.row_off[h];
+            mode = prune_mode((uint32_t)h, a.n_slots, w);
+        }
+        if (len && mode == 0) {
+            a.row_len[h] = 0;
+            acc[2] += len;
+        } else if (len && mode == 2) {
+            acc[3] += len;
+        } else if (len > kPruneLong) {
+#if !(FGI_PEXP & 1)
+            const uint32_t nch = (len + kChunk - 1) / kChunk;
+            const uint32_t q = atomicAdd(&s_nl, 1u);
+            if (q < kBlockLong) {
+                s_lh[q] = (uint32_t)h;
+                s_lc[q] = nch;
+            } else {   // list full: a row of its own
+                const uint32_t cb = (uint32_t)atomicAdd(&a.st[kPrChunks], (unsigned long long)nch);
+                prune_map_row(a.chunk_map, (uint32_t)h, cb, nch, 0, 1);
+            }
+#endif
+        } else if (len) {
+            eff = len;
+        }
+        uint32_t total;
+        const uint32_t pre = wave_excl_scan32(eff, total);
+        s_pre[wid][lane] = pre;
+        if (lane == 0) s_pre[wid][64] = total;
+        s_kept[wid][lane] = 0;
+        s_off[wid][lane] = off;
+        __builtin_amdgcn_wave_barrier();
+        // kShortPer slices of 64 flattened entries per step: every load and liveness gather of the
+        // step is issued before the first store (a slice's stores never pass its own loads, and the
+        // later slices are already in registers)
+        constexpr int kShortPer = 4;
+        for (uint32_t s0 = 0; s0 < total; s0 += 64 * kShortPer) {   // wave-uniform
+            uint32_t rr[kShortPer], col[kShortPer];
+            uint64_t tag[kShortPer], ro[kShortPer];
+            bool keep[kShortPer];
+#pragma unroll
+            for (int q = 0; q < kShortPer; ++q) {
+                const uint32_t f = s0 + 64 * q + lane;
+                uint32_t r = 0;
+                if (f < total) {
+#pragma unroll
+                    for (uint32_t step = 32; step >= 1; step >>= 1)   // the largest r with start <= f
+                        if (r + step < 64 && s_pre[wid][r + step] <= f) r += step;
+                }
+                rr[q] = r;
+                ro[q] = s_off[wid][r];
+                const uint32_t k = f < total ? f - s_pre[wid][r] : 0u;
+                col[q] = f < total ? pr_ld(a.pool_col + ro[q] + k) : 0u;
+                tag[q] = f < total ? pr_ld(a.pool_tag + ro[q] + k) : 0ull;
+            }
+#pragma unroll
+            for (int q = 0; q < kShortPer; ++q) keep[q] = (s0 + 64 * q + lane < total) && edge_live(a.node, col[q], tag[q]);
+#pragma unroll
+            for (int q = 0; q < kShortPer; ++q) {
+                const uint32_t sq = s0 + 64 * q;
+                if (sq >= total) break;   // wave-uniform
+                const uint32_t f = sq + lane;
+                const bool in = f < total;
+                const uint32_t r = rr[q];
+                const unsigned long long km = __ballot(keep[q]);
+                // lanes of this slice in the same row: from the row's first lane in the slice
+                const uint32_t first = in ? (s_pre[wid][r] > sq ? s_pre[wid][r] - sq : 0u) : 0u;
+                const unsigned long long seg = ((1ull << lane) - 1ull) & ~((1ull << first) - 1ull);
+                const uint32_t before = (uint32_t)__popcll(km & seg);
+                const uint32_t base_kept = in ? s_kept[wid][r] : 0u;
+                __builtin_amdgcn_wave_barrier();
+                if (keep[q]) {
+                    pr_st(a.pool_col + ro[q] + base_kept + before, col[q]);
+                    pr_st(a.pool_tag + ro[q] + base_kept + before, tag[q]);
+                }
+                // the row's last lane of this slice adds the slice's kept entries of the row
+                const bool last = in && (f + 1 == s_pre[wid][r + 1] || lane == 63 || f + 1 == total);
+                if (last) s_kept[wid][r] = base_kept + before + (keep[q] ? 1u : 0u);
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        if (eff) {
+            const uint32_t kept = s_kept[wid][lane];
+            a.row_len[h] = kept;
+            acc[0] += len;
+            acc[1] += kept;
+            acc[3] += kept;
+        }
+        __builtin_amdgcn_wave_barrier();
     }
 }
 
-__global__ void k_prune_scatter(uint32_t n, uint32_t n_slots, const unsigned long long* node,
-                                const uint64_t* __restrict__ row_off, const uint32_t* __restrict__ row_len,
-                                const uint32_t* __restrict__ pool_col, const uint64_t* __restrict__ pool_tag,
-                                const uint64_t* __restrict__ new_off, uint32_t* ncol, uint64_t* ntag) {
-    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+// one chunk of a long row (phase 2); thread t holds entries [8t, 8t + 8) of the chunk, in order
+__device__ void prune_chunk(const PruneArgs& a, uint32_t c, uint32_t* s_w, uint32_t& s_pfx, unsigned long long* acc) {
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const uint64_t m = a.chunk_map[c];
+    const uint32_t h = (uint32_t)m, first = (uint32_t)(m >> 32);
+    const uint32_t len = a.row_len[h];   // the row's last chunk rewrites it only after this chunk published
+    const uint64_t o = a.row_off[h];
+    const uint32_t base = (c - first) * kChunk;
+    uint32_t col[kChunkPer];
+    uint64_t tag[kChunkPer];
+#pragma unroll
+    for (int j = 0; j < kChunkPer; ++j) {
+        const uint32_t k = base + threadIdx.x * kChunkPer + j;
+        col[j] = k < len ? pr_ld(a.pool_col + o + k) : 0u;
+        tag[j] = k < len ? pr_ld(a.pool_tag + o + k) : 0ull;
+    }
+    uint32_t keep = 0;
+#pragma unroll
+    for (int j = 0; j < kChunkPer; ++j) {
+        const uint32_t k = base + threadIdx.x * kChunkPer + j;
+        keep |= (k < len && edge_live(a.node, col[j], tag[j])) ? (1u << j) : 0u;
+    }
+    const uint32_t cnt = (uint32_t)__popc(keep);
+    uint32_t x = cnt;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) s_w[wid] = x;
+    __syncthreads();   // every entry of the chunk is in registers (its liveness used them)
+    uint32_t before = x - cnt, all = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        before += q < wid ? s_w[q] : 0u;
+        all += s_w[q];
+    }
+    // the flag hands over no data (the count travels in it): relaxed, no release / acquire fences
+    // (MI355X_MICROARCH.md: an agent release writes back the XCD's L2, an acquire poll invalidates L1)
+    if (threadIdx.x == 0) __hip_atomic_store(&a.chunk_st[c], kChunkDone | all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wid == 0) {   // the row's earlier chunks: all published (loaded), their kept counts summed
+        uint32_t pfx = 0;
+        for (uint32_t j = first + lane; j < c; j += 64) {
+            uint32_t v = __hip_atomic_load(&a.chunk_st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            while (!(v & kChunkDone)) {
+                __builtin_amdgcn_s_sleep(2);
+                v = __hip_atomic_load(&a.chunk_st[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            pfx += v & ~kChunkDone;
+        }
+        for (int d = 32; d >= 1; d >>= 1) pfx += __shfl_xor(pfx, d, 64);
+        if (lane == 0) s_pfx = pfx;
+    }
+    __syncthreads();
+    const uint32_t pfx = s_pfx;
+    uint32_t at = pfx + before;
+#pragma unroll
+    for (int j = 0; j < kChunkPer; ++j)
+        if ((keep >> j) & 1u) {
+            pr_st(a.pool_col + o + at, col[j]);
+            pr_st(a.pool_tag + o + at, tag[j]);
+            ++at;
+        }
+    if (threadIdx.x == 0 && base + kChunk >= len) {   // the row's last chunk
+        a.row_len[h] = pfx + all;
+        acc[0] += len;
+        acc[1] += pfx + all;
+        acc[3] += pfx + all;
+    }
+    __syncthreads();   // s_w, s_pfx reused by the next chunk
+}
+
+__global__ __launch_bounds__(256) void k_prune(PruneArgs a) {
+    __shared__ uint32_t s_lh[kBlockLong], s_lc[kBlockLong];
+    __shared__ uint32_t s_nl, s_cb, s_w[4], s_pfx;
+    if (threadIdx.x == 0) s_nl = 0;
+    __syncthreads();
+    unsigned long long acc[4] = {0, 0, 0, 0};   // old, new, dropped, live
+    prune_short_rows(a, s_lh, s_lc, s_nl, acc);
+    __syncthreads();
+    // this block's long rows: one range of chunk indices
+    const uint32_t nl = std::min<uint32_t>(s_nl, kBlockLong);
+    if (threadIdx.x == 0) {
+        uint32_t tot = 0;
+        for (uint32_t q = 0; q < nl; ++q) tot += s_lc[q];
+        s_cb = tot ? (uint32_t)atomicAdd(&a.st[kPrChunks], (unsigned long long)tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t cb = s_cb;
+    for (uint32_t q = 0; q < nl; ++q) {
+        prune_map_row(a.chunk_map, s_lh[q], cb, s_lc[q], threadIdx.x, blockDim.x);
+        cb += s_lc[q];
+    }
+    cooperative_groups::this_grid().sync();
+    const uint32_t n_chunks = (uint32_t)__hip_atomic_load(&a.st[kPrChunks], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (uint32_t c = blockIdx.x; c < n_chunks; c += gridDim.x) prune_chunk(a, c, s_w, s_pfx, acc);
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        for (int d = 32; d >= 1; d >>= 1) acc[q] += __shfl_xor(acc[q], d, 64);
+    if (lane == 0) {
+        if (acc[0]) atomicAdd(&a.st[kPrOld], acc[0]);
+        if (acc[1]) atomicAdd(&a.st[kPrNew], acc[1]);
+        if (acc[2]) atomicAdd(&a.st[kPrDropped], acc[2]);
+        if (acc[3]) atomicAdd(&a.st[kPrLive], acc[3]);
+    }
+}
+
+// Defragmentation: every row copied to a fresh pool at the exclusive scan of its new capacity
+// (length + slack); one wave per row.
+__global__ void k_defrag_rows(uint32_t n, const uint64_t* __restrict__ new_off, const uint64_t* __restrict__ row_off,
+                              const uint32_t* __restrict__ row_len, const uint32_t* __restrict__ pool_col,
+                              const uint64_t* __restrict__ pool_tag, uint32_t* ncol, uint64_t* ntag) {
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t h = wave; h < n; h += nw) {
-        const int mode = prune_mode((uint32_t)h, n_slots, node[h]);
-        if (mode == 0) continue;
+    for (uint64_t h = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; h < n; h += nw) {
         const uint32_t len = row_len[h];
-        const uint64_t o = row_off[h];
-        uint64_t dst = new_off[h];
-        for (uint32_t base = 0; base < len; base += 64) {
-            const uint32_t k = base + lane;
-            uint32_t col = 0;
-            uint64_t tag = 0;
-            bool keep = false;
-            if (k < len) {
-                col = pool_col[o + k];
-                tag = pool_tag[o + k];
-                keep = (mode == 2) || edge_live(node, col, tag);
-            }
-            const unsigned long long mask = __ballot(keep);
-            const uint32_t before = __popcll(mask & ((1ull << lane) - 1ull));
-            if (keep) {
-                ncol[dst + before] = col;
-                ntag[dst + before] = tag;
-            }
-            dst += __popcll(mask);
+        const uint64_t o = row_off[h], d = new_off[h];
+        for (uint32_t k = lane; k < len; k += 64) {
+            ncol[d + k] = pool_col[o + k];
+            ntag[d + k] = pool_tag[o + k];
         }
     }
 }
 
-__global__ void k_prune_rows(uint32_t n, const uint64_t* __restrict__ new_off, const uint32_t* __restrict__ newlen,
-                             uint64_t* row_off, uint32_t* row_len, uint32_t* row_cap) {
+__device__ __forceinline__ uint32_t row_slack_cap(uint32_t len) { return len == 0 ? 0u : len + std::max<uint32_t>(4u, len / 8); }
+
+__global__ void k_defrag_caps(uint32_t n, const uint32_t* __restrict__ row_len, uint64_t* cap64) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h < n) cap64[h] = row_slack_cap(row_len[h]);
+}
+
+__global__ void k_defrag_apply(uint32_t n, const uint64_t* __restrict__ new_off, const uint64_t* __restrict__ cap64,
+                               uint64_t* row_off, uint32_t* row_cap) {
     const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
     if (h >= n) return;
     row_off[h] = new_off[h];
-    row_len[h] = newlen[h];
-    row_cap[h] = newlen[h];
+    row_cap[h] = (uint32_t)cap64[h];
 }
 
 // ---- dependency-list cache (pull levels) ------------------------------------------------------
@@ -1557,6 +1810,7 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
     if (!g) return FGI_EINVAL;
     switch (option) {
     case FGI_OPT_DEAD_FILTER: g->opt_dead_filter = value ? 1 : 0; return FGI_OK;
+    case FGI_OPT_DEFRAG_PCT: g->opt_defrag_pct = (int)std::max<int64_t>(0, std::min<int64_t>(100, value)); return FGI_OK;
     case FGI_OPT_DIRECTION:
         if (value < 0 || value > 2) return set_err(g, FGI_EINVAL, "direction must be 0, 1 or 2");
         g->opt_direction = (int)value;
@@ -2010,9 +2264,15 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
         if (sp.kind == FGI_STEP_BEGIN_COMPUTE || sp.kind == FGI_STEP_ADD_USED) out_bytes += stage_round(sp.n * 4);
         if (sp.kind == FGI_STEP_SET_OUTPUT) out_bytes += stage_round(sp.n);
     }
-    const size_t scr_words = 3 + kAccCount + 4 * (size_t)n_steps;
+    // scratch words: abort, ids, detached taken, accumulators, 4 counters per step, the pool top
+    const size_t scr_words = 3 + kAccCount + 4 * (size_t)n_steps + 1;
     const size_t scr_bytes = stage_round(scr_words * 8);
-    const size_t total = in_bytes + out_bytes + scr_bytes;
+    const size_t ptop_word = scr_words - 1;
+    // the ids are copied back with the results when they fit the previous batch's count (+25%)
+    const uint64_t spec = out_ids ? std::min<uint64_t>(cap, g->batch_ids_hint + g->batch_ids_hint / 4 + 4096) : 0;
+    const size_t res_off = in_bytes + scr_bytes;   // outputs follow the scratch words
+    const size_t ids_off = res_off + out_bytes;
+    const size_t total = ids_off + stage_round(spec * 4);
     if (g->bst_cap < total) {
         if (g->bst_h) hipHostFree(g->bst_h);
         dfree(g->bst_d);
@@ -2044,13 +2304,12 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
             bs[k].flags = reinterpret_cast<const uint8_t*>(D + in_off[4 * k + 3]);
         }
     }
-    unsigned long long* scr = reinterpret_cast<unsigned long long*>(D + in_bytes + out_bytes);
-    unsigned long long* scr_h = reinterpret_cast<unsigned long long*>(H + in_bytes + out_bytes);
+    unsigned long long* scr = reinterpret_cast<unsigned long long*>(D + in_bytes);
+    unsigned long long* scr_h = reinterpret_cast<unsigned long long*>(H + in_bytes);
     std::memset(scr_h, 0, scr_words * 8);
     hipEvent_t b0 = g->ev_w0, b1 = g->ev_w1;
     FGI_HIP(g, hipEventRecord(b0, st));
-    FGI_HIP(g, hipMemcpyAsync(D, H, in_bytes, hipMemcpyHostToDevice, st));
-    FGI_HIP(g, hipMemcpyAsync(scr, scr_h, scr_words * 8, hipMemcpyHostToDevice, st));
+    FGI_HIP(g, hipMemcpyAsync(D, H, in_bytes + scr_words * 8, hipMemcpyHostToDevice, st));   // one upload
     // per-step device temporaries
     for (uint32_t k = 0; k < n_steps; ++k) {
         const fgi_step& sp = steps[k];
@@ -2063,7 +2322,7 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
             case FGI_STEP_BEGIN_COMPUTE:
                 FGI_TRY(tmalloc(g, b.tmp[0], &b.cls, n));
                 FGI_TRY(tmalloc(g, b.tmp[1], &b.roots, n));
-                FGI_TRY(tmalloc(g, b.tmp[2], &b.out32, n));
+                b.out32 = reinterpret_cast<uint32_t*>(D + res_off + b.out_off);
                 break;
             case FGI_STEP_ADD_USED:
                 b.hcap = 64;
@@ -2072,10 +2331,10 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
                 FGI_TRY(tmalloc(g, b.tmp[1], &b.cand, n));
                 FGI_TRY(tmalloc(g, b.tmp[2], &b.pend, n));
                 FGI_TRY(tmalloc(g, b.tmp[3], &b.ovf, n));
-                FGI_TRY(tmalloc(g, b.tmp[4], &b.out32, n));
+                b.out32 = reinterpret_cast<uint32_t*>(D + res_off + b.out_off);
                 break;
             case FGI_STEP_SET_OUTPUT:
-                FGI_TRY(tmalloc(g, b.tmp[0], &b.out8, n));
+                b.out8 = reinterpret_cast<uint8_t*>(D + res_off + b.out_off);
                 FGI_TRY(tmalloc(g, b.tmp[1], &b.roots, n));
                 break;
             default:
@@ -2098,17 +2357,15 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
             release_events();
             return s;
         }
-        // results: counters, the pool top, every step's output, in one copy each, then one wait
-        for (uint32_t k = from; k < n_steps; ++k) {
-            const BatchStep& b = bs[k];
-            if (b.out32) FGI_HIP(g, hipMemcpyAsync(H + in_bytes + b.out_off, b.out32, steps[k].n * 4, hipMemcpyDeviceToHost, st));
-            if (b.out8) FGI_HIP(g, hipMemcpyAsync(H + in_bytes + b.out_off, b.out8, steps[k].n, hipMemcpyDeviceToHost, st));
-        }
-        FGI_HIP(g, hipMemcpyAsync(scr_h, scr, scr_words * 8, hipMemcpyDeviceToHost, st));
-        FGI_HIP(g, hipMemcpyAsync(&g->pool_top, g->pool_top_dev, sizeof(uint64_t), hipMemcpyDeviceToHost, st));
+        // results: the counters, the pool top and every step's output in one copy, the ids (as
+        // many as the previous batch had, +25%) in a second, then one wait
+        hipLaunchKernelGGL(kb_finish, dim3(1), dim3(64), 0, st, g->pool_top_dev, scr + ptop_word);
+        FGI_HIP(g, hipMemcpyAsync(H + in_bytes, D + in_bytes, scr_bytes + out_bytes, hipMemcpyDeviceToHost, st));
+        if (spec) FGI_HIP(g, hipMemcpyAsync(H + ids_off, g->bout, spec * 4, hipMemcpyDeviceToHost, st));
         FGI_HIP(g, hipEventRecord(b1, st));
         FGI_HIP(g, hipStreamSynchronize(st));
         ++syncs;
+        g->pool_top = scr_h[ptop_word];
         const unsigned long long ab = scr_h[0];
         if (!ab) break;
         const uint32_t k = (uint32_t)(ab & 0xFFFFFFFFull) - 1;
@@ -2135,16 +2392,23 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
     for (uint32_t k = 0; k < n_steps; ++k) {
         const fgi_step& sp = steps[k];
         if (!sp.out || !sp.n) continue;
-        const char* src = H + in_bytes + bs[k].out_off;
+        const char* src = H + res_off + bs[k].out_off;
         if (sp.kind == FGI_STEP_SET_OUTPUT) std::memcpy(sp.out, src, sp.n);
         else if (sp.kind == FGI_STEP_BEGIN_COMPUTE || sp.kind == FGI_STEP_ADD_USED) std::memcpy(sp.out, src, sp.n * 4);
     }
+    g->stale_est += scr_h[3 + 3] + scr_h[3 + 4];   // the cascades' E_trav + E_match (fgi_prune_step)
+#if FGI_PROBE
+    if (getenv("FGI_TRACE")) print_coop_probe();
+#endif
     const uint64_t n_ids = scr_h[1];
     if (out_n) *out_n = n_ids;
+    g->batch_ids_hint = n_ids;
     fgi_status ret = FGI_OK;
     if (out_ids) {
         if (n_ids > cap) {
             ret = FGI_ECAPACITY;
+        } else if (n_ids <= spec && from == 0) {
+            std::memcpy(out_ids, H + ids_off, n_ids * 4);
         } else if (n_ids) {
             FGI_HIP(g, hipMemcpyAsync(out_ids, g->bout, n_ids * 4, hipMemcpyDeviceToHost, st));
             FGI_HIP(g, hipStreamSynchronize(st));
@@ -2170,37 +2434,56 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
     return ret;
 }
 
-fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats) {
-    if (!g) return FGI_EINVAL;
-    FGI_TRY(single_only(g, "fgi_prune"));
-    hipSetDevice(g->device);
-    const auto t0 = std::chrono::steady_clock::now();
-    FGI_TRY(fold(g));
-    hipStream_t st = g->stream;
+// PruneUsedBy over the rows of handles [lo, hi) in place (queued, no synchronisation): the
+// counters land in st[kPrN].
+static fgi_status prune_range_launch(fgi_graph* g, uint32_t lo, uint32_t hi, Tmp& tmap, Tmp& tcst,
+                                     unsigned long long* st) {
+    hipStream_t s = g->stream;
+    // every chunk holds more than kPruneLong / 2 entries of a row: the pool bounds their number
+    const uint64_t max_chunks = g->pool_top / (kPruneLong / 2) + 1;
+    PruneArgs a{};
+    FGI_TRY(tmalloc(g, tmap, &a.chunk_map, max_chunks));
+    FGI_TRY(tmalloc(g, tcst, &a.chunk_st, max_chunks));
+    FGI_HIP(g, hipMemsetAsync(a.chunk_st, 0, max_chunks * sizeof(uint32_t), s));
+    static int per_cu = 0;
+    if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_prune, 256, 0) != hipSuccess || per_cu < 1))
+        per_cu = 1;
+    const uint64_t resident = (uint64_t)per_cu * (uint64_t)std::max(g->n_cu, 1);
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, nblk((uint64_t)(hi - lo) * 64)));
+    a.lo = lo;
+    a.hi = hi;
+    a.n_slots = g->n_slots;
+    a.node = reinterpret_cast<const unsigned long long*>(g->node);
+    a.row_off = g->row_off;
+    a.row_len = g->row_len;
+    a.pool_col = g->pool_col;
+    a.pool_tag = g->pool_tag;
+    a.st = st;
+    if (getenv("FGI_TRACE")) fprintf(stderr, "[fgi] prune [%u, %u): %u blocks (%d per CU)\n", lo, hi, grid, per_cu);
+    void* args[] = {&a};
+    FGI_HIP(g, hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_prune), dim3(grid), dim3(256), args, 0, s));
+    return FGI_OK;
+}
+
+// Copy every row to a fresh pool with slack (len + max(4, len / 8)): the holes pruning left go away.
+static fgi_status defragment(fgi_graph* g) {
+    hipStream_t s = g->stream;
     const uint32_t H = g->n_handles;
-    Tmp tl, to, ts;
-    uint32_t* newlen;
-    uint64_t* newoff;
-    FGI_TRY(tmalloc(g, tl, &newlen, H));
-    FGI_TRY(tmalloc(g, to, &newoff, H));
-    FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, 2 * sizeof(unsigned long long), st));
-    const uint32_t grid = std::min<uint64_t>(nblk((uint64_t)H * 64), 8192);
-    hipLaunchKernelGGL(k_prune_count, dim3(grid), dim3(256), 0, st, H, g->n_slots,
-                       reinterpret_cast<const unsigned long long*>(g->node), g->row_off, g->row_len, g->pool_col,
-                       g->pool_tag, newlen, g->misc_dev);
+    Tmp tc, to, ts;
+    uint64_t *cap64, *noff;
+    FGI_TRY(tmalloc(g, tc, &cap64, H));
+    FGI_TRY(tmalloc(g, to, &noff, H));
+    hipLaunchKernelGGL(k_defrag_caps, dim3(nblk(H)), dim3(256), 0, s, H, g->row_len, cap64);
     size_t tb = 0;
-    FGI_HIP(g, rocprim::exclusive_scan(nullptr, tb, newlen, newoff, (uint64_t)0, (size_t)H, rocprim::plus<uint64_t>(), st));
+    FGI_HIP(g, rocprim::exclusive_scan(nullptr, tb, cap64, noff, (uint64_t)0, (size_t)H, rocprim::plus<uint64_t>(), s));
     char* tmp;
     FGI_TRY(tmalloc(g, ts, &tmp, tb));
-    FGI_HIP(g, rocprim::exclusive_scan(tmp, tb, newlen, newoff, (uint64_t)0, (size_t)H, rocprim::plus<uint64_t>(), st));
-    unsigned long long eo[2];
-    uint64_t last_off = 0;
-    uint32_t last_len = 0;
-    FGI_TRY(d2h(g, eo, g->misc_dev, 2));
-    FGI_TRY(d2h(g, &last_off, newoff + H - 1, 1));
-    FGI_TRY(d2h(g, &last_len, newlen + H - 1, 1));
-    const uint64_t total = last_off + last_len;
-    const uint64_t cap = std::max<uint64_t>(total, 1024);
+    FGI_HIP(g, rocprim::exclusive_scan(tmp, tb, cap64, noff, (uint64_t)0, (size_t)H, rocprim::plus<uint64_t>(), s));
+    uint64_t last_off = 0, last_cap = 0;
+    FGI_TRY(d2h(g, &last_off, noff + H - 1, 1));
+    FGI_TRY(d2h(g, &last_cap, cap64 + H - 1, 1));
+    const uint64_t total = last_off + last_cap;
+    const uint64_t cap = std::max<uint64_t>(total + total / 8, 1024);
     uint32_t* ncol = nullptr;
     uint64_t* ntag = nullptr;
     FGI_TRY(dmalloc(g, &ncol, cap));
@@ -2208,19 +2491,12 @@ fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats) {
         hipFree(ncol);
         return FGI_ENOMEM;
     }
-    hipLaunchKernelGGL(k_prune_scatter, dim3(grid), dim3(256), 0, st, H, g->n_slots,
-                       reinterpret_cast<const unsigned long long*>(g->node), g->row_off, g->row_len, g->pool_col,
-                       g->pool_tag, newoff, ncol, ntag);
-    hipLaunchKernelGGL(k_prune_rows, dim3(nblk(H)), dim3(256), 0, st, H, newoff, newlen, g->row_off, g->row_len,
-                       g->row_cap);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>(nblk((uint64_t)H * 64), 8192);
+    hipLaunchKernelGGL(k_defrag_rows, dim3(grid), dim3(256), 0, s, H, noff, g->row_off, g->row_len, g->pool_col,
+                       g->pool_tag, ncol, ntag);
+    hipLaunchKernelGGL(k_defrag_apply, dim3(nblk(H)), dim3(256), 0, s, H, noff, cap64, g->row_off, g->row_cap);
     FGI_HIP(g, hipGetLastError());
-    FGI_HIP(g, hipStreamSynchronize(st));
-    if (stats) {
-        stats->old_edges = eo[0];
-        stats->new_edges = eo[1];
-        stats->pool_before = g->pool_top;
-        stats->pool_after = total;
-    }
+    FGI_HIP(g, hipStreamSynchronize(s));
     dfree(g->pool_col);
     dfree(g->pool_tag);
     g->pool_col = ncol;
@@ -2228,11 +2504,77 @@ fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats) {
     g->pool_cap = cap;
     g->pool_top = total;
     g->pool_epoch++;
-    touch(g);
     FGI_HIP(g, hipMemcpy(g->pool_top_dev, &g->pool_top, sizeof(uint64_t), hipMemcpyHostToDevice));
-    if (stats)
-        stats->kernel_ms =
-            std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return ensure_cstart(g, cap);
+}
+
+static fgi_status prune_rows(fgi_graph* g, uint32_t lo, uint32_t hi, bool allow_defrag, fgi_prune_stats* stats) {
+    FGI_TRY(single_only(g, "fgi_prune"));
+    hipSetDevice(g->device);
+    const auto t0 = std::chrono::steady_clock::now();
+    FGI_TRY(fold(g));
+    hipStream_t s = g->stream;
+    unsigned long long* st = g->misc_dev;
+    FGI_HIP(g, hipMemsetAsync(st, 0, kPrN * sizeof(unsigned long long), s));
+    hipEvent_t e0 = g->ev_w0, e1 = g->ev_w1;
+    FGI_HIP(g, hipEventRecord(e0, s));
+    Tmp tmap, tcst;
+    if (hi > lo) FGI_TRY(prune_range_launch(g, lo, hi, tmap, tcst, st));
+    FGI_HIP(g, hipEventRecord(e1, s));
+    unsigned long long c[kPrN];
+    FGI_TRY(d2h(g, c, st, kPrN));
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    touch(g);
+    const uint64_t pool_before = g->pool_top;
+    // the full pass knows every row's length: defragment when holes are most of the pool
+    if (allow_defrag && lo == 0 && hi == g->n_handles && g->opt_defrag_pct > 0 &&
+        (g->pool_top - std::min<uint64_t>(g->pool_top, c[kPrLive])) * 100 > (uint64_t)g->opt_defrag_pct * g->pool_top)
+        FGI_TRY(defragment(g));
+    if (stats) {
+        stats->old_edges = c[kPrOld];
+        stats->new_edges = c[kPrNew];
+        stats->pool_before = pool_before;
+        stats->pool_after = g->pool_top;
+        stats->kernel_ms = ms;
+        stats->total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+        stats->live_edges = c[kPrLive];
+        stats->dropped_edges = c[kPrDropped];
+        stats->first = lo;
+        stats->count = hi - lo;
+    }
+    g->stale_est = 0;
+    return FGI_OK;
+}
+
+fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats) {
+    if (!g) return FGI_EINVAL;
+    if (stats) *stats = fgi_prune_stats{};
+    return prune_rows(g, 0, g->n_handles, true, stats);
+}
+
+fgi_status fgi_prune_range(fgi_graph* g, uint32_t first, uint32_t count, fgi_prune_stats* stats) {
+    if (!g) return FGI_EINVAL;
+    if (stats) *stats = fgi_prune_stats{};
+    if (first > g->n_handles) return set_err(g, FGI_EINVAL, "first handle %u out of range", first);
+    const uint32_t hi = (uint32_t)std::min<uint64_t>((uint64_t)first + count, g->n_handles);
+    return prune_rows(g, first, hi, false, stats);
+}
+
+fgi_status fgi_prune_step(fgi_graph* g, uint32_t batch, uint32_t stale_pct, fgi_prune_stats* stats) {
+    if (!g || batch == 0) return FGI_EINVAL;
+    if (stats) *stats = fgi_prune_stats{};
+    // ComputedGraphPruner (Internal/ComputedGraphPruner.cs:50-110) walks the registry in batches;
+    // here a batch runs only while the estimated stale entries exceed stale_pct of the pool
+    if ((uint64_t)g->stale_est * 100 < (uint64_t)stale_pct * std::max<uint64_t>(g->pool_top, 1)) return FGI_OK;
+    const uint32_t lo = g->prune_cursor;
+    const uint32_t hi = (uint32_t)std::min<uint64_t>((uint64_t)lo + batch, g->n_handles);
+    const uint64_t est = g->stale_est;
+    FGI_TRY(prune_rows(g, lo, hi, false, stats));
+    g->prune_cursor = hi >= g->n_handles ? 0 : hi;
+    // the estimate shrinks by the share of the handles this batch covered
+    g->stale_est = hi >= g->n_handles ? 0 : est - est * (uint64_t)(hi - lo) / std::max<uint32_t>(g->n_handles, 1);
+    if (stats) stats->stale_estimate = est;
     return FGI_OK;
 }
 

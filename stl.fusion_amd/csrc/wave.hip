@@ -65,7 +65,17 @@ __device__ unsigned long long d_probe[kProbeLevels][kProbeBlocks][kProbePts];
         if (threadIdx.x == 0 && (L) < kProbeLevels && blockIdx.x < (uint32_t)kProbeBlocks) \
             d_probe[(L)][blockIdx.x][(k)] = wall_clock64();                            \
     } while (0)
+// cooperative waves: block 0's phase stamps per launch (ring of 64 launches)
+__device__ unsigned long long d_cprobe[64][10];
+__device__ unsigned int d_cprobe_n;
+#define CPROBE(k)                                                               \
+    do {                                                                        \
+        if (blockIdx.x == 0 && threadIdx.x == 0) d_cprobe[s_cp][(k)] = wall_clock64(); \
+    } while (0)
 #else
+#define CPROBE(k) \
+    do {          \
+    } while (0)
 #define PROBE(L, k) \
     do {            \
     } while (0)
@@ -1353,8 +1363,21 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
     __shared__ unsigned long long s_words[kFinalStage];
     // uniform across the grid: the word is written before the launch and not during it
     if (a.abort && __hip_atomic_load(a.abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+#if FGI_PROBE
+    __shared__ uint32_t s_cp;
+    if (threadIdx.x == 0 && blockIdx.x == 0) {
+        s_cp = atomicAdd(&d_cprobe_n, 1u) % 64;
+        for (int k = 0; k < 10; ++k) d_cprobe[s_cp][k] = 0;
+    }
+    __syncthreads();
+#endif
+    CPROBE(0);
     WaveCtr* ctr = a.ctr;
     const uint32_t n = a.n_dev ? (uint32_t)std::min<unsigned long long>(*a.n_dev, a.n_max) : a.n_max;
+    if (n == 0) {   // an empty cascade (no displaced node, nothing flagged InvalidateOnSetOutput)
+        if (blockIdx.x == 0 && threadIdx.x == 0) a.acc[kAccWaves] += 1;
+        return;
+    }
     const uint32_t gsize = gridDim.x * blockDim.x;
     const Out o0{a.row_off, a.row_len, a.inv_bm, a.fr_off[0], a.fr_len[0], a.escan[0], a.cstart[0], &ctr->lvl[0]};
     if (a.imm) {   // Invalidate(true) roots first: their CAS may change node words
@@ -1364,9 +1387,11 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
     }
     for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gsize)
         root_step<0>(i0 + threadIdx.x, a.roots, a.imm, n, 0u, a.n_handles, a.node, a.vis, o0, ctr);
+    CPROBE(1);
     uint64_t levels = 0, e_trav = 0, f_total = 0;
     for (int L = 0;; ++L) {
         grid.sync();   // level L's frontier (and its counter) is complete
+        if (L < 4) CPROBE(2 + L);
         if (threadIdx.x == 0) s_ft = coh_read(&ctr->lvl[L % kRing].ft);
         __syncthreads();
         const uint64_t F = s_ft >> 32, T = s_ft & 0xFFFFFFFFull;
@@ -1418,7 +1443,9 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
     }
     c = block_sum(c, s_red);
     if (threadIdx.x == 0) coh_xchg(a.cnt + blockIdx.x, c);
+    CPROBE(6);
     grid.sync();
+    CPROBE(7);
     unsigned long long part = 0;
     for (uint32_t k = threadIdx.x; k < blockIdx.x; k += blockDim.x) part += coh_read(a.cnt + k);
     const unsigned long long excl = block_sum(part, s_red);
@@ -1460,6 +1487,35 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
         __builtin_amdgcn_wave_barrier();
         run += all;
     }
+    // leave the state clean for the next cooperative wave (no k_wave_init, no k_fold between
+    // them): this block's visits folded into the node words, its bitmap words, its statistics
+    // entries and (block 0) the level counters this wave used cleared
+    __syncthreads();
+    CPROBE(8);
+    unsigned long long* vis64 = reinterpret_cast<unsigned long long*>(a.vis);
+    unsigned long long* invw = reinterpret_cast<unsigned long long*>(a.inv_bm);
+    for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x) {
+        unsigned long long v = vis64[w];
+        if (v) {
+            vis64[w] = 0ull;
+            for (; v; v &= v - 1) {
+                const uint64_t h = w * 64 + (uint64_t)(__ffsll((long long)v) - 1);
+                a.node[h] = visited_word(a.node[h]);
+            }
+        }
+        if (w - lo >= kFinalStage || s_words[w - lo]) invw[w] = 0ull;
+    }
+    if (threadIdx.x < (uint32_t)kStats) a.blk[(uint64_t)threadIdx.x * kStatBlocks + blockIdx.x] = 0ull;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            ctr->root_inv = 0;
+            ctr->root_flagged = 0;
+        }
+        const uint64_t used = std::min<uint64_t>(levels + 3, (uint64_t)kRing);
+        for (uint64_t i = threadIdx.x; i < used * (sizeof(LevelCtr) / 8); i += blockDim.x)
+            reinterpret_cast<unsigned long long*>(&ctr->lvl[0])[i] = 0ull;
+    }
+    CPROBE(9);
 }
 
 __global__ __launch_bounds__(kBlock) void k_wave_init(WaveCtr* ctr, unsigned long long* blk, uint32_t* inv_bm,
@@ -1678,9 +1734,28 @@ void launch_roots(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, con
 
 }  // namespace
 
+#if FGI_PROBE
+// block 0's phase times of the last cooperative waves (FGI_TRACE=1, probe build): entry -> roots
+// done -> level barriers -> final counts -> prefix barrier -> ids written -> cleaned up
+void print_coop_probe() {
+    static unsigned long long h[64][10];
+    unsigned int n = 0;
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(d_cprobe), sizeof(h)) != hipSuccess ||
+        hipMemcpyFromSymbol(&n, HIP_SYMBOL(d_cprobe_n), sizeof(n)) != hipSuccess)
+        return;
+    for (unsigned int i = (n > 8 ? n - 8 : 0); i < n; ++i) {
+        const unsigned long long* t = h[i % 64];
+        fprintf(stderr, "[coop] wave %u:", i);
+        for (int k = 1; k < 10; ++k)
+            if (t[k]) fprintf(stderr, " %d:+%.1f", k, (t[k] - t[0]) / 100.0);
+        fprintf(stderr, " us\n");
+    }
+}
+#endif
+
 // One push-only wave in a single cooperative launch (k_wave_coop): no host synchronisation. The roots
 // (n_max, or *n_dev of them) are device-resident; the invalidated handles are appended at
-// out[*out_n ..). Node words are folded by the next call that needs them (v_dirty).
+// out[*out_n ..). The wave folds its visits into the node words itself.
 fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev, const uint8_t* imm_dev,
                          const unsigned long long* n_dev, uint32_t* out, unsigned long long* out_n,
                          unsigned long long* acc, const unsigned long long* abort) {
@@ -1694,7 +1769,10 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
     const uint32_t G = std::max<uint32_t>((uint32_t)kStats, (uint32_t)std::max(g->n_cu, 1));
     if ((uint64_t)G > (uint64_t)per_cu * (uint64_t)std::max(g->n_cu, 1))
         return set_err(g, FGI_ENOTSUP, "cooperative wave: %u blocks cannot be resident", G);
-    hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm, (uint64_t)g->bm_words);
+    FGI_TRY(fold(g));   // visits of a level-launched wave
+    if (!g->coop_clean)
+        hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
+                           (uint64_t)g->bm_words);
     CoopArgs a{};
     a.roots = roots_dev;
     a.imm = imm_dev;
@@ -1724,8 +1802,8 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
     a.abort = abort;
     void* args[] = {&a};
     FGI_HIP(g, hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_wave_coop), dim3(G), dim3(kBlock), args, 0, s));
-    g->v_dirty = true;
-    if (imm_dev) note_words(g);
+    g->coop_clean = true;   // the wave folded its visits and cleared what it used
+    note_words(g);
     return FGI_OK;
 }
 
@@ -1786,6 +1864,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     bool allow_pull = wp0.direction != 1 && pull_ready(g, wp0);
     static_assert(sizeof(WaveCtr) % 8 == 0, "WaveCtr is cleared as 64-bit words");
     hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm, (uint64_t)g->bm_words);
+    g->coop_clean = false;
 #if FGI_PROBE
     {
         void* pp = nullptr;
@@ -1894,6 +1973,9 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     }
     if (imm_dev && n_roots) note_words(g);   // immediate roots changed node words
     g->last_wave_n = g->ctr_host->inv;
+    // entries this wave made stale: the invalidated nodes' rows and the matched entries pointing at
+    // them (fgi_prune_step's trigger)
+    g->stale_est += e_trav + g->ctr_host->e_match;
     if (n_roots) g->last_levels = (int)std::max<uint64_t>(levels, 1);
     const WaveCtr& c = *g->ctr_host;
     if (trace)
@@ -1951,6 +2033,7 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     FGI_TRY(ensure_cls(g));
     FGI_HIP(g, hipMemsetAsync(pv.sent_bm, 0, pv.sent_words * 4, s));
     hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm, (uint64_t)g->bm_words);
+    g->coop_clean = false;
     while (g->ev.size() < 2) {
         hipEvent_t e;
         FGI_HIP(g, hipEventCreateWithFlags(&e, event_flags()));

@@ -19,7 +19,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("FGI_LIBRARY") or os.path.join(_HERE, "lib", "libfgi.so")
 
 OK, EINVAL, ENOMEM, ECAPACITY, EDEVICE, ESTATE, ENOTSUP = range(7)
-OPT_DEAD_FILTER, OPT_DIRECTION, OPT_PULL_ALPHA, OPT_LEVEL_TIMING, OPT_PULL_BETA = 1, 2, 3, 4, 5
+OPT_DEAD_FILTER, OPT_DIRECTION, OPT_PULL_ALPHA, OPT_LEVEL_TIMING, OPT_PULL_BETA, OPT_DEFRAG_PCT = 1, 2, 3, 4, 5, 6
 DIR_AUTO, DIR_PUSH, DIR_PULL = 0, 1, 2
 NONE = 0xFFFFFFFF
 COMPUTING, CONSISTENT, INVALIDATED = 0, 1, 2
@@ -74,7 +74,12 @@ STEP_INVALIDATE, STEP_BEGIN_COMPUTE, STEP_ADD_USED, STEP_SET_OUTPUT = 1, 2, 3, 4
 
 class PruneStats(C.Structure):
     _fields_ = [("old_edges", C.c_uint64), ("new_edges", C.c_uint64), ("pool_before", C.c_uint64),
-                ("pool_after", C.c_uint64), ("kernel_ms", C.c_double)]
+                ("pool_after", C.c_uint64), ("kernel_ms", C.c_double), ("total_ms", C.c_double),
+                ("live_edges", C.c_uint64), ("dropped_edges", C.c_uint64), ("first", C.c_uint32),
+                ("count", C.c_uint32), ("stale_estimate", C.c_uint64)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 _u32p = C.POINTER(C.c_uint32)
@@ -103,6 +108,8 @@ SIGNATURES = {
     "fgi_last_wave_ids": [_G, _u32p, C.c_uint64, _u64p],
     "fgi_invalidate_all": [_G, _u32p, C.c_uint64, _u64p, C.POINTER(WaveStats)],
     "fgi_prune": [_G, C.POINTER(PruneStats)],
+    "fgi_prune_range": [_G, C.c_uint32, C.c_uint32, C.POINTER(PruneStats)],
+    "fgi_prune_step": [_G, C.c_uint32, C.c_uint32, C.POINTER(PruneStats)],
     "fgi_release": [_G, C.c_uint32, _u32p],
     "fgi_snapshot": [_G],
     "fgi_restore": [_G],
@@ -351,10 +358,12 @@ class Graph:
         n = C.c_uint64()
         if want_ids:
             cap = max(1, sum(1 for sp in steps if sp[0] != "add_used")) * self.n_handles
-            ids = np.zeros(cap, np.uint32)
-            self._check(self.lib.fgi_run_batch(self.h, len(steps), arr, _ptr(ids, C.c_uint32), cap, C.byref(n),
+            buf = getattr(self, "_ids_buf", None)
+            if buf is None or len(buf) < cap:
+                buf = self._ids_buf = np.empty(cap, np.uint32)   # reused across batches
+            self._check(self.lib.fgi_run_batch(self.h, len(steps), arr, _ptr(buf, C.c_uint32), cap, C.byref(n),
                                                C.byref(stats) if stats is not None else None), "run_batch")
-            return ids[:n.value].copy(), outs
+            return buf[:n.value].copy(), outs
         self._check(self.lib.fgi_run_batch(self.h, len(steps), arr, None, 0, C.byref(n),
                                            C.byref(stats) if stats is not None else None), "run_batch")
         return n.value, outs
@@ -396,6 +405,16 @@ class Graph:
     def prune(self) -> PruneStats:
         ps = PruneStats()
         self._check(self.lib.fgi_prune(self.h, C.byref(ps)), "prune")
+        return ps
+
+    def prune_range(self, first: int, count: int) -> PruneStats:
+        ps = PruneStats()
+        self._check(self.lib.fgi_prune_range(self.h, first, count, C.byref(ps)), "prune_range")
+        return ps
+
+    def prune_step(self, batch: int, stale_pct: int) -> PruneStats:
+        ps = PruneStats()
+        self._check(self.lib.fgi_prune_step(self.h, batch, stale_pct, C.byref(ps)), "prune_step")
         return ps
 
     def release(self, handles):

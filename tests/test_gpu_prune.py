@@ -1,0 +1,146 @@
+"""Incremental pruning (ComputedGraphPruner.cs:79-94, Computed.cs:400-419).
+
+(a) A batched prune sequence: fgi_prune_range over consecutive handle ranges (the pruner's walk
+    over the registry in batches), checked after every batch against the oracle's prune of the
+    same slots, and, once the walk has covered every handle, the whole edge set.
+(b) Long rows (hubs past the one-wave path): their in-place compaction keeps exactly the live
+    entries, in order.
+(c) fgi_prune_step runs only once waves have made enough entries stale, then walks the handles.
+(d) A full prune with and without defragmentation gives the same rows; defragmenting shrinks the
+    pool and leaves row slack.
+"""
+import numpy as np
+import pytest
+
+import fgo as O
+from harness import CONSISTENT, assert_states_equal, build_pair, canon_edges, oracle_edges, random_states
+from test_gpu_parity import _compare_wave, _edges_from_live
+
+pytestmark = pytest.mark.gpu
+
+
+def _rows_of(g, lo, hi, n):
+    """Engine rows of slots [lo, hi) as canonical (u, d, t) triples."""
+    u, d, t = g.export_edges()
+    a = canon_edges(u, d, t)
+    if len(a) == 0:
+        return a
+    return a[(a[:, 0] >= lo) & (a[:, 0] < min(hi, n))]
+
+
+def _oracle_rows(o, lo, hi, n):
+    a = oracle_edges(o, n)
+    if len(a) == 0:
+        return a
+    return a[(a[:, 0] >= lo) & (a[:, 0] < hi)]
+
+
+@pytest.mark.parametrize("batch", [500, 1337, 4000])
+def test_batched_prune_sequence_matches_pruner(pkg, gpu_available, batch):
+    rng = np.random.default_rng(29 + batch)
+    n = 4000
+    versions, flags = random_states(n, rng, p_delay=0.0)
+    src, dst, tags = _edges_from_live(versions, flags, rng, 40000, n, stale_p=0.5)
+    g, o = build_pair(pkg, n, versions, flags, src, dst, tags)
+    _compare_wave(g, o, n, rng.integers(0, n, 40).astype(np.uint32))   # lazily removed entries
+    olds = news = 0
+    for lo in range(0, g.n_handles, batch):
+        ps = g.prune_range(lo, batch)
+        oe, ne = o.prune_range(lo, batch)
+        assert (ps.first, ps.count) == (lo, min(batch, g.n_handles - lo))
+        # new counts agree; old ones may not: the engine keeps RemoveUsedBy'd entries until now
+        assert ps.new_edges == ne and ps.old_edges >= oe, (lo, ps.old_edges, ps.new_edges, oe, ne)
+        olds += ps.old_edges
+        news += ne
+        hi = min(lo + batch, n)
+        if lo < n:
+            assert np.array_equal(_rows_of(g, lo, hi, n), _oracle_rows(o, lo, hi, n)), lo
+    u, d, t = g.export_edges()
+    ge = canon_edges(u, d, t)
+    ge = ge[ge[:, 0] < n] if len(ge) else ge
+    assert np.array_equal(ge, oracle_edges(o, n))
+    assert news < olds
+    # waves after the walk agree
+    _compare_wave(g, o, n, rng.integers(0, n, 40).astype(np.uint32))
+    g.close()
+    o.close()
+
+
+def test_long_rows_compact_in_place(pkg, gpu_available):
+    n = 20000
+    rng = np.random.default_rng(31)
+    versions = O.version_of(5, np.arange(n))
+    flags = np.full(n, CONSISTENT, np.uint32)
+    # three hubs with 1,500 / 6,000 / 15,000 entries (the one-block path), 60% stale
+    src, dst = [], []
+    for hub, m in ((0, 1500), (1, 6000), (2, 15000)):
+        src.append(np.full(m, hub, np.uint32))
+        dst.append(rng.choice(np.arange(10, n, dtype=np.uint32), m, replace=False))
+    src = np.concatenate(src)
+    dst = np.concatenate(dst)
+    tags = versions[dst].copy()
+    tags[rng.random(len(tags)) < 0.6] += np.uint64(2)
+    g, o = build_pair(pkg, n, versions, flags, src, dst, tags)
+    before = [g.used_by(hub) for hub in (0, 1, 2)]
+    ps = g.prune()
+    oe, ne = o.prune()
+    assert (ps.old_edges, ps.new_edges) == (oe, ne)
+    u, d, t = g.export_edges()
+    assert np.array_equal(canon_edges(u, d, t), oracle_edges(o, n))
+    for hub, (bd, bt) in zip((0, 1, 2), before):   # the kept entries, in their order
+        dd, tt = g.used_by(hub)
+        keep = bt == versions[bd]
+        assert np.array_equal(dd, bd[keep]) and np.array_equal(tt, bt[keep])
+    assert 0 < ps.new_edges < ps.old_edges
+    g.close()
+    o.close()
+
+
+def test_prune_step_waits_for_stale_entries(pkg, gpu_available):
+    rng = np.random.default_rng(37)
+    n = 3000
+    versions, flags = random_states(n, rng, p_delay=0.0)
+    src, dst, tags = _edges_from_live(versions, flags, rng, 30000, n, stale_p=0.0)
+    g, o = build_pair(pkg, n, versions, flags, src, dst, tags)
+    ps = g.prune_step(1000, 1)
+    assert ps.count == 0 and ps.old_edges == 0                # nothing stale yet: no work
+    _compare_wave(g, o, n, rng.integers(0, n, 200).astype(np.uint32))
+    covered = 0
+    while covered < g.n_handles:
+        ps = g.prune_step(1000, 1)
+        if ps.count == 0:
+            break
+        assert ps.stale_estimate > 0
+        covered += ps.count
+    assert covered >= n
+    o.prune()
+    u, d, t = g.export_edges()
+    ge = canon_edges(u, d, t)
+    ge = ge[ge[:, 0] < n] if len(ge) else ge
+    assert np.array_equal(ge, oracle_edges(o, n))
+    g.close()
+    o.close()
+
+
+def test_defragmentation_keeps_rows(pkg, gpu_available):
+    rng = np.random.default_rng(41)
+    n = 5000
+    versions, flags = random_states(n, rng, p_delay=0.0)
+    src, dst, tags = _edges_from_live(versions, flags, rng, 60000, n, stale_p=0.7)
+    res = []
+    for pct in (0, 30):
+        g, o = build_pair(pkg, n, versions, flags, src, dst, tags)
+        g.set_option(pkg.fgi.OPT_DEFRAG_PCT, pct)
+        ps = g.prune()
+        u, d, t = g.export_edges()
+        res.append((canon_edges(u, d, t), ps.pool_before, ps.pool_after))
+        if pct:
+            assert ps.pool_after < ps.pool_before
+            # waves over the copied rows still agree
+            o.prune()
+            _compare_wave(g, o, n, rng.integers(0, n, 30).astype(np.uint32))
+        else:
+            assert ps.pool_after == ps.pool_before
+        g.close()
+        o.close()
+    assert np.array_equal(res[0][0], res[1][0])
