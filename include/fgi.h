@@ -287,13 +287,16 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *                            events (per-kernel figures for the roofline); 0 keeps only the
  *                            wave-boundary events, so measured waves carry no per-level markers
  *   FGI_OPT_DEFRAG_PCT  [60] fgi_prune copies the rows to a fresh pool when holes exceed this % of
- *                            it (0: never) */
+ *                            it (0: never)
+ *   FGI_OPT_PART_COLLECTIVES [0] a one-rank partition skips its collectives (identities there);
+ *                            1 runs them anyway (tests of the RCCL level loop on one GPU) */
 #define FGI_OPT_DEAD_FILTER 1
 #define FGI_OPT_DIRECTION 2
 #define FGI_OPT_PULL_ALPHA 3
 #define FGI_OPT_LEVEL_TIMING 4
 #define FGI_OPT_PULL_BETA 5
 #define FGI_OPT_DEFRAG_PCT 6
+#define FGI_OPT_PART_COLLECTIVES 7
 fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value);
 
 /* ---- multi-GPU (1-D vertex-range partition, RCCL all-to-all frontier exchange) --------------- */

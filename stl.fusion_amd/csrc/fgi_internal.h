@@ -242,6 +242,7 @@ struct fgi_graph {
     // options (fgi_set_option)
     int opt_dead_filter = 1;
     int opt_defrag_pct = 60;
+    int opt_part_coll = 0;             // FGI_OPT_PART_COLLECTIVES
     uint64_t stale_est = 0;            // entries waves made stale since the last prune (fgi_prune_step)
     uint32_t prune_cursor = 0;         // next handle of fgi_prune_step's walk
     int opt_direction = 0;
@@ -303,6 +304,8 @@ fgi_status build_rows_from_keys(fgi_graph* g, uint64_t m, uint64_t* keys, uint64
 fgi_status ensure_in_lists(fgi_graph* g);
 // Copy the first two entries of every slot's list into uin_head, then (re)build the pull
 // candidate segments (wave.hip).
+// orders every dependency list by weight[entry], descending (graph.hip)
+fgi_status sort_in_lists(fgi_graph* g, uint64_t total, const uint32_t* weight, uint32_t n_weight);
 fgi_status build_in_heads(fgi_graph* g);
 fgi_status build_candidates(fgi_graph* g);
 // Pull geometry of a graph: blocks of a pull level and the tiles each owns (0 blocks: the graph is

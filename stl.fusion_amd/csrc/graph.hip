@@ -1208,44 +1208,53 @@ fgi_status ensure_in_lists(fgi_graph* g) {
     // Order every list by the entries' own dependency counts (descending; ties by handle): the
     // nodes a wave reaches first are the ones with many dependencies, so a pull level finds a
     // parent in the frontier among the first entries (and in the two heads, most of the time).
-    if (total > 1) {
-        uint32_t ubits = 1;
-        while (ubits < 32 && (1ull << ubits) < H) ++ubits;
-        uint32_t max_len = 0;
-        {
-            Tmp tr, tm;
-            uint32_t* dmax;
-            FGI_TRY(tmalloc(g, tm, &dmax, 1));
-            size_t rb = 0;
-            FGI_HIP(g, rocprim::reduce(nullptr, rb, g->uin_len, dmax, 0u, (size_t)N, rocprim::maximum<uint32_t>(), s));
-            char* rt;
-            FGI_TRY(tmalloc(g, tr, &rt, rb));
-            FGI_HIP(g, rocprim::reduce(rt, rb, g->uin_len, dmax, 0u, (size_t)N, rocprim::maximum<uint32_t>(), s));
-            FGI_TRY(d2h(g, &max_len, dmax, 1));
-        }
-        uint32_t wbits = 1;
-        while (wbits < 32 && (1ull << wbits) <= max_len) ++wbits;
-        Tmp tk0, tk1, te, tt;
-        uint64_t *k0, *k1, *ends;
-        FGI_TRY(tmalloc(g, tk0, &k0, total));
-        FGI_TRY(tmalloc(g, tk1, &k1, total));
-        FGI_TRY(tmalloc(g, te, &ends, N));
-        hipLaunchKernelGGL(k_in_keys, dim3(nblk(total)), dim3(256), 0, s, total, g->uin_src, g->uin_len, N, ubits, k0);
-        hipLaunchKernelGGL(k_in_ends, dim3(nblk(N)), dim3(256), 0, s, N, g->uin_off, g->uin_len, ends);
-        size_t sb = 0;
-        FGI_HIP(g, rocprim::segmented_radix_sort_keys_desc(nullptr, sb, k0, k1, (unsigned)total, N, g->uin_off, ends, 0,
-                                                           ubits + wbits, s));
-        char* st;
-        FGI_TRY(tmalloc(g, tt, &st, sb));
-        FGI_HIP(g, rocprim::segmented_radix_sort_keys_desc(st, sb, k0, k1, (unsigned)total, N, g->uin_off, ends, 0,
-                                                           ubits + wbits, s));
-        hipLaunchKernelGGL(k_in_unkey, dim3(nblk(total)), dim3(256), 0, s, total, k1, ubits, g->uin_src);
-        FGI_HIP(g, hipGetLastError());
-        FGI_HIP(g, hipStreamSynchronize(s));
-    }
+    FGI_TRY(sort_in_lists(g, total, g->uin_len, N));
     FGI_TRY(build_in_heads(g));
     FGI_HIP(g, hipStreamSynchronize(s));
     g->uin_epoch = g->mut_epoch;
+    return FGI_OK;
+}
+
+// Orders every dependency list by weight[entry] (descending; ties by the larger id; entries at or
+// past n_weight weigh 0). total = entries over all lists.
+fgi_status sort_in_lists(fgi_graph* g, uint64_t total, const uint32_t* weight, uint32_t n_weight) {
+    if (total <= 1) return FGI_OK;
+    hipStream_t s = g->stream;
+    const uint32_t N = g->n_slots;
+    const uint64_t ids = std::max<uint64_t>(g->n_handles, n_weight);
+    uint32_t ubits = 1;
+    while (ubits < 32 && (1ull << ubits) < ids) ++ubits;
+    uint32_t max_w = 0;
+    {
+        Tmp tr, tm;
+        uint32_t* dmax;
+        FGI_TRY(tmalloc(g, tm, &dmax, 1));
+        size_t rb = 0;
+        FGI_HIP(g, rocprim::reduce(nullptr, rb, weight, dmax, 0u, (size_t)n_weight, rocprim::maximum<uint32_t>(), s));
+        char* rt;
+        FGI_TRY(tmalloc(g, tr, &rt, rb));
+        FGI_HIP(g, rocprim::reduce(rt, rb, weight, dmax, 0u, (size_t)n_weight, rocprim::maximum<uint32_t>(), s));
+        FGI_TRY(d2h(g, &max_w, dmax, 1));
+    }
+    uint32_t wbits = 1;
+    while (wbits < 32 && (1ull << wbits) <= max_w) ++wbits;
+    Tmp tk0, tk1, te, tt;
+    uint64_t *k0, *k1, *ends;
+    FGI_TRY(tmalloc(g, tk0, &k0, total));
+    FGI_TRY(tmalloc(g, tk1, &k1, total));
+    FGI_TRY(tmalloc(g, te, &ends, N));
+    hipLaunchKernelGGL(k_in_keys, dim3(nblk(total)), dim3(256), 0, s, total, g->uin_src, weight, n_weight, ubits, k0);
+    hipLaunchKernelGGL(k_in_ends, dim3(nblk(N)), dim3(256), 0, s, N, g->uin_off, g->uin_len, ends);
+    size_t sb = 0;
+    FGI_HIP(g, rocprim::segmented_radix_sort_keys_desc(nullptr, sb, k0, k1, (unsigned)total, N, g->uin_off, ends, 0,
+                                                       ubits + wbits, s));
+    char* st;
+    FGI_TRY(tmalloc(g, tt, &st, sb));
+    FGI_HIP(g, rocprim::segmented_radix_sort_keys_desc(st, sb, k0, k1, (unsigned)total, N, g->uin_off, ends, 0,
+                                                       ubits + wbits, s));
+    hipLaunchKernelGGL(k_in_unkey, dim3(nblk(total)), dim3(256), 0, s, total, k1, ubits, g->uin_src);
+    FGI_HIP(g, hipGetLastError());
+    FGI_HIP(g, hipStreamSynchronize(s));
     return FGI_OK;
 }
 
@@ -1295,16 +1304,18 @@ fgi_status build_candidates(fgi_graph* g) {
     FGI_TRY(d2h(g, &lp, pos + N - 1, 1));
     FGI_TRY(d2h(g, &lf, flag + N - 1, 1));
     const uint32_t total = lp + lf;
-    // hot heads (single-device graphs; a partition's heads are global ids)
+    // hot heads (a partition's heads are global ids: ranked over all n_global slots, their snapshot
+    // taken from the all-gathered invalidated bitmap)
     Tmp th;
     uint32_t* hot_rank = nullptr;
     g->n_hot = 0;
-    if (!g->part && g->n_handles < kHotFlag) {
+    PartView pv;
+    const uint32_t NH = part_view(g, &pv) ? pv.n_global : g->n_handles;
+    if (NH < kHotFlag) {
         if (!g->hot_id) {
             FGI_TRY(dmalloc(g, &g->hot_id, kHot));
             FGI_TRY(dmalloc(g, &g->hot_bm, kHot / 32));
         }
-        const uint32_t NH = g->n_handles;
         Tmp tc, tk0, tk1, tt;
         uint32_t* cnt;
         uint64_t *k0, *k1;
@@ -1810,6 +1821,7 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
     if (!g) return FGI_EINVAL;
     switch (option) {
     case FGI_OPT_DEAD_FILTER: g->opt_dead_filter = value ? 1 : 0; return FGI_OK;
+    case FGI_OPT_PART_COLLECTIVES: g->opt_part_coll = value ? 1 : 0; return FGI_OK;
     case FGI_OPT_DEFRAG_PCT: g->opt_defrag_pct = (int)std::max<int64_t>(0, std::min<int64_t>(100, value)); return FGI_OK;
     case FGI_OPT_DIRECTION:
         if (value < 0 || value > 2) return set_err(g, FGI_EINVAL, "direction must be 0, 1 or 2");

@@ -104,8 +104,12 @@ struct RcclComm final : PartComm {
     fgi_status allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out, uint32_t count) override {
         PartState* p = ps(g);
         hipStream_t s = g->stream;
-        FGI_NCCL(g, ncclAllReduce(dev_val, p->scalar, count, ncclUint64, ncclSum, p->comm, s));
-        FGI_HIP(g, hipMemcpyAsync(p->scalar_host, p->scalar, 8 * count, hipMemcpyDeviceToHost, s));
+        if (p->v.world > 1 || g->opt_part_coll) {
+            FGI_NCCL(g, ncclAllReduce(dev_val, p->scalar, count, ncclUint64, ncclSum, p->comm, s));
+            FGI_HIP(g, hipMemcpyAsync(p->scalar_host, p->scalar, 8 * count, hipMemcpyDeviceToHost, s));
+        } else {   // one rank: the sum is the value
+            FGI_HIP(g, hipMemcpyAsync(p->scalar_host, dev_val, 8 * count, hipMemcpyDeviceToHost, s));
+        }
         FGI_HIP(g, hipStreamSynchronize(s));
         for (uint32_t i = 0; i < count; ++i) out[i] = p->scalar_host[i];
         return FGI_OK;
@@ -326,6 +330,16 @@ __global__ void k_in_part_rows(uint64_t m, const uint64_t* __restrict__ k, const
     if (e + 1 == m || (uint32_t)(k[e + 1] >> 32) != d) len[d] = pos[e] + keep[e];   // row end, fixed below
 }
 
+// weight of a global slot for the list order: its non-stale dependencies in the global edge list
+__global__ void k_in_part_weight(uint64_t m, const uint64_t* __restrict__ keys, uint32_t stale_pct, uint64_t stale_seed,
+                                 uint32_t* w) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= m) return;
+    const uint64_t k = keys[e];
+    const uint32_t src = (uint32_t)(k >> 32), dst = (uint32_t)k;
+    if (!synth_stale(stale_pct, stale_seed, src, dst)) atomicAdd(w + dst, 1u);
+}
+
 __global__ void k_in_part_fix(uint32_t n, const uint64_t* __restrict__ off, uint32_t* len) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d < n && len[d]) len[d] -= (uint32_t)off[d];
@@ -409,7 +423,18 @@ static fgi_status part_build_in_lists(fgi_graph* g, const uint64_t* keys, uint64
                            g->uin_len);
         hipLaunchKernelGGL(k_in_part_fix, dim3((g->n_slots + 255) / 256), dim3(256), 0, s, g->n_slots, g->uin_off,
                            g->uin_len);
-        // global dependency ids carry no local weight: lists stay in id order
+        // as the single engine (build_in_lists): every list by its entries' own dependency counts,
+        // which every rank counts over the global edge list it holds
+        uint32_t* w = nullptr;
+        if (hipMalloc(&w, (size_t)p->v.n_global * 4) != hipSuccess) {
+            rc = set_err(g, FGI_ENOMEM, "list weights");
+            break;
+        }
+        hipMemsetAsync(w, 0, (size_t)p->v.n_global * 4, s);
+        hipLaunchKernelGGL(k_in_part_weight, dim3(nb), dim3(256), 0, s, m, keys, stale_pct, stale_seed, w);
+        rc = sort_in_lists(g, total, w, p->v.n_global);
+        hipFree(w);
+        if (rc != FGI_OK) break;
         rc = build_in_heads(g);
         if (rc != FGI_OK) break;
         if (hipStreamSynchronize(s) != hipSuccess) rc = set_err(g, FGI_EDEVICE, "dependency-list build");

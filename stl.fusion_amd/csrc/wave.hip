@@ -2031,7 +2031,9 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     hipStream_t s = g->stream;
     FGI_TRY(ensure_cstart(g, g->pool_top));
     FGI_TRY(ensure_cls(g));
-    FGI_HIP(g, hipMemsetAsync(pv.sent_bm, 0, pv.sent_words * 4, s));
+    // one rank: nothing is remote, the collectives are identities (skipped unless FGI_OPT_PART_COLLECTIVES)
+    const bool coll = pv.world > 1 || g->opt_part_coll;
+    if (coll) FGI_HIP(g, hipMemsetAsync(pv.sent_bm, 0, pv.sent_words * 4, s));
     hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm, (uint64_t)g->bm_words);
     g->coop_clean = false;
     while (g->ev.size() < 2) {
@@ -2059,6 +2061,8 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     const bool allow_pull = sums[3] == 0;
     const int direction = wp.direction;
     const RemoteArgs ra{pv.base, pv.n_local, pv.block, pv.world, pv.ver_all, pv.sent_bm, pv.send_buf, pv.send_cnt};
+    // the invalidated bitmap over all slots: all-gathered before pull levels (one rank: its own)
+    const uint32_t* front = coll ? pv.front_global : g->inv_bm;
     uint64_t f_global = sums[1], t_global = sums[2];
     uint64_t levels = 0, e_trav = 0, f_total = 0, sent_total = 0, push_edges = 0, push_f = 0;
     uint64_t pull_levels = 0, pull_launches = 0, expand_launches = 0;
@@ -2070,23 +2074,24 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
                           (direction == 2 || (direction == 0 && (t_global > wp.pull_threshold ||
                                                                  (last_pull && f_global > stay_pull_f))));
         const int buf = L & 1;
-        FGI_HIP(g, hipMemsetAsync(pv.send_cnt, 0, (size_t)pv.world * 8, s));
+        if (coll) FGI_HIP(g, hipMemsetAsync(pv.send_cnt, 0, (size_t)pv.world * 8, s));
         // the level's direction for its kernels: the flag's high word is zero (the ring slot was
         // cleared two levels ago or at wave start), so a 32-bit device-side set is the whole store
         if (pull) {
             FGI_HIP(g, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&g->ctr->lvl[L % kRing].pull), 1, 1, s));
-            FGI_TRY(part_allgather_front(g));
+            if (coll) FGI_TRY(part_allgather_front(g));
         }
-        hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp,
-                           collect_args(g, pv.n_local, wp, buf));
+        CollectArgs ca = collect_args(g, pv.n_local, wp, buf);
+        ca.inv = front;   // hot heads are global ids
+        hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp, ca);
         if (g->opt_level_timing) FGI_HIP(g, hipEventRecord(g->ev[0], s));
         hipLaunchKernelGGL(k_level<true>, dim3(wp.grid), dim3(kBlock), 0, s, L, wp, expand_args(g, buf),
-                           pull_args(g, g->n_slots, pv.front_global), node, g->vis_bm, out_for(g, buf ^ 1, nullptr),
+                           pull_args(g, g->n_slots, front), node, g->vis_bm, out_for(g, buf ^ 1, nullptr),
                            g->ctr, g->blk_stats, g->done, ra);
         if (g->opt_level_timing) FGI_HIP(g, hipEventRecord(g->ev[1], s));
         FGI_HIP(g, hipGetLastError());
         uint64_t n_recv = 0, n_sent = 0;
-        if (!pull) FGI_TRY(part_exchange(g, &n_recv, &n_sent));
+        if (!pull && coll) FGI_TRY(part_exchange(g, &n_recv, &n_sent));
         if (n_recv)
             hipLaunchKernelGGL(k_apply_recv, dim3(std::min<uint64_t>((n_recv + kBlock - 1) / kBlock, (uint64_t)g->n_cu * 8)),
                                dim3(kBlock), 0, s, L, n_recv, pv.recv_buf, pv.base, node, g->vis_bm,

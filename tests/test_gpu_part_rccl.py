@@ -1,7 +1,9 @@
 """The RCCL partition path itself (fgi_part_init + fgi_part_invalidate: the code bench.py runs for
 N > 1), at world size 1 on one GPU: the level loop, its all-reduces and exchanges go through a real
-RCCL communicator. Results must equal the oracle's bit-exactly (invalidated set, V_inv, E_trav,
-final node states), for push-only, pull-only and automatic direction, with and without stale edges."""
+RCCL communicator (FGI_OPT_PART_COLLECTIVES=1; a one-rank partition otherwise skips them, which
+is what bench.py --partition measures at N=1 — both are checked). Results must equal the oracle's
+bit-exactly (invalidated set, V_inv, E_trav, final node states), for push-only, pull-only and
+automatic direction, with and without stale edges."""
 import numpy as np
 import pytest
 import torch
@@ -13,13 +15,15 @@ pytestmark = pytest.mark.gpu
 
 @pytest.mark.parametrize("direction", [0, 1, 2])      # auto, push only, pull only
 @pytest.mark.parametrize("stale", [0, 50])
-def test_rccl_partition_world1_matches_oracle(pkg, gpu_available, stale, direction):
+@pytest.mark.parametrize("collectives", [1, 0])
+def test_rccl_partition_world1_matches_oracle(pkg, gpu_available, stale, direction, collectives):
     scale, ef, seed, sseed = 12, 16, 0x5EED0027, 0x5EED00C0
     n = 1 << scale
     g = pkg.Graph(n, rank=0, world=1)
     g.part_init(n, pkg.fgi.part_unique_id())
     g.part_synth_rmat(scale, ef, seed, stale, sseed)
     g.set_option(2, direction)
+    g.set_option(pkg.fgi.OPT_PART_COLLECTIVES, collectives)
     s, d = O.gen_rmat(scale, ef, seed)
     o = O.Oracle(n)
     o.load_graph(O.version_of(seed, np.arange(n)), None, s, d, O.gen_tags(s, d, seed, stale, sseed))
