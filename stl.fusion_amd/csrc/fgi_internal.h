@@ -273,6 +273,7 @@ struct fgi_graph {
     uint32_t* bout = nullptr;
     uint64_t bout_cap = 0;
     uint64_t batch_ids_hint = 0;       // the previous batch's id count (sizes the copy made with the results)
+    std::vector<hipEvent_t> batch_ev;  // fgi_run_batch per-cascade timing events (pairs)
     hipEvent_t ev_w0 = nullptr, ev_w1 = nullptr;
 
     // multi-GPU

@@ -1538,6 +1538,7 @@ fgi_status fgi_destroy(fgi_graph* g) {
     if (g->ctr_host) hipHostFree(g->ctr_host);
     if (g->misc_host) hipHostFree(g->misc_host);
     for (hipEvent_t e : g->ev) hipEventDestroy(e);
+    for (hipEvent_t e : g->batch_ev) hipEventDestroy(e);
     if (g->bst_h) hipHostFree(g->bst_h);
     dfree(g->bst_d);
     dfree(g->bout);
@@ -2110,21 +2111,31 @@ struct BatchStep {
 // Launches steps [from, n) of a batch; returns with the work queued (no synchronisation).
 static fgi_status batch_launch(fgi_graph* g, uint32_t from, uint32_t n_steps, const fgi_step* steps,
                                std::vector<BatchStep>& bs, unsigned long long* scr, const uint32_t* take,
-                               uint64_t n_take, std::vector<std::pair<hipEvent_t, hipEvent_t>>& wave_ev) {
+                               uint64_t n_take, bool timed, std::vector<std::pair<hipEvent_t, hipEvent_t>>& wave_ev) {
     hipStream_t st = g->stream;
     unsigned long long* abort = scr;
     unsigned long long* out_n = scr + 1;
     unsigned long long* cursor = scr + 2;
     unsigned long long* acc = scr + 3;
     auto* node = reinterpret_cast<unsigned long long*>(g->node);
+    // per-cascade timing (the wave share of fgi_batch_stats) only when asked for: timestamped
+    // markers between the launches cost device time of their own; the events are the graph's pool
     auto wave = [&](uint32_t n_max, const uint32_t* roots, const uint8_t* imm, const unsigned long long* n_dev) -> fgi_status {
         hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
+        if (timed) {
+            const size_t i = wave_ev.size();
+            while (g->batch_ev.size() < 2 * (i + 1)) {
+                hipEvent_t e;
+                FGI_HIP(g, hipEventCreate(&e));
+                g->batch_ev.push_back(e);
+            }
+            e0 = g->batch_ev[2 * i];
+            e1 = g->batch_ev[2 * i + 1];
             wave_ev.emplace_back(e0, e1);
-            hipEventRecord(e0, st);
+            FGI_HIP(g, hipEventRecord(e0, st));
         }
         FGI_TRY(run_wave_coop(g, n_max, roots, imm, n_dev, g->bout, out_n, acc, abort));
-        if (e1) hipEventRecord(e1, st);
+        if (e1) FGI_HIP(g, hipEventRecord(e1, st));
         return fold(g);
     };
     for (uint32_t k = from; k < n_steps; ++k) {
@@ -2355,20 +2366,12 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
     }
     const uint32_t* take = reinterpret_cast<const uint32_t*>(D);
     std::vector<std::pair<hipEvent_t, hipEvent_t>> wave_ev;
-    auto release_events = [&]() {
-        for (auto& e : wave_ev) {
-            hipEventDestroy(e.first);
-            hipEventDestroy(e.second);
-        }
-    };
+    const bool timed = stats && g->opt_level_timing;
     uint32_t syncs = 0, from = 0;
     g->last_wave_n = 0;
     while (true) {
-        fgi_status s = batch_launch(g, from, n_steps, steps, bs, scr, take, n_take, wave_ev);
-        if (s != FGI_OK) {
-            release_events();
-            return s;
-        }
+        fgi_status s = batch_launch(g, from, n_steps, steps, bs, scr, take, n_take, timed, wave_ev);
+        if (s != FGI_OK) return s;
         // results: the counters, the pool top and every step's output in one copy, the ids (as
         // many as the previous batch had, +25%) in a second, then one wait
         hipLaunchKernelGGL(kb_finish, dim3(1), dim3(64), 0, st, g->pool_top_dev, scr + ptop_word);
@@ -2383,11 +2386,7 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
         const uint32_t k = (uint32_t)(ab & 0xFFFFFFFFull) - 1;
         if ((ab >> 32) == kAbortPool) {   // grow the pool, then finish step k and run the rest
             const unsigned long long need = bs[k].cnt ? scr_h[3 + kAccCount + 4 * k + 3] : 0;
-            fgi_status s2 = ensure_pool(g, g->pool_top + need + std::max<uint64_t>(1ull << 20, 4 * n_add));
-            if (s2 != FGI_OK) {
-                release_events();
-                return s2;
-            }
+            FGI_TRY(ensure_pool(g, g->pool_top + need + std::max<uint64_t>(1ull << 20, 4 * n_add)));
             scr_h[0] = 0;
             FGI_HIP(g, hipMemcpyAsync(scr, scr_h, 8, hipMemcpyHostToDevice, st));
             bs[k].hcap = 0;   // marks the resumed step: relocation and pending entries only
@@ -2396,7 +2395,6 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
         }
         // out of detached handles at step k: steps before it are applied
         g->free_detached.resize(g->free_detached.size() - (size_t)scr_h[2]);
-        release_events();
         return set_err(g, FGI_ECAPACITY, "step %u: out of detached handles (%zu free)", k, g->free_detached.size());
     }
     // host bookkeeping: the detached handles taken, the per-step outputs
@@ -2442,7 +2440,6 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
         stats->host_syncs += syncs;
         stats->total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
-    release_events();
     return ret;
 }
 
