@@ -191,6 +191,7 @@ struct fgi_graph {
     // visitor. fold() applies the bits to the words before any mutation or state query.
     uint32_t* vis_bm = nullptr;
     bool v_dirty = false;              // vis_bm may hold set bits
+    bool vis_stale = false;            // fgi_restore left vis_bm's clearing to the next wave (flush_vis)
     bool coop_clean = false;           // wave counters, statistics and bitmaps clear (a cooperative wave left them so)
     // Expandable-class bitmap (Consistent, no delay: a first visit invalidates and expands), built
     // from the node words; pull levels read it instead of the words (2 MB vs 128 MB at 16M slots).
@@ -229,7 +230,6 @@ struct fgi_graph {
     uint32_t* hot_id = nullptr;        // [kHot] rank -> handle (FGI_NONE past n_hot)
     uint32_t* hot_bm = nullptr;        // [kHot / 32]
     uint32_t n_hot = 0;
-    uint32_t final_epoch = 0;          // launch epoch of k_final's status words
     uint4* sv[2] = {nullptr, nullptr};
     uint32_t* sv_cnt[2] = {nullptr, nullptr};   // [pull grid] survivors per block
     uint64_t cand_cap = 0;
@@ -322,6 +322,7 @@ inline void note_words(fgi_graph* g) {
 // Apply the visit bitmap to the node words and clear it (wave.hip). Every entry point that reads or
 // mutates node words outside a wave calls it first.
 fgi_status fold(fgi_graph* g);
+fgi_status flush_vis(fgi_graph* g);   // fgi_restore's deferred visit-bitmap clear, before any use but a wave's init
 #if FGI_PROBE
 void print_coop_probe();
 #endif

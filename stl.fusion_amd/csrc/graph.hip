@@ -1472,7 +1472,8 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
     hipMemset(g->row_cap, 0, H * sizeof(uint32_t));
     hipMemset(g->used_cnt, 0, H * sizeof(uint32_t));
     hipMemset(g->pool_top_dev, 0, sizeof(unsigned long long));
-    if (hipEventCreate(&g->ev_w0) != hipSuccess || hipEventCreate(&g->ev_w1) != hipSuccess) return fail(FGI_EDEVICE);
+    if (hipEventCreateWithFlags(&g->ev_w0, hipEventDisableSystemFence) != hipSuccess ||
+        hipEventCreateWithFlags(&g->ev_w1, hipEventDisableSystemFence) != hipSuccess) return fail(FGI_EDEVICE);
     g->free_detached.reserve(g->n_detached);
     for (uint32_t i = g->n_detached; i > 0; --i) g->free_detached.push_back(g->n_slots + i - 1);
     if (ensure_pool(g, std::max<uint64_t>(cfg->edge_capacity, 1024)) != FGI_OK) return fail(FGI_ENOMEM);
@@ -1801,7 +1802,8 @@ fgi_status fgi_restore(fgi_graph* g) {
         g->words_dirty = false;
         g->cls_valid = false;
     }
-    if (g->v_dirty) FGI_HIP(g, hipMemsetAsync(g->vis_bm, 0, g->bm_words * 4, s));
+    // the visit bits are cleared by the next wave's init kernel (or flush_vis before any other use)
+    if (g->v_dirty) g->vis_stale = true;
     g->v_dirty = false;
     if (g->mut_epoch == g->snap_mut_epoch) {
         // nothing but waves ran since the snapshot: rows and |_used| counts are unchanged. The
@@ -2112,6 +2114,7 @@ struct BatchStep {
 static fgi_status batch_launch(fgi_graph* g, uint32_t from, uint32_t n_steps, const fgi_step* steps,
                                std::vector<BatchStep>& bs, unsigned long long* scr, const uint32_t* take,
                                uint64_t n_take, bool timed, std::vector<std::pair<hipEvent_t, hipEvent_t>>& wave_ev) {
+    FGI_TRY(flush_vis(g));
     hipStream_t st = g->stream;
     unsigned long long* abort = scr;
     unsigned long long* out_n = scr + 1;

@@ -598,6 +598,7 @@ fgi_status fgi_part_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_facto
     FGI_HIP(g, hipMemsetAsync(g->node, 0, (size_t)g->n_handles * 8, s));
     FGI_HIP(g, hipMemsetAsync(g->vis_bm, 0, g->bm_words * 4, s));   // a new node table
     g->v_dirty = false;
+    g->vis_stale = false;
     note_words(g);
     hipLaunchKernelGGL(k_versions_local, dim3((p->v.n_local + 255) / 256), dim3(256), 0, s, p->v.n_local, p->v.base,
                        seed, reinterpret_cast<unsigned long long*>(g->node));

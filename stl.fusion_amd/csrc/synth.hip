@@ -85,6 +85,7 @@ fgi_status synth_versions(fgi_graph* g, uint32_t n, uint64_t seed) {
     FGI_HIP(g, hipMemsetAsync(g->node, 0, (size_t)g->n_handles * 8, g->stream));
     FGI_HIP(g, hipMemsetAsync(g->vis_bm, 0, g->bm_words * 4, g->stream));   // a new node table
     g->v_dirty = false;
+    g->vis_stale = false;
     note_words(g);
     hipLaunchKernelGGL(k_versions, dim3((n + 255) / 256), dim3(256), 0, g->stream, n, seed,
                        reinterpret_cast<unsigned long long*>(g->node));

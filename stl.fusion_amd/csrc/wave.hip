@@ -1225,27 +1225,18 @@ __global__ __launch_bounds__(kBlock) void k_apply_recv(int L, uint64_t n, const 
 }
 
 // ---- final collect: the invalidated bitmap -> the invalidated list -----------------------------
-// One pass, launched cooperatively (every block resident, so waiting on another block cannot
-// deadlock; a ticket counter would serialise ~1,000 atomics on one word): block t counts the set
-// bits of its 64-bit words [t * wpb, (t + 1) * wpb), publishes the count, adds up its
-// predecessors' counts (all of them at once) and writes every set bit's handle at that offset, in
-// ascending order: one 1,024-handle tile per wave, 16 handles per lane, staged in LDS and stored
-// coalesced. Status words carry the launch's epoch (bits 48-63) and a flag (bit 46), so they need
-// no reset. Tickets 0..kStats-1 also fold the per-block
-// statistics into the wave counters (one column each, coalesced sweeps).
-constexpr unsigned long long kStAgg = 1ull << 46, kStVal = kStAgg - 1;
-constexpr uint32_t kFinalStage = 1024;   // bitmap words a block keeps in LDS (8 KB)
-
-__global__ __launch_bounds__(kBlock) void k_final(const unsigned long long* __restrict__ inv64, uint64_t words,
-                                                  uint64_t wpb, unsigned long long* status, uint32_t epoch, WaveCtr* ctr,
-                                                  const unsigned long long* __restrict__ blk, uint32_t* out) {
+// Two launches, no inter-block waiting (a cooperative launch costs ~11 us of dispatch gap on this
+// stack, a ticket counter serialises ~1,000 atomics on one word): k_final_count — block t counts the
+// set bits of its 64-bit words [t * wpb, (t + 1) * wpb) and stores the count; tickets 0..kStats-1
+// also fold the per-block statistics into the wave counters (one column each, coalesced sweeps).
+// k_final_write — block t adds up its predecessors' counts (all of them in one round) and writes
+// every set bit's handle at that offset, in ascending order: one 1,024-handle tile per wave, 16
+// handles per lane, staged in LDS and stored coalesced.
+__global__ __launch_bounds__(kBlock) void k_final_count(const unsigned long long* __restrict__ inv64, uint64_t words,
+                                                        uint64_t wpb, unsigned long long* status, WaveCtr* ctr,
+                                                        const unsigned long long* __restrict__ blk) {
     __shared__ unsigned long long s_red[kBlock / 64];
-    __shared__ unsigned long long s_excl;
-    __shared__ uint32_t s_w[kBlock / 64];
-    __shared__ uint32_t s_stage[kBlock / 64][kPullTile];
-    __shared__ unsigned long long s_words[kFinalStage];   // the block's words, read once
     const uint32_t t = blockIdx.x;
-    const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
     if (t < (uint32_t)kStats) {
         const int k = t;
         unsigned long long* dst[kStats] = {&ctr->e_match,   &ctr->n_flagged, &ctr->pull_surv, &ctr->pull_edges,
@@ -1259,40 +1250,36 @@ __global__ __launch_bounds__(kBlock) void k_final(const unsigned long long* __re
     }
     const uint64_t lo = t * wpb, hi = std::min<uint64_t>(words, lo + wpb);
     unsigned long long c = 0;
-    for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x) {
-        const unsigned long long v = inv64[w];
-        if (w - lo < kFinalStage) s_words[w - lo] = v;
-        c += (unsigned long long)__popcll(v);
-    }
-    c = block_sum(c, s_red);   // (its barriers also publish s_words)
-    const unsigned long long ep = (unsigned long long)epoch << 48;
-    if (threadIdx.x == 0) coh_xchg(status + t, ep | kStAgg | c);
-    // every predecessor's count, read by all threads in one round (atomic loads at agent scope:
-    // served where the XCDs agree, without serialising like read-modify-writes on one word)
+    for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x) c += (unsigned long long)__popcll(inv64[w]);
+    c = block_sum(c, s_red);
+    if (threadIdx.x == 0) status[t] = c;
+}
+
+__global__ __launch_bounds__(kBlock) void k_final_write(const unsigned long long* __restrict__ inv64, uint64_t words,
+                                                        uint64_t wpb, const unsigned long long* __restrict__ status,
+                                                        WaveCtr* ctr, uint32_t* out) {
+    __shared__ unsigned long long s_red[kBlock / 64];
+    __shared__ unsigned long long s_excl;
+    __shared__ uint32_t s_w[kBlock / 64];
+    __shared__ uint32_t s_stage[kBlock / 64][kPullTile];
+    const uint32_t t = blockIdx.x;
+    const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
     unsigned long long part = 0;
-    for (uint32_t k = threadIdx.x; k < t; k += blockDim.x) {
-        unsigned long long v;
-        do {
-            v = __hip_atomic_load(status + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } while ((v & ~((1ull << 48) - 1)) != ep);
-        part += v & kStVal;
-    }
+    for (uint32_t k = threadIdx.x; k < t; k += blockDim.x) part += status[k];
     const unsigned long long excl = block_sum(part, s_red);
     if (threadIdx.x == 0) {
         s_excl = excl;
-        if (t == gridDim.x - 1) ctr->inv = excl + c;
+        if (t == gridDim.x - 1) ctr->inv = excl + status[t];
     }
     __syncthreads();
+    const uint64_t lo = t * wpb, hi = std::min<uint64_t>(words, lo + wpb);
     const uint16_t* bits16 = reinterpret_cast<const uint16_t*>(inv64);
     uint64_t run = s_excl;
     // rounds of one 16-word tile per wave
     for (uint64_t w0 = lo; w0 < hi; w0 += (uint64_t)(blockDim.x >> 6) * kTileWords) {   // block-uniform
         const uint64_t tw = w0 + (uint64_t)wid * kTileWords;                            // the wave's first word
         const uint64_t q = tw * 4 + lane;                                                // the lane's 16-bit chunk
-        const uint64_t wl = tw - lo + lane / 4;
-        const uint32_t m = (tw + lane / 4 >= hi) ? 0u
-                           : wl < kFinalStage ? (uint32_t)(s_words[wl] >> (16 * (lane & 3))) & 0xFFFFu
-                                              : (uint32_t)bits16[q];
+        const uint32_t m = (tw + lane / 4 >= hi) ? 0u : (uint32_t)bits16[q];
         uint32_t tot;
         const uint32_t ex = wave_excl_scan((uint32_t)__popc(m), tot);
         __syncthreads();
@@ -1311,6 +1298,8 @@ __global__ __launch_bounds__(kBlock) void k_final(const unsigned long long* __re
         run += all;
     }
 }
+
+constexpr uint32_t kFinalStage = 1024;   // bitmap words a block keeps in LDS (8 KB), k_wave_coop
 
 // ---- a whole (push-only) wave in one launch ---------------------------------------------------
 // Streaming batches (fgi_run_batch) queue mutation steps and waves back to back and synchronise once
@@ -1519,7 +1508,7 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_wave_init(WaveCtr* ctr, unsigned long long* blk, uint32_t* inv_bm,
-                                                      uint64_t bm_words) {
+                                                      uint32_t* vis_bm, uint64_t bm_words) {
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
     unsigned long long* c = reinterpret_cast<unsigned long long*>(ctr);
@@ -1528,6 +1517,11 @@ __global__ __launch_bounds__(kBlock) void k_wave_init(WaveCtr* ctr, unsigned lon
     uint4* f4 = reinterpret_cast<uint4*>(inv_bm);
     for (uint64_t i = tid; i < bm_words / 4; i += nthr) f4[i] = make_uint4(0u, 0u, 0u, 0u);
     for (uint64_t i = bm_words / 4 * 4 + tid; i < bm_words; i += nthr) inv_bm[i] = 0u;
+    if (vis_bm) {   // fgi_restore's deferred clear
+        uint4* v4 = reinterpret_cast<uint4*>(vis_bm);
+        for (uint64_t i = tid; i < bm_words / 4; i += nthr) v4[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (uint64_t i = bm_words / 4 * 4 + tid; i < bm_words; i += nthr) vis_bm[i] = 0u;
+    }
 }
 
 // ---- fold / class bitmap -----------------------------------------------------------------------
@@ -1554,7 +1548,15 @@ __global__ __launch_bounds__(kBlock) void k_build_cls(uint32_t n, const unsigned
 
 }  // namespace
 
+fgi_status flush_vis(fgi_graph* g) {
+    if (!g->vis_stale) return FGI_OK;
+    FGI_HIP(g, hipMemsetAsync(g->vis_bm, 0, g->bm_words * 4, g->stream));
+    g->vis_stale = false;
+    return FGI_OK;
+}
+
 fgi_status fold(fgi_graph* g) {
+    FGI_TRY(flush_vis(g));
     if (!g->v_dirty) return FGI_OK;
     const uint32_t H = g->n_handles;
     hipLaunchKernelGGL(k_fold, dim3(std::min<uint32_t>((H + kBlock - 1) / kBlock, 8192)), dim3(kBlock), 0, g->stream, H,
@@ -1698,26 +1700,17 @@ ExpandArgs expand_args(fgi_graph* g, int buf) {
 
 // the invalidated bitmap -> the invalidated list and V_inv (ctr->inv)
 hipError_t launch_final(fgi_graph* g, uint32_t n_handles) {
-    uint64_t words = ((uint64_t)n_handles + 63) / 64;
-    static int per_cu = 0;
-    if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_final, kBlock, 0) != hipSuccess || per_cu < 1))
-        per_cu = 1;
-    const uint64_t resident = (uint64_t)per_cu * (uint64_t)std::max(g->n_cu, 1);
-    uint32_t G = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(kFinalBlocks, resident),
-                                               std::max<uint64_t>(kStats, (words + 255) / 256));
-    G = std::max<uint32_t>(G, (uint32_t)kStats);
-    uint64_t wpb = (words + G - 1) / G;
+    const uint64_t words = ((uint64_t)n_handles + 63) / 64;
+    uint32_t G = (uint32_t)std::min<uint64_t>(kFinalBlocks, std::max<uint64_t>(kStats, (words + 255) / 256));
+    const uint64_t wpb = (words + G - 1) / G;
     const auto* inv64 = reinterpret_cast<const unsigned long long*>(g->inv_bm);
-    // status words apart from the pull prefixes a collect may still read
+    // per-block counts apart from the pull prefixes a collect may still read
     unsigned long long* st = g->bsum + 6ull * kStatBlocks;
-    g->final_epoch = (g->final_epoch + 1) & 0xFFFFu;
-    if (g->final_epoch == 0) g->final_epoch = 1;
-    uint32_t ep = g->final_epoch;
-    WaveCtr* ctr = g->ctr;
-    const unsigned long long* blk = g->blk_stats;
-    uint32_t* out = g->inv;
-    void* args[] = {&inv64, &words, &wpb, &st, &ep, &ctr, &blk, &out};
-    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_final), dim3(G), dim3(kBlock), args, 0, g->stream);
+    hipLaunchKernelGGL(k_final_count, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb, st, g->ctr,
+                       (const unsigned long long*)g->blk_stats);
+    hipLaunchKernelGGL(k_final_write, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb,
+                       (const unsigned long long*)st, g->ctr, g->inv);
+    return hipGetLastError();
 }
 
 void launch_roots(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev, uint32_t base,
@@ -1772,7 +1765,7 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
     FGI_TRY(fold(g));   // visits of a level-launched wave
     if (!g->coop_clean)
         hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
-                           (uint64_t)g->bm_words);
+                           (uint32_t*)nullptr, (uint64_t)g->bm_words);
     CoopArgs a{};
     a.roots = roots_dev;
     a.imm = imm_dev;
@@ -1863,7 +1856,9 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     if (wp0.direction == 2 && n_roots) FGI_TRY(ensure_in_lists(g));
     bool allow_pull = wp0.direction != 1 && pull_ready(g, wp0);
     static_assert(sizeof(WaveCtr) % 8 == 0, "WaveCtr is cleared as 64-bit words");
-    hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm, (uint64_t)g->bm_words);
+    hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
+                       g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
+    g->vis_stale = false;
     g->coop_clean = false;
 #if FGI_PROBE
     {
@@ -2034,7 +2029,9 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     // one rank: nothing is remote, the collectives are identities (skipped unless FGI_OPT_PART_COLLECTIVES)
     const bool coll = pv.world > 1 || g->opt_part_coll;
     if (coll) FGI_HIP(g, hipMemsetAsync(pv.sent_bm, 0, pv.sent_words * 4, s));
-    hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm, (uint64_t)g->bm_words);
+    hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
+                       g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
+    g->vis_stale = false;
     g->coop_clean = false;
     while (g->ev.size() < 2) {
         hipEvent_t e;
