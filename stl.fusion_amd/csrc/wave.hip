@@ -56,6 +56,7 @@ namespace fgi {
 namespace {
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
+constexpr int kProbeLevelsOff = 1 << 20;   // a level index no probe records (cooperative waves)
 
 #if FGI_PROBE
 constexpr int kProbeLevels = 8, kProbePts = 8, kProbeBlocks = 2048;
@@ -658,7 +659,7 @@ struct ExpandArgs {
 // PART: multi-GPU rank — dependant slots outside [ra.base, ra.base + ra.n_local) are remote: their
 // tag is checked against the version replica and matching targets are forwarded once per wave.
 template <bool PART>
-__device__ __forceinline__ void expand_level(uint64_t F, uint64_t T, uint32_t mult, const ExpandArgs& x,
+__device__ __forceinline__ void expand_level(int L, uint64_t F, uint64_t T, uint32_t mult, const ExpandArgs& x,
                                              const unsigned long long* node, uint32_t* vis, const Out& o, Emit& em,
                                              uint32_t* eb, MsgEmit<PART>& me, uint32_t* s_rel, uint32_t* s_base,
                                              unsigned long long* blk, unsigned long long (*s_st)[kStats],
@@ -694,6 +695,7 @@ __device__ __forceinline__ void expand_level(uint64_t F, uint64_t T, uint32_t mu
             }
         }
         __syncthreads();
+        PROBE(L, 4);
         uint32_t dst[kEPT];
         uint64_t pos[kEPT];
 #pragma unroll
@@ -737,6 +739,10 @@ __device__ __forceinline__ void expand_level(uint64_t F, uint64_t T, uint32_t mu
             for (int j = 0; j < kEPT; ++j)
                 if (dst[j] != 0xFFFFFFFFu && bit_of(vis, dst[j])) dst[j] = 0xFFFFFFFFu;
         }
+#if FGI_PROBE
+        if (dst[0] == 0xFFFFFFFEu) __builtin_trap();   // never: orders the probe after the loads
+#endif
+        PROBE(L, 5);
         uint64_t tag[kEPT];
         unsigned long long w[kEPT];
 #pragma unroll
@@ -761,9 +767,11 @@ __device__ __forceinline__ void expand_level(uint64_t F, uint64_t T, uint32_t mu
         // the chunk's winners (at most cedges) are staged over the chunk map, flushed before the
         // next chunk refills it
         __syncthreads();
+        PROBE(L, 6);
 #pragma unroll
         for (int j = 0; j < kEPT; ++j) emit_push<kChunkEmitCap>(em, eb, (win_mask >> j) & 1u, dst[j], o);
         emit_flush<kChunkEmitCap>(em, eb, 1, o);
+        PROBE(L, 7);
         if constexpr (PART) msg_flush(me, kMsgCap / 2, ra);
     }
     if constexpr (PART) msg_flush(me, 1, ra);
@@ -1184,7 +1192,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_level(int L, WaveParams wp, Expan
     if (blockIdx.x >= active) return;
     emit_init(em);
     PROBE(L, 1);
-    expand_level<PART>(F, T, mult, x, node, vis, o, em, s_x, me, s_rel, s_base, blk, s_st, ra);
+    expand_level<PART>(L, F, T, mult, x, node, vis, o, em, s_x, me, s_rel, s_base, blk, s_st, ra);
     PROBE(L, 2);
     publish_ft(o.ln, done, active);
     PROBE(L, 3);
@@ -1400,7 +1408,7 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
         const Out o{a.row_off, a.row_len,        a.inv_bm, a.fr_off[buf ^ 1], a.fr_len[buf ^ 1],
                     a.escan[buf ^ 1], a.cstart[buf ^ 1], &ctr->lvl[(L + 1) % kRing]};
         emit_init(em);
-        expand_level<false>(F, T, level_mult(T, gridDim.x), x, a.node, a.vis, o, em, s_x, me, s_rel, s_base, a.blk,
+        expand_level<false>(kProbeLevelsOff, F, T, level_mult(T, gridDim.x), x, a.node, a.vis, o, em, s_x, me, s_rel, s_base, a.blk,
                             s_st, RemoteArgs{});
     }
     // final collect (as k_final, with a grid barrier instead of waiting on status words)
@@ -1809,11 +1817,12 @@ void print_probe(fgi_graph* g, int L0, int L1) {
         const bool pull = g->ctr_host->lvl[l % kRing].pull != 0;
         // phase boundaries in order: pull 0 entry, 1 staged, 7 last batch (wave 0), 2 loop done
         // (wave 0), 3 all waves, 4 write-back + stats, 5 sums published, 6 exit; push 0 entry,
-        // 1 set up, 2 expanded, 3 published
+        // 1 set up, 4 chunk map (last chunk), 5 edges + dead filter, 6 tags / words / visits,
+        // 7 winners emitted, 2 expanded, 3 published
         const int pull_pts[] = {0, 1, 7, 2, 3, 4, 5, 6};
-        const int push_pts[] = {0, 1, 2, 3};
+        const int push_pts[] = {0, 1, 4, 5, 6, 7, 2, 3};
         const int* pts = pull ? pull_pts : push_pts;
-        const int np = pull ? 8 : 4;
+        const int np = 8;
         unsigned long long t_lo = ~0ull, t_hi = 0, s_hi = 0;
         std::vector<std::vector<double>> d(np);
         for (int b = 0; b < kProbeBlocks; ++b) {
