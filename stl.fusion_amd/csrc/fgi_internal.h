@@ -184,6 +184,7 @@ struct fgi_graph {
     uint64_t roots_cap = 0;
     uint64_t last_wave_n = 0;
     int last_levels = 4;               // non-empty levels of the last wave (sizes the first level group)
+    bool coop_warm = false;            // a cooperative launch has run (coop_warm)
 
     // Visit bitmap over handles: bit h set = node h was visited by a wave since the
     // last fold. A visit's effect is a pure function of the node word, and every second visit is a
@@ -322,7 +323,8 @@ inline void note_words(fgi_graph* g) {
 // Apply the visit bitmap to the node words and clear it (wave.hip). Every entry point that reads or
 // mutates node words outside a wave calls it first.
 fgi_status fold(fgi_graph* g);
-fgi_status flush_vis(fgi_graph* g);   // fgi_restore's deferred visit-bitmap clear, before any use but a wave's init
+fgi_status flush_vis(fgi_graph* g);
+fgi_status coop_warm(fgi_graph* g);   // first cooperative launch of the graph's process, outside timed spans   // fgi_restore's deferred visit-bitmap clear, before any use but a wave's init
 #if FGI_PROBE
 void print_coop_probe();
 #endif

@@ -873,6 +873,23 @@ __device__ void prune_chunk(const PruneArgs& a, uint32_t c, uint32_t* s_w, uint3
 
 __global__ void k_coop_warm(uint32_t) {}
 
+}  // namespace
+
+// The runtime sets up cooperative launches on their first use in a process, which costs tens of ms:
+// paid once per graph before the first timed cooperative launch (prune, streaming batches), not at
+// fgi_create, so processes that never launch cooperatively never pay it.
+fgi_status coop_warm(fgi_graph* g) {
+    if (g->coop_warm) return FGI_OK;
+    uint32_t zero = 0;
+    void* args[] = {&zero};
+    FGI_HIP(g, hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_coop_warm), dim3(1), dim3(64), args, 0, g->stream));
+    FGI_HIP(g, hipStreamSynchronize(g->stream));
+    g->coop_warm = true;
+    return FGI_OK;
+}
+
+namespace {
+
 __global__ __launch_bounds__(256) void k_prune(PruneArgs a) {
     __shared__ uint32_t s_lh[kBlockLong], s_lc[kBlockLong];
     __shared__ uint32_t s_nl, s_cb, s_w[4], s_pfx;
@@ -1482,17 +1499,6 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
     g->free_detached.reserve(g->n_detached);
     for (uint32_t i = g->n_detached; i > 0; --i) g->free_detached.push_back(g->n_slots + i - 1);
     if (ensure_pool(g, std::max<uint64_t>(cfg->edge_capacity, 1024)) != FGI_OK) return fail(FGI_ENOMEM);
-    // the runtime sets up cooperative launches (and loads a kernel's code object) on first use, which
-    // costs tens of ms: pay it here rather than inside the first prune or streaming batch
-    {
-        int per_cu = 0;
-        (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_prune, 256, 0);
-        uint32_t zero = 0;
-        void* args[] = {&zero};
-        if (hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_coop_warm), dim3(1), dim3(64), args, 0, g->stream) !=
-            hipSuccess)
-            return fail(FGI_EDEVICE);
-    }
     if (hipDeviceSynchronize() != hipSuccess) return fail(FGI_EDEVICE);
     *out = g;
     return FGI_OK;
@@ -2219,8 +2225,9 @@ static fgi_status batch_launch(fgi_graph* g, uint32_t from, uint32_t n_steps, co
 
 fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, uint32_t* out_ids, uint64_t cap,
                          uint64_t* out_n, fgi_batch_stats* stats) {
-    const auto t0 = std::chrono::steady_clock::now();
     if (!g || (n_steps && !steps)) return FGI_EINVAL;
+    FGI_TRY(coop_warm(g));   // once per graph, before the call's timed span
+    const auto t0 = std::chrono::steady_clock::now();
     if (out_n) *out_n = 0;
     uint64_t n_waves = 0, n_begin = 0, n_add = 0;
     for (uint32_t k = 0; k < n_steps; ++k) {   // the single calls' argument checks
@@ -2478,6 +2485,7 @@ static fgi_status prune_range_launch(fgi_graph* g, uint32_t lo, uint32_t hi, Tmp
     static int per_cu = 0;
     if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_prune, 256, 0) != hipSuccess || per_cu < 1))
         per_cu = 1;
+    FGI_TRY(coop_warm(g));
     const uint64_t resident = (uint64_t)per_cu * (uint64_t)std::max(g->n_cu, 1);
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, nblk((uint64_t)(hi - lo) * 64)));
     a.lo = lo;

@@ -1785,6 +1785,7 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
     if ((uint64_t)G > (uint64_t)per_cu * (uint64_t)std::max(g->n_cu, 1))
         return set_err(g, FGI_ENOTSUP, "cooperative wave: %u blocks cannot be resident", G);
     FGI_TRY(fold(g));   // visits of a level-launched wave
+    FGI_TRY(coop_warm(g));
     if (!g->coop_clean)
         hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
                            (uint32_t*)nullptr, (uint64_t)g->bm_words);

@@ -313,3 +313,28 @@ def test_compute_method_lifecycle_random(pkg, gpu_available, path):
     ge = canon_edges(u, d, t)
     ge = ge[ge[:, 0] < n] if len(ge) else ge
     assert np.array_equal(ge, oracle_edges(p.o, n))
+
+
+def test_waves_of_alternating_shapes(pkg, gpu_available):
+    """One graph, restored between waves whose shapes alternate (a 256-root wave that pulls, a
+    one-node wave without levels): each wave matches the oracle bit-exactly, whatever the previous
+    wave's level grouping and pull-list state."""
+    scale, ef, seed = 13, 16, 0x5EED0024
+    n = 1 << scale
+    g = pkg.Graph(n)
+    g.synth_rmat(scale, ef, seed, 0, 0)
+    s, dd = O.gen_rmat(scale, ef, seed)
+    o = _oracle_from_synth(n, seed, s, dd, O.gen_tags(s, dd, seed))
+    deg = np.bincount(s, minlength=n)
+    big = O.gen_roots(256, n, 0x5EED1024, deg)
+    small = np.nonzero(deg == 0)[0][:1].astype(np.uint32)   # a node without dependants
+    g.snapshot()
+    o.snapshot()
+    shapes = []
+    for roots in (big, small, big, small, small, big, big):
+        g.restore()
+        o.restore()
+        ids, ws = _compare_wave(g, o, n, roots)
+        shapes.append(ws.pull_levels)
+    # (the first wave builds the pull-list cache and runs push-only)
+    assert max(shapes) > 0 and shapes[1] == 0, shapes
