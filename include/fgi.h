@@ -280,7 +280,7 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *   FGI_OPT_DEAD_FILTER [1]  skip edges whose dependant was invalidated in an earlier level using
  *                            a per-wave bitmap (E_match then counts examined edges only)
  *   FGI_OPT_DIRECTION   [0]  0 auto (push/pull per level), 1 push only, 2 pull only
- *   FGI_OPT_PULL_ALPHA  [14] auto: pull when frontier edges > total edges / alpha
+ *   FGI_OPT_PULL_ALPHA  [28] auto: pull when frontier edges > total edges / alpha
  *   FGI_OPT_PULL_BETA   [24] auto: after a pull level, pull again while the frontier holds more
  *                            than n_slots / beta nodes (0: the alpha rule only)
  *   FGI_OPT_LEVEL_TIMING [1] with a stats argument, time every level's traversal launch with HIP
