@@ -187,7 +187,9 @@ __device__ __forceinline__ void block_stats_add(unsigned long long* blk, unsigne
     if (threadIdx.x < kStats) {
         unsigned long long t = 0;
         for (uint32_t q = 0; q < blockDim.x / 64; ++q) t += s[q][threadIdx.x];
-        if (t) blk[(uint64_t)threadIdx.x * kStatBlocks + blockIdx.x] += t;
+        // a returnless atomic: nothing in this launch reads the columns, so no round trip is waited for
+        if (t) __hip_atomic_fetch_add(blk + (uint64_t)threadIdx.x * kStatBlocks + blockIdx.x, t, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -1123,7 +1125,8 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
         if (sl < p.n_slots) {
             const unsigned long long wm = s.wm[2 * i] | ((unsigned long long)s.wm[2 * i + 1] << 32);
             vis64[sl >> 6] = wm | s.vm[2 * i] | ((unsigned long long)s.vm[2 * i + 1] << 32);
-            if (wm) inv64[sl >> 6] |= wm;
+            // returnless: the word's earlier bits need not be read back (nothing in this launch reads it)
+            if (wm) __hip_atomic_fetch_or(inv64 + (sl >> 6), wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     bs[0] = ws.w;
