@@ -288,6 +288,8 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *                            wave-boundary events, so measured waves carry no per-level markers
  *   FGI_OPT_DEFRAG_PCT  [60] fgi_prune copies the rows to a fresh pool when holes exceed this % of
  *                            it (0: never)
+ *   FGI_OPT_PULL_TPB    [0]  pull tiles (1,024 slots) per block, 1..32; 0 sizes the grid from the CU
+ *                            count (measurement / tests: results never depend on it)
  *   FGI_OPT_PART_COLLECTIVES [0] a one-rank partition skips its collectives (identities there);
  *                            1 runs them anyway (tests of the RCCL level loop on one GPU) */
 #define FGI_OPT_DEAD_FILTER 1
@@ -297,6 +299,7 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
 #define FGI_OPT_PULL_BETA 5
 #define FGI_OPT_DEFRAG_PCT 6
 #define FGI_OPT_PART_COLLECTIVES 7
+#define FGI_OPT_PULL_TPB 8
 fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value);
 
 /* ---- multi-GPU (1-D vertex-range partition, RCCL all-to-all frontier exchange) --------------- */

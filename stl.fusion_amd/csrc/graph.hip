@@ -1857,6 +1857,11 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
         g->opt_pull_alpha = (int)value;
         return FGI_OK;
     case FGI_OPT_LEVEL_TIMING: g->opt_level_timing = value ? 1 : 0; return FGI_OK;
+    case FGI_OPT_PULL_TPB:
+        if (value < 0 || value > 32) return set_err(g, FGI_EINVAL, "pull tiles per block must be 0..32");
+        g->opt_pull_tpb = (int)value;
+        g->uin_epoch = 0;   // the candidate lists are segmented per pull block: rebuilt for the new grid
+        return FGI_OK;
     case FGI_OPT_PULL_BETA:
         if (value < 0) return set_err(g, FGI_EINVAL, "beta must be >= 0");
         g->opt_pull_beta = (int)value;

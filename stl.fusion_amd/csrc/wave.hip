@@ -232,44 +232,51 @@ __device__ bool last_block(unsigned long long* done, uint64_t G) {
 }
 
 // Called by the last block: exclusive prefixes over blocks of `ncols` (<= 3) columns
-// src[q * G + k] into dst[q * G + k], column totals into tot[q]. Every value is read in ONE round
-// (thread t holds blocks [t * kPer, t * kPer + kPer) of every column: the reads are agent-scope
-// atomics, performed at the coherence point, each a round trip), then one block scan per column.
-constexpr uint32_t kEpiloguePer = 8;    // G <= kBlock * kEpiloguePer (kLevelGridMax)
+// src[q * G + k] into dst[q * G + k], column totals into tot[q]. In rounds of kBlock * kEpiloguePer
+// blocks (one round up to 2,048 blocks): every value of a round is read at once (thread t holds
+// kEpiloguePer consecutive blocks of every column; the reads are agent-scope atomics, performed at
+// the coherence point, each a round trip), then one block scan per column, carried across rounds.
+constexpr uint32_t kEpiloguePer = 8;
 __device__ void prefix_columns(unsigned long long* src, unsigned long long* dst, int ncols, uint64_t G,
                                unsigned long long* tot, unsigned long long* s_red) {
     const uint32_t lane = lane_id(), wid = threadIdx.x >> 6, W = blockDim.x >> 6;
-    const uint64_t k0 = (uint64_t)threadIdx.x * kEpiloguePer;
-    unsigned long long xs[3][kEpiloguePer];
+    const uint64_t R = (uint64_t)blockDim.x * kEpiloguePer;
+    unsigned long long carry[3] = {0, 0, 0};
+    for (uint64_t r0 = 0; r0 < G; r0 += R) {   // block-uniform
+        const uint64_t k0 = r0 + (uint64_t)threadIdx.x * kEpiloguePer;
+        unsigned long long xs[3][kEpiloguePer];
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
+        for (int q = 0; q < 3; ++q)
 #pragma unroll
-        for (uint32_t j = 0; j < kEpiloguePer; ++j)
-            xs[q][j] = (q < ncols && k0 + j < G) ? coh_read(src + q * G + k0 + j) : 0ull;
+            for (uint32_t j = 0; j < kEpiloguePer; ++j)
+                xs[q][j] = (q < ncols && k0 + j < G) ? coh_read(src + q * G + k0 + j) : 0ull;
 #pragma unroll
-    for (int q = 0; q < 3; ++q) {
-        if (q >= ncols) break;
-        unsigned long long loc = 0;
+        for (int q = 0; q < 3; ++q) {
+            if (q >= ncols) break;
+            unsigned long long loc = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < kEpiloguePer; ++j) loc += xs[q][j];
-        unsigned long long t;
-        const unsigned long long x = wave_excl_scan64(loc, t);
-        __syncthreads();
-        if (lane == 0) s_red[wid] = t;
-        __syncthreads();
-        unsigned long long run = x, all = 0;
-        for (uint32_t j = 0; j < W; ++j) {
-            if (j < wid) run += s_red[j];
-            all += s_red[j];
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < kEpiloguePer; ++j)
-            if (k0 + j < G) {
-                dst[q * G + k0 + j] = run;
-                run += xs[q][j];
+            for (uint32_t j = 0; j < kEpiloguePer; ++j) loc += xs[q][j];
+            unsigned long long t;
+            const unsigned long long x = wave_excl_scan64(loc, t);
+            __syncthreads();
+            if (lane == 0) s_red[wid] = t;
+            __syncthreads();
+            unsigned long long run = carry[q] + x, all = 0;
+            for (uint32_t j = 0; j < W; ++j) {
+                if (j < wid) run += s_red[j];
+                all += s_red[j];
             }
-        if (threadIdx.x == 0) tot[q] = all;
+#pragma unroll
+            for (uint32_t j = 0; j < kEpiloguePer; ++j)
+                if (k0 + j < G) {
+                    dst[q * G + k0 + j] = run;
+                    run += xs[q][j];
+                }
+            carry[q] += all;
+        }
     }
+    if (threadIdx.x == 0)
+        for (int q = 0; q < ncols; ++q) tot[q] = carry[q];
 }
 
 // ---- frontier lists -------------------------------------------------------------------------------
@@ -832,7 +839,7 @@ struct PullArgs {
 // totals are per-thread register sums. Candidates whose heads missed but whose list goes on are
 // queued in LDS and scanned at the wave's flush (pull_tails). Candidates neither hit nor queued,
 // and queued ones whose scan found nothing, are this level's survivors.
-constexpr uint32_t kMaxIter = 16;           // tiles per pull block (kMaxIter * kPullTile slots)
+constexpr uint32_t kMaxIter = 32;           // tiles per pull block (kMaxIter * kPullTile slots)
 constexpr uint32_t kTailCap = kChunk;       // queued candidates
 constexpr uint32_t kTileWords = kPullTile / 64;
 constexpr uint32_t kOwnWords = 2 * kMaxIter * kTileWords;   // owned 32-bit bitmap words
@@ -849,6 +856,10 @@ struct PullLds {
     uint32_t sn;                                    // survivors written
     uint32_t wn;                                    // expandable winners listed
 };
+
+// k_level's LDS (32-bit words): push — the chunk map, then the chunk's winners; pull — the tail queue
+// (kTailCap) and PullLds at kChunk + 4
+constexpr uint32_t kLevelLds = std::max<uint32_t>(kChunkEmitCap + 8, kChunk + 4 + (sizeof(PullLds) + 3) / 4);
 
 // a thread's winners: count, those with a non-empty row, their row lengths
 struct WinSum {
@@ -1174,14 +1185,14 @@ __global__ __launch_bounds__(kBlock, 5) void k_level(int L, WaveParams wp, Expan
                                                   const unsigned long long* node, uint32_t* vis, Out o, WaveCtr* ctr,
                                                   unsigned long long* blk, unsigned long long* done, RemoteArgs ra) {
     // push: the chunk map (s_rel, s_base), then the chunk's winners over it; pull: queue + buffers
-    __shared__ __align__(16) uint32_t s_x[kChunkEmitCap + 8];
+    __shared__ __align__(16) uint32_t s_x[kLevelLds];
     uint32_t* s_rel = s_x;                    // [kChunk + 1]
     uint32_t* s_base = s_x + kChunk + 4;      // [kChunk + 2], 16-byte aligned
     __shared__ Emit em;
     __shared__ MsgEmit<PART> me;
     __shared__ unsigned long long s_st[kBlock / 64][kStats];
     __shared__ unsigned long long s_red[kBlock / 64];
-    static_assert(sizeof(PullLds) <= (kChunk + 2) * 4 && kTailCap <= kChunk, "pull LDS");
+    static_assert(sizeof(PullLds) <= (kLevelLds - kChunk - 4) * 4 && kTailCap <= kChunk, "pull LDS");
     PROBE(L, 0);
     LevelCtr& lc = ctr->lvl[L % kRing];
     o.ln = &ctr->lvl[(L + 1) % kRing];
@@ -1625,18 +1636,23 @@ unsigned event_flags() {
     return f;
 }
 
-// the last-block epilogues read every block's sums in one round (kEpiloguePer per thread)
-constexpr uint32_t kLevelGridMax = kBlock * kEpiloguePer;
-static_assert(kLevelGridMax <= kStatBlocks && kFinalBlocks <= kLevelGridMax, "epilogue geometry");
+// the level grid is bounded by the per-block statistics rows (the epilogues take any grid)
+constexpr uint32_t kLevelGridMax = kStatBlocks;
+static_assert(kFinalBlocks <= kLevelGridMax, "epilogue geometry");
 
 }  // namespace
 
 // 5 resident blocks per CU (k_level launch bounds); a pull block owns at most kMaxIter tiles, so a
-// larger graph gets more blocks, up to kLevelGridMax (67M slots per device); beyond that, no pull.
+// larger graph gets more blocks, up to kLevelGridMax (134M slots per device); beyond that, no pull.
+// FGI_OPT_PULL_TPB fixes the tiles per block instead (tests: every grid takes the same results).
 void pull_geometry(const fgi_graph* g, uint32_t* grid, uint32_t* tpb) {
     const uint64_t n_tiles = ((uint64_t)g->n_slots + kPullTile - 1) / kPullTile;
     uint64_t G = std::min<uint64_t>((uint64_t)g->n_cu * 5, kLevelGridMax);
     uint64_t t = (n_tiles + G - 1) / G;
+    if (g->opt_pull_tpb > 0) {
+        t = std::min<uint64_t>((uint64_t)g->opt_pull_tpb, kMaxIter);
+        G = (n_tiles + t - 1) / t;
+    }
     if (t > kMaxIter) {
         t = kMaxIter;
         G = (n_tiles + t - 1) / t;

@@ -21,6 +21,7 @@ LIB_PATH = os.environ.get("FGI_LIBRARY") or os.path.join(_HERE, "lib", "libfgi.s
 OK, EINVAL, ENOMEM, ECAPACITY, EDEVICE, ESTATE, ENOTSUP = range(7)
 OPT_DEAD_FILTER, OPT_DIRECTION, OPT_PULL_ALPHA, OPT_LEVEL_TIMING, OPT_PULL_BETA, OPT_DEFRAG_PCT = 1, 2, 3, 4, 5, 6
 OPT_PART_COLLECTIVES = 7
+OPT_PULL_TPB = 8
 DIR_AUTO, DIR_PUSH, DIR_PULL = 0, 1, 2
 NONE = 0xFFFFFFFF
 COMPUTING, CONSISTENT, INVALIDATED = 0, 1, 2

@@ -128,3 +128,35 @@ def test_configs1_full_scale24_wave_properties(pkg, gpu_available):
     want = closure_bfs(n, u, d, t, ver, roots)
     assert np.array_equal(want, inv), (int(want.sum()), int(inv.sum()))
     assert ws.v_inv == 7_370_581 and ws.e_trav == 261_303_996
+
+
+@pytest.mark.parametrize("direction", [0, 2])
+def test_pull_grid_geometry_invariance(pkg, gpu_available, direction):
+    """Pull levels split the slots into blocks of `tpb` 1,024-slot tiles (FGI_OPT_PULL_TPB; 0 sizes the
+    grid from the CU count). R-MAT scale 22 (4,096 tiles, 50% stale edges) with tpb = 1 runs 4,096 pull
+    blocks — past one round of the last-block prefix epilogue — and tpb = 32 the largest blocks; every
+    geometry must give the same wave as the default: set, V_inv, E_trav and every final node word."""
+    scale, ef = 22, 16
+    n = 1 << scale
+    out = []
+    for tpb in (0, 1, 32):
+        g = pkg.Graph(n)
+        g.set_option(pkg.fgi.OPT_DIRECTION, direction)
+        g.set_option(pkg.fgi.OPT_PULL_TPB, tpb)
+        g.synth_rmat(scale, ef, SEED, 50, STALE_SEED)
+        deg, _ = g.degrees()
+        roots = O.gen_roots(4096, n, ROOT_SEED, deg[:n])
+        g.snapshot()
+        ws = pkg.WaveStats()
+        for _ in range(2):   # the second wave (automatic direction: the first builds the pull lists)
+            g.restore()
+            ws = pkg.WaveStats()
+            ids = g.invalidate(roots, stats=ws)
+        v, f = g.dump_states()
+        out.append((np.sort(ids), ws.v_inv, ws.e_trav, ws.pull_levels, v, f))
+        g.close()
+    for tpb, r in zip((1, 32), out[1:]):
+        assert r[3] > 0, f"tpb {tpb}: no pull level ran"
+        assert np.array_equal(r[0], out[0][0]), f"tpb {tpb}: invalidated sets differ"
+        assert (r[1], r[2]) == (out[0][1], out[0][2]), (tpb, r[1:3], out[0][1:3])
+        assert np.array_equal(r[4], out[0][4]) and np.array_equal(r[5], out[0][5]), f"tpb {tpb}: final states differ"
