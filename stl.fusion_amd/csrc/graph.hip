@@ -979,20 +979,29 @@ __global__ void k_in_count(uint32_t n, const unsigned long long* __restrict__ no
     }
 }
 
-__global__ void k_in_fill(uint32_t n, const unsigned long long* __restrict__ node, const uint64_t* __restrict__ row_off,
-                          const uint32_t* __restrict__ row_len, const uint32_t* __restrict__ pool_col,
-                          const uint64_t* __restrict__ pool_tag, const uint64_t* __restrict__ uin_off,
-                          uint32_t* cursor, uint32_t* uin_src) {
+// One sort pair per pool position: a live entry (d, tag == version(d)) of row u gives
+// key = (d << wbits) | (wmax - weight(u)), value = u; dead entries and row slack get a key past every
+// live one (bit `top`), so an ascending stable sort leaves the lists, each ordered by weight
+// descending, in the first `total` positions.
+__global__ void k_in_pairs(uint32_t n, uint32_t n_slots, const unsigned long long* __restrict__ node,
+                           const uint64_t* __restrict__ row_off, const uint32_t* __restrict__ row_len,
+                           const uint32_t* __restrict__ pool_col, const uint64_t* __restrict__ pool_tag,
+                           const uint32_t* __restrict__ weight, uint32_t wbits, uint32_t wmax, uint32_t top,
+                           uint64_t* keys, uint32_t* vals) {
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint64_t dead = 1ull << top;
     for (uint64_t u = wave; u < n; u += nw) {
         const uint32_t len = row_len[u];
         const uint64_t o = row_off[u];
+        const uint64_t wk = (uint64_t)(wmax - (u < n_slots ? weight[u] : 0u));
         for (uint32_t k = lane; k < len; k += 64) {
             const uint32_t d = pool_col[o + k];
             const uint64_t t = pool_tag[o + k];
-            if (t != 0 && (node[d] & kVMask) == t) uin_src[uin_off[d] + atomicAdd(&cursor[d], 1u)] = (uint32_t)u;
+            const bool live = t != 0 && (node[d] & kVMask) == t;
+            keys[o + k] = live ? (((uint64_t)d << wbits) | wk) : dead;
+            vals[o + k] = (uint32_t)u;
         }
     }
 }
@@ -1202,7 +1211,7 @@ fgi_status ensure_in_lists(fgi_graph* g) {
     FGI_HIP(g, hipMemsetAsync(g->uin_len, 0, (size_t)N * 4, s));
     hipLaunchKernelGGL(k_in_count, dim3(grid), dim3(256), 0, s, H, reinterpret_cast<const unsigned long long*>(g->node),
                        g->row_off, g->row_len, g->pool_col, g->pool_tag, g->uin_len);
-    Tmp ts, tc;
+    Tmp ts;
     size_t tb = 0;
     FGI_HIP(g, rocprim::exclusive_scan(nullptr, tb, g->uin_len, g->uin_off, (uint64_t)0, (size_t)N,
                                        rocprim::plus<uint64_t>(), s));
@@ -1221,16 +1230,48 @@ fgi_status ensure_in_lists(fgi_graph* g) {
         FGI_TRY(dmalloc(g, &g->uin_src, cap));
         g->uin_cap = cap;
     }
-    uint32_t* cursor;
-    FGI_TRY(tmalloc(g, tc, &cursor, N));
-    FGI_HIP(g, hipMemsetAsync(cursor, 0, (size_t)N * 4, s));
-    hipLaunchKernelGGL(k_in_fill, dim3(grid), dim3(256), 0, s, H, reinterpret_cast<const unsigned long long*>(g->node),
-                       g->row_off, g->row_len, g->pool_col, g->pool_tag, g->uin_off, cursor, g->uin_src);
-    FGI_HIP(g, hipGetLastError());
-    // Order every list by the entries' own dependency counts (descending; ties by handle): the
-    // nodes a wave reaches first are the ones with many dependencies, so a pull level finds a
-    // parent in the frontier among the first entries (and in the two heads, most of the time).
-    FGI_TRY(sort_in_lists(g, total, g->uin_len, N));
+    // Fill and order the lists with one stable radix sort of (dependant, weight) pairs over the pool:
+    // every list ordered by its entries' own dependency counts (descending; ties in pool order), so a
+    // pull level finds a parent in the frontier among the first entries (in the two heads, mostly).
+    uint32_t wmax = 0;
+    {
+        Tmp tr, tm;
+        uint32_t* dmax;
+        FGI_TRY(tmalloc(g, tm, &dmax, 1));
+        size_t rb = 0;
+        FGI_HIP(g, rocprim::reduce(nullptr, rb, g->uin_len, dmax, 0u, (size_t)N, rocprim::maximum<uint32_t>(), s));
+        char* rt;
+        FGI_TRY(tmalloc(g, tr, &rt, rb));
+        FGI_HIP(g, rocprim::reduce(rt, rb, g->uin_len, dmax, 0u, (size_t)N, rocprim::maximum<uint32_t>(), s));
+        FGI_TRY(d2h(g, &wmax, dmax, 1));
+    }
+    uint32_t wbits = 1, dbits = 1;
+    while (wbits < 32 && (1ull << wbits) <= wmax) ++wbits;
+    while (dbits < 32 && (1ull << dbits) < N) ++dbits;
+    const uint32_t top = dbits + wbits;   // the dead-entry bit
+    const uint64_t P = g->pool_top;
+    if (total && P) {
+        if (top >= 64) return set_err(g, FGI_EINVAL, "dependency-list sort key needs %u bits", top + 1);
+        Tmp tk0, tk1, tv0, tv1, tt;
+        uint64_t *k0, *k1;
+        uint32_t *v0, *v1;
+        FGI_TRY(tmalloc(g, tk0, &k0, P));
+        FGI_TRY(tmalloc(g, tk1, &k1, P));
+        FGI_TRY(tmalloc(g, tv0, &v0, P));
+        FGI_TRY(tmalloc(g, tv1, &v1, P));
+        FGI_HIP(g, hipMemsetAsync(k0, 0xFF, P * sizeof(uint64_t), s));   // row slack: dead keys
+        hipLaunchKernelGGL(k_in_pairs, dim3(grid), dim3(256), 0, s, H, N,
+                           reinterpret_cast<const unsigned long long*>(g->node), g->row_off, g->row_len, g->pool_col,
+                           g->pool_tag, g->uin_len, wbits, wmax, top, k0, v0);
+        FGI_HIP(g, hipGetLastError());
+        size_t sb = 0;
+        FGI_HIP(g, rocprim::radix_sort_pairs(nullptr, sb, k0, k1, v0, v1, (size_t)P, 0, top + 1, s));
+        char* st;
+        FGI_TRY(tmalloc(g, tt, &st, sb));
+        FGI_HIP(g, rocprim::radix_sort_pairs(st, sb, k0, k1, v0, v1, (size_t)P, 0, top + 1, s));
+        FGI_HIP(g, hipMemcpyAsync(g->uin_src, v1, total * sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+        FGI_HIP(g, hipStreamSynchronize(s));   // the temporaries go back to the cache
+    }
     FGI_TRY(build_in_heads(g));
     FGI_HIP(g, hipStreamSynchronize(s));
     g->uin_epoch = g->mut_epoch;
