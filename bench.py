@@ -310,7 +310,8 @@ def main():
                                    "4,096-root batched invalidation (BASELINE.json configs[1])",
                          "layered_1m": "1.05M-node compute-method graph, fan-out 8, depth 6, 1k roots (configs[0])",
                          "rmat27": "R-MAT scale 27, edge factor 8 (configs[2])",
-                         "rmat24_churn": "configs[1] graph with 50% stale edges (configs[3])"}[args.config],
+                         "rmat24_churn": "configs[1] graph with 50% stale edges (configs[3])"}.get(
+                args.config, f"R-MAT scale {cfg.get('scale')}, edge factor {cfg.get('edge_factor')} (size sweep)"),
             "nodes": n, "edges": int(n_edges), "roots": int(len(roots)),
             "parallelism": (f"vertex-partition x{world} (RCCL all-gather counts + send/recv frontier)"
                             if partitioned else "single"),

@@ -20,6 +20,11 @@ CONFIGS = {
     # configs[2]: R-MAT scale 27, edge factor 8 (~1B edges), vertex-partitioned over 2/4/8 GPUs
     "rmat27": dict(kind="rmat", scale=27, edge_factor=8, seed=0x5EED0027, stale_pct=0, stale_seed=0,
                    roots=4096, roots_seed=0x5EED1027),
+    # graph-size sweep on one device (not BASELINE configs): configs[1]'s generator at scales 25 / 26
+    "rmat25": dict(kind="rmat", scale=25, edge_factor=16, seed=0x5EED0025, stale_pct=0, stale_seed=0,
+                   roots=4096, roots_seed=0x5EED1025),
+    "rmat26": dict(kind="rmat", scale=26, edge_factor=16, seed=0x5EED0026, stale_pct=0, stale_seed=0,
+                   roots=4096, roots_seed=0x5EED1026),
     # configs[3]: config 2's graph with 50% stale (version-mismatched) edges
     "rmat24_churn": dict(kind="rmat", scale=24, edge_factor=16, seed=0x5EED0024, stale_pct=50,
                          stale_seed=0x5EED00C0, roots=4096, roots_seed=0x5EED1024),
