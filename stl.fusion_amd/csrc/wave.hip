@@ -1010,12 +1010,27 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
         c[j] = load_cand(src + seg + i, i < cnt, (uint32_t)s_lo);
     }
     {
+        // every word's loads are issued before the first LDS store (one memory round trip, not one
+        // per grid-stride step)
         const uint64_t w_lo = s_lo >> 5, w_end = ((uint64_t)p.n_slots + 31) >> 5;
-        for (uint32_t i = threadIdx.x; i < 2 * wp.tpb * kTileWords; i += blockDim.x) {
-            const bool in = w_lo + i < w_end;
-            s.vm[i] = in ? vis[w_lo + i] : ~0u;
-            s.cs[i] = in ? p.cls[w_lo + i] : 0u;
-            s.wm[i] = 0;
+        const uint32_t nw = 2 * wp.tpb * kTileWords;
+        constexpr uint32_t kPer = kOwnWords / kBlock;
+        uint32_t vv[kPer], cc[kPer];
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) {
+            const uint32_t i = threadIdx.x + k * kBlock;
+            const bool in = i < nw && w_lo + i < w_end;
+            vv[k] = in ? vis[w_lo + i] : ~0u;
+            cc[k] = in ? p.cls[w_lo + i] : 0u;
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < kPer; ++k) {
+            const uint32_t i = threadIdx.x + k * kBlock;
+            if (i < nw) {
+                s.vm[i] = vv[k];
+                s.cs[i] = cc[k];
+                s.wm[i] = 0;
+            }
         }
     }
     if (threadIdx.x == 0) {
