@@ -351,7 +351,7 @@ struct PartView {
     uint64_t sent_words;
     uint32_t* send_buf;         // [world][block] outgoing target ids per owner
     uint32_t* recv_buf;         // [world * block] incoming, concatenated
-    unsigned long long* send_cnt;   // [world] device counters
+    unsigned long long* send_cnt;   // [world + 2] device counters (targets per owner, then next F, T)
     uint32_t* front_global;     // [n_global bits] all-gathered invalidated bitmap (pull levels)
     uint64_t front_words_global;
     unsigned long long* scratch_u64;
@@ -359,7 +359,7 @@ struct PartView {
 bool part_view(fgi_graph* g, PartView* v);
 // Exchange this level's messages: counts by all-gather, payload by grouped send/recv over RCCL.
 // Returns the number of target ids received (concatenated at recv_buf) and sent.
-fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent);
+fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent, uint64_t* glob);
 // Sum of count (1..4) device u64 over all ranks, returned on the host.
 fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out,
                               uint32_t count = 1);

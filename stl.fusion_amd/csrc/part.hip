@@ -43,8 +43,11 @@ struct PartComm {
     // sum of `count` device u64 over all ranks, returned on the host (synchronises the stream)
     virtual fgi_status allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out, uint32_t count) = 0;
     // this level's forwarded targets: send_buf[q] (send_cnt[q] entries) to owner q; the targets
-    // received from every other rank are concatenated at recv_buf
-    virtual fgi_status exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent) = 0;
+    // received from every other rank are concatenated at recv_buf. send_cnt[world, world + 1] carry
+    // the rank's local {F, T} of the next level, summed with the targets sent by all ranks into
+    // glob = {sum F, sum T, sum sent} on the way (the count all-gather doubles as the level's
+    // all-reduce, so a push level synchronises the host once)
+    virtual fgi_status exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent, uint64_t* glob) = 0;
     // every rank's local invalidated-bitmap words inv_bm[0, block/32) into front_global
     virtual fgi_status allgather_front(fgi_graph* g) = 0;
 };
@@ -53,13 +56,26 @@ struct PartState {
     PartView v{};
     ncclComm_t comm = nullptr;
     std::unique_ptr<PartComm> ops;
-    unsigned long long* all_cnt = nullptr;     // [world * world] device
+    unsigned long long* all_cnt = nullptr;     // [world * (world + 2)] device
     unsigned long long* all_cnt_host = nullptr;
     unsigned long long* scalar = nullptr;      // device scratch for all-reduce
     unsigned long long* scalar_host = nullptr;
 };
 
 static PartState* ps(fgi_graph* g) { return reinterpret_cast<PartState*>(g->part); }
+
+// c: [W][W + 2] all-gathered counts (targets sent by q to r, then q's next-level F, T)
+template <typename C>
+static void sum_counts(const C* c, uint32_t W, uint64_t* glob) {
+    const uint32_t S = W + 2;
+    glob[0] = glob[1] = glob[2] = 0;
+    for (uint32_t q = 0; q < W; ++q) {
+        glob[0] += c[(size_t)q * S + W];
+        glob[1] += c[(size_t)q * S + W + 1];
+        for (uint32_t r = 0; r < W; ++r)
+            if (r != q) glob[2] += c[(size_t)q * S + r];
+    }
+}
 
 fgi_status part_destroy(fgi_graph* g) {
     PartState* p = ps(g);
@@ -114,19 +130,20 @@ struct RcclComm final : PartComm {
         for (uint32_t i = 0; i < count; ++i) out[i] = p->scalar_host[i];
         return FGI_OK;
     }
-    fgi_status exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent) override {
+    fgi_status exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent, uint64_t* glob) override {
         PartState* p = ps(g);
-        const uint32_t W = p->v.world, R = p->v.rank;
+        const uint32_t W = p->v.world, R = p->v.rank, S = W + 2;
         hipStream_t s = g->stream;
-        FGI_NCCL(g, ncclAllGather(p->v.send_cnt, p->all_cnt, W, ncclUint64, p->comm, s));
-        FGI_HIP(g, hipMemcpyAsync(p->all_cnt_host, p->all_cnt, (size_t)W * W * 8, hipMemcpyDeviceToHost, s));
+        FGI_NCCL(g, ncclAllGather(p->v.send_cnt, p->all_cnt, S, ncclUint64, p->comm, s));
+        FGI_HIP(g, hipMemcpyAsync(p->all_cnt_host, p->all_cnt, (size_t)W * S * 8, hipMemcpyDeviceToHost, s));
         FGI_HIP(g, hipStreamSynchronize(s));
-        const unsigned long long* c = p->all_cnt_host;   // c[q * W + r]: sent by q to r
+        const unsigned long long* c = p->all_cnt_host;   // c[q * S + r]: sent by q to r; c[q * S + W + i]: q's F, T
+        sum_counts(c, W, glob);
         uint64_t recv = 0, sent = 0;
         FGI_NCCL(g, ncclGroupStart());
         for (uint32_t q = 0; q < W; ++q) {
             if (q == R) continue;
-            const uint64_t to_q = c[R * W + q], from_q = c[q * W + R];
+            const uint64_t to_q = c[R * S + q], from_q = c[q * S + R];
             if (to_q)
                 FGI_NCCL(g, ncclSend(p->v.send_buf + (uint64_t)q * p->v.block, to_q, ncclUint32, (int)q, p->comm, s));
             if (from_q) FGI_NCCL(g, ncclRecv(p->v.recv_buf + recv, from_q, ncclUint32, (int)q, p->comm, s));
@@ -156,11 +173,11 @@ struct LocalGroup {
     uint64_t gen = 0;
     bool failed = false;
     std::vector<uint64_t> vals;   // [P][4] all-reduce contributions
-    std::vector<uint64_t> cnt;    // [P][P] targets rank r forwards to owner q
+    std::vector<uint64_t> cnt;    // [P][P + 2] targets rank r forwards to owner q, then r's F, T
 
     explicit LocalGroup(std::vector<fgi_graph*> g) : gs(std::move(g)) {
         vals.assign(gs.size() * 4, 0);
-        cnt.assign(gs.size() * gs.size(), 0);
+        cnt.assign(gs.size() * (gs.size() + 2), 0);
     }
     bool arrive() {
         std::unique_lock<std::mutex> lk(mu);
@@ -211,30 +228,32 @@ struct LocalComm final : PartComm {
         if (!grp->arrive()) return peer_failed(g);   // nobody overwrites vals before all have read them
         return FGI_OK;
     }
-    fgi_status exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent) override {
+    fgi_status exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent, uint64_t* glob) override {
         PartState* p = ps(g);
-        const uint32_t W = p->v.world, R = rank;
-        FGI_HIP(g, hipMemcpyAsync(p->all_cnt_host, p->v.send_cnt, (size_t)W * 8, hipMemcpyDeviceToHost, g->stream));
+        const uint32_t W = p->v.world, R = rank, S = W + 2;
+        FGI_HIP(g, hipMemcpyAsync(p->all_cnt_host, p->v.send_cnt, (size_t)S * 8, hipMemcpyDeviceToHost, g->stream));
         FGI_HIP(g, hipStreamSynchronize(g->stream));   // also: this rank's send buffers are complete
         {
             std::lock_guard<std::mutex> lk(grp->mu);
-            for (uint32_t q = 0; q < W; ++q) grp->cnt[(size_t)R * W + q] = p->all_cnt_host[q];
+            for (uint32_t q = 0; q < S; ++q) grp->cnt[(size_t)R * S + q] = p->all_cnt_host[q];
         }
         if (!grp->arrive()) return peer_failed(g);
+        sum_counts(grp->cnt.data(), W, glob);
         uint64_t recv = 0, sent = 0;
         for (uint32_t q = 0; q < W; ++q) {
             if (q == R) continue;
-            const uint64_t from_q = grp->cnt[(size_t)q * W + R];
+            const uint64_t from_q = grp->cnt[(size_t)q * S + R];
             if (from_q) {
                 PartState* pq = ps(grp->gs[q]);
                 FGI_HIP(g, hipMemcpyAsync(p->v.recv_buf + recv, pq->v.send_buf + (uint64_t)R * pq->v.block, from_q * 4,
                                           hipMemcpyDefault, g->stream));
             }
             recv += from_q;
-            sent += grp->cnt[(size_t)R * W + q];
+            sent += grp->cnt[(size_t)R * S + q];
         }
-        // the senders refill their buffers only after the level's closing all-reduce, which every
-        // rank enters after synchronising its stream (these copies included)
+        // the senders refill their buffers (and counts) only after every rank's copies are done
+        FGI_HIP(g, hipStreamSynchronize(g->stream));
+        if (!grp->arrive()) return peer_failed(g);
         *n_recv = recv;
         *n_sent = sent;
         return FGI_OK;
@@ -253,8 +272,8 @@ struct LocalComm final : PartComm {
     }
 };
 
-fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent) {
-    return ps(g)->ops->exchange(g, n_recv, n_sent);
+fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent, uint64_t* glob) {
+    return ps(g)->ops->exchange(g, n_recv, n_sent, glob);
 }
 
 fgi_status part_allgather_front(fgi_graph* g) { return ps(g)->ops->allgather_front(g); }
@@ -504,14 +523,15 @@ static fgi_status part_alloc(fgi_graph* g, uint32_t n_global) {
     if (hipMalloc(&p->v.sent_bm, p->v.sent_words * 4) != hipSuccess) return fail("sent bitmap");
     if (hipMalloc(&p->v.send_buf, (size_t)W * block * 4) != hipSuccess) return fail("send buffer");
     if (hipMalloc(&p->v.recv_buf, (size_t)W * block * 4) != hipSuccess) return fail("recv buffer");
-    if (hipMalloc(&p->v.send_cnt, (size_t)W * 8) != hipSuccess) return fail("counts");
-    if (hipMalloc(&p->all_cnt, (size_t)W * W * 8) != hipSuccess) return fail("counts");
+    if (hipMalloc(&p->v.send_cnt, (size_t)(W + 2) * 8) != hipSuccess) return fail("counts");
+    if (hipMalloc(&p->all_cnt, (size_t)W * (W + 2) * 8) != hipSuccess) return fail("counts");
     if (hipMalloc(&p->scalar, 32) != hipSuccess) return fail("scalar");
     p->v.front_words_global = (uint64_t)n_global / 32 + 2;
     if (hipMalloc(&p->v.front_global, p->v.front_words_global * 4) != hipSuccess) return fail("frontier bitmap");
     if (hipMemset(p->v.front_global, 0, p->v.front_words_global * 4) != hipSuccess) return fail("frontier bitmap");
     if (hipMalloc(&p->v.scratch_u64, 32) != hipSuccess) return fail("scratch");
-    if (hipHostMalloc(reinterpret_cast<void**>(&p->all_cnt_host), (size_t)W * W * 8) != hipSuccess) return fail("host");
+    if (hipHostMalloc(reinterpret_cast<void**>(&p->all_cnt_host), (size_t)W * (W + 2) * 8) != hipSuccess)
+        return fail("host");
     if (hipHostMalloc(reinterpret_cast<void**>(&p->scalar_host), 32) != hipSuccess) return fail("host");
     return FGI_OK;
 }

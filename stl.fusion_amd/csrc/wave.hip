@@ -2072,10 +2072,14 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
 // ---- multi-GPU wave -------------------------------------------------------------------------------
 // The partitioned wave, one call per rank: levels in lockstep, collectives through the rank's
 // PartComm (RCCL over xGMI with one process per GPU, or device copies between the graphs of an
-// in-process group, one host thread per rank — the same level sequence either way). Per level one
-// all-reduce of {frontier, frontier edges} decides push vs pull (Beamer's alpha / beta rules, as
-// run_wave) and termination; a pull level first all-gathers the invalidated bitmap; a push level
-// adds the exchange (counts all-gather, then payloads) and applies the received targets.
+// in-process group, one host thread per rank — the same level sequence either way). A pull level
+// all-gathers the invalidated bitmap, pulls, and all-reduces {frontier, frontier edges} of the next
+// level, which decide push vs pull (Beamer's alpha / beta rules, as run_wave) and termination. A
+// push level synchronises the host once: its counts all-gather (payload sizes, then the payloads;
+// the received targets are applied) also carries every rank's local next {F, T}. The targets
+// forwarded bound the winners they add, so F + sent >= the next frontier (0: the wave is done) and T
+// scales by the local edges per winner — direction is a cost choice, the result does not depend on
+// it. A level whose winners are all remote falls back to the all-reduce (termination is exact).
 fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                          fgi_wave_stats* stats) {
     PartView pv;
@@ -2119,6 +2123,7 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     // the invalidated bitmap over all slots: all-gathered before pull levels (one rank: its own)
     const uint32_t* front = coll ? pv.front_global : g->inv_bm;
     uint64_t f_global = sums[1], t_global = sums[2];
+    const double avg_deg = (double)sums[0] / std::max<uint64_t>(1, pv.n_global);
     uint64_t levels = 0, e_trav = 0, f_total = 0, sent_total = 0, push_edges = 0, push_f = 0;
     uint64_t pull_levels = 0, pull_launches = 0, expand_launches = 0;
     double expand_ms = 0, pull_ms = 0;
@@ -2145,20 +2150,36 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
                            g->ctr, g->blk_stats, g->done, ra);
         if (g->opt_level_timing) FGI_HIP(g, hipEventRecord(g->ev[1], s));
         FGI_HIP(g, hipGetLastError());
-        uint64_t n_recv = 0, n_sent = 0;
-        if (!pull && coll) FGI_TRY(part_exchange(g, &n_recv, &n_sent));
+        uint64_t n_recv = 0, n_sent = 0, glob[3] = {0, 0, 0};
+        const bool exch = !pull && coll;
+        if (exch) {
+            FGI_HIP(g, hipMemcpyAsync(pv.send_cnt + pv.world, &g->ctr->lvl[(L + 1) % kRing].F, 16,
+                                      hipMemcpyDeviceToDevice, s));
+            // the level's counters ride on the exchange's stream synchronisation
+            FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
+            FGI_TRY(part_exchange(g, &n_recv, &n_sent, glob));
+        }
         if (n_recv)
             hipLaunchKernelGGL(k_apply_recv, dim3(std::min<uint64_t>((n_recv + kBlock - 1) / kBlock, (uint64_t)g->n_cu * 8)),
                                dim3(kBlock), 0, s, L, n_recv, pv.recv_buf, pv.base, node, g->vis_bm,
                                out_for(g, buf ^ 1, nullptr), g->ctr, g->blk_stats, g->done);
         FGI_HIP(g, hipGetLastError());
         sent_total += n_sent;
-        // the counter copy rides on the all-reduce's stream synchronisation
-        FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
-        uint64_t ft[2] = {0, 0};
-        FGI_TRY(part_allreduce_sum(g, &g->ctr->lvl[(L + 1) % kRing].F, ft, 2));
-        f_global = ft[0];
-        t_global = ft[1];
+        // every winner remote (the wave's tail): whether the received targets add any is known only
+        // after they are applied, so the exact all-reduce decides termination (no empty level)
+        if (exch && (glob[0] != 0 || glob[2] == 0)) {
+            f_global = glob[0] + glob[2];
+            t_global = glob[0] ? (uint64_t)((double)glob[1] * (double)f_global / (double)glob[0])
+                               : (uint64_t)((double)glob[2] * avg_deg);
+            if (glob[2] && !t_global) t_global = 1;
+        } else {
+            // the counter copy rides on the all-reduce's stream synchronisation
+            FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
+            uint64_t ft[2] = {0, 0};
+            FGI_TRY(part_allreduce_sum(g, &g->ctr->lvl[(L + 1) % kRing].F, ft, 2));
+            f_global = ft[0];
+            t_global = ft[1];
+        }
         const LevelCtr& lc = g->ctr_host->lvl[L % kRing];
         ++levels;
         e_trav += lc.T;
