@@ -10,8 +10,11 @@ engine runs over RCCL. Same decomposition as part.hip:
   (ncclAllGather + ncclSend/Recv on the GPU; all_gather here), owners apply them;
 - pull level: the frontier bitmap is all-gathered and every rank pulls its own unvisited slots
   over their dependency lists (global parent ids), stopping at the first parent in the frontier;
-- per level one all_reduce(sum) of {frontier size, frontier edges}: termination and the push/pull
-  choice (Beamer's alpha and beta rules, as the engine's run_part_wave).
+- {frontier size, frontier edges} of the next level decide termination and the push/pull choice
+  (Beamer's alpha and beta rules, as the engine's run_part_wave): after a pull level by one
+  all_reduce(sum); after a push level from the counts all-gather, which also carries every rank's
+  local next {F, T} — F + forwarded targets bounds the next frontier, T scales by local edges per
+  winner — except when every winner is remote, where the all_reduce decides (exact termination).
 
 Visits follow SURVEY.md §8(a) R0 (Computed.cs:162-230): Invalidated -> no-op; Computing -> flag
 InvalidateOnSetOutput; Consistent without delay -> Invalidated + expand; Consistent with delay ->
@@ -93,13 +96,16 @@ class RankModel:
         dist.all_reduce(e_total)
         levels = 0
         last_pull = False
+        known = None   # {frontier, its edges} from the last push level's counts all-gather
         while True:
-            # one all-reduce per level of {frontier, its edges} (run_part_wave): termination and
-            # Beamer's rules — pull when the edges exceed E / alpha, keep pulling after a pull while
-            # the frontier holds more than N / beta nodes
-            ft = torch.tensor([len(front), sum(len(self.rows.get(u, ())) for u in front)], dtype=torch.int64)
-            dist.all_reduce(ft)
-            n_front, edges = int(ft[0]), int(ft[1])
+            # termination and Beamer's rules — pull when the edges exceed E / alpha, keep pulling
+            # after a pull while the frontier holds more than N / beta nodes
+            if known is None:
+                ft = torch.tensor([len(front), sum(len(self.rows.get(u, ())) for u in front)], dtype=torch.int64)
+                dist.all_reduce(ft)
+                n_front, edges = int(ft[0]), int(ft[1])
+            else:
+                (n_front, edges), known = known, None
             if n_front == 0:
                 break
             pull = direction == "pull" or (direction == "auto" and (edges > int(e_total) // alpha or
@@ -134,11 +140,19 @@ class RankModel:
                         elif not self.sent[d]:
                             self.sent[d] = True
                             out[q].append(d)
-                # counts then payload (ncclAllGather of counts + ncclSend/ncclRecv on the GPU)
-                cnt = torch.tensor([len(o) for o in out], dtype=torch.int64)
-                all_cnt = [torch.zeros(self.world, dtype=torch.int64) for _ in range(self.world)]
+                # counts (+ local next F, T) then payload (ncclAllGather + ncclSend/ncclRecv on the GPU)
+                f_loc, t_loc = len(nxt), sum(len(self.rows.get(u, ())) for u in nxt)
+                cnt = torch.tensor([len(o) for o in out] + [f_loc, t_loc], dtype=torch.int64)
+                all_cnt = [torch.zeros(self.world + 2, dtype=torch.int64) for _ in range(self.world)]
                 dist.all_gather(all_cnt, cnt)
-                width = max(1, int(max(int(c.max()) for c in all_cnt)))
+                f_sum = sum(int(c[self.world]) for c in all_cnt)
+                t_sum = sum(int(c[self.world + 1]) for c in all_cnt)
+                sent = sum(int(c[:self.world].sum()) for c in all_cnt)
+                if f_sum or not sent:
+                    n_est = f_sum + sent
+                    t_est = int(t_sum * n_est / f_sum) if f_sum else int(sent * int(e_total) / self.n)
+                    known = (n_est, max(t_est, 1) if sent else t_est)
+                width = max(1, int(max(int(c[:self.world].max()) for c in all_cnt)))
                 pay = torch.full((self.world, width), -1, dtype=torch.int64)
                 for q, o in enumerate(out):
                     if o:
