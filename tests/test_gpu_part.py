@@ -132,6 +132,9 @@ def test_partitioned_8_ranks_at_scale_matches_single_engine(pkg, gpu_available, 
     assert np.array_equal(ids, ids1), (len(ids), len(ids1))
     assert sum(x.v_inv for x in stats) == ws.v_inv and sum(x.e_trav for x in stats) == ws.e_trav
     assert sum(x.pull_levels for x in stats) > 0 and sum(x.remote_msgs for x in stats) > 0
+    # push levels decide from the counts all-gather's bound, pull levels and an all-remote tail from
+    # the all-reduce: the loop runs exactly the cascade's depth (no empty level)
+    assert all(x.levels == ws.levels for x in stats), ([x.levels for x in stats], ws.levels)
     for r, g in enumerate(gs):
         v, f = g.dump_states()
         lo, hi = r * block, min(n, (r + 1) * block)
