@@ -162,7 +162,12 @@ fgi_status fgi_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, con
                              fgi_wave_stats* stats /*nullable*/);
 /* dependant.AddUsed(used) for each pair (IComputedImpl.AddUsed/AddUsedBy, Computed.cs:347-385,
  * reached from ComputedExt.UseNew / TryUseExisting, Internal/ComputedExt.cs:13-22, 70-76).
- * out_result[i] gets an FGI_USED_* code. Pairs in one call are applied as one batch. */
+ * out_result[i] gets an FGI_USED_* code. Pairs in one call are applied as one batch.
+ * Deviation from SURVEY.md §8(b)'s sketch `(src_slot, dst_slot, dst_version)`: the pairs are node
+ * handles, as the reference's AddUsed takes node objects (Computed.cs:347, `AddUsed(IComputedImpl
+ * used)`), not (input, version) keys. The dependant's version is its node's own (a handle names one
+ * node: a slot's current node, or a detached one), so an entry can never carry a version the
+ * dependant node does not have, and a detached (displaced, still Computing) dependant is addressable. */
 fgi_status fgi_add_used(fgi_graph* g, uint32_t n, const uint32_t* dependant, const uint32_t* used,
                         uint32_t* out_result /*nullable*/);
 /* Computed<T>.TrySetOutput (Computed.cs:141-160) for each handle: Computing -> Consistent;
@@ -186,6 +191,17 @@ fgi_status fgi_invalidate(fgi_graph* g, uint32_t n_roots, const uint32_t* roots,
 fgi_status fgi_invalidate_dev(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev,
                               const uint8_t* immediately_dev, uint32_t* out_ids_dev, uint64_t* out_n,
                               fgi_wave_stats* stats);
+/* The same wave as fgi_invalidate, with the invalidated set returned as a bitmap over handles: bit h of
+ * out_bits[h / 64] set = handle h was invalidated by this wave; `words` >= (n_slots + n_detached + 63)
+ * / 64 (else FGI_ECAPACITY). *out_n = V_inv. A 16.8M-slot graph's bitmap is 2 MB against 29.5 MB of
+ * ids for configs[1]'s 7.4M-node wave: the host decodes it where it consumes the set. The id list
+ * stays available through fgi_last_wave_ids / fgi_wave_ids_dev (made on demand). out_bits may be NULL. */
+fgi_status fgi_invalidate_bits(fgi_graph* g, uint32_t n_roots, const uint32_t* roots, const uint8_t* immediately,
+                               uint64_t* out_bits, uint64_t words, uint64_t* out_n, fgi_wave_stats* stats);
+/* Page-locked host memory for the calls' host arrays (roots in, ids / bitmaps out): copies from and
+ * to it run at full PCIe rate without a staging copy (SURVEY.md §8(b) "Ownership"). */
+fgi_status fgi_alloc_pinned(uint64_t bytes, void** out);
+fgi_status fgi_free_pinned(void* p);
 /* Device pointer to the last wave's invalidated-slot list (valid until the next call). */
 fgi_status fgi_wave_ids_dev(fgi_graph* g, const uint32_t** ids_dev, uint64_t* n);
 /* Host copy of the last wave's invalidated handles — e.g. the displacement cascade of

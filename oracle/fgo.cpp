@@ -666,6 +666,23 @@ uint64_t fgo_used_by(const fgo* o, uint32_t h, uint32_t* dst, uint64_t* tag, uin
     return i;
 }
 
+uint64_t fgo_export_used_by(const fgo* o, uint32_t* slot, uint32_t* dst, uint64_t* tag, uint64_t cap) {
+    uint64_t i = 0;
+    for (uint32_t s = 0; s < o->n_slots; ++s) {
+        const Node* n = o->last[s];
+        if (!n) continue;
+        n->used_by.apply([&](const UsedByEntry& e) {
+            if (i < cap) {
+                if (slot) slot[i] = s;
+                if (dst) dst[i] = e.slot;
+                if (tag) tag[i] = e.version;
+            }
+            ++i;
+        });
+    }
+    return i;
+}
+
 uint32_t fgo_used_count(const fgo* o, uint32_t h) {
     if (h >= o->nodes.size()) return 0;
     return (uint32_t)o->nodes[h].used.size();

@@ -117,6 +117,9 @@ void fgo_clear_log(fgo* o);
 uint64_t fgo_used_by(const fgo* o, uint32_t h, uint32_t* dst, uint64_t* tag, uint64_t cap);
 uint32_t fgo_used_count(const fgo* o, uint32_t h);
 uint64_t fgo_total_used_by(const fgo* o);   /* sum of |_usedBy| over all live nodes */
+/* Every slot's most recent node's `_usedBy` entries as (slot, dependant slot, tag) triples, slots
+ * ascending (test bulk export; *_used_by per node for the same thing one node at a time). */
+uint64_t fgo_export_used_by(const fgo* o, uint32_t* slot, uint32_t* dst, uint64_t* tag, uint64_t cap);
 
 /* Snapshot / restore of the whole object graph (bench: reset from a pristine copy). */
 int fgo_snapshot(fgo* o);

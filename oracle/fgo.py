@@ -51,6 +51,7 @@ _SIG = {
     "fgo_inv_log": ([_O, _u32p, C.c_uint64], C.c_uint64),
     "fgo_clear_log": ([_O], None),
     "fgo_used_by": ([_O, C.c_uint32, _u32p, _u64p, C.c_uint64], C.c_uint64),
+    "fgo_export_used_by": ([C.c_void_p, _u32p, _u32p, _u64p, C.c_uint64], C.c_uint64),
     "fgo_used_count": ([_O, C.c_uint32], C.c_uint32),
     "fgo_total_used_by": ([_O], C.c_uint64),
     "fgo_snapshot": ([_O], C.c_int),
@@ -238,6 +239,13 @@ class Oracle:
         d, t = np.zeros(n, np.uint32), np.zeros(n, np.uint64)
         self.l.fgo_used_by(self.o, h, _p(d, C.c_uint32), _p(t, C.c_uint64), n)
         return d, t
+
+    def export_used_by(self):
+        """(slot, dependant slot, tag) of every slot's most recent node's `_usedBy` entries."""
+        n = self.l.fgo_export_used_by(self.o, None, None, None, 0)
+        s, d, t = np.zeros(n, np.uint32), np.zeros(n, np.uint32), np.zeros(n, np.uint64)
+        self.l.fgo_export_used_by(self.o, _p(s, C.c_uint32), _p(d, C.c_uint32), _p(t, C.c_uint64), n)
+        return s, d, t
 
     def used_count(self, h):
         return self.l.fgo_used_count(self.o, h)

@@ -183,6 +183,8 @@ struct fgi_graph {
     uint8_t* imm_buf = nullptr;
     uint64_t roots_cap = 0;
     uint64_t last_wave_n = 0;
+    bool want_ids = true;              // run_wave writes the invalidated list (false: bitmap and count only)
+    bool ids_valid = false;            // inv holds the last wave's list (else ensure_ids rebuilds it)
     int last_levels = 4;               // non-empty levels of the last wave (sizes the first level group)
     bool coop_warm = false;            // a cooperative launch has run (coop_warm)
 
@@ -295,6 +297,9 @@ fgi_status ensure_cstart(fgi_graph* g, uint64_t total_edges);
 // Run one cascade wave from `n_roots` device-resident roots. Fills stats (nullable).
 fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                     fgi_wave_stats* stats);
+// The last single-device wave's invalidated list in g->inv (rebuilt from the invalidated bitmap if
+// the wave ran in bitmap mode).
+fgi_status ensure_ids(fgi_graph* g);
 // Build rows from device edge keys (src << 32 | dst) + optional tags; pool must be empty.
 // Consumes `keys`/`tags` buffers (they may be overwritten). If tags == nullptr the tag of each
 // edge is synth_version(ver_seed, dst) (+1 if stale by hash).

@@ -1901,7 +1901,15 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
     case FGI_OPT_PULL_TPB:
         if (value < 0 || value > 32) return set_err(g, FGI_EINVAL, "pull tiles per block must be 0..32");
         g->opt_pull_tpb = (int)value;
-        g->uin_epoch = 0;   // the candidate lists are segmented per pull block: rebuilt for the new grid
+        // the candidate lists are segmented per pull block: rebuilt for the new grid. A partition's
+        // dependency lists come from its load (part_build_in_lists), which a wave never redoes, so its
+        // candidates are re-segmented here over the lists it has.
+        if (!g->part) {
+            g->uin_epoch = 0;
+        } else if (g->uin_src && g->uin_epoch == g->mut_epoch) {
+            hipSetDevice(g->device);
+            return build_candidates(g);
+        }
         return FGI_OK;
     case FGI_OPT_PULL_BETA:
         if (value < 0) return set_err(g, FGI_EINVAL, "beta must be >= 0");
@@ -1933,6 +1941,7 @@ static fgi_status copy_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64
     if (out_n) *out_n = n;
     if (!out_ids) return FGI_OK;
     if (n > cap) return FGI_ECAPACITY;
+    FGI_TRY(ensure_ids(g));
     return d2h(g, out_ids, g->inv, n);
 }
 
@@ -1956,14 +1965,51 @@ fgi_status fgi_invalidate_dev(fgi_graph* g, uint32_t n_roots, const uint32_t* ro
     FGI_TRY(run_wave(g, n_roots, roots_dev, imm_dev, stats));
     if (out_n) *out_n = g->last_wave_n;
     if (out_ids_dev && g->last_wave_n) {
+        FGI_TRY(ensure_ids(g));
         FGI_HIP(g, hipMemcpyAsync(out_ids_dev, g->inv, g->last_wave_n * 4, hipMemcpyDeviceToDevice, g->stream));
         FGI_HIP(g, hipStreamSynchronize(g->stream));
     }
     return FGI_OK;
 }
 
+fgi_status fgi_invalidate_bits(fgi_graph* g, uint32_t n_roots, const uint32_t* roots, const uint8_t* immediately,
+                               uint64_t* out_bits, uint64_t words, uint64_t* out_n, fgi_wave_stats* stats) {
+    if (!g || (n_roots && !roots)) return FGI_EINVAL;
+    FGI_TRY(single_only(g, "fgi_invalidate_bits"));
+    hipSetDevice(g->device);
+    const uint64_t need = ((uint64_t)g->n_handles + 63) / 64;
+    if (out_bits && words < need)
+        return set_err(g, FGI_ECAPACITY, "bitmap of %llu words needs %llu", (unsigned long long)words,
+                       (unsigned long long)need);
+    FGI_TRY(stage_roots(g, n_roots));
+    FGI_TRY(h2d(g, g->roots_buf, roots, n_roots));
+    if (immediately) FGI_TRY(h2d(g, g->imm_buf, immediately, n_roots));
+    g->want_ids = false;   // the final collect only counts; the list is made on demand (ensure_ids)
+    const fgi_status st = run_wave(g, n_roots, g->roots_buf, immediately ? g->imm_buf : nullptr, stats);
+    g->want_ids = true;
+    FGI_TRY(st);
+    if (out_n) *out_n = g->last_wave_n;
+    if (!out_bits) return FGI_OK;
+    // the wave's invalidated bitmap (bit h of 32-bit word h / 32 = bit h of 64-bit word h / 64)
+    return d2h(g, out_bits, reinterpret_cast<const uint64_t*>(g->inv_bm), need);
+}
+
+fgi_status fgi_alloc_pinned(uint64_t bytes, void** out) {
+    if (!out) return FGI_EINVAL;
+    *out = nullptr;
+    if (bytes == 0) return FGI_OK;
+    return hipHostMalloc(out, bytes, hipHostMallocDefault) == hipSuccess ? FGI_OK : FGI_ENOMEM;
+}
+
+fgi_status fgi_free_pinned(void* p) {
+    if (!p) return FGI_OK;
+    return hipHostFree(p) == hipSuccess ? FGI_OK : FGI_EINVAL;
+}
+
 fgi_status fgi_wave_ids_dev(fgi_graph* g, const uint32_t** ids_dev, uint64_t* n) {
     if (!g || !ids_dev) return FGI_EINVAL;
+    hipSetDevice(g->device);
+    if (!g->part) FGI_TRY(ensure_ids(g));
     *ids_dev = g->inv;
     if (n) *n = g->last_wave_n;
     return FGI_OK;
@@ -2568,7 +2614,11 @@ static fgi_status defragment(fgi_graph* g) {
     FGI_TRY(d2h(g, &last_off, noff + H - 1, 1));
     FGI_TRY(d2h(g, &last_cap, cap64 + H - 1, 1));
     const uint64_t total = last_off + last_cap;
-    const uint64_t cap = std::max<uint64_t>(total + total / 8, 1024);
+    // pool positions are 32-bit in the traversal kernels (ensure_pool's limit): a defragmented pool
+    // that would not fit below 2^32 is not made — the rows stay where they are
+    constexpr uint64_t kMaxPool = 1ull << 32;
+    if (total > kMaxPool) return FGI_OK;
+    const uint64_t cap = std::min<uint64_t>(std::max<uint64_t>(total + total / 8, 1024), kMaxPool);
     uint32_t* ncol = nullptr;
     uint64_t* ntag = nullptr;
     FGI_TRY(dmalloc(g, &ncol, cap));
@@ -2611,6 +2661,9 @@ static fgi_status prune_rows(fgi_graph* g, uint32_t lo, uint32_t hi, bool allow_
     float ms = 0;
     hipEventElapsedTime(&ms, e0, e1);
     touch(g);
+    // rows compacted in place: a snapshot's row descriptors no longer describe them (entries moved
+    // left, freed slack reused by later appends), so fgi_restore must refuse as after a rebuild
+    if (c[kPrNew] != c[kPrOld] || c[kPrDropped] != 0) g->pool_epoch++;
     const uint64_t pool_before = g->pool_top;
     // the full pass knows every row's length: defragment when holes are most of the pool
     if (allow_defrag && lo == 0 && hi == g->n_handles && g->opt_defrag_pct > 0 &&

@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <condition_variable>
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <mutex>
@@ -495,6 +496,17 @@ fgi_status fgi_part_init(fgi_graph* g, uint32_t n_global, const uint8_t* id128) 
         return set_err(g, FGI_EDEVICE, "ncclCommInitRank: %s", ncclGetErrorString(r));
     }
     p->ops.reset(new RcclComm());
+    // the engine is built against /opt/rocm's RCCL headers; a process that loaded another librccl
+    // with the same soname first (e.g. torch's) binds the engine to that one: say so once
+    static bool warned = false;
+    int v = 0;
+    if (!warned && ncclGetVersion(&v) == ncclSuccess && v != NCCL_VERSION_CODE) {
+        Dl_info info{};
+        const char* f = (dladdr(reinterpret_cast<void*>(&ncclGetVersion), &info) && info.dli_fname) ? info.dli_fname : "?";
+        fprintf(stderr, "[fgi] warning: collectives bound to RCCL %d (%s), not the RCCL %d libfgi was built against\n", v,
+                f, (int)NCCL_VERSION_CODE);
+        warned = true;
+    }
     return FGI_OK;
 }
 

@@ -1285,9 +1285,12 @@ __global__ __launch_bounds__(kBlock) void k_apply_recv(int L, uint64_t n, const 
 // k_final_write — block t adds up its predecessors' counts (all of them in one round) and writes
 // every set bit's handle at that offset, in ascending order: one 1,024-handle tile per wave, 16
 // handles per lane, staged in LDS and stored coalesced.
+// total = 1 (bitmap mode, no k_final_write follows): the last block also sums the counts into
+// ctr->inv (V_inv).
 __global__ __launch_bounds__(kBlock) void k_final_count(const unsigned long long* __restrict__ inv64, uint64_t words,
                                                         uint64_t wpb, unsigned long long* status, WaveCtr* ctr,
-                                                        const unsigned long long* __restrict__ blk) {
+                                                        const unsigned long long* __restrict__ blk, int total,
+                                                        unsigned long long* done) {
     __shared__ unsigned long long s_red[kBlock / 64];
     const uint32_t t = blockIdx.x;
     if (t < (uint32_t)kStats) {
@@ -1305,7 +1308,16 @@ __global__ __launch_bounds__(kBlock) void k_final_count(const unsigned long long
     unsigned long long c = 0;
     for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x) c += (unsigned long long)__popcll(inv64[w]);
     c = block_sum(c, s_red);
-    if (threadIdx.x == 0) status[t] = c;
+    if (!total) {
+        if (threadIdx.x == 0) status[t] = c;
+        return;
+    }
+    if (threadIdx.x == 0) coh_xchg(status + t, c);
+    if (!last_block(done, gridDim.x)) return;
+    unsigned long long all = 0;
+    for (uint32_t k = threadIdx.x; k < gridDim.x; k += blockDim.x) all += coh_read(status + k);
+    all = block_sum(all, s_red);
+    if (threadIdx.x == 0) ctr->inv = all;
 }
 
 __global__ __launch_bounds__(kBlock) void k_final_write(const unsigned long long* __restrict__ inv64, uint64_t words,
@@ -1754,8 +1766,8 @@ ExpandArgs expand_args(fgi_graph* g, int buf) {
     return ExpandArgs{g->fr_off[buf], g->escan[buf], g->cstart[buf], g->pool_col, g->pool_tag, g->opt_dead_filter};
 }
 
-// the invalidated bitmap -> the invalidated list and V_inv (ctr->inv)
-hipError_t launch_final(fgi_graph* g, uint32_t n_handles) {
+// the invalidated bitmap -> V_inv (ctr->inv) and, with ids, the invalidated list
+hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true) {
     const uint64_t words = ((uint64_t)n_handles + 63) / 64;
     uint32_t G = (uint32_t)std::min<uint64_t>(kFinalBlocks, std::max<uint64_t>(kStats, (words + 255) / 256));
     const uint64_t wpb = (words + G - 1) / G;
@@ -1763,9 +1775,10 @@ hipError_t launch_final(fgi_graph* g, uint32_t n_handles) {
     // per-block counts apart from the pull prefixes a collect may still read
     unsigned long long* st = g->bsum + 6ull * kStatBlocks;
     hipLaunchKernelGGL(k_final_count, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb, st, g->ctr,
-                       (const unsigned long long*)g->blk_stats);
-    hipLaunchKernelGGL(k_final_write, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb,
-                       (const unsigned long long*)st, g->ctr, g->inv);
+                       (const unsigned long long*)g->blk_stats, ids ? 0 : 1, g->done);
+    if (ids)
+        hipLaunchKernelGGL(k_final_write, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb,
+                           (const unsigned long long*)st, g->ctr, g->inv);
     return hipGetLastError();
 }
 
@@ -1962,7 +1975,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                                out_for(g, buf ^ 1, nullptr), g->ctr, g->blk_stats, g->done, RemoteArgs{});
             if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L + 1], s));
         }
-        FGI_HIP(g, launch_final(g, g->n_handles));   // idempotent: repeated if the wave goes on
+        FGI_HIP(g, launch_final(g, g->n_handles, g->want_ids));   // idempotent: repeated if the wave goes on
         final_done = true;
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
@@ -2015,7 +2028,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         }
     }
     if (!final_done) {   // no roots
-        FGI_HIP(g, launch_final(g, g->n_handles));
+        FGI_HIP(g, launch_final(g, g->n_handles, g->want_ids));
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
         FGI_HIP(g, hipStreamSynchronize(s));
@@ -2026,6 +2039,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     }
     if (imm_dev && n_roots) note_words(g);   // immediate roots changed node words
     g->last_wave_n = g->ctr_host->inv;
+    g->ids_valid = g->want_ids;
     // entries this wave made stale: the invalidated nodes' rows and the matched entries pointing at
     // them (fgi_prune_step's trigger)
     g->stale_est += e_trav + g->ctr_host->e_match;
@@ -2066,6 +2080,15 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         stats->f_total += f_total;
         stats->total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
+    return FGI_OK;
+}
+
+fgi_status ensure_ids(fgi_graph* g) {
+    if (g->ids_valid) return FGI_OK;
+    // the bitmap of the last wave is intact until the next wave starts: list it now
+    FGI_HIP(g, launch_final(g, g->n_handles, true));
+    FGI_HIP(g, hipStreamSynchronize(g->stream));
+    g->ids_valid = true;
     return FGI_OK;
 }
 
@@ -2204,6 +2227,7 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     FGI_HIP(g, hipEventRecord(g->ev_w1, s));
     FGI_HIP(g, hipStreamSynchronize(s));
     g->last_wave_n = g->ctr_host->inv;
+    g->ids_valid = true;
     if (stats) {
         const WaveCtr& c = *g->ctr_host;
         const uint64_t v = c.inv;

@@ -106,6 +106,9 @@ SIGNATURES = {
     "fgi_set_output": [_G, C.c_uint32, _u32p, _u8p, _u32p, C.c_uint64, _u64p, C.POINTER(WaveStats)],
     "fgi_invalidate": [_G, C.c_uint32, _u32p, _u8p, _u32p, C.c_uint64, _u64p, C.POINTER(WaveStats)],
     "fgi_invalidate_dev": [_G, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, _u64p, C.POINTER(WaveStats)],
+    "fgi_invalidate_bits": [_G, C.c_uint32, _u32p, _u8p, C.c_void_p, C.c_uint64, _u64p, C.POINTER(WaveStats)],
+    "fgi_alloc_pinned": [C.c_uint64, C.POINTER(C.c_void_p)],
+    "fgi_free_pinned": [C.c_void_p],
     "fgi_wave_ids_dev": [_G, C.POINTER(C.c_void_p), _u64p],
     "fgi_last_wave_ids": [_G, _u32p, C.c_uint64, _u64p],
     "fgi_invalidate_all": [_G, _u32p, C.c_uint64, _u64p, C.POINTER(WaveStats)],
@@ -380,6 +383,22 @@ class Graph:
                                             C.byref(stats) if stats is not None else None), "invalidate")
         return n.value
 
+    def invalidate_bits(self, roots, immediately=None, stats: Optional[WaveStats] = None,
+                        out_ptr: int = 0) -> Tuple[Optional[np.ndarray], int]:
+        """fgi_invalidate_bits: the wave's invalidated set as a bitmap over handles (uint64 words,
+        bit h of word h // 64). With out_ptr (a caller-owned, e.g. pinned, buffer of
+        (n_handles + 63) // 64 words) the bitmap lands there and (None, V_inv) is returned."""
+        r = _u32(roots)
+        imm = None if immediately is None else _u8(immediately)
+        words = (self.n_handles + 63) // 64
+        bits = None if out_ptr else np.zeros(words, np.uint64)
+        n = C.c_uint64()
+        dst = C.c_void_p(out_ptr) if out_ptr else bits.ctypes.data_as(C.c_void_p)
+        self._check(self.lib.fgi_invalidate_bits(self.h, len(r), _ptr(r, C.c_uint32), _ptr(imm, C.c_uint8), dst, words,
+                                                 C.byref(n), C.byref(stats) if stats is not None else None),
+                    "invalidate_bits")
+        return bits, n.value
+
     def invalidate_dev(self, n_roots: int, roots_ptr: int, imm_ptr: int = 0,
                        stats: Optional[WaveStats] = None) -> int:
         n = C.c_uint64()
@@ -462,6 +481,38 @@ class Graph:
         out = np.zeros(n.value, np.uint32)
         self._check(self.lib.fgi_part_export_ids(self.h, _ptr(out, C.c_uint32), n.value, C.byref(n)), "part_export_ids")
         return out
+
+
+def bits_to_ids(bits: np.ndarray) -> np.ndarray:
+    """Handles whose bit is set in a fgi_invalidate_bits bitmap, ascending."""
+    b = np.unpackbits(np.ascontiguousarray(bits, np.uint64).view(np.uint8), bitorder="little")
+    return np.flatnonzero(b).astype(np.uint32)
+
+
+class Pinned:
+    """fgi_alloc_pinned / fgi_free_pinned: page-locked host memory (nbytes) as a numpy view."""
+
+    def __init__(self, nbytes: int, dtype=np.uint8):
+        self.lib = load_library()
+        p = C.c_void_p()
+        st = self.lib.fgi_alloc_pinned(nbytes, C.byref(p))
+        if st != OK:
+            raise FgiError(st, f"fgi_alloc_pinned({nbytes})")
+        self.ptr = p.value or 0
+        n = nbytes // np.dtype(dtype).itemsize
+        self.array = np.ctypeslib.as_array(C.cast(p, C.POINTER(C.c_uint8)), (nbytes,)).view(dtype)[:n] if nbytes else \
+            np.zeros(0, dtype)
+
+    def close(self):
+        if self.ptr:
+            self.lib.fgi_free_pinned(C.c_void_p(self.ptr))
+            self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def part_unique_id() -> bytes:

@@ -175,6 +175,18 @@ bool ComputedRegistry::SetOutput(Computed& c) {
 void ComputedRegistry::RunWave(const uint32_t* roots, size_t n_roots, const uint8_t* imm) {
     uint64_t n = 0;
     last_ = fgi_wave_stats{};
+    // the bitmap (n_handles / 8 bytes) costs less to bring back than the id list (4 B per node) once a
+    // wave invalidates more than 1/32 of the handles; the previous wave's size predicts this one's
+    const uint64_t words = ((uint64_t)n_handles_ + 63) / 64;
+    const bool use_bits = WaveOutput == 2 || (WaveOutput == 0 && pred_v_ * 32 > (uint64_t)n_handles_);
+    if (use_bits) {
+        if (!bits_) bits_.reset(new uint64_t[words]);
+        uint64_t* bits = bits_.get();
+        Check(fgi_invalidate_bits(g_, (uint32_t)n_roots, roots, imm, bits, words, &n, &last_), "fgi_invalidate_bits");
+        pred_v_ = n;
+        DispatchBits(bits, words, n);
+        return;
+    }
     uint32_t* ids = IdsBuffer(1024);
     fgi_status s = fgi_invalidate(g_, (uint32_t)n_roots, roots, imm, ids, ids_cap_, &n, &last_);
     if (s == FGI_ECAPACITY) {   // the wave itself completed; fetch the ids with the right size
@@ -182,45 +194,77 @@ void ComputedRegistry::RunWave(const uint32_t* roots, size_t n_roots, const uint
         s = fgi_last_wave_ids(g_, ids, n, &n);
     }
     Check(s, "fgi_invalidate");
+    pred_v_ = n;
     Dispatch(ids, n);
 }
 
 // The post-wave fan-out (fusion.hpp, "Threading"). Reference: InvalidatedHandlerSet.Invoke
 // (Internal/InvalidatedHandlerSet.cs:100-127) per node; one `$sys-c.Invalidate` per replica call
 // (Client/Internal/RpcInboundComputeCall.cs:53-62, 102-106), batched per peer here.
-void ComputedRegistry::Dispatch(const uint32_t* ids, uint64_t n) {
+// Reentrant: peer sinks, batch handlers and Invalidated handlers are user code and may run waves
+// themselves (a handler invalidating another node is the reference's normal pattern). While this
+// fan-out runs it owns the ids buffer (a nested wave gets a fresh one) and its host objects are
+// resolved before the first callback, so a nested BeginCompute that replaces a slot's node cannot
+// redirect this wave's handlers to the new node.
+void ComputedRegistry::Dispatch(const uint32_t* ids, uint64_t n) { DispatchImpl(ids, nullptr, 0, n); }
+
+// The same fan-out over the wave's invalidated bitmap (fgi_invalidate_bits): each gather thread
+// decodes its own range of words, so the ids are never materialised as a list (unless a batch
+// handler wants them: chunks of BatchChunk are decoded for it).
+void ComputedRegistry::DispatchBits(const uint64_t* bits, uint64_t words, uint64_t n) {
+    DispatchImpl(nullptr, bits, words, n);
+}
+
+void ComputedRegistry::DispatchImpl(const uint32_t* ids, const uint64_t* bits, uint64_t words, uint64_t n) {
     const auto t0 = std::chrono::steady_clock::now();
+    std::unique_ptr<uint32_t[]> own;
+    uint64_t own_cap = 0;
+    if (ids_ && ids && ids == ids_.get()) {
+        own = std::move(ids_);
+        own_cap = ids_cap_;
+        ids_cap_ = 0;
+    }
+    std::unique_ptr<uint64_t[]> own_bits;
+    if (bits_ && bits && bits == bits_.get()) own_bits = std::move(bits_);
     const uint32_t P = (uint32_t)peers_.size();
-    fan_.ids = n;
-    fan_.objects = fan_.calls = fan_.batches = 0;
-    fan_.peers_hit = 0;
-    fan_.peer_calls.assign(P, 0);
-    fan_.peer_batches.assign(P, 0);
+    FanoutStats fan;
+    fan.ids = n;
+    fan.peer_calls.assign(P, 0);
+    fan.peer_batches.assign(P, 0);
     // 1. parallel gather: per thread, per peer call ids (ids ascending -> handle order), freed
-    //    subscription entries, and the ids that have host objects
+    //    subscription entries, and the host objects of the ids (read-only lookups)
     uint32_t T = 1;
     if (n >= kParallelMin) {
         T = FanoutThreads ? FanoutThreads : std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
         T = (uint32_t)std::min<uint64_t>(T, (n + kParallelMin - 1) / kParallelMin * 4);
     }
-    fan_.threads = T;
+    fan.threads = T;
+    fan.bitmap = bits ? 1u : 0u;
     struct Part {
         std::vector<std::vector<uint64_t>> calls;
-        std::vector<uint32_t> freed, objs;
+        std::vector<uint32_t> freed;
+        std::vector<std::pair<uint32_t, std::shared_ptr<Computed>>> objs;
     };
     std::vector<Part> parts(T);
     const bool any_subs = !subs_.empty() && !sub_head_.empty();
     auto gather = [&](uint32_t t) {
         Part& pt = parts[t];
         pt.calls.resize(P);
-        const uint64_t lo = n * t / T, hi = n * (t + 1) / T;
-        for (uint64_t i = lo; i < hi; ++i) {
-            const uint32_t h = ids[i];
-            if (h >= n_handles_) continue;
-            if (has_obj_[h]) pt.objs.push_back(h);
-            if (!any_subs || h >= sub_head_.size()) continue;
+        auto visit = [&](const uint32_t h) {
+            if (h >= n_handles_) return;
+            if (has_obj_[h]) {
+                std::shared_ptr<Computed> c;
+                if (h < n_slots_) {
+                    c = current_[h];
+                } else {
+                    auto it = detached_.find(h);
+                    if (it != detached_.end()) c = it->second;
+                }
+                pt.objs.emplace_back(h, std::move(c));
+            }
+            if (!any_subs || h >= sub_head_.size()) return;
             uint32_t e = sub_head_[h];
-            if (e == kNone) continue;
+            if (e == kNone) return;
             sub_head_[h] = kNone;   // a call completes once (each handle is in one range only)
             while (e != kNone) {
                 const Sub& sb = subs_[e];
@@ -228,6 +272,14 @@ void ComputedRegistry::Dispatch(const uint32_t* ids, uint64_t n) {
                 pt.freed.push_back(e);
                 e = sb.next;
             }
+        };
+        if (bits) {   // ascending handles of this thread's words
+            const uint64_t lo = words * t / T, hi = words * (t + 1) / T;
+            for (uint64_t w = lo; w < hi; ++w)
+                for (uint64_t m = bits[w]; m; m &= m - 1) visit((uint32_t)(w * 64 + (uint64_t)__builtin_ctzll(m)));
+        } else {
+            const uint64_t lo = n * t / T, hi = n * (t + 1) / T;
+            for (uint64_t i = lo; i < hi; ++i) visit(ids[i]);
         }
     };
     if (T == 1) {
@@ -239,7 +291,20 @@ void ComputedRegistry::Dispatch(const uint32_t* ids, uint64_t n) {
         gather(0);
         for (auto& x : th) x.join();
     }
-    fan_.gather_ms = ms_since(t0);
+    for (auto& pt : parts) sub_free_.insert(sub_free_.end(), pt.freed.begin(), pt.freed.end());
+    // detached nodes leave the engine now (before any callback can hand their handles out again)
+    for (auto& pt : parts)
+        for (auto& o : pt.objs) {
+            const uint32_t h = o.first;
+            if (h < n_slots_ || !o.second) continue;
+            auto it = detached_.find(h);
+            if (it != detached_.end() && it->second == o.second) {
+                detached_.erase(it);
+                has_obj_[h] = 0;
+                fgi_release(g_, 1, &h);
+            }
+        }
+    fan.gather_ms = ms_since(t0);
     // 2. per peer: its call ids in handle order, PeerBatch per sink call
     std::vector<uint64_t> buf;
     for (uint32_t q = 0; q < P; ++q) {
@@ -258,45 +323,53 @@ void ComputedRegistry::Dispatch(const uint32_t* ids, uint64_t n) {
         const size_t B = std::max<size_t>(1, PeerBatch);
         for (uint64_t o = 0; o < tot; o += B) {
             const size_t k = (size_t)std::min<uint64_t>(B, tot - o);
-            if (peers_[q]) peers_[q](q, data + o, k);
-            ++fan_.peer_batches[q];
+            if (q < peers_.size() && peers_[q]) peers_[q](q, data + o, k);
+            ++fan.peer_batches[q];
         }
-        fan_.peer_calls[q] = tot;
-        fan_.calls += tot;
-        fan_.batches += fan_.peer_batches[q];
-        ++fan_.peers_hit;
+        fan.peer_calls[q] = tot;
+        fan.calls += tot;
+        fan.batches += fan.peer_batches[q];
+        ++fan.peers_hit;
     }
-    for (auto& pt : parts) sub_free_.insert(sub_free_.end(), pt.freed.begin(), pt.freed.end());
     // 3. the registry-level handler class, over the whole list
     if (OnInvalidatedBatch) {
         const size_t C = std::max<size_t>(1, BatchChunk);
-        for (uint64_t o = 0; o < n; o += C) OnInvalidatedBatch(ids + o, (size_t)std::min<uint64_t>(C, n - o));
+        if (bits) {
+            std::vector<uint32_t> chunk;
+            chunk.reserve((size_t)std::min<uint64_t>(C, n));
+            for (uint64_t w = 0; w < words; ++w)
+                for (uint64_t m = bits[w]; m; m &= m - 1) {
+                    chunk.push_back((uint32_t)(w * 64 + (uint64_t)__builtin_ctzll(m)));
+                    if (chunk.size() == C) {
+                        OnInvalidatedBatch(chunk.data(), chunk.size());
+                        chunk.clear();
+                    }
+                }
+            if (!chunk.empty()) OnInvalidatedBatch(chunk.data(), chunk.size());
+        } else {
+            for (uint64_t o = 0; o < n; o += C) OnInvalidatedBatch(ids + o, (size_t)std::min<uint64_t>(C, n - o));
+        }
     }
     // 4. host objects: OnUnregister, then each node's handler set, exactly once
     for (auto& pt : parts) {
-        for (const uint32_t h : pt.objs) {
-            std::shared_ptr<Computed> c;
-            if (h < n_slots_) {
-                c = current_[h];
-            } else {
-                auto it = detached_.find(h);
-                if (it != detached_.end()) {
-                    c = it->second;
-                    detached_.erase(it);
-                    has_obj_[h] = 0;
-                    fgi_release(g_, 1, &h);
-                }
-            }
+        for (auto& o : pt.objs) {
+            Computed* c = o.second.get();
             if (!c || c->fired_) continue;
-            ++fan_.objects;
+            ++fan.objects;
             c->fired_ = true;
-            if (h < n_slots_ && OnUnregister) OnUnregister(*c);
+            if (o.first < n_slots_ && OnUnregister) OnUnregister(*c);
             InvalidatedHandlerSet hs = std::move(c->handlers_);
             c->handlers_.Clear();
             hs.Invoke(*c);
         }
     }
-    fan_.dispatch_ms = ms_since(t0);
+    fan.dispatch_ms = ms_since(t0);
+    fan_ = std::move(fan);
+    if (own && own_cap > ids_cap_) {   // hand the (larger) buffer back for the next wave
+        ids_ = std::move(own);
+        ids_cap_ = own_cap;
+    }
+    if (own_bits && !bits_) bits_ = std::move(own_bits);
 }
 
 uint32_t ComputedRegistry::AddPeer(PeerSink sink) {

@@ -19,7 +19,8 @@
 //
 // Threading: one registry = one dispatcher thread (the ABI is externally synchronised). After each
 // wave the dispatcher fans the returned ids out (Dispatch):
-//   1. in parallel over contiguous id ranges (ids come in ascending order): per-peer call-id lists
+//   1. in parallel over contiguous id ranges (ids come in ascending order), or over ranges of the
+//      wave's invalidated bitmap when the wave returned one (large waves): per-peer call-id lists
 //      (subscriptions are consumed: a call completes once), and the ids that have host objects;
 //   2. per peer, its call ids in handle order, cut into batches of at most PeerBatch — one sink
 //      call per batch (what one `$sys-c.Invalidate` message per peer per batch would carry);
@@ -116,6 +117,7 @@ struct FanoutStats {
     uint64_t batches = 0;        // peer sink invocations
     uint32_t peers_hit = 0;      // peers that received at least one batch
     uint32_t threads = 0;        // threads of the parallel phase
+    uint32_t bitmap = 0;         // 1: dispatched from the wave's invalidated bitmap (fgi_invalidate_bits)
     double dispatch_ms = 0;      // whole Dispatch
     double gather_ms = 0;        // parallel phase (subscriptions -> per-peer lists)
     std::vector<uint64_t> peer_calls, peer_batches;   // per peer id
@@ -171,6 +173,10 @@ class ComputedRegistry {
     size_t PeerBatch = 4096;
     uint32_t FanoutThreads = 0;   // 0: hardware concurrency, capped at 16
 
+    // how a wave's invalidated set comes back: 0 auto (the bitmap once the previous wave invalidated
+    // more than 1/32 of the handles), 1 the id list, 2 the bitmap (fgi_invalidate_bits)
+    int WaveOutput = 0;
+
     std::function<void(Computed&)> OnRegister, OnUnregister;
     // registry-level handler class: the wave's invalidated handles, BatchChunk at a time
     std::function<void(const uint32_t* ids, size_t n)> OnInvalidatedBatch;
@@ -192,6 +198,8 @@ class ComputedRegistry {
     // the engine's ids of the last call into ids_ (grown without zero-fill, reused across waves)
     uint32_t* IdsBuffer(uint64_t need);
     void Dispatch(const uint32_t* ids, uint64_t n);
+    void DispatchBits(const uint64_t* bits, uint64_t words, uint64_t n);
+    void DispatchImpl(const uint32_t* ids, const uint64_t* bits, uint64_t words, uint64_t n);
     void FlushScope();
     LTag NextVersion(LTag current);
     void MoveSubs(uint32_t from, uint32_t to);
@@ -210,6 +218,8 @@ class ComputedRegistry {
     FanoutStats fan_;
     std::unique_ptr<uint32_t[]> ids_;
     uint64_t ids_cap_ = 0;
+    std::unique_ptr<uint64_t[]> bits_;   // the last bitmap-mode wave's invalidated bitmap
+    uint64_t pred_v_ = 0;                // the previous wave's V_inv (picks the output form)
     // subscriptions: per handle a singly-linked list in one pool (kNone-terminated), free list
     std::vector<PeerSink> peers_;
     std::vector<uint32_t> sub_head_;

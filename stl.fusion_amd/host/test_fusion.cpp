@@ -205,6 +205,42 @@ static void prune() {
     CHECK(pr.first == 2 && pr.second == 1 && a->UsedBy().size() == 1);
 }
 
+// Handlers that run waves of their own (a normal pattern in the reference: an Invalidated handler
+// invalidating another node, MutableState.OnInvalidated recomputing). The nested waves must not
+// disturb the outer fan-out: every invalidated node fires once, the outer wave's handlers stay on
+// the nodes it invalidated even when a handler replaces a slot's node (BeginCompute).
+static void reentrant_handlers() {
+    ComputedRegistry r(64);
+    auto a = Compute(r, "a");
+    auto b = Compute(r, "b", {a});
+    auto x = Compute(r, "x");
+    auto y = Compute(r, "y", {x});
+    auto z = Compute(r, "z");
+    int fa = 0, fb = 0, fy = 0, fz = 0, fa2 = 0, batches = 0;
+    std::shared_ptr<Computed> a2;
+    a->OnInvalidated([&](Computed&) { ++fa; });
+    y->OnInvalidated([&](Computed&) { ++fy; });
+    z->OnInvalidated([&](Computed&) { ++fz; });
+    b->OnInvalidated([&](Computed&) {
+        ++fb;
+        x->Invalidate();   // a nested wave from an Invalidated handler
+    });
+    r.OnInvalidatedBatch = [&](const uint32_t*, size_t) {
+        if (batches++) return;
+        z->Invalidate();             // a nested wave from the batch handler
+        a2 = r.BeginCompute("a");    // ... and a recompute of a slot the outer wave invalidated
+        CHECK(r.SetOutput(*a2));
+        a2->OnInvalidated([&](Computed&) { ++fa2; });
+    };
+    a->Invalidate();
+    r.OnInvalidatedBatch = nullptr;
+    CHECK(fa == 1 && fb == 1 && fy == 1 && fz == 1 && fa2 == 0);
+    CHECK(a->IsInvalidated() && b->IsInvalidated() && x->IsInvalidated() && y->IsInvalidated() && z->IsInvalidated());
+    CHECK(a2 && r.Get("a") == a2 && a2->IsConsistent());
+    a2->Invalidate();
+    CHECK(fa2 == 1 && fa == 1);
+}
+
 // TodoApp-style replica fan-out at BASELINE.json configs[4]'s size (DESIGN.md §Host fan-out):
 // 10,000 hubs x 1,000 leaves = 10M leaves (1% with an invalidation delay), every leaf computed
 // held by one RPC client (peer = leaf % 100, call id = leaf), as RpcInboundComputeCall keeps the
@@ -260,7 +296,10 @@ static void fanout_10m() {
         sc[k] = H + k;
     }
     std::string runs;
-    for (uint32_t threads : {16u, 1u}) {
+    const uint32_t run_threads[3] = {16u, 16u, 1u}, run_output[3] = {1u, 2u, 2u};   // id list, then bitmap
+    for (int run = 0; run < 3; ++run) {
+        const uint32_t threads = run_threads[run];
+        r.WaveOutput = (int)run_output[run];
         std::fill(got.begin(), got.end(), 0);
         std::fill(sum.begin(), sum.end(), 0);
         std::fill(last.begin(), last.end(), 0);
@@ -276,6 +315,7 @@ static void fanout_10m() {
         const fgi_wave_stats& w = r.LastWave();
         CHECK(w.v_inv == H + undelayed);
         CHECK(f.ids == w.v_inv && f.calls == undelayed && order_bad == 0);
+        CHECK(f.bitmap == (run_output[run] == 2 ? 1u : 0u));
         uint64_t min_b = ~0ull, max_b = 0, tot = 0;
         bool sums_ok = true;
         for (uint32_t q = 0; q < P; ++q) {
@@ -293,11 +333,11 @@ static void fanout_10m() {
         CHECK(tot == undelayed && sums_ok);
         char line[768];
         std::snprintf(line, sizeof line,
-                      "%s{\"threads\": %u, \"v_inv\": %llu, \"wave_kernel_ms\": %.3f, \"wave_call_ms\": %.3f, "
+                      "%s{\"threads\": %u, \"output\": \"%s\", \"v_inv\": %llu, \"wave_kernel_ms\": %.3f, \"wave_call_ms\": %.3f, "
                       "\"invalidate_call_ms\": %.3f, \"dispatch_ms\": %.3f, \"gather_ms\": %.3f, \"subscribe_ms\": %.1f, "
                       "\"calls\": %llu, \"batches\": %llu, \"peers\": %u, \"batches_per_peer\": [%llu, %llu], "
                       "\"peer_batch\": %zu}",
-                      runs.empty() ? "" : ", ", f.threads, (unsigned long long)w.v_inv, w.kernel_ms, w.total_ms, call_ms,
+                      runs.empty() ? "" : ", ", f.threads, f.bitmap ? "bitmap" : "ids", (unsigned long long)w.v_inv, w.kernel_ms, w.total_ms, call_ms,
                       f.dispatch_ms, f.gather_ms, sub_ms, (unsigned long long)f.calls, (unsigned long long)f.batches,
                       f.peers_hit, (unsigned long long)min_b, (unsigned long long)max_b, r.PeerBatch);
         runs += line;
@@ -329,6 +369,7 @@ int main(int argc, char** argv) {
         add_used_states();
         register_displacement();
         prune();
+        reentrant_handlers();
     } catch (const FgiError& e) {
         std::fprintf(stderr, "FgiError %d: %s\n", (int)e.status, e.what());
         return 2;

@@ -1,10 +1,12 @@
-"""CPU check of the numpy BFS that test_gpu_scale.py uses as the exact checker of the full-size
-configs[1] wave: on smaller R-MAT graphs (with stale edges) it must give the oracle's set."""
+"""CPU check of the independent closure checker (tests/closure_check.py) that test_gpu_scale.py and
+test_gpu_configs.py use on the full-size configs[1] / [2] / [3] waves: on smaller R-MAT graphs (with
+stale edges) its least closure must be the oracle's set, the oracle's own wave must pass every check,
+and a wave with a node missing or added must fail them."""
 import numpy as np
 import pytest
 
 import fgo as O
-from test_gpu_scale import closure_bfs
+from closure_check import DeviceEdges
 
 
 @pytest.mark.parametrize("scale,stale", [(12, 0), (14, 30)])
@@ -17,11 +19,20 @@ def test_closure_bfs_matches_oracle(fgo, scale, stale):
     ver = O.version_of(seed, np.arange(n))
     o.load_graph(ver, None, s, d, t)
     roots = O.gen_roots(64, n, 0x5EED1024, np.bincount(s, minlength=n))
-    o.invalidate_slots(roots)
+    st = o.invalidate_slots(roots)
+    ids = np.sort(o.inv_log())
     want = np.zeros(n, bool)
-    want[o.inv_log()] = True
-    got = closure_bfs(n, s, d, t, ver, roots)
+    want[ids] = True
+    e = DeviceEdges(n, s, d, t, ver, device="cpu")
+    got = e.least_closure(roots).numpy()
     assert np.array_equal(got, want)
+    assert e.check_wave(ids, roots, st.e_trav) == len(ids)
+    # a node short (a non-root) or a node too many must be caught
+    extra = np.setdiff1d(np.arange(n), ids)[:1]
+    non_root = np.setdiff1d(ids, roots)
+    for bad in (np.setdiff1d(ids, non_root[-1:]), np.sort(np.concatenate([ids, extra]))):
+        with pytest.raises(AssertionError):
+            e.check_wave(bad, roots, st.e_trav)
 
 
 def test_parallel_oracle_import_is_thread_count_independent(fgo):

@@ -54,6 +54,8 @@ def test_host_fanout_10m_leaves(gpu_available):
     for run in rec["runs"]:
         assert 9_800_000 < run["calls"] < 10_000_000   # exact counts are checked in C++
         assert run["peers"] == 100
+    # the id-list form and the bitmap form (fgi_invalidate_bits) of the same wave
+    assert [r["output"] for r in rec["runs"]] == ["ids", "bitmap", "bitmap"]
     out = os.environ.get("FGI_FANOUT_OUT")
     if out:
         with open(out, "w") as f:

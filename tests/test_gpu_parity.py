@@ -338,3 +338,38 @@ def test_waves_of_alternating_shapes(pkg, gpu_available):
         shapes.append(ws.pull_levels)
     # (the first wave builds the pull-list cache and runs push-only)
     assert max(shapes) > 0 and shapes[1] == 0, shapes
+
+
+@pytest.mark.parametrize("scale,stale", [(13, 0), (20, 50)])
+def test_bitmap_output_equals_id_list(pkg, gpu_available, scale, stale):
+    """fgi_invalidate_bits returns the wave's invalidated set as a bitmap over handles: the same set
+    as fgi_invalidate's id list, the same statistics and final states; the id list is still
+    available afterwards (fgi_last_wave_ids builds it from the bitmap on demand)."""
+    seed, sseed = 0x5EED0024, 0x5EED00C0
+    n = 1 << scale
+    g = pkg.Graph(n, n_detached=64)
+    g.synth_rmat(scale, 16, seed, stale, sseed)
+    deg, _ = g.degrees()
+    roots = O.gen_roots(4096 if scale > 13 else 64, n, 0x5EED1024, deg[:n])
+    imm = (np.arange(len(roots)) % 7 == 0).astype(np.uint8)
+    g.snapshot()
+    ws = pkg.WaveStats()
+    ids = g.invalidate(roots, imm, stats=ws)
+    v1, f1 = g.dump_states()
+    for pinned in (False, True):
+        g.restore()
+        wb = pkg.WaveStats()
+        if pinned:
+            buf = pkg.fgi.Pinned(((g.n_handles + 63) // 64) * 8, np.uint64)
+            _, nb = g.invalidate_bits(roots, imm, stats=wb, out_ptr=buf.ptr)
+            bits = buf.array.copy()
+            buf.close()
+        else:
+            bits, nb = g.invalidate_bits(roots, imm, stats=wb)
+        got = pkg.fgi.bits_to_ids(bits)
+        assert nb == len(ids) == wb.v_inv and np.array_equal(got, np.sort(ids))
+        assert (wb.v_inv, wb.e_trav) == (ws.v_inv, ws.e_trav)
+        assert np.array_equal(g.last_wave_ids(), np.sort(ids))   # the list, made on demand
+        v2, f2 = g.dump_states()
+        assert np.array_equal(v1, v2) and np.array_equal(f1, f2)
+    g.close()

@@ -144,3 +144,29 @@ def test_defragmentation_keeps_rows(pkg, gpu_available):
         g.close()
         o.close()
     assert np.array_equal(res[0][0], res[1][0])
+
+
+def test_restore_after_in_place_prune(pkg, gpu_available):
+    """snapshot -> begin_compute -> fgi_prune_range (rows compacted in place) -> fgi_restore: the
+    snapshot's row descriptors no longer describe the compacted rows, so restore must refuse
+    (FGI_ESTATE) — or, if it restores, leave a graph whose waves still match the oracle's."""
+    rng = np.random.default_rng(43)
+    n = 3000
+    versions, flags = random_states(n, rng, p_delay=0.0)
+    src, dst, tags = _edges_from_live(versions, flags, rng, 30000, n, stale_p=0.5)
+    g, o = build_pair(pkg, n, versions, flags, src, dst, tags)
+    g.snapshot()
+    o.snapshot()
+    slots = rng.choice(np.nonzero(versions)[0], 40, replace=False).astype(np.uint32)
+    newv = (versions[slots] + np.uint64(2)).astype(np.uint64)
+    g.begin_compute(slots, newv)
+    for s_, v_ in zip(slots, newv):
+        o.begin_compute(int(s_), int(v_))
+    g.prune_range(0, g.n_handles)
+    try:
+        g.restore()
+    except pkg.FgiError as e:
+        assert e.status == pkg.fgi.ESTATE
+        return
+    o.restore()
+    _compare_wave(g, o, n, rng.integers(0, n, 60).astype(np.uint32))

@@ -4,12 +4,13 @@
     against the oracle, bit-exact — invalidated set, V_inv, E_trav and every final node word —
     on the push, pull and automatic paths, with 0% and 50% stale edges.
 (b) the full configs[1] wave that bench.py times (R-MAT scale 24, 16.8M slots, 263M edges, 4,096
-    roots): the oracle's object graph would take minutes here, so the result is checked through
-    size-independent properties over the engine's exported edge set (fgi_export_edges):
+    roots), and configs[3]'s (the same graph, 50% stale edges): the oracle's object graph would take
+    minutes here, so the result is checked through size-independent properties over the engine's
+    exported edge set (fgi_export_edges; tests/closure_check.py):
       closure  — every version-matching `_usedBy` entry of an invalidated node leads to an
                  invalidated node (Computed.cs:212-216 recurses into it);
       witness  — every invalidated non-root has an invalidated parent holding a matching entry;
-      and, exactly, the least closure computed by an independent level-synchronous numpy BFS.
+      and, exactly, the least closure computed independently (torch gather / scatter fixpoint).
 """
 import os
 
@@ -63,34 +64,14 @@ def test_configs1_generator_scale20_bit_exact(pkg, gpu_available, stale):
     g.close()
 
 
-def closure_bfs(n, u, d, t, ver, roots):
-    """Least set containing the roots and closed under version-matching entries, by a level-
-    synchronous BFS over (u -> d) in numpy (all nodes Consistent, no delays: a visit invalidates)."""
-    deg = np.bincount(u, minlength=n).astype(np.int64)
-    indptr = np.zeros(n + 1, np.int64)
-    np.cumsum(deg, out=indptr[1:])
-    live = t == ver[d]
-    seen = np.zeros(n, bool)
-    front = np.unique(roots).astype(np.int64)
-    seen[front] = True
-    while len(front):
-        cnt = deg[front]
-        tot = int(cnt.sum())
-        if tot == 0:
-            break
-        starts = indptr[front]
-        off = np.repeat(starts - (np.cumsum(cnt) - cnt), cnt) + np.arange(tot, dtype=np.int64)
-        off = off[live[off]]
-        nxt = d[off]
-        nxt = np.unique(nxt[~seen[nxt]]).astype(np.int64)
-        seen[nxt] = True
-        front = nxt
-    return seen
-
-
-def test_configs1_full_scale24_wave_properties(pkg, gpu_available):
+@pytest.mark.parametrize("config", ["rmat24", "rmat24_churn"])
+def test_configs1_full_scale24_wave_properties(pkg, gpu_available, config):
+    """configs[1] (and configs[3]: the same graph with 50% stale edges) at full size: the wave
+    bench.py times, against the least closure computed independently (numpy-free: torch's gather /
+    scatter over the exported edges, tests/closure_check.py), plus the final node states."""
+    from closure_check import DeviceEdges
     from stl_fusion_amd import workloads as W
-    cfg = W.CONFIGS["rmat24"]
+    cfg = W.CONFIGS[config]
     n = W.n_slots(cfg)
     g = pkg.Graph(n)
     W.build(g, cfg)
@@ -98,36 +79,26 @@ def test_configs1_full_scale24_wave_properties(pkg, gpu_available):
     assert len(roots) == 4096
     # the edge set before the wave (an invalidated node's `_usedBy` is cleared, Computed.cs:217)
     u, d, t = g.export_edges()
+    assert len(u) == 263_432_932
+    ver = O.version_of(cfg["seed"], np.arange(n))
+    if cfg["stale_pct"]:
+        stale = t != ver[d]
+        assert 0.49 < stale.mean() < 0.51
+    edges = DeviceEdges(n, u, d, t, ver)
+    del u, d, t
     ws = pkg.WaveStats()
     ids = g.invalidate(roots, stats=ws)
     assert len(ids) == ws.v_inv and len(np.unique(ids)) == len(ids)
     _, f = g.dump_states()
     g.close()
-    assert len(u) == 263_432_932
-    ver = O.version_of(cfg["seed"], np.arange(n))
     inv = np.zeros(n, bool)
     inv[ids] = True
     # node states: exactly the returned set is Invalidated, everything else still Consistent
     assert np.array_equal((f[:n] & 3) == INVALIDATED, inv)
     assert np.all((f[:n] & 3)[~inv] == CONSISTENT)
-    # roots (all Consistent, no delay) are invalidated
-    assert inv[roots].all()
-    # closure: every matching entry of an invalidated node reaches an invalidated node
-    m = inv[u] & (t == ver[d])
-    assert inv[d[m]].all(), "an invalidated node has a matching dependant the wave did not invalidate"
-    # witness: every invalidated non-root has an invalidated parent with a matching entry
-    has_parent = np.zeros(n, bool)
-    has_parent[d[m]] = True
-    is_root = np.zeros(n, bool)
-    is_root[roots] = True
-    assert not np.any(inv & ~is_root & ~has_parent), "an invalidated node has no invalidated parent"
-    # E_trav: sum of |_usedBy| over the invalidated nodes
-    assert ws.e_trav == int(np.bincount(u, minlength=n)[inv].astype(np.int64).sum())
-    del m, has_parent
-    # exactly the least closure (an independent BFS)
-    want = closure_bfs(n, u, d, t, ver, roots)
-    assert np.array_equal(want, inv), (int(want.sum()), int(inv.sum()))
-    assert ws.v_inv == 7_370_581 and ws.e_trav == 261_303_996
+    edges.check_wave(ids, roots, ws.e_trav)
+    if not cfg["stale_pct"]:
+        assert ws.v_inv == 7_370_581 and ws.e_trav == 261_303_996
 
 
 @pytest.mark.parametrize("direction", [0, 2])
