@@ -324,9 +324,25 @@ fgi_status fgi_part_unique_id(uint8_t* id128);
 /* Join the partitioned engine: this graph owns slots [rank*ceil(N/world), ...) of a global
  * N = n_global slots; cfg->rank/world must be set. */
 fgi_status fgi_part_init(fgi_graph* g, uint32_t n_global, const uint8_t* id128);
-/* Partitioned R-MAT: every rank generates the same global edge set and keeps the rows it owns. */
+/* Partitioned R-MAT: every rank walks the global edge sequence by index (edge i is a pure function of
+ * i) and keeps only its share — the rows of its slots and the dependency entries of its slots —
+ * without materialising the global edge list. */
 fgi_status fgi_part_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_factor, uint64_t seed,
                                uint32_t stale_pct, uint64_t stale_seed);
+/* Bulk import into a partitioned graph (ComputedRegistry.Register, ComputedRegistry.cs:72-105, without
+ * displacement; the single-device fgi_register_nodes refuses a partition). Every rank is given the
+ * same global node list (the host broadcasts it): each rank installs the nodes of the slots it owns
+ * and records every listed version in its replica (ver_all), against which it checks the tags of
+ * edges into other ranks' slots. No collective runs. */
+fgi_status fgi_part_register_nodes(fgi_graph* g, uint32_t n, const uint32_t* slot, const uint64_t* version,
+                                   const uint32_t* state_flags);
+/* Bulk import of `_usedBy` entries with global ids (IComputedImpl.AddUsedBy body, Computed.cs:381-382;
+ * set semantics). Every rank is given the same batch: it keeps the rows of the `used` slots it owns
+ * (entries keep global dependant ids) and the dependency entries of the dependants it owns, from
+ * which it rebuilds its pull lists (the reference's `_used`, Computed.cs:36, 365-366). No collective
+ * runs. */
+fgi_status fgi_part_load_edges(fgi_graph* g, uint64_t m, const uint32_t* used, const uint32_t* dependant,
+                               const uint64_t* tag);
 /* Collective wave: every rank passes the same global root list; each rank reports the
  * invalidated slots it owns (global ids) and its own share of the statistics. */
 fgi_status fgi_part_invalidate(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev,

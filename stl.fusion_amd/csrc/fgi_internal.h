@@ -72,6 +72,47 @@ __host__ __device__ inline uint64_t synth_version(uint64_t seed, uint32_t slot) 
     return (sm64(seed ^ (uint64_t)slot) & ((1ull << 55) - 1)) | 1ull;
 }
 
+// R-MAT edge i of a (scale, seed) graph (oracle/synth.cpp): per level l,
+// u = sm64(sm64(seed) ^ (i << 6 | l)) >> 11 against 0.57 / 0.76 / 0.95 * 2^53, endpoints scrambled by
+// a bijection of [0, 2^scale)
+__host__ __device__ inline uint32_t rmat_scramble(uint64_t x, uint32_t scale, uint64_t seed) {
+    const uint64_t mask = (scale >= 64) ? ~0ull : ((1ull << scale) - 1);
+    const uint64_t k1 = sm64(seed ^ 0xA5A5A5A5A5A5A5A5ull) | 1ull;
+    const uint64_t k2 = sm64(seed ^ 0x5A5A5A5A5A5A5A5Aull) | 1ull;
+    const uint64_t c = sm64(seed ^ 0x0123456789ABCDEFull);
+    const uint32_t s1 = (scale + 1) / 2, s2 = scale / 2 ? scale / 2 : 1;
+    x = (x * k1) & mask;
+    x ^= x >> s1;
+    x = (x + c) & mask;
+    x = (x * k2) & mask;
+    x ^= x >> s2;
+    return (uint32_t)x;
+}
+__host__ __device__ inline void rmat_edge(uint64_t i, uint32_t scale, uint64_t seed, uint32_t* src, uint32_t* dst) {
+    const uint64_t one = 1ull << 53;
+    const uint64_t tA = one / 100 * 57, tAB = one / 100 * 76, tABC = one / 100 * 95;
+    const uint64_t ks = sm64(seed);
+    uint64_t s = 0, d = 0;
+    for (uint32_t l = 0; l < scale; ++l) {
+        const uint64_t u = sm64(ks ^ ((i << 6) | l)) >> 11;
+        const uint64_t bit = 1ull << (scale - 1 - l);
+        if (u >= tA) {
+            if (u < tAB) d |= bit;
+            else if (u < tABC) s |= bit;
+            else {
+                s |= bit;
+                d |= bit;
+            }
+        }
+    }
+    *src = rmat_scramble(s, scale, seed);
+    *dst = rmat_scramble(d, scale, seed);
+}
+// stale edge of the churn workloads (configs[3]): tag = version + 1
+__host__ __device__ inline bool synth_stale(uint32_t stale_pct, uint64_t stale_seed, uint32_t src, uint32_t dst) {
+    return stale_pct && (sm64(stale_seed ^ sm64(((uint64_t)src << 32) | dst)) % 100) < stale_pct;
+}
+
 // ---- wave bookkeeping -------------------------------------------------------------------------
 constexpr int kRing = 64;               // per-level counters live in a ring (deep waves roll over)
 constexpr int kBlock = 256;             // threads per block for the traversal kernels
@@ -308,6 +349,9 @@ fgi_status ensure_ids(fgi_graph* g);
 fgi_status build_rows_from_keys(fgi_graph* g, uint64_t m, uint64_t* keys, uint64_t* tags,
                                 uint64_t ver_seed, uint32_t stale_pct, uint64_t stale_seed,
                                 uint32_t src_base = 0, uint32_t dst_base = 0);
+// Existing live rows + m new entries given as host arrays (keys: used handle << 32 | dependant id).
+fgi_status load_rows(fgi_graph* g, uint64_t m, const uint64_t* host_keys, const uint64_t* host_tags, uint32_t src_base,
+                     uint32_t dst_base);
 // Build the pull dependency-list cache if the graph changed since it was built.
 fgi_status ensure_in_lists(fgi_graph* g);
 // Copy the first two entries of every slot's list into uin_head, then (re)build the pull
@@ -370,6 +414,8 @@ fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, u
                               uint32_t count = 1);
 // all-gather every rank's local invalidated-bitmap words into front_global (part.hip)
 fgi_status part_allgather_front(fgi_graph* g);
+// Rebuild a partition's pull lists from its dependency-entry store if rows or versions changed.
+fgi_status part_ensure_lists(fgi_graph* g);
 // Partitioned wave over global root ids (wave.hip): run_part_wave drives the phases below.
 fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                          fgi_wave_stats* stats);

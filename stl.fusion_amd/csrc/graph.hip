@@ -1473,9 +1473,24 @@ fgi_status build_rows_from_keys(fgi_graph* g, uint64_t m, uint64_t* keys, uint64
     return FGI_OK;
 }
 
+// Existing live rows + m new entries (host keys: used handle << 32 | dependant id, host tags),
+// rebuilt in one sort (set semantics across both).
+fgi_status load_rows(fgi_graph* g, uint64_t m, const uint64_t* host_keys, const uint64_t* host_tags, uint32_t src_base,
+                     uint32_t dst_base) {
+    FGI_TRY(fold(g));
+    Tmp tk, tt;
+    uint64_t *keys, *tags, m0 = 0;
+    FGI_TRY(gather_live(g, tk, tt, &keys, &tags, m, &m0));
+    FGI_TRY(h2d(g, keys + m0, host_keys, m));
+    FGI_TRY(h2d(g, tags + m0, host_tags, m));
+    return build_rows_from_keys(g, m0 + m, keys, tags, 0, 0, 0, src_base, dst_base);
+}
+
 }  // namespace fgi
 
 using namespace fgi;
+
+static fgi_status single_only(fgi_graph* g, const char* what);
 
 extern "C" {
 
@@ -1622,6 +1637,7 @@ fgi_status fgi_stream(fgi_graph* g, void** stream) {
 fgi_status fgi_register_nodes(fgi_graph* g, uint32_t n, const uint32_t* slot, const uint64_t* version,
                               const uint32_t* state_flags) {
     if (!g || (n && (!slot || !version))) return FGI_EINVAL;
+    FGI_TRY(single_only(g, "fgi_register_nodes"));
     for (uint32_t i = 0; i < n; ++i) {
         if (slot[i] >= g->n_slots) return set_err(g, FGI_EINVAL, "slot %u out of range", slot[i]);
         if (version[i] > kVMask) return set_err(g, FGI_EINVAL, "version of slot %u exceeds 2^56-1", slot[i]);
@@ -1654,24 +1670,16 @@ fgi_status fgi_register_nodes(fgi_graph* g, uint32_t n, const uint32_t* slot, co
 fgi_status fgi_load_edges(fgi_graph* g, uint64_t m, const uint32_t* used, const uint32_t* dependant_slot,
                           const uint64_t* tag) {
     if (!g || (m && (!used || !dependant_slot || !tag))) return FGI_EINVAL;
+    FGI_TRY(single_only(g, "fgi_load_edges"));
     for (uint64_t e = 0; e < m; ++e) {
         if (used[e] >= g->n_handles || dependant_slot[e] >= g->n_slots)
             return set_err(g, FGI_EINVAL, "edge %llu out of range", (unsigned long long)e);
         if (tag[e] == 0) return set_err(g, FGI_EINVAL, "edge %llu has tag 0 (LTags are positive)", (unsigned long long)e);
     }
     hipSetDevice(g->device);
-    FGI_TRY(fold(g));
-    // existing live rows + the new entries, rebuilt in one sort (set semantics across both)
-    Tmp tk, tt;
-    uint64_t *keys, *tags, m0 = 0;
-    FGI_TRY(gather_live(g, tk, tt, &keys, &tags, m, &m0));
-    if (m) {
-        std::vector<uint64_t> hk(m);
-        for (uint64_t e = 0; e < m; ++e) hk[e] = ((uint64_t)used[e] << 32) | dependant_slot[e];
-        FGI_TRY(h2d(g, keys + m0, hk.data(), m));
-        FGI_TRY(h2d(g, tags + m0, tag, m));
-    }
-    return build_rows_from_keys(g, m0 + m, keys, tags, 0, 0, 0);
+    std::vector<uint64_t> hk(m);
+    for (uint64_t e = 0; e < m; ++e) hk[e] = ((uint64_t)used[e] << 32) | dependant_slot[e];
+    return load_rows(g, m, hk.data(), tag, 0, 0);
 }
 
 fgi_status fgi_get_state(fgi_graph* g, uint32_t n, const uint32_t* handle, uint64_t* version, uint32_t* state_flags) {

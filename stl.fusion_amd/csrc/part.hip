@@ -61,6 +61,14 @@ struct PartState {
     unsigned long long* all_cnt_host = nullptr;
     unsigned long long* scalar = nullptr;      // device scratch for all-reduce
     unsigned long long* scalar_host = nullptr;
+    // In-store: the dependency entries of the owned slots, as loaded (dependant local << 32 | used
+    // global, tag). The owners of the `used` ends hold these entries in their rows; the owner of the
+    // dependant keeps its own copy so it can rebuild its pull lists (part_rebuild_lists) without an
+    // exchange whenever its node versions change.
+    uint64_t* in_keys = nullptr;
+    uint64_t* in_tags = nullptr;
+    uint64_t in_n = 0, in_cap = 0;
+    uint32_t* weight = nullptr;                // [n_global] live dependencies per slot (list order)
 };
 
 static PartState* ps(fgi_graph* g) { return reinterpret_cast<PartState*>(g->part); }
@@ -92,6 +100,9 @@ fgi_status part_destroy(fgi_graph* g) {
     hipFree(p->scalar);
     hipFree(p->v.front_global);
     hipFree(p->v.scratch_u64);
+    hipFree(p->in_keys);
+    hipFree(p->in_tags);
+    hipFree(p->weight);
     if (p->all_cnt_host) hipHostFree(p->all_cnt_host);
     if (p->scalar_host) hipHostFree(p->scalar_host);
     delete p;
@@ -296,43 +307,89 @@ __global__ void k_versions_local(uint32_t n, uint32_t base, uint64_t seed, unsig
     if (i < n) node[i] = synth_version(seed, base + i) | kW_Consistent;
 }
 
-__global__ void k_own_flags(uint64_t m, const uint64_t* __restrict__ keys, uint32_t base, uint32_t n_local,
-                            uint32_t* flag) {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < m) flag[e] = ((uint32_t)(keys[e] >> 32) - base) < n_local ? 1u : 0u;
-}
-
-__global__ void k_own_compact(uint64_t m, const uint64_t* __restrict__ keys, const uint32_t* __restrict__ flag,
-                              const uint32_t* __restrict__ pos, uint32_t base, uint64_t* out) {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < m && flag[e]) {
-        const uint64_t k = keys[e];
-        out[pos[e]] = ((uint64_t)((uint32_t)(k >> 32) - base) << 32) | (uint32_t)k;
+// Row-range R-MAT (fgi_part_synth_rmat): edge i is a pure function of i, so every rank walks the
+// global edge sequence and keeps only its share — the rows of the slots it owns (used == src) and the
+// dependency-list entries of the slots it owns (dependant == dst, not stale) — without materialising
+// the global edge list (at configs[2] that is 1.07G edges, 8.6 GB of keys per rank). Block b walks the
+// contiguous edges [b * per, (b + 1) * per). Pass 0 counts both shares per block and adds every live
+// edge to its dependant's weight (the list order: a slot's live dependencies over the whole graph);
+// pass 1 writes the shares at the blocks' exclusive offsets (wave ballots, LDS cursors).
+constexpr uint32_t kGenBlocks = 4096;
+__global__ __launch_bounds__(256) void k_rmat_part(uint64_t m, uint64_t per, uint32_t scale, uint64_t seed, uint32_t base,
+                                                   uint32_t n_local, uint32_t stale_pct, uint64_t stale_seed, int fill,
+                                                   unsigned long long* blk_cnt, const unsigned long long* blk_off,
+                                                   uint64_t* rows, uint64_t* ins, uint32_t* weight) {
+    __shared__ unsigned long long s_cur[2];
+    __shared__ unsigned long long s_red[2][4];
+    const uint64_t lo = (uint64_t)blockIdx.x * per, hi = lo + per < m ? lo + per : m;
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (fill && threadIdx.x < 2) s_cur[threadIdx.x] = blk_off[threadIdx.x * kGenBlocks + blockIdx.x];
+    __syncthreads();
+    unsigned long long nr = 0, ni = 0;
+    for (uint64_t i0 = lo; i0 < hi; i0 += blockDim.x) {   // block-uniform
+        const uint64_t i = i0 + threadIdx.x;
+        bool own_row = false, own_in = false;
+        uint32_t s = 0, d = 0;
+        if (i < hi) {
+            rmat_edge(i, scale, seed, &s, &d);
+            own_row = s - base < n_local;
+            const bool live = !synth_stale(stale_pct, stale_seed, s, d);
+            own_in = live && d - base < n_local;
+            if (!fill && live) atomicAdd(weight + d, 1u);
+        }
+        if (!fill) {
+            nr += own_row;
+            ni += own_in;
+            continue;
+        }
+        const unsigned long long mr = __ballot(own_row), mi = __ballot(own_in);
+        unsigned long long br = 0, bi = 0;
+        if (lane == 0) {
+            if (mr) br = atomicAdd(&s_cur[0], (unsigned long long)__popcll(mr));
+            if (mi) bi = atomicAdd(&s_cur[1], (unsigned long long)__popcll(mi));
+        }
+        br = __shfl(br, 0, 64);
+        bi = __shfl(bi, 0, 64);
+        const unsigned long long lt = (1ull << lane) - 1ull;
+        if (own_row) rows[br + __popcll(mr & lt)] = ((uint64_t)(s - base) << 32) | d;
+        if (own_in) ins[bi + __popcll(mi & lt)] = ((uint64_t)(d - base) << 32) | s;
+    }
+    if (fill) return;
+    for (int dd = 32; dd >= 1; dd >>= 1) {
+        nr += __shfl_xor(nr, dd, 64);
+        ni += __shfl_xor(ni, dd, 64);
+    }
+    if (lane == 0) {
+        s_red[0][wid] = nr;
+        s_red[1][wid] = ni;
+    }
+    __syncthreads();
+    if (threadIdx.x < 2) {
+        unsigned long long t = 0;
+        for (uint32_t q = 0; q < blockDim.x / 64; ++q) t += s_red[threadIdx.x][q];
+        blk_cnt[threadIdx.x * kGenBlocks + blockIdx.x] = t;
     }
 }
 
-// dependency lists of the owned slots from the global edge sequence: (dst_local << 32 | src_global)
-// for every non-stale edge whose dependant this rank owns
-__device__ __forceinline__ bool synth_stale(uint32_t stale_pct, uint64_t stale_seed, uint32_t src, uint32_t dst) {
-    return stale_pct && (sm64(stale_seed ^ sm64(((uint64_t)src << 32) | dst)) % 100) < stale_pct;
+__global__ void k_in_tags_synth(uint64_t m, const uint64_t* __restrict__ keys, uint32_t base, uint64_t seed,
+                                uint64_t* tags) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < m) tags[e] = synth_version(seed, (uint32_t)(keys[e] >> 32) + base);
 }
 
-__global__ void k_in_part_flags(uint64_t m, const uint64_t* __restrict__ keys, uint32_t base, uint32_t n_local,
-                                uint32_t stale_pct, uint64_t stale_seed, uint32_t* flag) {
+// the in-store's live entries (tag == version of the dependant's node): flag for the compaction
+__global__ void k_in_live(uint64_t m, const uint64_t* __restrict__ keys, const uint64_t* __restrict__ tags,
+                          const unsigned long long* __restrict__ node, uint32_t* flag) {
     const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= m) return;
-    const uint64_t k = keys[e];
-    const uint32_t src = (uint32_t)(k >> 32), dst = (uint32_t)k;
-    flag[e] = (dst - base < n_local && !synth_stale(stale_pct, stale_seed, src, dst)) ? 1u : 0u;
+    const uint64_t t = tags[e];
+    flag[e] = (t != 0 && (node[(uint32_t)(keys[e] >> 32)] & kVMask) == t) ? 1u : 0u;
 }
 
-__global__ void k_in_part_compact(uint64_t m, const uint64_t* __restrict__ keys, const uint32_t* __restrict__ flag,
-                                  const uint32_t* __restrict__ pos, uint32_t base, uint64_t* out) {
+__global__ void k_compact64(uint64_t m, const uint64_t* __restrict__ in, const uint32_t* __restrict__ flag,
+                            const uint32_t* __restrict__ pos, uint64_t* out) {
     const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < m && flag[e]) {
-        const uint64_t k = keys[e];
-        out[pos[e]] = ((uint64_t)((uint32_t)k - base) << 32) | (uint32_t)(k >> 32);
-    }
+    if (e < m && flag[e]) out[pos[e]] = in[e];
 }
 
 __global__ void k_in_part_unique(uint64_t m, const uint64_t* __restrict__ k, uint32_t* keep) {
@@ -350,63 +407,105 @@ __global__ void k_in_part_rows(uint64_t m, const uint64_t* __restrict__ k, const
     if (e + 1 == m || (uint32_t)(k[e + 1] >> 32) != d) len[d] = pos[e] + keep[e];   // row end, fixed below
 }
 
-// weight of a global slot for the list order: its non-stale dependencies in the global edge list
-__global__ void k_in_part_weight(uint64_t m, const uint64_t* __restrict__ keys, uint32_t stale_pct, uint64_t stale_seed,
-                                 uint32_t* w) {
-    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= m) return;
-    const uint64_t k = keys[e];
-    const uint32_t src = (uint32_t)(k >> 32), dst = (uint32_t)k;
-    if (!synth_stale(stale_pct, stale_seed, src, dst)) atomicAdd(w + dst, 1u);
-}
-
 __global__ void k_in_part_fix(uint32_t n, const uint64_t* __restrict__ off, uint32_t* len) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d < n && len[d]) len[d] -= (uint32_t)off[d];
 }
 
-}  // namespace
+// fgi_part_register_nodes: every listed slot's version goes into the replica; the owner installs the
+// node (as fgi_register_nodes: the slot must be empty)
+__global__ void k_part_register(uint32_t n, const uint32_t* __restrict__ slot, const uint64_t* __restrict__ version,
+                                const uint32_t* __restrict__ flags, uint32_t base, uint32_t n_local, uint64_t* ver_all,
+                                unsigned long long* node, uint32_t* row_len, unsigned long long* err) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t s = slot[i];
+    const uint64_t v = version[i];
+    ver_all[s] = v;
+    const uint32_t h = s - base;
+    if (h >= n_local) return;
+    if (word_is_current(node[h])) {
+        atomicAdd(err, 1ull);
+        return;
+    }
+    node[h] = v ? flags_to_word(v, flags ? flags[i] : FGI_CONSISTENT) : 0ull;
+    row_len[h] = 0;
+}
 
-fgi_status synth_rmat_keys(fgi_graph* g, uint32_t scale, uint32_t edge_factor, uint64_t seed, uint64_t** keys,
-                           uint64_t* m);
+// fgi_part_load_edges: every edge of the batch that is live when loaded adds to its dependant's weight
+__global__ void k_part_weight(uint64_t m, const uint32_t* __restrict__ dep, const uint64_t* __restrict__ tag,
+                              const uint64_t* __restrict__ ver_all, uint32_t* weight) {
+    const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (e < m && tag[e] == ver_all[dep[e]]) atomicAdd(weight + dep[e], 1u);
+}
 
-// Builds g->uin_* for the owned slots from the global keys. flag/pos are caller scratch of m
-// entries; *tmp is a scan scratch the caller frees.
-static fgi_status part_build_in_lists(fgi_graph* g, const uint64_t* keys, uint64_t m, uint32_t stale_pct,
-                                      uint64_t stale_seed, uint32_t* flag, uint32_t* pos, void** tmp) {
-    PartState* p = ps(g);
+inline uint32_t nblk(uint64_t n) { return (uint32_t)((n + 255) / 256); }
+
+// exclusive scan of flag[0, m) into pos; returns the total (synchronises the stream)
+fgi_status scan_flags(fgi_graph* g, const uint32_t* flag, uint32_t* pos, uint64_t m, uint64_t* total) {
     hipStream_t s = g->stream;
-    const uint32_t nb = (uint32_t)((m + 255) / 256);
-    hipLaunchKernelGGL(k_in_part_flags, dim3(nb), dim3(256), 0, s, m, keys, p->v.base, p->v.n_local, stale_pct,
-                       stale_seed, flag);
     size_t tb = 0;
     rocprim::exclusive_scan(nullptr, tb, flag, pos, 0u, (size_t)m, rocprim::plus<uint32_t>(), s);
-    hipFree(*tmp);
-    *tmp = nullptr;
-    FGI_HIP(g, hipMalloc(tmp, tb));
-    rocprim::exclusive_scan(*tmp, tb, flag, pos, 0u, (size_t)m, rocprim::plus<uint32_t>(), s);
+    void* tmp = nullptr;
+    FGI_HIP(g, hipMalloc(&tmp, std::max<size_t>(tb, 16)));
+    rocprim::exclusive_scan(tmp, tb, flag, pos, 0u, (size_t)m, rocprim::plus<uint32_t>(), s);
     uint32_t lp = 0, lf = 0;
-    FGI_HIP(g, hipMemcpyAsync(&lp, pos + m - 1, 4, hipMemcpyDeviceToHost, s));
-    FGI_HIP(g, hipMemcpyAsync(&lf, flag + m - 1, 4, hipMemcpyDeviceToHost, s));
-    FGI_HIP(g, hipStreamSynchronize(s));
-    const uint64_t mi = (uint64_t)lp + lf;
+    hipMemcpyAsync(&lp, pos + m - 1, 4, hipMemcpyDeviceToHost, s);
+    hipMemcpyAsync(&lf, flag + m - 1, 4, hipMemcpyDeviceToHost, s);
+    const hipError_t e = hipStreamSynchronize(s);
+    hipFree(tmp);
+    FGI_HIP(g, e);
+    *total = (uint64_t)lp + lf;
+    return FGI_OK;
+}
+
+}  // namespace
+
+// The owned slots' dependency lists (pull levels) from the in-store: its live entries (tag == the
+// owned dependant node's version: the reference's d._used, Computed.cs:365-366) sorted and
+// deduplicated into lists of global used ids, each ordered by the entries' weights (as the single
+// engine: most-depended-on first), then the heads and the pull candidates. Local to the rank.
+static fgi_status part_rebuild_lists(fgi_graph* g) {
+    PartState* p = ps(g);
+    hipStream_t s = g->stream;
+    const uint64_t m = p->in_n;
+    g->uin_epoch = 0;
+    if (p->v.block % 32 != 0) return FGI_OK;   // pull levels all-gather whole bitmap words per rank
     FGI_HIP(g, hipMemsetAsync(g->uin_len, 0, (size_t)g->n_slots * 4, s));
     FGI_HIP(g, hipMemsetAsync(g->uin_off, 0, (size_t)g->n_slots * 8, s));
-    if (mi == 0) {
-        if (!g->uin_src) FGI_HIP(g, hipMalloc(&g->uin_src, 1024 * 4));
-        return build_in_heads(g);
+    if (!g->uin_src) {
+        FGI_HIP(g, hipMalloc(&g->uin_src, 1024 * 4));
+        g->uin_cap = 1024;
     }
+    uint32_t *flag = nullptr, *pos = nullptr, *keep = nullptr, *kpos = nullptr;
     uint64_t *k1 = nullptr, *k2 = nullptr;
-    uint32_t *keep = nullptr, *kpos = nullptr;
     void* st = nullptr;
     fgi_status rc = FGI_OK;
+    uint64_t mi = 0;
     do {
+        if (m) {
+            if (hipMalloc(&flag, m * 4) != hipSuccess || hipMalloc(&pos, m * 4) != hipSuccess) {
+                rc = set_err(g, FGI_ENOMEM, "dependency-list build buffers");
+                break;
+            }
+            hipLaunchKernelGGL(k_in_live, dim3(nblk(m)), dim3(256), 0, s, m, p->in_keys, p->in_tags,
+                               reinterpret_cast<const unsigned long long*>(g->node), flag);
+            rc = scan_flags(g, flag, pos, m, &mi);
+            if (rc != FGI_OK) break;
+        }
+        if (mi == 0) {
+            rc = build_in_heads(g);
+            break;
+        }
         if (hipMalloc(&k1, mi * 8) != hipSuccess || hipMalloc(&k2, mi * 8) != hipSuccess ||
             hipMalloc(&keep, mi * 4) != hipSuccess || hipMalloc(&kpos, mi * 4) != hipSuccess) {
             rc = set_err(g, FGI_ENOMEM, "dependency-list build buffers");
             break;
         }
-        hipLaunchKernelGGL(k_in_part_compact, dim3(nb), dim3(256), 0, s, m, keys, flag, pos, p->v.base, k1);
+        hipLaunchKernelGGL(k_compact64, dim3(nblk(m)), dim3(256), 0, s, m, p->in_keys, flag, pos, k1);
+        hipFree(flag);
+        hipFree(pos);
+        flag = pos = nullptr;
         size_t sb = 0;
         rocprim::radix_sort_keys(nullptr, sb, k1, k2, (size_t)mi, 0, 64, s);
         if (hipMalloc(&st, std::max(sb, (size_t)16)) != hipSuccess) {
@@ -414,23 +513,11 @@ static fgi_status part_build_in_lists(fgi_graph* g, const uint64_t* keys, uint64
             break;
         }
         rocprim::radix_sort_keys(st, sb, k1, k2, (size_t)mi, 0, 64, s);
-        const uint32_t nb2 = (uint32_t)((mi + 255) / 256);
-        hipLaunchKernelGGL(k_in_part_unique, dim3(nb2), dim3(256), 0, s, mi, k2, keep);
-        size_t tb2 = 0;
-        rocprim::exclusive_scan(nullptr, tb2, keep, kpos, 0u, (size_t)mi, rocprim::plus<uint32_t>(), s);
-        hipFree(st);
-        st = nullptr;
-        if (hipMalloc(&st, std::max(tb2, (size_t)16)) != hipSuccess) {
-            rc = set_err(g, FGI_ENOMEM, "scan temp");
-            break;
-        }
-        rocprim::exclusive_scan(st, tb2, keep, kpos, 0u, (size_t)mi, rocprim::plus<uint32_t>(), s);
-        uint32_t a = 0, b = 0;
-        hipMemcpyAsync(&a, kpos + mi - 1, 4, hipMemcpyDeviceToHost, s);
-        hipMemcpyAsync(&b, keep + mi - 1, 4, hipMemcpyDeviceToHost, s);
-        hipStreamSynchronize(s);
-        const uint64_t total = (uint64_t)a + b;
-        if (total > g->uin_cap || !g->uin_src) {
+        hipLaunchKernelGGL(k_in_part_unique, dim3(nblk(mi)), dim3(256), 0, s, mi, k2, keep);
+        uint64_t total = 0;
+        rc = scan_flags(g, keep, kpos, mi, &total);
+        if (rc != FGI_OK) break;
+        if (total > g->uin_cap) {
             hipFree(g->uin_src);
             g->uin_src = nullptr;
             if (hipMalloc(&g->uin_src, std::max<uint64_t>(total, 1024) * 4) != hipSuccess) {
@@ -439,32 +526,66 @@ static fgi_status part_build_in_lists(fgi_graph* g, const uint64_t* keys, uint64
             }
             g->uin_cap = std::max<uint64_t>(total, 1024);
         }
-        hipLaunchKernelGGL(k_in_part_rows, dim3(nb2), dim3(256), 0, s, mi, k2, keep, kpos, g->uin_src, g->uin_off,
+        hipLaunchKernelGGL(k_in_part_rows, dim3(nblk(mi)), dim3(256), 0, s, mi, k2, keep, kpos, g->uin_src, g->uin_off,
                            g->uin_len);
-        hipLaunchKernelGGL(k_in_part_fix, dim3((g->n_slots + 255) / 256), dim3(256), 0, s, g->n_slots, g->uin_off,
-                           g->uin_len);
-        // as the single engine (build_in_lists): every list by its entries' own dependency counts,
-        // which every rank counts over the global edge list it holds
-        uint32_t* w = nullptr;
-        if (hipMalloc(&w, (size_t)p->v.n_global * 4) != hipSuccess) {
-            rc = set_err(g, FGI_ENOMEM, "list weights");
-            break;
-        }
-        hipMemsetAsync(w, 0, (size_t)p->v.n_global * 4, s);
-        hipLaunchKernelGGL(k_in_part_weight, dim3(nb), dim3(256), 0, s, m, keys, stale_pct, stale_seed, w);
-        rc = sort_in_lists(g, total, w, p->v.n_global);
-        hipFree(w);
+        hipLaunchKernelGGL(k_in_part_fix, dim3(nblk(g->n_slots)), dim3(256), 0, s, g->n_slots, g->uin_off, g->uin_len);
+        rc = sort_in_lists(g, total, p->weight, p->v.n_global);
         if (rc != FGI_OK) break;
         rc = build_in_heads(g);
         if (rc != FGI_OK) break;
         if (hipStreamSynchronize(s) != hipSuccess) rc = set_err(g, FGI_EDEVICE, "dependency-list build");
     } while (0);
+    hipFree(flag);
+    hipFree(pos);
     hipFree(k1);
     hipFree(k2);
     hipFree(keep);
     hipFree(kpos);
     hipFree(st);
+    if (rc == FGI_OK) g->uin_epoch = g->mut_epoch;   // rows, versions and lists agree
     return rc;
+}
+
+fgi_status part_ensure_lists(fgi_graph* g) {
+    PartState* p = ps(g);
+    if (!p || g->uin_epoch == g->mut_epoch || p->in_n == 0) return FGI_OK;
+    return part_rebuild_lists(g);
+}
+
+// append m device entries (keys: dependant local << 32 | used global, tags) to the in-store
+static fgi_status part_store_in(fgi_graph* g, const uint64_t* keys, const uint64_t* tags, uint64_t m) {
+    PartState* p = ps(g);
+    if (m == 0) return FGI_OK;
+    if (p->in_n + m > p->in_cap) {
+        const uint64_t cap = std::max<uint64_t>(p->in_n + m, p->in_cap + p->in_cap / 2);
+        uint64_t *nk = nullptr, *nt = nullptr;
+        if (hipMalloc(&nk, cap * 8) != hipSuccess || hipMalloc(&nt, cap * 8) != hipSuccess) {
+            hipFree(nk);
+            return set_err(g, FGI_ENOMEM, "dependency-entry store");
+        }
+        if (p->in_n) {
+            FGI_HIP(g, hipMemcpyAsync(nk, p->in_keys, p->in_n * 8, hipMemcpyDeviceToDevice, g->stream));
+            FGI_HIP(g, hipMemcpyAsync(nt, p->in_tags, p->in_n * 8, hipMemcpyDeviceToDevice, g->stream));
+            FGI_HIP(g, hipStreamSynchronize(g->stream));
+        }
+        hipFree(p->in_keys);
+        hipFree(p->in_tags);
+        p->in_keys = nk;
+        p->in_tags = nt;
+        p->in_cap = cap;
+    }
+    FGI_HIP(g, hipMemcpyAsync(p->in_keys + p->in_n, keys, m * 8, hipMemcpyDefault, g->stream));
+    FGI_HIP(g, hipMemcpyAsync(p->in_tags + p->in_n, tags, m * 8, hipMemcpyDefault, g->stream));
+    FGI_HIP(g, hipStreamSynchronize(g->stream));
+    p->in_n += m;
+    return FGI_OK;
+}
+
+static void part_clear_store(PartState* p) {
+    hipFree(p->in_keys);
+    hipFree(p->in_tags);
+    p->in_keys = p->in_tags = nullptr;
+    p->in_n = p->in_cap = 0;
 }
 
 }  // namespace fgi
@@ -542,6 +663,8 @@ static fgi_status part_alloc(fgi_graph* g, uint32_t n_global) {
     if (hipMalloc(&p->v.front_global, p->v.front_words_global * 4) != hipSuccess) return fail("frontier bitmap");
     if (hipMemset(p->v.front_global, 0, p->v.front_words_global * 4) != hipSuccess) return fail("frontier bitmap");
     if (hipMalloc(&p->v.scratch_u64, 32) != hipSuccess) return fail("scratch");
+    if (hipMalloc(&p->weight, (size_t)n_global * 4) != hipSuccess) return fail("list weights");
+    if (hipMemset(p->weight, 0, (size_t)n_global * 4) != hipSuccess) return fail("list weights");
     if (hipHostMalloc(reinterpret_cast<void**>(&p->all_cnt_host), (size_t)W * (W + 2) * 8) != hipSuccess)
         return fail("host");
     if (hipHostMalloc(reinterpret_cast<void**>(&p->scalar_host), 32) != hipSuccess) return fail("host");
@@ -626,72 +749,163 @@ fgi_status fgi_part_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_facto
                                                          p->v.n_global);
     hipSetDevice(g->device);
     hipStream_t s = g->stream;
-    const uint32_t N = p->v.n_global;
+    const uint32_t N = p->v.n_global, base = p->v.base, nl = p->v.n_local;
     FGI_HIP(g, hipMemsetAsync(g->node, 0, (size_t)g->n_handles * 8, s));
     FGI_HIP(g, hipMemsetAsync(g->vis_bm, 0, g->bm_words * 4, s));   // a new node table
     g->v_dirty = false;
     g->vis_stale = false;
     note_words(g);
-    hipLaunchKernelGGL(k_versions_local, dim3((p->v.n_local + 255) / 256), dim3(256), 0, s, p->v.n_local, p->v.base,
-                       seed, reinterpret_cast<unsigned long long*>(g->node));
+    hipLaunchKernelGGL(k_versions_local, dim3((nl + 255) / 256), dim3(256), 0, s, nl, base, seed,
+                       reinterpret_cast<unsigned long long*>(g->node));
     hipLaunchKernelGGL(k_versions_all, dim3((N + 255) / 256), dim3(256), 0, s, N, seed, p->v.ver_all);
-    // every rank generates the global edge sequence and keeps the rows of the slots it owns
-    uint64_t* keys = nullptr;
-    uint64_t m = 0;
-    FGI_TRY(synth_rmat_keys(g, scale, edge_factor, seed, &keys, &m));
-    uint32_t *flag = nullptr, *pos = nullptr;
-    uint64_t* own = nullptr;
-    void* tmp = nullptr;
+    part_clear_store(p);
+    FGI_HIP(g, hipMemsetAsync(p->weight, 0, (size_t)N * 4, s));
+    // the rank's rows and dependency entries, generated by edge-index range (k_rmat_part)
+    const uint64_t m = (uint64_t)edge_factor << scale;
+    const uint64_t per = (m + kGenBlocks - 1) / kGenBlocks;
+    unsigned long long *cnt = nullptr, *off = nullptr;
+    uint64_t *rows = nullptr, *ins = nullptr, *tags = nullptr;
     auto cleanup = [&]() {
-        hipFree(keys);
-        hipFree(flag);
-        hipFree(pos);
-        hipFree(own);
-        hipFree(tmp);
+        hipFree(cnt);
+        hipFree(off);
+        hipFree(rows);
+        hipFree(ins);
+        hipFree(tags);
     };
     fgi_status st = FGI_OK;
     do {
-        if (hipMalloc(&flag, m * 4) != hipSuccess || hipMalloc(&pos, m * 4) != hipSuccess) {
-            st = set_err(g, FGI_ENOMEM, "partition filter buffers");
+        if (hipMalloc(&cnt, 2 * kGenBlocks * 8) != hipSuccess || hipMalloc(&off, 2 * kGenBlocks * 8) != hipSuccess) {
+            st = set_err(g, FGI_ENOMEM, "generator counts");
             break;
         }
-        const uint32_t nb = (uint32_t)((m + 255) / 256);
-        hipLaunchKernelGGL(k_own_flags, dim3(nb), dim3(256), 0, s, m, keys, p->v.base, p->v.n_local, flag);
-        size_t tb = 0;
-        rocprim::exclusive_scan(nullptr, tb, flag, pos, 0u, (size_t)m, rocprim::plus<uint32_t>(), s);
-        if (hipMalloc(&tmp, tb) != hipSuccess) {
-            st = set_err(g, FGI_ENOMEM, "scan temp");
+        hipLaunchKernelGGL(k_rmat_part, dim3(kGenBlocks), dim3(256), 0, s, m, per, scale, seed, base, nl, stale_pct,
+                           stale_seed, 0, cnt, (const unsigned long long*)nullptr, (uint64_t*)nullptr, (uint64_t*)nullptr,
+                           p->weight);
+        std::vector<unsigned long long> hc(2 * kGenBlocks), ho(2 * kGenBlocks);
+        if (hipMemcpyAsync(hc.data(), cnt, hc.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            st = set_err(g, FGI_EDEVICE, "generator count pass");
             break;
         }
-        rocprim::exclusive_scan(tmp, tb, flag, pos, 0u, (size_t)m, rocprim::plus<uint32_t>(), s);
-        uint32_t lp = 0, lf = 0;
-        hipMemcpyAsync(&lp, pos + m - 1, 4, hipMemcpyDeviceToHost, s);
-        hipMemcpyAsync(&lf, flag + m - 1, 4, hipMemcpyDeviceToHost, s);
-        hipStreamSynchronize(s);
-        const uint64_t mo = (uint64_t)lp + lf;
-        if (hipMalloc(&own, (mo ? mo : 1) * 8) != hipSuccess) {
-            st = set_err(g, FGI_ENOMEM, "owned keys");
+        uint64_t tot[2] = {0, 0};
+        for (int c = 0; c < 2; ++c)
+            for (uint32_t b = 0; b < kGenBlocks; ++b) {
+                ho[c * kGenBlocks + b] = tot[c];
+                tot[c] += hc[c * kGenBlocks + b];
+            }
+        const uint64_t mo = tot[0], mi = tot[1];
+        if (hipMalloc(&rows, std::max<uint64_t>(mo, 1) * 8) != hipSuccess ||
+            hipMalloc(&ins, std::max<uint64_t>(mi, 1) * 8) != hipSuccess ||
+            hipMalloc(&tags, std::max<uint64_t>(mi, 1) * 8) != hipSuccess) {
+            st = set_err(g, FGI_ENOMEM, "owned edges");
             break;
         }
-        hipLaunchKernelGGL(k_own_compact, dim3(nb), dim3(256), 0, s, m, keys, flag, pos, p->v.base, own);
+        FGI_HIP(g, hipMemcpyAsync(off, ho.data(), ho.size() * 8, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_rmat_part, dim3(kGenBlocks), dim3(256), 0, s, m, per, scale, seed, base, nl, stale_pct,
+                           stale_seed, 1, cnt, (const unsigned long long*)off, rows, ins, (uint32_t*)nullptr);
+        if (mi) hipLaunchKernelGGL(k_in_tags_synth, dim3(nblk(mi)), dim3(256), 0, s, mi, ins, base, seed, tags);
         if (hipStreamSynchronize(s) != hipSuccess) {
-            st = set_err(g, FGI_EDEVICE, "partition filter");
+            st = set_err(g, FGI_EDEVICE, "generator fill pass");
             break;
         }
-        // dependency lists of the owned slots (pull levels), while the global keys are at hand
-        if (p->v.block % 32 == 0) {
-            st = part_build_in_lists(g, keys, m, stale_pct, stale_seed, flag, pos, &tmp);
-            if (st != FGI_OK) break;
-        }
-        hipFree(keys);
-        keys = nullptr;
-        st = build_rows_from_keys(g, mo, own, nullptr, seed, stale_pct, stale_seed, p->v.base, p->v.base);
-        // the pull candidates carry row lengths: (re)built once the rows exist
-        if (st == FGI_OK && p->v.block % 32 == 0) st = build_candidates(g);
-        g->uin_epoch = (p->v.block % 32 == 0) ? g->mut_epoch : 0;   // rows and lists of one edge set
+        hipFree(cnt);
+        hipFree(off);
+        cnt = off = nullptr;
+        // rows: (owned used << 32 | global dependant), tags synthesised from global ids
+        st = build_rows_from_keys(g, mo, rows, nullptr, seed, stale_pct, stale_seed, base, base);
+        if (st != FGI_OK) break;
+        hipFree(rows);
+        rows = nullptr;
+        st = part_store_in(g, ins, tags, mi);
+        if (st != FGI_OK) break;
+        st = part_rebuild_lists(g);
     } while (0);
     cleanup();
     return st;
+}
+
+fgi_status fgi_part_register_nodes(fgi_graph* g, uint32_t n, const uint32_t* slot, const uint64_t* version,
+                                   const uint32_t* state_flags) {
+    if (!g || (n && (!slot || !version))) return FGI_EINVAL;
+    if (!g->part) return set_err(g, FGI_ESTATE, "fgi_part_register_nodes: partition not initialised");
+    PartState* p = ps(g);
+    for (uint32_t i = 0; i < n; ++i) {
+        if (slot[i] >= p->v.n_global) return set_err(g, FGI_EINVAL, "slot %u out of range", slot[i]);
+        if (version[i] > kVMask) return set_err(g, FGI_EINVAL, "version of slot %u exceeds 2^56-1", slot[i]);
+        if (state_flags && (state_flags[i] & 3u) == 3u) return set_err(g, FGI_EINVAL, "bad state for slot %u", slot[i]);
+    }
+    if (n == 0) return FGI_OK;
+    hipSetDevice(g->device);
+    hipStream_t s = g->stream;
+    FGI_TRY(fold(g));
+    uint32_t *ds = nullptr, *df = nullptr;
+    uint64_t* dv = nullptr;
+    fgi_status st = FGI_OK;
+    if (hipMalloc(&ds, (size_t)n * 4) != hipSuccess || hipMalloc(&dv, (size_t)n * 8) != hipSuccess ||
+        (state_flags && hipMalloc(&df, (size_t)n * 4) != hipSuccess)) {
+        st = set_err(g, FGI_ENOMEM, "register buffers");
+    } else {
+        hipMemcpyAsync(ds, slot, (size_t)n * 4, hipMemcpyHostToDevice, s);
+        hipMemcpyAsync(dv, version, (size_t)n * 8, hipMemcpyHostToDevice, s);
+        if (df) hipMemcpyAsync(df, state_flags, (size_t)n * 4, hipMemcpyHostToDevice, s);
+        hipMemsetAsync(p->scalar, 0, 8, s);
+        hipLaunchKernelGGL(k_part_register, dim3(nblk(n)), dim3(256), 0, s, n, ds, dv, df, p->v.base, p->v.n_local,
+                           p->v.ver_all, reinterpret_cast<unsigned long long*>(g->node), g->row_len, p->scalar);
+        unsigned long long bad = 0;
+        hipMemcpyAsync(&bad, p->scalar, 8, hipMemcpyDeviceToHost, s);
+        if (hipStreamSynchronize(s) != hipSuccess) st = set_err(g, FGI_EDEVICE, "register");
+        else if (bad) st = set_err(g, FGI_ESTATE, "%llu owned slots already had a current node", bad);
+    }
+    hipFree(ds);
+    hipFree(dv);
+    hipFree(df);
+    touch(g);          // versions changed: the pull lists are rebuilt before the next wave
+    note_words(g);
+    return st;
+}
+
+fgi_status fgi_part_load_edges(fgi_graph* g, uint64_t m, const uint32_t* used, const uint32_t* dependant,
+                               const uint64_t* tag) {
+    if (!g || (m && (!used || !dependant || !tag))) return FGI_EINVAL;
+    if (!g->part) return set_err(g, FGI_ESTATE, "fgi_part_load_edges: partition not initialised");
+    PartState* p = ps(g);
+    const uint32_t base = p->v.base, nl = p->v.n_local, N = p->v.n_global;
+    std::vector<uint64_t> rk, rt, ik, it;
+    for (uint64_t e = 0; e < m; ++e) {
+        if (used[e] >= N || dependant[e] >= N)
+            return set_err(g, FGI_EINVAL, "edge %llu out of range", (unsigned long long)e);
+        if (tag[e] == 0) return set_err(g, FGI_EINVAL, "edge %llu has tag 0 (LTags are positive)", (unsigned long long)e);
+        if (used[e] - base < nl) {   // a row this rank owns: (local used, global dependant)
+            rk.push_back(((uint64_t)(used[e] - base) << 32) | dependant[e]);
+            rt.push_back(tag[e]);
+        }
+        if (dependant[e] - base < nl) {   // a dependency entry of a slot this rank owns
+            ik.push_back(((uint64_t)(dependant[e] - base) << 32) | used[e]);
+            it.push_back(tag[e]);
+        }
+    }
+    hipSetDevice(g->device);
+    hipStream_t s = g->stream;
+    FGI_TRY(load_rows(g, rk.size(), rk.data(), rt.data(), base, base));
+    // list weights: every rank sees the whole batch (and every version, ver_all)
+    if (m) {
+        uint32_t* dd = nullptr;
+        uint64_t* dt = nullptr;
+        fgi_status st = FGI_OK;
+        if (hipMalloc(&dd, m * 4) != hipSuccess || hipMalloc(&dt, m * 8) != hipSuccess) {
+            st = set_err(g, FGI_ENOMEM, "weight buffers");
+        } else {
+            hipMemcpyAsync(dd, dependant, m * 4, hipMemcpyHostToDevice, s);
+            hipMemcpyAsync(dt, tag, m * 8, hipMemcpyHostToDevice, s);
+            hipLaunchKernelGGL(k_part_weight, dim3(nblk(m)), dim3(256), 0, s, m, dd, dt, p->v.ver_all, p->weight);
+            if (hipStreamSynchronize(s) != hipSuccess) st = set_err(g, FGI_EDEVICE, "weights");
+        }
+        hipFree(dd);
+        hipFree(dt);
+        FGI_TRY(st);
+    }
+    FGI_TRY(part_store_in(g, ik.data(), it.data(), ik.size()));
+    return part_rebuild_lists(g);
 }
 
 fgi_status fgi_part_invalidate(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,

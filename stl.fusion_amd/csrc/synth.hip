@@ -8,20 +8,6 @@
 namespace fgi {
 namespace {
 
-__device__ __forceinline__ uint32_t scramble(uint64_t x, uint32_t scale, uint64_t seed) {
-    const uint64_t mask = (scale >= 64) ? ~0ull : ((1ull << scale) - 1);
-    const uint64_t k1 = sm64(seed ^ 0xA5A5A5A5A5A5A5A5ull) | 1ull;
-    const uint64_t k2 = sm64(seed ^ 0x5A5A5A5A5A5A5A5Aull) | 1ull;
-    const uint64_t c = sm64(seed ^ 0x0123456789ABCDEFull);
-    const uint32_t s1 = (scale + 1) / 2, s2 = scale / 2 ? scale / 2 : 1;
-    x = (x * k1) & mask;
-    x ^= x >> s1;
-    x = (x + c) & mask;
-    x = (x * k2) & mask;
-    x ^= x >> s2;
-    return (uint32_t)x;
-}
-
 __global__ void k_versions(uint32_t n, uint64_t seed, unsigned long long* node) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     if (s < n) node[s] = synth_version(seed, s) | kW_Consistent;
@@ -49,24 +35,10 @@ __global__ void k_gen_layered(uint32_t levels, uint32_t width, uint32_t fanout, 
 }
 
 __global__ void k_gen_rmat(uint64_t m, uint32_t scale, uint64_t seed, uint64_t* keys) {
-    const uint64_t one = 1ull << 53;
-    const uint64_t tA = one / 100 * 57, tAB = one / 100 * 76, tABC = one / 100 * 95;
-    const uint64_t ks = sm64(seed);
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
-        uint64_t s = 0, d = 0;
-        for (uint32_t l = 0; l < scale; ++l) {
-            const uint64_t u = sm64(ks ^ ((i << 6) | l)) >> 11;
-            const uint64_t bit = 1ull << (scale - 1 - l);
-            if (u >= tA) {
-                if (u < tAB) d |= bit;
-                else if (u < tABC) s |= bit;
-                else {
-                    s |= bit;
-                    d |= bit;
-                }
-            }
-        }
-        keys[i] = ((uint64_t)scramble(s, scale, seed) << 32) | scramble(d, scale, seed);
+        uint32_t s, d;
+        rmat_edge(i, scale, seed, &s, &d);
+        keys[i] = ((uint64_t)s << 32) | d;
     }
 }
 

@@ -2109,6 +2109,7 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     if (!part_view(g, &pv)) return set_err(g, FGI_ESTATE, "partition not initialised");
     const auto t0 = std::chrono::steady_clock::now();
     hipStream_t s = g->stream;
+    FGI_TRY(part_ensure_lists(g));
     FGI_TRY(ensure_cstart(g, g->pool_top));
     FGI_TRY(ensure_cls(g));
     // one rank: nothing is remote, the collectives are identities (skipped unless FGI_OPT_PART_COLLECTIVES)

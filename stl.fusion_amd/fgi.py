@@ -126,6 +126,8 @@ SIGNATURES = {
     "fgi_part_unique_id": [_u8p],
     "fgi_part_init": [_G, C.c_uint32, _u8p],
     "fgi_part_synth_rmat": [_G, C.c_uint32, C.c_uint32, C.c_uint64, C.c_uint32, C.c_uint64],
+    "fgi_part_register_nodes": [_G, C.c_uint32, _u32p, _u64p, _u32p],
+    "fgi_part_load_edges": [_G, C.c_uint64, _u32p, _u32p, _u64p],
     "fgi_part_invalidate": [_G, C.c_uint32, C.c_void_p, C.c_void_p, _u64p, C.POINTER(WaveStats)],
     "fgi_part_export_ids": [_G, _u32p, C.c_uint64, _u64p],
     "fgi_part_init_local": [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32],
@@ -465,6 +467,19 @@ class Graph:
     def part_synth_rmat(self, scale, edge_factor, seed, stale_pct=0, stale_seed=0):
         self._check(self.lib.fgi_part_synth_rmat(self.h, scale, edge_factor, seed, stale_pct, stale_seed),
                     "part_synth_rmat")
+
+    def part_register_nodes(self, slots, versions, state_flags=None):
+        """fgi_part_register_nodes: global slot ids; every rank gets the same list."""
+        s, v = _u32(slots), _u64(versions)
+        f = None if state_flags is None else _u32(state_flags)
+        self._check(self.lib.fgi_part_register_nodes(self.h, len(s), _ptr(s, C.c_uint32), _ptr(v, C.c_uint64),
+                                                     _ptr(f, C.c_uint32)), "part_register_nodes")
+
+    def part_load_edges(self, used, dependant, tags):
+        """fgi_part_load_edges: global ids; every rank gets the same batch."""
+        u, d, t = _u32(used), _u32(dependant), _u64(tags)
+        self._check(self.lib.fgi_part_load_edges(self.h, len(u), _ptr(u, C.c_uint32), _ptr(d, C.c_uint32),
+                                                 _ptr(t, C.c_uint64)), "part_load_edges")
 
     def part_invalidate(self, n_roots: int, roots_ptr: int, imm_ptr: int = 0,
                         stats: Optional[WaveStats] = None) -> int:

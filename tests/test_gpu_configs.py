@@ -169,3 +169,38 @@ def test_configs2_rmat27_single_gpu_wave(pkg, rmat27):
     assert all(np.array_equal(sets[0], x) for x in sets[1:])
     assert 40_000_000 < len(sets[0]) < 43_000_000   # 41.3M
     g.set_option(pkg.fgi.OPT_DIRECTION, 0)
+
+
+def test_configs2_rmat27_eight_partitions_match_single_engine(pkg, rmat27):
+    """configs[2] as the multi-GPU engine runs it: 8 vertex-range partitions of the R-MAT 27 graph
+    (each generated by row range, fgi_part_synth_rmat), driven in one process by run_part_wave's
+    level loop on 8 host threads (fgi_part_local_invalidate: device copies for the collectives),
+    against the single engine on the same graph and roots — the same invalidated set, V_inv, E_trav
+    and final node words, slot by slot."""
+    from stl_fusion_amd import workloads as W
+    g, roots, edges, m = rmat27
+    cfg = W.CONFIGS["rmat27"]
+    n = W.n_slots(cfg)
+    g.restore()
+    g.set_option(pkg.fgi.OPT_DIRECTION, 0)
+    ws = pkg.WaveStats()
+    ids1 = np.sort(g.invalidate(roots, stats=ws))
+    v1, f1 = g.dump_states()
+    P = 8
+    block = -(-n // P)
+    gs = [pkg.Graph(block, rank=r, world=P) for r in range(P)]
+    pkg.fgi.part_init_local(gs, n)
+    for x in gs:
+        x.part_synth_rmat(cfg["scale"], cfg["edge_factor"], cfg["seed"])
+    assert sum(x.degrees()[1] for x in gs) == m   # the rows of the 8 ranks are the whole edge set
+    stats = pkg.fgi.part_local_invalidate(gs, roots)
+    ids = np.sort(np.concatenate([x.part_export_ids() for x in gs]))
+    assert np.array_equal(ids, ids1), (len(ids), len(ids1))
+    assert sum(s.v_inv for s in stats) == ws.v_inv and sum(s.e_trav for s in stats) == ws.e_trav
+    assert sum(s.pull_levels for s in stats) > 0 and sum(s.remote_msgs for s in stats) > 0
+    for r, x in enumerate(gs):
+        v, f = x.dump_states()
+        lo, hi = r * block, min(n, (r + 1) * block)
+        assert np.array_equal(v[:hi - lo], v1[lo:hi]) and np.array_equal(f[:hi - lo], f1[lo:hi]), r
+    for x in gs:
+        x.close()
