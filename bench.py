@@ -131,6 +131,16 @@ def profiled_traffic(kname, config_scale, live_avg_ms):
     return None, "no matching profiles/*_summary.json"
 
 
+
+def dump_maps():
+    """FGI_MAPS_OUT=<file>: this process's /proc/self/maps (every library mapped by now), so the PCs of
+    a crash at exit (e.g. under rocprofv3) can be mapped to libraries and symbols."""
+    path = os.environ.get("FGI_MAPS_OUT")
+    if path:
+        with open("/proc/self/maps") as src, open(path, "w") as dst:
+            dst.write(src.read())
+
+
 def main():
     # Libraries (RCCL prints a banner on communicator init) must not write to stdout: the driver
     # reads exactly one JSON line from it. Route fd 1 to stderr and keep a handle on the real one.
@@ -440,3 +450,4 @@ def main():
 
 if __name__ == "__main__":
     main()
+    dump_maps()

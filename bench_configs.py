@@ -256,6 +256,16 @@ def run_stream(pkg, W, args):
     return out
 
 
+
+def dump_maps():
+    """FGI_MAPS_OUT=<file>: this process's /proc/self/maps (every library mapped by now), so the PCs of
+    a crash at exit (e.g. under rocprofv3) can be mapped to libraries and symbols."""
+    path = os.environ.get("FGI_MAPS_OUT")
+    if path:
+        with open("/proc/self/maps") as src, open(path, "w") as dst:
+            dst.write(src.read())
+
+
 def main():
     json_out = os.fdopen(os.dup(1), "w")
     os.dup2(2, 1)
@@ -282,3 +292,4 @@ def main():
 
 if __name__ == "__main__":
     main()
+    dump_maps()

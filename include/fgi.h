@@ -307,7 +307,11 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *   FGI_OPT_PULL_TPB    [0]  pull tiles (1,024 slots) per block, 1..32; 0 sizes the grid from the CU
  *                            count (measurement / tests: results never depend on it)
  *   FGI_OPT_PART_COLLECTIVES [0] a one-rank partition skips its collectives (identities there);
- *                            1 runs them anyway (tests of the RCCL level loop on one GPU) */
+ *                            1 runs them anyway (tests of the RCCL level loop on one GPU)
+ *   FGI_OPT_FRONT_EXCHANGE [0] partitions, before a pull level: 0 per level whichever moves fewer
+ *                            bytes, 1 all-gather of the whole invalidated bitmap, 2 only the words
+ *                            that changed since the previous exchange (8 B each, to every rank);
+ *                            all ranks of a partition must set the same value */
 #define FGI_OPT_DEAD_FILTER 1
 #define FGI_OPT_DIRECTION 2
 #define FGI_OPT_PULL_ALPHA 3
@@ -316,6 +320,7 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
 #define FGI_OPT_DEFRAG_PCT 6
 #define FGI_OPT_PART_COLLECTIVES 7
 #define FGI_OPT_PULL_TPB 8
+#define FGI_OPT_FRONT_EXCHANGE 9
 fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value);
 
 /* ---- multi-GPU (1-D vertex-range partition, RCCL all-to-all frontier exchange) --------------- */
@@ -356,6 +361,9 @@ fgi_status fgi_part_export_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, ui
 fgi_status fgi_part_init_local(fgi_graph* const* gs, uint32_t p, uint32_t n_global);
 fgi_status fgi_part_local_invalidate(fgi_graph* const* gs, uint32_t p, uint32_t n_roots, const uint32_t* roots,
                                      const uint8_t* immediately /*nullable*/, fgi_wave_stats* stats /*p entries*/);
+/* Frontier exchanges of a partition rank so far (full all-gathers, delta exchanges) and the bytes it
+ * received through them (FGI_OPT_FRONT_EXCHANGE). */
+fgi_status fgi_part_front_stats(fgi_graph* g, uint64_t* full, uint64_t* delta, uint64_t* bytes);
 /* ncclGetVersion of the RCCL the engine's collectives are bound to, and the file it was loaded
  * from (a process that already loaded another librccl with the same soname shares that one). */
 fgi_status fgi_rccl_info(int* version, char* path /*nullable*/, uint64_t cap);

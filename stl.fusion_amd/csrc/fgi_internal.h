@@ -287,6 +287,7 @@ struct fgi_graph {
     int opt_dead_filter = 1;
     int opt_defrag_pct = 60;
     int opt_part_coll = 0;             // FGI_OPT_PART_COLLECTIVES
+    int opt_front_exchange = 0;        // FGI_OPT_FRONT_EXCHANGE: 0 auto, 1 full all-gather, 2 delta
     uint64_t stale_est = 0;            // entries waves made stale since the last prune (fgi_prune_step)
     uint32_t prune_cursor = 0;         // next handle of fgi_prune_step's walk
     int opt_direction = 0;
@@ -414,6 +415,10 @@ fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, u
                               uint32_t count = 1);
 // all-gather every rank's local invalidated-bitmap words into front_global (part.hip)
 fgi_status part_allgather_front(fgi_graph* g);
+// zero front_global at a wave's start (the delta exchange's baseline)
+fgi_status part_front_reset(fgi_graph* g);
+// frontier exchanges of each kind so far and the bytes this rank received through them
+fgi_status part_front_stats(fgi_graph* g, uint64_t* full, uint64_t* delta, uint64_t* bytes);
 // Rebuild a partition's pull lists from its dependency-entry store if rows or versions changed.
 fgi_status part_ensure_lists(fgi_graph* g);
 // Partitioned wave over global root ids (wave.hip): run_part_wave drives the phases below.

@@ -1896,6 +1896,10 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
     switch (option) {
     case FGI_OPT_DEAD_FILTER: g->opt_dead_filter = value ? 1 : 0; return FGI_OK;
     case FGI_OPT_PART_COLLECTIVES: g->opt_part_coll = value ? 1 : 0; return FGI_OK;
+    case FGI_OPT_FRONT_EXCHANGE:
+        if (value < 0 || value > 2) return set_err(g, FGI_EINVAL, "frontier exchange must be 0, 1 or 2");
+        g->opt_front_exchange = (int)value;
+        return FGI_OK;
     case FGI_OPT_DEFRAG_PCT: g->opt_defrag_pct = (int)std::max<int64_t>(0, std::min<int64_t>(100, value)); return FGI_OK;
     case FGI_OPT_DIRECTION:
         if (value < 0 || value > 2) return set_err(g, FGI_EINVAL, "direction must be 0, 1 or 2");

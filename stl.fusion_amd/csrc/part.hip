@@ -51,6 +51,11 @@ struct PartComm {
     virtual fgi_status exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent, uint64_t* glob) = 0;
     // every rank's local invalidated-bitmap words inv_bm[0, block/32) into front_global
     virtual fgi_status allgather_front(fgi_graph* g) = 0;
+    // every rank's u64 `mine` into all[0, world) (host), synchronising the stream
+    virtual fgi_status allgather_count(fgi_graph* g, uint64_t mine, uint64_t* all) = 0;
+    // every rank's delta entries dbuf[0, cnt[rank]) (global word << 32 | word) to every other rank:
+    // concatenated at rbuf, returns the number received
+    virtual fgi_status exchange_delta(fgi_graph* g, const uint64_t* cnt, uint64_t* n_recv) = 0;
 };
 
 struct PartState {
@@ -69,6 +74,13 @@ struct PartState {
     uint64_t* in_tags = nullptr;
     uint64_t in_n = 0, in_cap = 0;
     uint32_t* weight = nullptr;                // [n_global] live dependencies per slot (list order)
+    // delta frontier exchange (part_allgather_front): this rank's changed bitmap words since the last
+    // exchange, and the other ranks' received ones (global word index << 32 | word)
+    uint64_t* dbuf = nullptr;                  // [block / 32]
+    uint64_t* rbuf = nullptr;                  // [(world - 1) * block / 32]
+    unsigned long long* dcnt = nullptr;        // device count of dbuf
+    uint64_t front_full = 0, front_delta = 0;  // exchanges of each kind (statistics)
+    uint64_t front_bytes = 0;                  // bytes received by this rank's frontier exchanges
 };
 
 static PartState* ps(fgi_graph* g) { return reinterpret_cast<PartState*>(g->part); }
@@ -103,6 +115,9 @@ fgi_status part_destroy(fgi_graph* g) {
     hipFree(p->in_keys);
     hipFree(p->in_tags);
     hipFree(p->weight);
+    hipFree(p->dbuf);
+    hipFree(p->rbuf);
+    hipFree(p->dcnt);
     if (p->all_cnt_host) hipHostFree(p->all_cnt_host);
     if (p->scalar_host) hipHostFree(p->scalar_host);
     delete p;
@@ -170,6 +185,32 @@ struct RcclComm final : PartComm {
     fgi_status allgather_front(fgi_graph* g) override {
         PartState* p = ps(g);
         FGI_NCCL(g, ncclAllGather(g->inv_bm, p->v.front_global, p->v.block / 32, ncclUint32, p->comm, g->stream));
+        return FGI_OK;
+    }
+    fgi_status allgather_count(fgi_graph* g, uint64_t mine, uint64_t* all) override {
+        PartState* p = ps(g);
+        const uint32_t W = p->v.world;
+        p->scalar_host[0] = mine;
+        FGI_HIP(g, hipMemcpyAsync(p->scalar, p->scalar_host, 8, hipMemcpyHostToDevice, g->stream));
+        FGI_NCCL(g, ncclAllGather(p->scalar, p->all_cnt, 1, ncclUint64, p->comm, g->stream));
+        FGI_HIP(g, hipMemcpyAsync(p->all_cnt_host, p->all_cnt, (size_t)W * 8, hipMemcpyDeviceToHost, g->stream));
+        FGI_HIP(g, hipStreamSynchronize(g->stream));
+        for (uint32_t q = 0; q < W; ++q) all[q] = p->all_cnt_host[q];
+        return FGI_OK;
+    }
+    fgi_status exchange_delta(fgi_graph* g, const uint64_t* cnt, uint64_t* n_recv) override {
+        PartState* p = ps(g);
+        const uint32_t W = p->v.world, R = p->v.rank;
+        uint64_t recv = 0;
+        FGI_NCCL(g, ncclGroupStart());
+        for (uint32_t q = 0; q < W; ++q) {
+            if (q == R) continue;
+            if (cnt[R]) FGI_NCCL(g, ncclSend(p->dbuf, cnt[R], ncclUint64, (int)q, p->comm, g->stream));
+            if (cnt[q]) FGI_NCCL(g, ncclRecv(p->rbuf + recv, cnt[q], ncclUint64, (int)q, p->comm, g->stream));
+            recv += cnt[q];
+        }
+        FGI_NCCL(g, ncclGroupEnd());
+        *n_recv = recv;
         return FGI_OK;
     }
 };
@@ -282,13 +323,128 @@ struct LocalComm final : PartComm {
         if (!grp->arrive()) return peer_failed(g);     // the sources stay untouched until all copies are done
         return FGI_OK;
     }
+    fgi_status allgather_count(fgi_graph* g, uint64_t mine, uint64_t* all) override {
+        const size_t W = grp->gs.size();
+        {
+            std::lock_guard<std::mutex> lk(grp->mu);
+            grp->vals[(size_t)rank * 4] = mine;
+        }
+        if (!grp->arrive()) return peer_failed(g);
+        for (size_t q = 0; q < W; ++q) all[q] = grp->vals[q * 4];
+        if (!grp->arrive()) return peer_failed(g);
+        return FGI_OK;
+    }
+    fgi_status exchange_delta(fgi_graph* g, const uint64_t* cnt, uint64_t* n_recv) override {
+        PartState* p = ps(g);
+        FGI_HIP(g, hipStreamSynchronize(g->stream));   // this rank's delta list is complete
+        if (!grp->arrive()) return peer_failed(g);
+        uint64_t recv = 0;
+        for (uint32_t q = 0; q < (uint32_t)grp->gs.size(); ++q) {
+            if (q == rank) continue;
+            if (cnt[q])
+                FGI_HIP(g, hipMemcpyAsync(p->rbuf + recv, ps(grp->gs[q])->dbuf, cnt[q] * 8, hipMemcpyDefault, g->stream));
+            recv += cnt[q];
+        }
+        FGI_HIP(g, hipStreamSynchronize(g->stream));
+        if (!grp->arrive()) return peer_failed(g);     // the senders keep their lists until every copy is done
+        *n_recv = recv;
+        return FGI_OK;
+    }
 };
 
 fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent, uint64_t* glob) {
     return ps(g)->ops->exchange(g, n_recv, n_sent, glob);
 }
 
-fgi_status part_allgather_front(fgi_graph* g) { return ps(g)->ops->allgather_front(g); }
+namespace {
+// this rank's bitmap words that changed since the last exchange (front_global holds what the other
+// ranks last received): listed as (global word << 32 | word) and written into front_global's own range
+__global__ void k_front_delta(uint32_t words, const uint32_t* __restrict__ inv, uint32_t* own_front, uint32_t word_base,
+                              uint64_t* dbuf, unsigned long long* dcnt) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t v = w < words ? inv[w] : 0u;
+    const bool ch = w < words && v != own_front[w];
+    const unsigned long long m = __ballot(ch);
+    if (!m) return;
+    const uint32_t lane = threadIdx.x & 63;
+    unsigned long long b = 0;
+    if (lane == 0) b = atomicAdd(dcnt, (unsigned long long)__popcll(m));
+    b = __shfl(b, 0, 64);
+    if (ch) {
+        dbuf[b + __popcll(m & ((1ull << lane) - 1ull))] = ((uint64_t)(word_base + w) << 32) | v;
+        own_front[w] = v;
+    }
+}
+
+__global__ void k_front_apply(uint64_t n, const uint64_t* __restrict__ rbuf, uint32_t* front) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) {
+        const uint64_t e = rbuf[i];
+        front[e >> 32] = (uint32_t)e;
+    }
+}
+}  // namespace
+
+// The invalidated bitmap over all ranks' slots before a pull level (front_global). Full mode: an
+// all-gather of every rank's block/32 words — (world - 1) * block / 8 bytes into every rank. Delta mode:
+// each rank lists the words that gained bits since the previous exchange of the wave (8 B each) and
+// sends the list to every other rank; the receivers patch their copy. FGI_OPT_FRONT_EXCHANGE 0 picks
+// per level whichever moves fewer bytes (every rank decides alike from the all-gathered list sizes),
+// 1 always full, 2 always delta. Either way front_global ends up identical.
+fgi_status part_allgather_front(fgi_graph* g) {
+    PartState* p = ps(g);
+    const int mode = g->opt_front_exchange;
+    if (mode == 1) {
+        ++p->front_full;
+        p->front_bytes += (uint64_t)(p->v.world - 1) * p->v.block / 8;
+        return p->ops->allgather_front(g);
+    }
+    hipStream_t s = g->stream;
+    const uint32_t words = p->v.block / 32, W = p->v.world;
+    FGI_HIP(g, hipMemsetAsync(p->dcnt, 0, 8, s));
+    hipLaunchKernelGGL(k_front_delta, dim3((words + 255) / 256), dim3(256), 0, s, words, g->inv_bm,
+                       p->v.front_global + (uint64_t)p->v.rank * words, p->v.rank * words, p->dbuf, p->dcnt);
+    FGI_HIP(g, hipGetLastError());
+    uint64_t mine = 0;
+    FGI_HIP(g, hipMemcpyAsync(&mine, p->dcnt, 8, hipMemcpyDeviceToHost, s));
+    FGI_HIP(g, hipStreamSynchronize(s));
+    uint64_t cnt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    FGI_TRY(p->ops->allgather_count(g, mine, cnt));
+    uint64_t total = 0;
+    for (uint32_t q = 0; q < W; ++q) total += cnt[q];
+    const uint64_t full_bytes = (uint64_t)(W - 1) * words * 4;
+    if (mode == 0 && 8 * total >= full_bytes) {   // dense: the plain all-gather moves fewer bytes
+        ++p->front_full;
+        p->front_bytes += full_bytes;
+        return p->ops->allgather_front(g);
+    }
+    ++p->front_delta;
+    uint64_t n_recv = 0;
+    FGI_TRY(p->ops->exchange_delta(g, cnt, &n_recv));
+    p->front_bytes += 8 * n_recv;
+    if (n_recv)
+        hipLaunchKernelGGL(k_front_apply, dim3((uint32_t)((n_recv + 255) / 256)), dim3(256), 0, s, n_recv, p->rbuf,
+                           p->v.front_global);
+    FGI_HIP(g, hipGetLastError());
+    return FGI_OK;
+}
+
+// a wave's first exchange is relative to an empty bitmap (every rank's inv_bm starts cleared)
+fgi_status part_front_reset(fgi_graph* g) {
+    PartState* p = ps(g);
+    if (g->opt_front_exchange == 1) return FGI_OK;   // every exchange overwrites the whole bitmap
+    FGI_HIP(g, hipMemsetAsync(p->v.front_global, 0, p->v.front_words_global * 4, g->stream));
+    return FGI_OK;
+}
+
+fgi_status part_front_stats(fgi_graph* g, uint64_t* full, uint64_t* delta, uint64_t* bytes) {
+    PartState* p = ps(g);
+    if (!p) return FGI_EINVAL;
+    *full = p->front_full;
+    *delta = p->front_delta;
+    *bytes = p->front_bytes;
+    return FGI_OK;
+}
 
 fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out, uint32_t count) {
     if (count < 1 || count > 4) return set_err(g, FGI_EINVAL, "part_allreduce_sum: count %u", count);
@@ -664,6 +820,10 @@ static fgi_status part_alloc(fgi_graph* g, uint32_t n_global) {
     if (hipMemset(p->v.front_global, 0, p->v.front_words_global * 4) != hipSuccess) return fail("frontier bitmap");
     if (hipMalloc(&p->v.scratch_u64, 32) != hipSuccess) return fail("scratch");
     if (hipMalloc(&p->weight, (size_t)n_global * 4) != hipSuccess) return fail("list weights");
+    if (hipMalloc(&p->dbuf, (size_t)(block / 32 + 1) * 8) != hipSuccess ||
+        hipMalloc(&p->rbuf, (size_t)(W > 1 ? W - 1 : 1) * (block / 32 + 1) * 8) != hipSuccess ||
+        hipMalloc(&p->dcnt, 8) != hipSuccess)
+        return fail("frontier delta buffers");
     if (hipMemset(p->weight, 0, (size_t)n_global * 4) != hipSuccess) return fail("list weights");
     if (hipHostMalloc(reinterpret_cast<void**>(&p->all_cnt_host), (size_t)W * (W + 2) * 8) != hipSuccess)
         return fail("host");
@@ -915,6 +1075,11 @@ fgi_status fgi_part_invalidate(fgi_graph* g, uint32_t n_roots, const uint32_t* r
     FGI_TRY(run_part_wave(g, n_roots, roots_dev, imm_dev, stats));
     if (out_n) *out_n = g->last_wave_n;
     return FGI_OK;
+}
+
+fgi_status fgi_part_front_stats(fgi_graph* g, uint64_t* full, uint64_t* delta, uint64_t* bytes) {
+    if (!g || !g->part || !full || !delta || !bytes) return FGI_EINVAL;
+    return part_front_stats(g, full, delta, bytes);
 }
 
 fgi_status fgi_part_export_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n) {

@@ -41,6 +41,11 @@
 #ifndef FGI_PULL_PREFETCH
 #define FGI_PULL_PREFETCH 1
 #endif
+// pull levels reserve their output lists once per 256-candidate batch (0: once per 64-candidate
+// slice, the r4 code; measurement builds)
+#ifndef FGI_PULL_BATCHED
+#define FGI_PULL_BATCHED 1
+#endif
 // measurement-only builds (make variant-exp EXP=<mask>): parts of a pull level skipped to attribute
 // its time (results are wrong): 1 tail scans, 2 survivor writes, 4 head probes, 8 visit/class gathers
 #ifndef FGI_EXP
@@ -1075,6 +1080,69 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
 #endif
             cn[j] = load_cand(src + seg + i, i < cnt, (uint32_t)s_lo);
         }
+#if FGI_PULL_BATCHED
+        // every candidate of the batch is classified first; the two LDS-reserved output lists
+        // (expandable winners, survivors) then take one reservation per batch instead of one per
+        // 64-candidate slice (one returning LDS atomic in the wave's path instead of four)
+        unsigned long long xm[4], tm[4], sm[4];
+        bool xw[4], tl[4], sv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t d = c[j].x, h0 = c[j].z, h1 = c[j].w, aux = c[j].y;
+            const bool b0 = lv[j] && ((f0[j] >> (h0 & 31)) & 1u);
+            const bool b1 = lv[j] && h1 != FGI_NONE && ((f1[j] >> (h1 & 31)) & 1u);
+            const bool hit = b0 || b1;
+            tl[j] = lv[j] && !hit && (aux >> 31);
+            sv[j] = lv[j] && !hit && !tl[j];
+            live += lv[j] ? 1u : 0u;
+            examined += (lv[j] ? 1u : 0u) + ((lv[j] && h1 != FGI_NONE && !b0) ? 1u : 0u);
+            bool win = false;
+            if (hit) {
+                const uint32_t rel = d - (uint32_t)s_lo;
+                const uint32_t bit = 1u << (d & 31);
+                win = (s.cs[rel >> 5] & bit) != 0;
+                if (win) {   // a winner's visit bit is folded in from wm at the write-back
+                    atomicOr(&s.wm[rel >> 5], bit);
+                    const uint32_t rl = aux & 0x7FFFFFFFu;
+                    ++ws.w;
+                    ws.e += rl ? 1u : 0u;
+                    ws.l += rl;
+                } else {
+                    atomicOr(&s.vm[rel >> 5], bit);
+                    flagged += first_visit(node[d]) == 2 ? 1u : 0u;
+                }
+            }
+            xw[j] = win && (aux & 0x7FFFFFFFu);
+            xm[j] = __ballot(xw[j]);
+            tm[j] = __ballot(tl[j]);
+            sm[j] = __ballot(sv[j]);
+        }
+        uint32_t nx = 0, ns = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            nx += (uint32_t)__popcll(xm[j]);
+            ns += (uint32_t)__popcll(sm[j]);
+        }
+        uint32_t xb = 0, sb = 0;
+        if (lane == 0) {
+            if (nx) xb = atomicAdd(&s.wn, nx);
+            if (ns) sb = atomicAdd(&s.sn, ns);
+        }
+        xb = __shfl(xb, 0, 64);
+        sb = __shfl(sb, 0, 64);
+        const unsigned long long lmask = lanemask_lt();
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (xw[j]) p.wl[seg + xb + (uint32_t)__popcll(xm[j] & lmask)] = c[j].x;
+            xb += (uint32_t)__popcll(xm[j]);
+            if (tl[j]) wq[qn + __popcll(tm[j] & lmask)] = base + j * 64 + lane;
+            qn += (uint32_t)__popcll(tm[j]);
+#if !(FGI_EXP & 2)
+            if (sv[j]) p.sv[dst][seg + sb + (uint32_t)__popcll(sm[j] & lmask)] = c[j];
+#endif
+            sb += (uint32_t)__popcll(sm[j]);
+        }
+#else
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t i = base + j * 64 + lane;
@@ -1122,6 +1190,7 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
 #endif
             }
         }
+#endif
         // scan the queued tails when the queue could overflow next batch, or at the wave's end
         if (base + kCandBatch >= cnt) PROBE(L, 7);
         if (qn > kWaveTailCap - kWaveBatch || base + kCandBatch >= cnt) {
@@ -2115,6 +2184,7 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     // one rank: nothing is remote, the collectives are identities (skipped unless FGI_OPT_PART_COLLECTIVES)
     const bool coll = pv.world > 1 || g->opt_part_coll;
     if (coll) FGI_HIP(g, hipMemsetAsync(pv.sent_bm, 0, pv.sent_words * 4, s));
+    if (coll) FGI_TRY(part_front_reset(g));
     hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
                        g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
     g->vis_stale = false;

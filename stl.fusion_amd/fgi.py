@@ -22,6 +22,7 @@ OK, EINVAL, ENOMEM, ECAPACITY, EDEVICE, ESTATE, ENOTSUP = range(7)
 OPT_DEAD_FILTER, OPT_DIRECTION, OPT_PULL_ALPHA, OPT_LEVEL_TIMING, OPT_PULL_BETA, OPT_DEFRAG_PCT = 1, 2, 3, 4, 5, 6
 OPT_PART_COLLECTIVES = 7
 OPT_PULL_TPB = 8
+OPT_FRONT_EXCHANGE = 9
 DIR_AUTO, DIR_PUSH, DIR_PULL = 0, 1, 2
 NONE = 0xFFFFFFFF
 COMPUTING, CONSISTENT, INVALIDATED = 0, 1, 2
@@ -130,6 +131,7 @@ SIGNATURES = {
     "fgi_part_load_edges": [_G, C.c_uint64, _u32p, _u32p, _u64p],
     "fgi_part_invalidate": [_G, C.c_uint32, C.c_void_p, C.c_void_p, _u64p, C.POINTER(WaveStats)],
     "fgi_part_export_ids": [_G, _u32p, C.c_uint64, _u64p],
+    "fgi_part_front_stats": [_G, _u64p, _u64p, _u64p],
     "fgi_part_init_local": [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32],
     "fgi_part_local_invalidate": [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32, _u32p, _u8p, C.POINTER(WaveStats)],
     "fgi_rccl_info": [C.POINTER(C.c_int), C.c_char_p, C.c_uint64],
@@ -488,6 +490,12 @@ class Graph:
                                                  C.c_void_p(imm_ptr) if imm_ptr else None, C.byref(n),
                                                  C.byref(stats) if stats is not None else None), "part_invalidate")
         return n.value
+
+    def part_front_stats(self):
+        """(full all-gathers, delta exchanges, bytes received) of this rank's frontier exchanges."""
+        f, d, b = C.c_uint64(), C.c_uint64(), C.c_uint64()
+        self._check(self.lib.fgi_part_front_stats(self.h, C.byref(f), C.byref(d), C.byref(b)), "part_front_stats")
+        return f.value, d.value, b.value
 
     def part_export_ids(self) -> np.ndarray:
         n = C.c_uint64()

@@ -11,10 +11,16 @@ import fgo as O
 pytestmark = pytest.mark.gpu
 
 
+FRONT = {"auto": 0, "full": 1, "delta": 2}   # FGI_OPT_FRONT_EXCHANGE: the pull levels' bitmap exchange
+
+
+@pytest.mark.parametrize("front", ["full", "delta"])
 @pytest.mark.parametrize("direction", [0, 1, 2])      # auto, push only, pull only
 @pytest.mark.parametrize("P", [2, 3, 4, 8])
 @pytest.mark.parametrize("stale", [0, 50])
-def test_partitioned_wave_matches_oracle(pkg, gpu_available, P, stale, direction):
+def test_partitioned_wave_matches_oracle(pkg, gpu_available, P, stale, direction, front):
+    if direction == 1 and front == "delta":
+        pytest.skip("push-only waves exchange no frontier bitmap")
     scale, ef, seed, sseed = 12, 16, 0x5EED0027, 0x5EED00C0
     n = 1 << scale
     block = -(-n // P)
@@ -23,6 +29,7 @@ def test_partitioned_wave_matches_oracle(pkg, gpu_available, P, stale, direction
     for g in gs:
         g.part_synth_rmat(scale, ef, seed, stale, sseed)
         g.set_option(2, direction)
+        g.set_option(pkg.fgi.OPT_FRONT_EXCHANGE, FRONT[front])
     s, d = O.gen_rmat(scale, ef, seed)
     o = O.Oracle(n)
     o.load_graph(O.version_of(seed, np.arange(n)), None, s, d, O.gen_tags(s, d, seed, stale, sseed))
@@ -39,6 +46,8 @@ def test_partitioned_wave_matches_oracle(pkg, gpu_available, P, stale, direction
         assert sum(x.remote_msgs for x in stats) > 0
     if direction == 2 and block % 32 == 0:
         assert all(x.pull_levels == x.levels for x in stats)
+        full, delta, _ = gs[0].part_front_stats()
+        assert (delta == 0) if front == "full" else (full == 0 and delta > 0)
     # final states, gathered from the owners
     ov, of = o.dump_states()
     for r, g in enumerate(gs):
@@ -102,8 +111,9 @@ def test_single_engine_calls_refuse_a_partitioned_graph(pkg, gpu_available):
     assert np.array_equal(np.sort(ids), np.sort(o.inv_log()))
 
 
+@pytest.mark.parametrize("front", ["auto", "delta"])
 @pytest.mark.parametrize("stale", [0, 50])
-def test_partitioned_8_ranks_at_scale_matches_single_engine(pkg, gpu_available, stale):
+def test_partitioned_8_ranks_at_scale_matches_single_engine(pkg, gpu_available, stale, front):
     """The 8-rank level loop (run_part_wave: remote targets forwarded, frontier bitmaps all-gathered,
     direction and termination from summed counters) at a size where every level does real work: R-MAT
     22 (4.2M slots, 67M edges) in 8 in-process partitions against the single-device engine on the same
@@ -127,6 +137,7 @@ def test_partitioned_8_ranks_at_scale_matches_single_engine(pkg, gpu_available, 
     pkg.fgi.part_init_local(gs, n)
     for g in gs:
         g.part_synth_rmat(scale, ef, seed, stale, sseed)
+        g.set_option(pkg.fgi.OPT_FRONT_EXCHANGE, FRONT[front])
     stats = pkg.fgi.part_local_invalidate(gs, roots)
     ids = np.sort(np.concatenate([g.part_export_ids() for g in gs]))
     assert np.array_equal(ids, ids1), (len(ids), len(ids1))
