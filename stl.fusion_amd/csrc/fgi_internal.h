@@ -146,6 +146,13 @@ struct LevelCtr {
     unsigned long long pad1;
 };
 
+// A level's frontier totals: a push producer leaves them packed in ft (the single engine does not
+// unpack them: the next kernel and the host read ft directly, which saves the producer's last-block
+// hand-off; a partition's producers unpack them into F / T for the all-reduce), a pull level's last
+// block writes F / T (ft stays 0). F == 0 means no frontier entry, and then T == 0 too.
+__host__ __device__ inline uint64_t lvl_F(const LevelCtr& c) { return c.F ? c.F : (c.ft >> 32); }
+__host__ __device__ inline uint64_t lvl_T(const LevelCtr& c) { return c.F ? c.T : (c.ft & 0xFFFFFFFFull); }
+
 struct WaveCtr {
     unsigned long long inv;         // invalidated handles of the wave (V_inv; the final collect)
     unsigned long long e_match;

@@ -46,6 +46,10 @@
 #ifndef FGI_PULL_BATCHED
 #define FGI_PULL_BATCHED 1
 #endif
+// push levels with fewer edges skip the dead-edge filter (measurement builds: -DFGI_FILTER_MIN=0)
+#ifndef FGI_FILTER_MIN
+#define FGI_FILTER_MIN (1 << 20)
+#endif
 // measurement-only builds (make variant-exp EXP=<mask>): parts of a pull level skipped to attribute
 // its time (results are wrong): 1 tail scans, 2 survivor writes, 4 head probes, 8 visit/class gathers
 #ifndef FGI_EXP
@@ -62,6 +66,7 @@ namespace {
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 constexpr int kProbeLevelsOff = 1 << 20;   // a level index no probe records (cooperative waves)
+constexpr uint64_t kFilterMin = FGI_FILTER_MIN;
 
 #if FGI_PROBE
 constexpr int kProbeLevels = 8, kProbePts = 8, kProbeBlocks = 2048;
@@ -560,12 +565,15 @@ __device__ __forceinline__ void root_step(uint32_t i, const uint32_t* __restrict
     if (lane_id() == 0 && ws) atomicAdd(&ctr->root_inv, (unsigned long long)ws);
 }
 
+// publish: unpack level 0's totals into F / T (the partitioned wave all-reduces those words);
+// the single engine reads the packed counter (lvl_F / lvl_T) and skips the hand-off
 template <int IMM>
 __global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ roots, const uint8_t* __restrict__ imm,
                                                   uint32_t n, uint32_t base, uint32_t n_range, unsigned long long* node,
-                                                  uint32_t* vis, Out o, WaveCtr* ctr, unsigned long long* done) {
+                                                  uint32_t* vis, Out o, WaveCtr* ctr, unsigned long long* done,
+                                                  int publish) {
     root_step<IMM>(blockIdx.x * blockDim.x + threadIdx.x, roots, imm, n, base, n_range, node, vis, o, ctr);
-    publish_ft(o.ln, done, gridDim.x);
+    if (publish) publish_ft(o.ln, done, gridDim.x);
 }
 
 // ---- the level's direction ------------------------------------------------------------------------
@@ -583,10 +591,11 @@ struct WaveParams {
 __device__ __forceinline__ bool level_pulls(const WaveCtr* ctr, int L, const WaveParams& wp) {
     const LevelCtr& lc = ctr->lvl[L % kRing];
     if (wp.multi) return lc.pull != 0;
-    if (lc.F == 0 || wp.direction == 1) return false;
+    const uint64_t F = lvl_F(lc), T = lvl_T(lc);
+    if (F == 0 || wp.direction == 1) return false;
     if (wp.direction == 2) return true;
     const bool prev_pull = L > 0 && ctr->lvl[(L + kRing - 1) % kRing].pull != 0;
-    return lc.T > wp.pull_threshold || (prev_pull && lc.F > wp.stay_pull_f);
+    return T > wp.pull_threshold || (prev_pull && F > wp.stay_pull_f);
 }
 
 // fine chunks per expand chunk: as large as kEPT allows while every block still gets two chunks
@@ -626,7 +635,7 @@ constexpr int kCollectThreads = 256;
 // heads' snapshot; otherwise nothing to do.
 __global__ __launch_bounds__(kCollectThreads) void k_collect(int L, WaveCtr* ctr, WaveParams wp, CollectArgs c) {
     const LevelCtr& lc = ctr->lvl[L % kRing];
-    if (lc.F == 0) return;
+    if (lvl_F(lc) == 0) return;
     if (level_pulls(ctr, L, wp)) {
         // one entry per lane, 64 bits per wave (n_hot and the grid stride are multiples of 64)
         unsigned long long* hot64 = reinterpret_cast<unsigned long long*>(c.hot_bm);
@@ -642,7 +651,7 @@ __global__ __launch_bounds__(kCollectThreads) void k_collect(int L, WaveCtr* ctr
     const uint32_t lane = lane_id();
     const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
     for (uint64_t b = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < G; b += W) {   // wave-uniform
-        const uint64_t e0 = c.pre[G + b], e1 = b + 1 < G ? c.pre[G + b + 1] : lc.F;
+        const uint64_t e0 = c.pre[G + b], e1 = b + 1 < G ? c.pre[G + b + 1] : lvl_F(lc);
         uint64_t es = c.pre[2 * G + b];
         const uint64_t base = c.seg[b];
         for (uint64_t i0 = 0; i0 < e1 - e0; i0 += 64) {
@@ -763,8 +772,10 @@ __device__ __forceinline__ void expand_level(int L, uint64_t F, uint64_t T, uint
                 if (dst[j] != 0xFFFFFFFFu) dst[j] -= ra.base;   // local handle
         }
         // edges to nodes visited earlier need neither the tag nor the gather (the bitmap is read
-        // without synchronisation: a stale 0 only costs the gather and an atomic that finds the bit)
-        if (x.dead_filter) {
+        // without synchronisation: a stale 0 only costs the gather and an atomic that finds the bit).
+        // Below kFilterMin edges a level is latency-bound: the filter's extra dependent read costs
+        // more than the gathers it saves, so small levels go straight to the tag / word gathers.
+        if (x.dead_filter == 2 || (x.dead_filter == 1 && T >= (uint64_t)kFilterMin)) {
 #pragma unroll
             for (int j = 0; j < kEPT; ++j)
                 if (dst[j] != 0xFFFFFFFFu && bit_of(vis, dst[j])) dst[j] = 0xFFFFFFFFu;
@@ -1296,7 +1307,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_level(int L, WaveParams wp, Expan
         pull_epilogue(L, p, o.ln, done, bs, s_red);
         return;
     }
-    const uint64_t F = lc.F, T = lc.T;
+    const uint64_t F = lvl_F(lc), T = lvl_T(lc);
     if (F == 0) return;
     const uint32_t mult = level_mult(T, gridDim.x);
     if (blockIdx.x == 0 && threadIdx.x == 0) lc.mult = mult;
@@ -1308,7 +1319,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_level(int L, WaveParams wp, Expan
     PROBE(L, 1);
     expand_level<PART>(L, F, T, mult, x, node, vis, o, em, s_x, me, s_rel, s_base, blk, s_st, ra);
     PROBE(L, 2);
-    publish_ft(o.ln, done, active);
+    if constexpr (PART) publish_ft(o.ln, done, active);   // the host all-reduces F / T
     PROBE(L, 3);
 }
 
@@ -1852,15 +1863,16 @@ hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true) {
 }
 
 void launch_roots(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev, uint32_t base,
-                  uint32_t n_range) {
+                  uint32_t n_range, int publish) {
     const uint32_t nb = (n_roots + kBlock - 1) / kBlock;
     auto* node = reinterpret_cast<unsigned long long*>(g->node);
     const Out o = out_for(g, 0, &g->ctr->lvl[0]);
+    // the immediate roots' launch never publishes: the second launch adds to the same counter
     if (imm_dev)
         hipLaunchKernelGGL(k_roots<1>, dim3(nb), dim3(kBlock), 0, g->stream, roots_dev, imm_dev, n_roots, base, n_range,
-                           node, g->vis_bm, o, g->ctr, g->done);
+                           node, g->vis_bm, o, g->ctr, g->done, 0);
     hipLaunchKernelGGL(k_roots<0>, dim3(nb), dim3(kBlock), 0, g->stream, roots_dev, imm_dev, n_roots, base, n_range, node,
-                       g->vis_bm, o, g->ctr, g->done);
+                       g->vis_bm, o, g->ctr, g->done, publish);
 }
 
 }  // namespace
@@ -2009,7 +2021,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
     if (n_roots) {
         g->v_dirty = true;
-        launch_roots(g, n_roots, roots_dev, imm_dev, 0u, g->n_handles);
+        launch_roots(g, n_roots, roots_dev, imm_dev, 0u, g->n_handles, 0);
     }
     const auto* node = reinterpret_cast<const unsigned long long*>(g->node);
     // Levels run in groups between host synchronisations (one ~30 us round trip each); the first
@@ -2064,32 +2076,33 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                     ++expand_launches;
                 }
             }
-            if (lc.F) {
+            const uint64_t lF = lvl_F(lc), lT = lvl_T(lc);
+            if (lF) {
                 ++levels;
-                e_trav += lc.T;
-                f_total += lc.F;
+                e_trav += lT;
+                f_total += lF;
                 if (lc.pull) {
                     ++pull_levels;
                 } else {
-                    expand_edges += lc.T;
-                    expand_f += lc.F;
+                    expand_edges += lT;
+                    expand_f += lF;
                 }
             }
             if (trace)
                 fprintf(stderr, "[fgi] level %d %s: frontier %llu edges %llu chunk x%llu k_level %.3f ms\n", l,
-                        lc.pull ? "pull" : "push", (unsigned long long)lc.F, (unsigned long long)lc.T,
+                        lc.pull ? "pull" : "push", (unsigned long long)lF, (unsigned long long)lT,
                         (unsigned long long)lc.mult, ms);
         }
 #if FGI_PROBE
         if (trace) print_probe(g, L0, L);
 #endif
-        done = g->ctr_host->lvl[L % kRing].F == 0;
+        done = lvl_F(g->ctr_host->lvl[L % kRing]) == 0;
         group = 4;
         // also when the wave is already done (its level groups are sized from the previous wave's
         // depth, so a repeated wave after a mutation finishes in one group): the next wave pulls
         if (!allow_pull && wp0.direction == 0) {
             bool heavy = false;
-            for (int l = L0; l <= L; ++l) heavy |= g->ctr_host->lvl[l % kRing].T > wp.pull_threshold;
+            for (int l = L0; l <= L; ++l) heavy |= lvl_T(g->ctr_host->lvl[l % kRing]) > wp.pull_threshold;
             if (heavy) {
                 FGI_TRY(ensure_in_lists(g));
                 allow_pull = pull_ready(g, wp0);
@@ -2196,7 +2209,7 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     }
     FGI_HIP(g, hipEventRecord(g->ev_w0, s));
     g->v_dirty = true;
-    if (n_roots) launch_roots(g, n_roots, roots_dev, imm_dev, pv.base, pv.n_local);
+    if (n_roots) launch_roots(g, n_roots, roots_dev, imm_dev, pv.base, pv.n_local, 1);
     if (imm_dev && n_roots) note_words(g);
     FGI_HIP(g, hipGetLastError());
     const auto* node = reinterpret_cast<const unsigned long long*>(g->node);
