@@ -293,10 +293,8 @@ fgi_status fgi_export_edges(fgi_graph* g, uint32_t* used, uint32_t* dependant_sl
 fgi_status fgi_stream(fgi_graph* g, void** stream);
 /* Traversal options (defaults in brackets). Results never depend on them; they exist so tests can
  * pin each code path and benches can compare them.
- *   FGI_OPT_DEAD_FILTER [1]  skip edges whose dependant was visited in an earlier level using the
- *                            per-wave visit bitmap (E_match then counts examined edges only): 1 on push
- *                            levels of at least 2^20 edges (smaller ones are latency-bound), 2 on every
- *                            push level, 0 never
+ *   FGI_OPT_DEAD_FILTER [1]  skip edges whose dependant was invalidated in an earlier level using
+ *                            a per-wave bitmap (E_match then counts examined edges only)
  *   FGI_OPT_DIRECTION   [0]  0 auto (push/pull per level), 1 push only, 2 pull only
  *   FGI_OPT_PULL_ALPHA  [28] auto: pull when frontier edges > total edges / alpha
  *   FGI_OPT_PULL_BETA   [24] auto: after a pull level, pull again while the frontier holds more

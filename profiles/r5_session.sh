@@ -6,7 +6,7 @@ tag=$1; shift
 out=gpurun_out/$tag
 mkdir -p "$out"
 sel=${*:-tests}
-timeout -k 10 900 python -u -m pytest $sel -m gpu -v --timeout 300 --timeout-method thread > "$out/gpu_tests.log" 2>&1
+FGI_PART_MEM_OUT=$out/part_mem.json FGI_FANOUT_OUT=$out/fanout.json timeout -k 10 900 python -u -m pytest $sel -m gpu -v --timeout 300 --timeout-method thread > "$out/gpu_tests.log" 2>&1
 rc=$?
 tail -3 "$out/gpu_tests.log"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc: no further GPU step"; exit $rc; fi

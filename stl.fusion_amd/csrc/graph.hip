@@ -1894,10 +1894,7 @@ fgi_status fgi_restore(fgi_graph* g) {
 fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
     if (!g) return FGI_EINVAL;
     switch (option) {
-    case FGI_OPT_DEAD_FILTER:
-        if (value < 0 || value > 2) return set_err(g, FGI_EINVAL, "dead filter must be 0, 1 or 2");
-        g->opt_dead_filter = (int)value;
-        return FGI_OK;
+    case FGI_OPT_DEAD_FILTER: g->opt_dead_filter = value ? 1 : 0; return FGI_OK;
     case FGI_OPT_PART_COLLECTIVES: g->opt_part_coll = value ? 1 : 0; return FGI_OK;
     case FGI_OPT_FRONT_EXCHANGE:
         if (value < 0 || value > 2) return set_err(g, FGI_EINVAL, "frontier exchange must be 0, 1 or 2");

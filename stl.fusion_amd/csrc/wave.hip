@@ -41,15 +41,6 @@
 #ifndef FGI_PULL_PREFETCH
 #define FGI_PULL_PREFETCH 1
 #endif
-// pull levels reserve their output lists once per 256-candidate batch (0: once per 64-candidate
-// slice, the r4 code; measurement builds)
-#ifndef FGI_PULL_BATCHED
-#define FGI_PULL_BATCHED 1
-#endif
-// push levels with fewer edges skip the dead-edge filter (measurement builds: -DFGI_FILTER_MIN=0)
-#ifndef FGI_FILTER_MIN
-#define FGI_FILTER_MIN (1 << 20)
-#endif
 // measurement-only builds (make variant-exp EXP=<mask>): parts of a pull level skipped to attribute
 // its time (results are wrong): 1 tail scans, 2 survivor writes, 4 head probes, 8 visit/class gathers
 #ifndef FGI_EXP
@@ -66,7 +57,6 @@ namespace {
 
 __device__ __forceinline__ uint32_t lane_id() { return __lane_id(); }
 constexpr int kProbeLevelsOff = 1 << 20;   // a level index no probe records (cooperative waves)
-constexpr uint64_t kFilterMin = FGI_FILTER_MIN;
 
 #if FGI_PROBE
 constexpr int kProbeLevels = 8, kProbePts = 8, kProbeBlocks = 2048;
@@ -773,9 +763,9 @@ __device__ __forceinline__ void expand_level(int L, uint64_t F, uint64_t T, uint
         }
         // edges to nodes visited earlier need neither the tag nor the gather (the bitmap is read
         // without synchronisation: a stale 0 only costs the gather and an atomic that finds the bit).
-        // Below kFilterMin edges a level is latency-bound: the filter's extra dependent read costs
-        // more than the gathers it saves, so small levels go straight to the tag / word gathers.
-        if (x.dead_filter == 2 || (x.dead_filter == 1 && T >= (uint64_t)kFilterMin)) {
+        // Kept on small levels too: without it their edges into visited nodes each pay an atomic
+        // on the visit bitmap instead (A/B, profiles/r5a_ab: push levels 57 vs 60-67 us per wave)
+        if (x.dead_filter) {
 #pragma unroll
             for (int j = 0; j < kEPT; ++j)
                 if (dst[j] != 0xFFFFFFFFu && bit_of(vis, dst[j])) dst[j] = 0xFFFFFFFFu;
@@ -1091,69 +1081,6 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
 #endif
             cn[j] = load_cand(src + seg + i, i < cnt, (uint32_t)s_lo);
         }
-#if FGI_PULL_BATCHED
-        // every candidate of the batch is classified first; the two LDS-reserved output lists
-        // (expandable winners, survivors) then take one reservation per batch instead of one per
-        // 64-candidate slice (one returning LDS atomic in the wave's path instead of four)
-        unsigned long long xm[4], tm[4], sm[4];
-        bool xw[4], tl[4], sv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t d = c[j].x, h0 = c[j].z, h1 = c[j].w, aux = c[j].y;
-            const bool b0 = lv[j] && ((f0[j] >> (h0 & 31)) & 1u);
-            const bool b1 = lv[j] && h1 != FGI_NONE && ((f1[j] >> (h1 & 31)) & 1u);
-            const bool hit = b0 || b1;
-            tl[j] = lv[j] && !hit && (aux >> 31);
-            sv[j] = lv[j] && !hit && !tl[j];
-            live += lv[j] ? 1u : 0u;
-            examined += (lv[j] ? 1u : 0u) + ((lv[j] && h1 != FGI_NONE && !b0) ? 1u : 0u);
-            bool win = false;
-            if (hit) {
-                const uint32_t rel = d - (uint32_t)s_lo;
-                const uint32_t bit = 1u << (d & 31);
-                win = (s.cs[rel >> 5] & bit) != 0;
-                if (win) {   // a winner's visit bit is folded in from wm at the write-back
-                    atomicOr(&s.wm[rel >> 5], bit);
-                    const uint32_t rl = aux & 0x7FFFFFFFu;
-                    ++ws.w;
-                    ws.e += rl ? 1u : 0u;
-                    ws.l += rl;
-                } else {
-                    atomicOr(&s.vm[rel >> 5], bit);
-                    flagged += first_visit(node[d]) == 2 ? 1u : 0u;
-                }
-            }
-            xw[j] = win && (aux & 0x7FFFFFFFu);
-            xm[j] = __ballot(xw[j]);
-            tm[j] = __ballot(tl[j]);
-            sm[j] = __ballot(sv[j]);
-        }
-        uint32_t nx = 0, ns = 0;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            nx += (uint32_t)__popcll(xm[j]);
-            ns += (uint32_t)__popcll(sm[j]);
-        }
-        uint32_t xb = 0, sb = 0;
-        if (lane == 0) {
-            if (nx) xb = atomicAdd(&s.wn, nx);
-            if (ns) sb = atomicAdd(&s.sn, ns);
-        }
-        xb = __shfl(xb, 0, 64);
-        sb = __shfl(sb, 0, 64);
-        const unsigned long long lmask = lanemask_lt();
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (xw[j]) p.wl[seg + xb + (uint32_t)__popcll(xm[j] & lmask)] = c[j].x;
-            xb += (uint32_t)__popcll(xm[j]);
-            if (tl[j]) wq[qn + __popcll(tm[j] & lmask)] = base + j * 64 + lane;
-            qn += (uint32_t)__popcll(tm[j]);
-#if !(FGI_EXP & 2)
-            if (sv[j]) p.sv[dst][seg + sb + (uint32_t)__popcll(sm[j] & lmask)] = c[j];
-#endif
-            sb += (uint32_t)__popcll(sm[j]);
-        }
-#else
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t i = base + j * 64 + lane;
@@ -1201,7 +1128,6 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
 #endif
             }
         }
-#endif
         // scan the queued tails when the queue could overflow next batch, or at the wave's end
         if (base + kCandBatch >= cnt) PROBE(L, 7);
         if (qn > kWaveTailCap - kWaveBatch || base + kCandBatch >= cnt) {

@@ -13,7 +13,9 @@ configs[2]  R-MAT scale 27, edge factor 8 (134M slots, 1.07G edges, 4,096 roots)
             checked against the least closure computed independently with torch over the exported
             edge set (closure, witness, E_trav, exact set; tests/closure_check.py), on the
             automatic path (its first wave builds the pull lists), again from the snapshot (pull
-            lists ready) and push-only.
+            lists ready) and push-only; then 8 vertex-range partitions of the same graph (the
+            multi-GPU engine's level loop, in one process) against the single engine, with the
+            resident memory per partition measured after the build.
 """
 import os
 
@@ -188,10 +190,19 @@ def test_configs2_rmat27_eight_partitions_match_single_engine(pkg, rmat27):
     v1, f1 = g.dump_states()
     P = 8
     block = -(-n // P)
+    import json
+    import torch
+    free0 = torch.cuda.mem_get_info()[0]
     gs = [pkg.Graph(block, rank=r, world=P) for r in range(P)]
     pkg.fgi.part_init_local(gs, n)
     for x in gs:
         x.part_synth_rmat(cfg["scale"], cfg["edge_factor"], cfg["seed"])
+    torch.cuda.synchronize()
+    per_rank_gb = (free0 - torch.cuda.mem_get_info()[0]) / P / 2**30   # resident after the build
+    if os.environ.get("FGI_PART_MEM_OUT"):
+        json.dump({"workload": "configs[2] R-MAT 27, 8 partitions", "resident_gib_per_rank": per_rank_gb},
+                  open(os.environ["FGI_PART_MEM_OUT"], "w"))
+    assert per_rank_gb < 16, per_rank_gb
     assert sum(x.degrees()[1] for x in gs) == m   # the rows of the 8 ranks are the whole edge set
     stats = pkg.fgi.part_local_invalidate(gs, roots)
     ids = np.sort(np.concatenate([x.part_export_ids() for x in gs]))

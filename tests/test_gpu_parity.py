@@ -91,8 +91,7 @@ def test_wave_layered_config1_shape(pkg, gpu_available):
 
 
 PATHS = {  # name -> (direction, dead filter)
-    "push_nofilter": (1, 0), "push": (1, 2), "push_default": (1, 1), "pull": (2, 1), "auto": (0, 2),
-    "auto_alpha2": (0, 1)}
+    "push_nofilter": (1, 0), "push": (1, 1), "pull": (2, 1), "auto": (0, 1), "auto_alpha2": (0, 1)}
 
 
 def _set_path(g, name):
