@@ -41,6 +41,10 @@
 #ifndef FGI_PULL_PREFETCH
 #define FGI_PULL_PREFETCH 1
 #endif
+// measurement builds: the dead-edge filter only on push levels of at least this many edges
+#ifndef FGI_FILTER_MIN
+#define FGI_FILTER_MIN 0
+#endif
 // measurement-only builds (make variant-exp EXP=<mask>): parts of a pull level skipped to attribute
 // its time (results are wrong): 1 tail scans, 2 survivor writes, 4 head probes, 8 visit/class gathers
 #ifndef FGI_EXP
@@ -763,9 +767,8 @@ __device__ __forceinline__ void expand_level(int L, uint64_t F, uint64_t T, uint
         }
         // edges to nodes visited earlier need neither the tag nor the gather (the bitmap is read
         // without synchronisation: a stale 0 only costs the gather and an atomic that finds the bit).
-        // Kept on small levels too: without it their edges into visited nodes each pay an atomic
-        // on the visit bitmap instead (A/B, profiles/r5a_ab: push levels 57 vs 60-67 us per wave)
-        if (x.dead_filter) {
+        // Kept on small levels too (make variant-filtermin measures the alternative)
+        if (x.dead_filter && T >= (uint64_t)FGI_FILTER_MIN) {
 #pragma unroll
             for (int j = 0; j < kEPT; ++j)
                 if (dst[j] != 0xFFFFFFFFu && bit_of(vis, dst[j])) dst[j] = 0xFFFFFFFFu;
