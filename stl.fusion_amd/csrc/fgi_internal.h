@@ -127,7 +127,6 @@ constexpr int kDoneGroups = 16;         // two-level completion counters (last-b
 constexpr int kDoneStride = 16;         // 128 B apart
 constexpr uint32_t kFinalBlocks = 1024; // grid of the final collect (invalidated bitmap -> list)
 constexpr uint32_t kHot = 65536;        // hot list heads (pull probes through an 8 KB snapshot)
-constexpr uint32_t kHotFlag = 0x80000000u;
 constexpr int kAccCount = 8;            // batch accumulators (fgi_run_batch; run_wave_coop's acc)
 
 // Per-level counters. The producers of level L's frontier (roots, push emits, received targets)
@@ -276,11 +275,13 @@ struct fgi_graph {
     uint32_t* cand_seg = nullptr;      // [pull grid + 1]
     uint32_t* wl = nullptr;            // [n_slots] a pull level's expandable winners, per block at cand_seg
     // Hot heads: the (at most kHot) handles that head the most lists get a rank; candidate entries
-    // name them as kHotFlag | rank, and a pull level probes them in hot_bm, a snapshot of their
+    // name them by a bit index past the bitmap's end (hot_w0), where a pull level finds a snapshot of their
     // invalidated bits taken before the level (8 KB: L1-resident) instead of the whole bitmap.
     uint32_t* hot_id = nullptr;        // [kHot] rank -> handle (FGI_NONE past n_hot)
-    uint32_t* hot_bm = nullptr;        // [kHot / 32]
     uint32_t n_hot = 0;
+    uint64_t hot_w0 = 0;               // the snapshot's first word in the bitmap a pull level probes
+                                       // (inv_bm, or a partition's front_global): kHot / 32 words
+                                       // allocated past its end; a hot head's code is 32 * hot_w0 + rank
     uint4* sv[2] = {nullptr, nullptr};
     uint32_t* sv_cnt[2] = {nullptr, nullptr};   // [pull grid] survivors per block
     uint64_t cand_cap = 0;

@@ -1076,23 +1076,25 @@ __global__ void k_hot_pick(uint32_t k_max, const uint64_t* __restrict__ sorted, 
     hot_rank[(uint32_t)key] = k;
 }
 
-__device__ __forceinline__ uint32_t head_code(uint32_t h, const uint32_t* hot_rank) {
+// a list head as the pull level probes it: its bit in the invalidated bitmap, or, for a hot head, its
+// bit in the snapshot that follows the bitmap (bit hot_bit0 + rank)
+__device__ __forceinline__ uint32_t head_code(uint32_t h, const uint32_t* hot_rank, uint32_t hot_bit0) {
     if (h == FGI_NONE || !hot_rank) return h;
     const uint32_t r = hot_rank[h];
-    return r != FGI_NONE ? (kHotFlag | r) : h;
+    return r != FGI_NONE ? (hot_bit0 + r) : h;
 }
 
 __global__ void k_cand_fill(uint32_t n, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos,
                             const uint64_t* __restrict__ uin_head, const uint32_t* __restrict__ uin_len,
-                            const uint32_t* __restrict__ row_len, const uint32_t* __restrict__ hot_rank, uint4* cand,
-                            unsigned long long* too_long) {
+                            const uint32_t* __restrict__ row_len, const uint32_t* __restrict__ hot_rank,
+                            uint32_t hot_bit0, uint4* cand, unsigned long long* too_long) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= n || !flag[d]) return;
     const uint32_t p = pos[d], rl = row_len[d];
     if (rl >> 31) atomicAdd(too_long, 1ull);
     const uint64_t h = uin_head[d];
-    cand[p] = make_uint4(d, (rl & 0x7FFFFFFFu) | (uin_len[d] > 2 ? 0x80000000u : 0u), head_code((uint32_t)h, hot_rank),
-                         head_code((uint32_t)(h >> 32), hot_rank));
+    cand[p] = make_uint4(d, (rl & 0x7FFFFFFFu) | (uin_len[d] > 2 ? 0x80000000u : 0u),
+                         head_code((uint32_t)h, hot_rank, hot_bit0), head_code((uint32_t)(h >> 32), hot_rank, hot_bit0));
 }
 
 // segment base of pull block b: the candidates before its first slot b * tpb * kPullTile
@@ -1373,12 +1375,13 @@ fgi_status build_candidates(fgi_graph* g) {
     uint32_t* hot_rank = nullptr;
     g->n_hot = 0;
     PartView pv;
-    const uint32_t NH = part_view(g, &pv) ? pv.n_global : g->n_handles;
-    if (NH < kHotFlag) {
-        if (!g->hot_id) {
-            FGI_TRY(dmalloc(g, &g->hot_id, kHot));
-            FGI_TRY(dmalloc(g, &g->hot_bm, kHot / 32));
-        }
+    const bool part = part_view(g, &pv);
+    const uint32_t NH = part ? pv.n_global : g->n_handles;
+    // the snapshot sits past the end of the bitmap a pull level probes (allocated with kHot / 32
+    // spare words): the single engine's invalidated bitmap, a partition's all-gathered one
+    g->hot_w0 = part ? pv.front_words_global : g->bm_words;
+    if (g->hot_w0 * 32 + kHot < (uint64_t)FGI_NONE) {
+        if (!g->hot_id) FGI_TRY(dmalloc(g, &g->hot_id, kHot));
         Tmp tc, tk0, tk1, tt;
         uint32_t* cnt;
         uint64_t *k0, *k1;
@@ -1402,7 +1405,7 @@ fgi_status build_candidates(fgi_graph* g) {
     }
     FGI_HIP(g, hipMemsetAsync(g->misc_dev + 15, 0, sizeof(unsigned long long), s));
     hipLaunchKernelGGL(k_cand_fill, dim3(nblk(N)), dim3(256), 0, s, N, flag, pos, g->uin_head, g->uin_len, g->row_len,
-                       hot_rank, g->cand, g->misc_dev + 15);
+                       hot_rank, (uint32_t)(g->hot_w0 * 32), g->cand, g->misc_dev + 15);
     hipLaunchKernelGGL(k_cand_seg, dim3(nblk(G + 1)), dim3(256), 0, s, G, (uint64_t)tpb * kPullTile, N, pos, total,
                        g->cand_seg);
     FGI_HIP(g, hipGetLastError());
@@ -1533,7 +1536,8 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
         dmalloc(g, &g->uin_head, g->n_slots + 1))
         return fail(FGI_ENOMEM);
     g->bm_words = (H + 63) / 64 * 2 + 2;
-    if (dmalloc(g, &g->vis_bm, g->bm_words) || dmalloc(g, &g->inv_bm, g->bm_words) ||
+    // the invalidated bitmap carries the hot heads' snapshot past its end (build_candidates)
+    if (dmalloc(g, &g->vis_bm, g->bm_words) || dmalloc(g, &g->inv_bm, g->bm_words + kHot / 32) ||
         dmalloc(g, &g->cls_bm, g->bm_words) || dmalloc(g, &g->uin_more, g->bm_words))
         return fail(FGI_ENOMEM);
     hipMemset(g->done, 0, (size_t)(kDoneGroups + 1) * kDoneStride * sizeof(unsigned long long));
@@ -1592,7 +1596,6 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->wl);
     dfree(g->cand_seg);
     dfree(g->hot_id);
-    dfree(g->hot_bm);
     for (int k = 0; k < 2; ++k) {
         dfree(g->sv[k]);
         dfree(g->sv_cnt[k]);

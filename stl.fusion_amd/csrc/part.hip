@@ -815,9 +815,10 @@ static fgi_status part_alloc(fgi_graph* g, uint32_t n_global) {
     if (hipMalloc(&p->v.send_cnt, (size_t)(W + 2) * 8) != hipSuccess) return fail("counts");
     if (hipMalloc(&p->all_cnt, (size_t)W * (W + 2) * 8) != hipSuccess) return fail("counts");
     if (hipMalloc(&p->scalar, 32) != hipSuccess) return fail("scalar");
-    p->v.front_words_global = (uint64_t)n_global / 32 + 2;
-    if (hipMalloc(&p->v.front_global, p->v.front_words_global * 4) != hipSuccess) return fail("frontier bitmap");
-    if (hipMemset(p->v.front_global, 0, p->v.front_words_global * 4) != hipSuccess) return fail("frontier bitmap");
+    // even, so the hot heads' snapshot past its end (kHot / 32 words, build_candidates) is 64-bit aligned
+    p->v.front_words_global = ((uint64_t)n_global / 32 + 3) & ~1ull;
+    if (hipMalloc(&p->v.front_global, (p->v.front_words_global + kHot / 32) * 4) != hipSuccess) return fail("frontier bitmap");
+    if (hipMemset(p->v.front_global, 0, (p->v.front_words_global + kHot / 32) * 4) != hipSuccess) return fail("frontier bitmap");
     if (hipMalloc(&p->v.scratch_u64, 32) != hipSuccess) return fail("scratch");
     if (hipMalloc(&p->weight, (size_t)n_global * 4) != hipSuccess) return fail("list weights");
     if (hipMalloc(&p->dbuf, (size_t)(block / 32 + 1) * 8) != hipSuccess ||

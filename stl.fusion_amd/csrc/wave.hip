@@ -156,6 +156,10 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 }
 
 __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+// set bits of the wave-uniform mask m below this lane (two mbcnt instructions)
+__device__ __forceinline__ uint32_t rank_in(unsigned long long m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 
 __device__ __forceinline__ unsigned long long block_sum(unsigned long long v, unsigned long long* s_red) {
 #pragma unroll
@@ -349,7 +353,7 @@ __device__ __forceinline__ void emit_push(Emit& e, uint32_t* buf, bool win, uint
     if (lane_id() == 0) base = atomicAdd(&e.n, (uint32_t)__popcll(m));
     base = __shfl(base, 0, 64);
     if (win) {
-        const uint32_t idx = base + (uint32_t)__popcll(m & lanemask_lt());
+        const uint32_t idx = base + rank_in(m);
         if (idx < CAP) {
             buf[idx] = h;
         } else {
@@ -478,7 +482,7 @@ __device__ __forceinline__ void msg_push(MsgEmit<true>& me, bool send, uint32_t 
     if (lane_id() == 0) base = atomicAdd(&me.n, (uint32_t)__popcll(m));
     base = __shfl(base, 0, 64);
     if (send) {
-        const uint32_t idx = base + (uint32_t)__popcll(m & lanemask_lt());
+        const uint32_t idx = base + rank_in(m);
         if (idx < kMsgCap) {
             me.d[idx] = dst;
         } else {
@@ -829,7 +833,6 @@ struct PullArgs {
     const uint32_t* front_rd;                // invalidated bitmap (multi-GPU: all-gathered, global ids)
     uint32_t* inv_bm;                        // this device's invalidated bitmap (owned words |= winners)
     const uint32_t* __restrict__ cls;        // expandable-class bitmap
-    const uint32_t* hot_bm;                  // the hot heads' invalidated bits (kHotFlag | rank)
     uint32_t* wl;                            // per block (at its segment base): expandable winners
     unsigned long long* bsum;                // [3][grid] per-block sums, then [3][grid] prefixes
     const uint32_t* __restrict__ cand_seg;   // [grid + 1] segment bases
@@ -878,11 +881,9 @@ struct WinSum {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// the bitmap word holding a list head's invalidated bit: a hot head's in the snapshot (the bit
-// index is the rank, whose low 5 bits the code keeps), any other in the invalidated bitmap
-__device__ __forceinline__ const uint32_t* head_word(const PullArgs& p, uint32_t h) {
-    return (h & kHotFlag) ? p.hot_bm + ((h & ~kHotFlag) >> 5) : p.front_rd + (h >> 5);
-}
+// the bitmap word holding a list head's invalidated bit: a hot head's code indexes the snapshot
+// that follows the invalidated bitmap (g->hot_w0), any other head the bitmap itself
+__device__ __forceinline__ const uint32_t* head_word(const PullArgs& p, uint32_t h) { return p.front_rd + (h >> 5); }
 
 // an entry past the list reads as a dead candidate at the block's first slot
 __device__ __forceinline__ uint4 load_cand(const uint4* p, bool in, uint32_t s_lo) {
@@ -938,7 +939,7 @@ __device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, 
         examined += (u2 != FGI_NONE ? 1u : 0u) + (u3 != FGI_NONE ? 1u : 0u);
         const bool more = in && !hit && len > 4;
         const unsigned long long mm = __ballot(more);
-        if (more) q[nlong + __popcll(mm & lanemask_lt())] = qi;   // below every entry still unread
+        if (more) q[nlong + rank_in(mm)] = qi;   // below every entry still unread
         nlong += (uint32_t)__popcll(mm);
         if (in && hit) {
             const uint32_t d = c.x, rel = (uint32_t)(d - s_lo);
@@ -952,7 +953,7 @@ __device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, 
             uint32_t sb = 0;
             if (lane == 0) sb = atomicAdd(&s.sn, (uint32_t)__popcll(sm));
             sb = __shfl(sb, 0, 64);
-            if (surv) p.sv[dst][seg + sb + (uint32_t)__popcll(sm & lanemask_lt())] = c;
+            if (surv) p.sv[dst][seg + sb + rank_in(sm)] = c;
         }
         tails += in ? 1u : 0u;
     }
@@ -1095,10 +1096,11 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
             const bool surv = lv[j] && !hit && !tail;
             live += lv[j] ? 1u : 0u;
             examined += (lv[j] ? 1u : 0u) + ((lv[j] && h1 != FGI_NONE && !b0) ? 1u : 0u);
+            bool win = false;
             if (hit) {
                 const uint32_t rel = d - (uint32_t)s_lo;
                 const uint32_t bit = 1u << (d & 31);
-                const bool win = (s.cs[rel >> 5] & bit) != 0;
+                win = (s.cs[rel >> 5] & bit) != 0;
                 if (win) {   // a winner's visit bit is folded in from wm at the write-back
                     atomicOr(&s.wm[rel >> 5], bit);
                     const uint32_t rl = aux & 0x7FFFFFFFu;
@@ -1110,16 +1112,16 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
                     flagged += first_visit(node[d]) == 2 ? 1u : 0u;
                 }
             }
-            const bool xw = hit && (aux & 0x7FFFFFFFu) && ((s.cs[(d - (uint32_t)s_lo) >> 5] >> (d & 31)) & 1u);
+            const bool xw = win && (aux & 0x7FFFFFFFu);
             const unsigned long long xm = __ballot(xw);
             if (xm) {
                 uint32_t xb = 0;
                 if (lane == 0) xb = atomicAdd(&s.wn, (uint32_t)__popcll(xm));
                 xb = __shfl(xb, 0, 64);
-                if (xw) p.wl[seg + xb + (uint32_t)__popcll(xm & lanemask_lt())] = d;
+                if (xw) p.wl[seg + xb + rank_in(xm)] = d;
             }
             const unsigned long long tm = __ballot(tail);
-            if (tail) wq[qn + __popcll(tm & lanemask_lt())] = i;
+            if (tail) wq[qn + rank_in(tm)] = i;
             qn += (uint32_t)__popcll(tm);
             const unsigned long long sm = __ballot(surv);
             if (sm) {
@@ -1127,7 +1129,7 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
                 if (lane == 0) sb = atomicAdd(&s.sn, (uint32_t)__popcll(sm));
                 sb = __shfl(sb, 0, 64);
 #if !(FGI_EXP & 2)
-                if (surv) p.sv[dst][seg + sb + (uint32_t)__popcll(sm & lanemask_lt())] = c[j];
+                if (surv) p.sv[dst][seg + sb + rank_in(sm)] = c[j];
 #endif
             }
         }
@@ -1736,7 +1738,7 @@ CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, const WaveParams& wp, i
     c.escan = g->escan[buf];
     c.cstart = g->cstart[buf];
     c.hot_id = g->hot_id;
-    c.hot_bm = g->hot_bm;
+    c.hot_bm = g->inv_bm + g->hot_w0;
     c.n_hot = g->n_hot;
     c.inv = g->inv_bm;
     return c;
@@ -1759,7 +1761,6 @@ PullArgs pull_args(fgi_graph* g, uint32_t n_slots, const uint32_t* front_rd) {
     p.inv_bm = g->inv_bm;
     p.wl = g->wl;
     p.cls = g->cls_bm;
-    p.hot_bm = g->hot_bm;
     p.bsum = g->bsum;
     p.cand_seg = g->cand_seg;
     p.c[0] = g->cand;
@@ -2156,8 +2157,10 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     const bool allow_pull = sums[3] == 0;
     const int direction = wp.direction;
     const RemoteArgs ra{pv.base, pv.n_local, pv.block, pv.world, pv.ver_all, pv.sent_bm, pv.send_buf, pv.send_cnt};
-    // the invalidated bitmap over all slots: all-gathered before pull levels (one rank: its own)
-    const uint32_t* front = coll ? pv.front_global : g->inv_bm;
+    // the invalidated bitmap over all slots: all-gathered before pull levels (one rank without
+    // collectives: its own words copied in, so the hot snapshot past its end is where the candidates
+    // expect it)
+    const uint32_t* front = pv.front_global;
     uint64_t f_global = sums[1], t_global = sums[2];
     const double avg_deg = (double)sums[0] / std::max<uint64_t>(1, pv.n_global);
     uint64_t levels = 0, e_trav = 0, f_total = 0, sent_total = 0, push_edges = 0, push_f = 0;
@@ -2176,9 +2179,11 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
         if (pull) {
             FGI_HIP(g, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&g->ctr->lvl[L % kRing].pull), 1, 1, s));
             if (coll) FGI_TRY(part_allgather_front(g));
+            else FGI_HIP(g, hipMemcpyAsync(pv.front_global, g->inv_bm, (size_t)pv.block / 32 * 4, hipMemcpyDeviceToDevice, s));
         }
         CollectArgs ca = collect_args(g, pv.n_local, wp, buf);
         ca.inv = front;   // hot heads are global ids
+        ca.hot_bm = pv.front_global + g->hot_w0;
         hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp, ca);
         if (g->opt_level_timing) FGI_HIP(g, hipEventRecord(g->ev[0], s));
         hipLaunchKernelGGL(k_level<true>, dim3(wp.grid), dim3(kBlock), 0, s, L, wp, expand_args(g, buf),
