@@ -87,7 +87,11 @@ typedef struct fgi_wave_stats {
     uint64_t roots;            /* root entries submitted */
     uint64_t levels;           /* BFS levels with a non-empty frontier */
     uint64_t v_inv;            /* Consistent -> Invalidated transitions (= expanded nodes) */
-    uint64_t e_trav;           /* sum of |_usedBy| over invalidated nodes (TEPS numerator) */
+    uint64_t e_trav;           /* sum of |_usedBy| over invalidated nodes (TEPS numerator). Exact on a
+                                  graph's first wave (and after fgi_restore / fgi_prune); after earlier
+                                  waves it also counts the entries RemoveUsedBy would have removed
+                                  (Computed.cs:387-398), which the engine drops lazily at the next prune,
+                                  so it can exceed the reference's count until then */
     uint64_t e_match;          /* traversed edges whose tag == version of the dst slot's node */
     uint64_t n_flagged;        /* visits that only set InvalidateOnSetOutput / DelayStarted */
     uint64_t alg_bytes;        /* algorithmic HBM bytes of the wave */

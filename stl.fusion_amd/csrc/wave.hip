@@ -156,6 +156,12 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 }
 
 __device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << lane_id()) - 1ull; }
+// lane 0's value in every lane (a scalar read; every lane of the wave active)
+__device__ __forceinline__ uint32_t from_lane0(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ unsigned long long from_lane0(unsigned long long v) {
+    return ((unsigned long long)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+           __builtin_amdgcn_readfirstlane((uint32_t)v);
+}
 // set bits of the wave-uniform mask m below this lane (two mbcnt instructions)
 __device__ __forceinline__ uint32_t rank_in(unsigned long long m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
@@ -322,7 +328,7 @@ __device__ __forceinline__ void emit_one(bool win, uint32_t h, const Out& o) {
     const unsigned long long ex = wave_excl_scan64(mine, tot);
     unsigned long long base = 0;
     if (lane_id() == 0 && tot) base = atomicAdd(&o.ln->ft, tot);
-    base = __shfl(base, 0, 64) + ex;
+    base = from_lane0(base) + ex;
     if (win && len) write_entry(o, base >> 32, base & 0xFFFFFFFFull, off, len);
 }
 
@@ -351,7 +357,7 @@ __device__ __forceinline__ void emit_push(Emit& e, uint32_t* buf, bool win, uint
     if (!m) return;
     uint32_t base = 0;
     if (lane_id() == 0) base = atomicAdd(&e.n, (uint32_t)__popcll(m));
-    base = __shfl(base, 0, 64);
+    base = from_lane0(base);
     if (win) {
         const uint32_t idx = base + rank_in(m);
         if (idx < CAP) {
@@ -480,7 +486,7 @@ __device__ __forceinline__ void msg_push(MsgEmit<true>& me, bool send, uint32_t 
     if (!m) return;
     uint32_t base = 0;
     if (lane_id() == 0) base = atomicAdd(&me.n, (uint32_t)__popcll(m));
-    base = __shfl(base, 0, 64);
+    base = from_lane0(base);
     if (send) {
         const uint32_t idx = base + rank_in(m);
         if (idx < kMsgCap) {
@@ -916,7 +922,7 @@ __device__ __forceinline__ void pull_hit(const PullArgs& p, PullLds& s, uint64_t
 // the ones whose list goes past entry 3 without a hit, 8 lanes per candidate over entries 4.. in
 // steps of 8 (early exit); the next candidate's list is located while the current one is scanned.
 // q (the wave's queue of candidate indices) is reused for pass 2's list.
-__device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, int dst, const unsigned long long* node,
+__device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, uint4* sv_out, const unsigned long long* node,
                                            uint64_t s_lo, uint64_t seg, uint32_t* q, uint32_t nq, PullLds& s,
                                            uint32_t& flagged, uint32_t& examined, uint32_t& tails, WinSum& ws) {
     const uint32_t lane = lane_id();
@@ -952,8 +958,8 @@ __device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, 
         if (sm) {
             uint32_t sb = 0;
             if (lane == 0) sb = atomicAdd(&s.sn, (uint32_t)__popcll(sm));
-            sb = __shfl(sb, 0, 64);
-            if (surv) p.sv[dst][seg + sb + rank_in(sm)] = c;
+            sb = from_lane0(sb);
+            if (surv) sv_out[sb + rank_in(sm)] = c;
         }
         tails += in ? 1u : 0u;
     }
@@ -992,7 +998,7 @@ __device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, 
                 pull_hit(p, s, s_lo, seg, d, win, c.y, ws);
                 if (!win) flagged += first_visit(node[d]) == 2 ? 1u : 0u;
             } else {
-                p.sv[dst][seg + atomicAdd(&s.sn, 1u)] = c;
+                sv_out[atomicAdd(&s.sn, 1u)] = c;
             }
         }
     }
@@ -1011,6 +1017,8 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
     const int dst = (int)(npull & 1);
     const uint4* src = p.c[sid];
     const uint32_t cnt = npull == 0 ? p.cand_seg[b + 1] - p.cand_seg[b] : p.sv_cnt[sid - 1][b];
+    uint4* const sv_out = p.sv[dst] + seg;     // this level's survivors (the block's segment)
+    uint32_t* const wl_out = p.wl + seg;       // this level's expandable winners
     // the first batch's entries are requested before the owned words are staged
     // (FGI_PULL_PREFETCH=0 builds the variant without the look-ahead, for measurement)
     uint4 c[4];
@@ -1117,8 +1125,8 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
             if (xm) {
                 uint32_t xb = 0;
                 if (lane == 0) xb = atomicAdd(&s.wn, (uint32_t)__popcll(xm));
-                xb = __shfl(xb, 0, 64);
-                if (xw) p.wl[seg + xb + rank_in(xm)] = d;
+                xb = from_lane0(xb);
+                if (xw) wl_out[xb + rank_in(xm)] = d;
             }
             const unsigned long long tm = __ballot(tail);
             if (tail) wq[qn + rank_in(tm)] = i;
@@ -1127,9 +1135,9 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
             if (sm) {
                 uint32_t sb = 0;
                 if (lane == 0) sb = atomicAdd(&s.sn, (uint32_t)__popcll(sm));
-                sb = __shfl(sb, 0, 64);
+                sb = from_lane0(sb);
 #if !(FGI_EXP & 2)
-                if (surv) p.sv[dst][seg + sb + rank_in(sm)] = c[j];
+                if (surv) sv_out[sb + rank_in(sm)] = c[j];
 #endif
             }
         }
@@ -1137,7 +1145,7 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
         if (base + kCandBatch >= cnt) PROBE(L, 7);
         if (qn > kWaveTailCap - kWaveBatch || base + kCandBatch >= cnt) {
             __builtin_amdgcn_wave_barrier();
-            pull_tails(p, src, dst, node, s_lo, seg, wq, (FGI_EXP & 1) ? 0u : qn, s, flagged, examined_tail, tails, ws);
+            pull_tails(p, src, sv_out, node, s_lo, seg, wq, (FGI_EXP & 1) ? 0u : qn, s, flagged, examined_tail, tails, ws);
             __builtin_amdgcn_wave_barrier();
             qn = 0;
         }
