@@ -126,7 +126,11 @@ constexpr int kPullTile = 1024;         // slots per pull tile (one block iterat
 constexpr int kDoneGroups = 16;         // two-level completion counters (last-block epilogues)
 constexpr int kDoneStride = 16;         // 128 B apart
 constexpr uint32_t kFinalBlocks = 1024; // grid of the final collect (invalidated bitmap -> list)
-constexpr uint32_t kHot = 65536;        // hot list heads (pull probes through an 8 KB snapshot)
+#ifndef FGI_HOT
+#define FGI_HOT 262144                  // measurement builds: make variant-hot HOT=<n> (a multiple of 256)
+#endif
+constexpr uint32_t kHot = FGI_HOT;      // most hot list heads (pull probes through a snapshot of kHot / 8 B)
+constexpr uint32_t kHotMin = 65536;     // fewest: 8 KB (a graph's count: build_candidates, hot_count)
 constexpr int kAccCount = 8;            // batch accumulators (fgi_run_batch; run_wave_coop's acc)
 
 // Per-level counters. The producers of level L's frontier (roots, push emits, received targets)

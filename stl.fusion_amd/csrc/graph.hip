@@ -1064,9 +1064,10 @@ __global__ void k_head_keys(uint32_t n, const uint32_t* __restrict__ cnt, uint64
 }
 
 // ranks 0..kHot-1 to the most frequent heads (keys sorted by count, descending)
-__global__ void k_hot_pick(uint32_t k_max, const uint64_t* __restrict__ sorted, uint32_t* hot_id, uint32_t* hot_rank) {
+__global__ void k_hot_pick(uint32_t k_max, uint32_t n_hot, const uint64_t* __restrict__ sorted, uint32_t* hot_id,
+                           uint32_t* hot_rank) {
     const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= kHot) return;
+    if (k >= n_hot) return;
     const uint64_t key = k < k_max ? sorted[k] : 0ull;
     if ((key >> 32) == 0) {
         hot_id[k] = FGI_NONE;
@@ -1333,6 +1334,15 @@ fgi_status build_in_heads(fgi_graph* g) {
 
 // The pull candidate segments for the graph's pull geometry (see fgi_internal.h). A graph too large
 // to pull on one device, or with a row of 2^31 entries or more, gets none (its waves push).
+// Hot heads for a graph of n handles: one per 512 handles, a power of two in [kHotMin, kHot]. A/B on
+// one box (profiles/r5e_ab.txt): 64 Ki -> 256 Ki heads took configs[2]'s pull levels from 1.105 to
+// 1.020 ms per wave; on configs[1] a snapshot past 64 Ki costs more to refresh than it saves.
+uint32_t hot_count(uint64_t n) {
+    uint32_t k = kHotMin;
+    while (k < kHot && k < n / 512) k <<= 1;
+    return k;
+}
+
 fgi_status build_candidates(fgi_graph* g) {
     g->cand_grid = 0;
     uint32_t G = 0, tpb = 0;
@@ -1398,10 +1408,11 @@ fgi_status build_candidates(fgi_graph* g) {
         char* st;
         FGI_TRY(tmalloc(g, tt, &st, sb));
         FGI_HIP(g, rocprim::radix_sort_keys_desc(st, sb, k0, k1, (size_t)NH, 0, 64, s));
-        hipLaunchKernelGGL(k_hot_pick, dim3(kHot / 256), dim3(256), 0, s, NH, k1, g->hot_id, hot_rank);
+        const uint32_t n_hot = hot_count(NH);
+        hipLaunchKernelGGL(k_hot_pick, dim3(n_hot / 256), dim3(256), 0, s, NH, n_hot, k1, g->hot_id, hot_rank);
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipStreamSynchronize(s));
-        g->n_hot = kHot;
+        g->n_hot = n_hot;
     }
     FGI_HIP(g, hipMemsetAsync(g->misc_dev + 15, 0, sizeof(unsigned long long), s));
     hipLaunchKernelGGL(k_cand_fill, dim3(nblk(N)), dim3(256), 0, s, N, flag, pos, g->uin_head, g->uin_len, g->row_len,

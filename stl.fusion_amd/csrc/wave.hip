@@ -308,12 +308,53 @@ struct Out {
     LevelCtr* ln;
 };
 
+// A frontier entry: its row (offset, length) and exclusive edge offset es, and the chunk map entries
+// of the fine chunks whose first edge lies in [es, es + len). Lane-local form (rare overflow paths).
 __device__ __forceinline__ void write_entry(const Out& o, uint64_t idx, uint64_t es, uint32_t off, uint32_t len) {
     o.nfr_off[idx] = off;
     o.nfr_len[idx] = len;
     o.nescan[idx] = es;
     const uint64_t c_lo = (es + kFine - 1) / kFine, c_hi = (es + len - 1) / kFine;
     for (uint64_t c = c_lo; c <= c_hi; ++c) o.ncstart[c] = (uint32_t)idx;
+}
+
+// The chunk map entries of one frontier entry per lane (has: the lane holds an entry, len > 0). A
+// hub's row spans thousands of fine chunks: a span longer than kSpanSerial chunks is written by the
+// whole wave, one lane per chunk, instead of by its own lane (a 1 M-edge row would otherwise be
+// ~4,000 dependent store issues in one lane, the push level's slowest block). Edge offsets < 2^32.
+// Every lane of the wave calls it.
+constexpr uint32_t kSpanSerial = 4;
+__device__ __forceinline__ void write_span(uint32_t* cstart, bool has, uint32_t idx, uint64_t es, uint32_t len) {
+    uint32_t c_lo = 0, c_hi = 0;
+    bool big = false;
+    if (has) {
+        c_lo = (uint32_t)((es + kFine - 1) / kFine);
+        c_hi = (uint32_t)((es + len - 1) / kFine);
+        if (c_hi + 1 - c_lo <= kSpanSerial) {
+            for (uint32_t c = c_lo; c <= c_hi; ++c) cstart[c] = idx;
+        } else {
+            big = true;
+        }
+    }
+    unsigned long long m = __ballot(big);
+    while (m) {   // wave-uniform
+        const int src = __builtin_ctzll(m);
+        m &= m - 1;
+        const uint32_t lo = __builtin_amdgcn_readlane(c_lo, src), hi = __builtin_amdgcn_readlane(c_hi, src);
+        const uint32_t id = __builtin_amdgcn_readlane(idx, src);
+        for (uint32_t c = lo + lane_id(); c <= hi; c += 64) cstart[c] = id;
+    }
+}
+
+// write_entry for one entry per lane; every lane of the wave calls it
+__device__ __forceinline__ void write_entry_wave(const Out& o, bool has, uint64_t idx, uint64_t es, uint32_t off,
+                                                 uint32_t len) {
+    if (has) {
+        o.nfr_off[idx] = off;
+        o.nfr_len[idx] = len;
+        o.nescan[idx] = es;
+    }
+    write_span(o.ncstart, has, (uint32_t)idx, es, len);
 }
 
 __device__ __forceinline__ void mark_invalidated(uint32_t* inv_bm, uint32_t h) { atomicOr(inv_bm + (h >> 5), 1u << (h & 31)); }
@@ -329,7 +370,7 @@ __device__ __forceinline__ void emit_one(bool win, uint32_t h, const Out& o) {
     unsigned long long base = 0;
     if (lane_id() == 0 && tot) base = atomicAdd(&o.ln->ft, tot);
     base = from_lane0(base) + ex;
-    if (win && len) write_entry(o, base >> 32, base & 0xFFFFFFFFull, off, len);
+    write_entry_wave(o, win && len, base >> 32, base & 0xFFFFFFFFull, off, len);
 }
 
 // Block-level emission: winners are staged in LDS (buf) and appended in batches: one packed
@@ -427,10 +468,10 @@ __device__ __forceinline__ void emit_flush(Emit& e, uint32_t* buf, uint32_t at, 
     uint64_t idx = (e.base >> 32) + be + wex_e;
     uint64_t es = (e.base & 0xFFFFFFFFull) + bl + wex_l;
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
+    for (int k = 0; k < kPer; ++k) {   // block-uniform: every lane calls write_entry_wave
         const uint32_t i = threadIdx.x + k * kBlock;
+        uint32_t len = 0, off = 0;
         if (i < n) {
-            uint32_t len, off;
             if constexpr (kStage2) {
                 off = buf[i];
                 len = buf[kChunk + i];
@@ -439,11 +480,11 @@ __device__ __forceinline__ void emit_flush(Emit& e, uint32_t* buf, uint32_t at, 
                 len = o.row_len[h];   // an L2 hit now
                 off = len ? (uint32_t)o.row_off[h] : 0u;
             }
-            if (len) {
-                write_entry(o, idx, es, off, len);
-                ++idx;
-                es += len;
-            }
+        }
+        write_entry_wave(o, len != 0, idx, es, off, len);
+        if (len) {
+            ++idx;
+            es += len;
         }
     }
     __syncthreads();
@@ -666,14 +707,13 @@ __global__ __launch_bounds__(kCollectThreads) void k_collect(int L, WaveCtr* ctr
             const uint32_t off = in ? (uint32_t)c.row_off[d] : 0u;   // pool positions are < 2^32
             uint32_t tot;
             const uint32_t ex = wave_excl_scan(len, tot);
+            const uint64_t idx = e0 + i, e = es + ex;
             if (in) {
-                const uint64_t idx = e0 + i, e = es + ex;
                 c.fr_off[idx] = off;
                 c.fr_len[idx] = len;
                 c.escan[idx] = e;
-                const uint64_t c_lo = (e + kFine - 1) / kFine, c_hi = (e + len - 1) / kFine;
-                for (uint64_t q = c_lo; q <= c_hi; ++q) c.cstart[q] = (uint32_t)idx;
             }
+            write_span(c.cstart, in && len, (uint32_t)idx, e, len);
             es += tot;
         }
     }
@@ -1016,7 +1056,10 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
     const int sid = npull == 0 ? 0 : 1 + (int)((npull - 1) & 1);
     const int dst = (int)(npull & 1);
     const uint4* src = p.c[sid];
-    const uint32_t cnt = npull == 0 ? p.cand_seg[b + 1] - p.cand_seg[b] : p.sv_cnt[sid - 1][b];
+    // a block's survivors are a subset of its candidate segment: the count read back is clamped to it,
+    // so a corrupt count cannot walk into the next block's segment
+    const uint32_t seg_n = (uint32_t)(p.cand_seg[b + 1] - seg);
+    const uint32_t cnt = npull == 0 ? seg_n : min(p.sv_cnt[sid - 1][b], seg_n);
     uint4* const sv_out = p.sv[dst] + seg;     // this level's survivors (the block's segment)
     uint32_t* const wl_out = p.wl + seg;       // this level's expandable winners
     // the first batch's entries are requested before the owned words are staged
