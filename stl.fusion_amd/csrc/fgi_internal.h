@@ -130,7 +130,14 @@ constexpr uint32_t kFinalBlocks = 1024; // grid of the final collect (invalidate
 #define FGI_HOT 262144                  // measurement builds: make variant-hot HOT=<n> (a multiple of 256)
 #endif
 constexpr uint32_t kHot = FGI_HOT;      // most hot list heads (pull probes through a snapshot of kHot / 8 B)
-constexpr uint32_t kHotMin = 65536;     // fewest: 8 KB (a graph's count: build_candidates, hot_count)
+#ifndef FGI_LDS_HOT
+#define FGI_LDS_HOT 2048                // measurement builds: make variant-ldshot LDSHOT=<words>
+#endif
+constexpr uint32_t kLdsHot = FGI_LDS_HOT;   // hot snapshot words a pull block keeps in LDS (8 KB)
+// fewest hot heads: 8 KB, or what the LDS copy holds (a graph's count: build_candidates, hot_count)
+constexpr uint32_t kHotMin = kLdsHot * 32 > 65536 ? kLdsHot * 32 : 65536;
+// resident k_level blocks per CU: LDS-bound once the LDS snapshot passes 8 KB (160 KB per CU)
+constexpr uint32_t kLevelOcc = kLdsHot <= 2048 ? 5 : kLdsHot <= 4096 ? 4 : 3;
 constexpr int kAccCount = 8;            // batch accumulators (fgi_run_batch; run_wave_coop's acc)
 
 // Per-level counters. The producers of level L's frontier (roots, push emits, received targets)

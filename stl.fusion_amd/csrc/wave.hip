@@ -155,7 +155,6 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
     return v;
 }
 
-__device__ __forceinline__ unsigned long long lanemask_lt() { return (1ull << lane_id()) - 1ull; }
 // lane 0's value in every lane (a scalar read; every lane of the wave active)
 __device__ __forceinline__ uint32_t from_lane0(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
 __device__ __forceinline__ unsigned long long from_lane0(unsigned long long v) {
@@ -245,14 +244,19 @@ __device__ bool last_block(unsigned long long* done, uint64_t G) {
     return last;
 }
 
-// Called by the last block: exclusive prefixes over blocks of `ncols` (<= 3) columns
-// src[q * G + k] into dst[q * G + k], column totals into tot[q]. In rounds of kBlock * kEpiloguePer
-// blocks (one round up to 2,048 blocks): every value of a round is read at once (thread t holds
-// kEpiloguePer consecutive blocks of every column; the reads are agent-scope atomics, performed at
-// the coherence point, each a round trip), then one block scan per column, carried across rounds.
+// Called by the last block: exclusive prefixes over blocks of three columns, packed per block in
+// src[k] (bits 48-63, 32-47, 0-31: pack3), into dst[q * G + k], column totals into tot[q]. In rounds
+// of kBlock * kEpiloguePer blocks (one round up to 2,048 blocks): every word of a round is read at
+// once (thread t holds kEpiloguePer consecutive blocks; the reads are agent-scope atomics, performed
+// at the coherence point, each a round trip: one CU's atomics are the epilogue's cost, so the columns
+// are read as one word), then one block scan per column, carried across rounds.
 constexpr uint32_t kEpiloguePer = 8;
-__device__ void prefix_columns(unsigned long long* src, unsigned long long* dst, int ncols, uint64_t G,
-                               unsigned long long* tot, unsigned long long* s_red) {
+__host__ __device__ constexpr unsigned long long pack3(unsigned long long a, unsigned long long b, unsigned long long c) {
+    return (a << 48) | (b << 32) | c;
+}
+__device__ void prefix_columns(unsigned long long* src, unsigned long long* dst, uint64_t G, unsigned long long* tot) {
+    constexpr int ncols = 3;
+    __shared__ unsigned long long s_sc[3][kBlock / 64];
     const uint32_t lane = lane_id(), wid = threadIdx.x >> 6, W = blockDim.x >> 6;
     const uint64_t R = (uint64_t)blockDim.x * kEpiloguePer;
     unsigned long long carry[3] = {0, 0, 0};
@@ -260,25 +264,30 @@ __device__ void prefix_columns(unsigned long long* src, unsigned long long* dst,
         const uint64_t k0 = r0 + (uint64_t)threadIdx.x * kEpiloguePer;
         unsigned long long xs[3][kEpiloguePer];
 #pragma unroll
-        for (int q = 0; q < 3; ++q)
-#pragma unroll
-            for (uint32_t j = 0; j < kEpiloguePer; ++j)
-                xs[q][j] = (q < ncols && k0 + j < G) ? coh_read(src + q * G + k0 + j) : 0ull;
+        for (uint32_t j = 0; j < kEpiloguePer; ++j) {
+            const unsigned long long v = k0 + j < G ? coh_read(src + k0 + j) : 0ull;
+            xs[0][j] = v >> 48;
+            xs[1][j] = (v >> 32) & 0xFFFFull;
+            xs[2][j] = v & 0xFFFFFFFFull;
+        }
+        // the three columns' wave scans share one pair of barriers
+        unsigned long long x[3];
 #pragma unroll
         for (int q = 0; q < 3; ++q) {
-            if (q >= ncols) break;
             unsigned long long loc = 0;
 #pragma unroll
             for (uint32_t j = 0; j < kEpiloguePer; ++j) loc += xs[q][j];
             unsigned long long t;
-            const unsigned long long x = wave_excl_scan64(loc, t);
-            __syncthreads();
-            if (lane == 0) s_red[wid] = t;
-            __syncthreads();
-            unsigned long long run = carry[q] + x, all = 0;
+            x[q] = wave_excl_scan64(loc, t);
+            if (lane == 0) s_sc[q][wid] = t;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            unsigned long long run = carry[q] + x[q], all = 0;
             for (uint32_t j = 0; j < W; ++j) {
-                if (j < wid) run += s_red[j];
-                all += s_red[j];
+                if (j < wid) run += s_sc[q][j];
+                all += s_sc[q][j];
             }
 #pragma unroll
             for (uint32_t j = 0; j < kEpiloguePer; ++j)
@@ -288,6 +297,7 @@ __device__ void prefix_columns(unsigned long long* src, unsigned long long* dst,
                 }
             carry[q] += all;
         }
+        __syncthreads();   // s_sc is rewritten by the next round
     }
     if (threadIdx.x == 0)
         for (int q = 0; q < ncols; ++q) tot[q] = carry[q];
@@ -414,6 +424,23 @@ __device__ __forceinline__ void emit_push(Emit& e, uint32_t* buf, bool win, uint
     }
 }
 
+// Push chunks: the winner's row (offset, length) was gathered right after its visit (and its
+// invalidated bit set there), so the flush reads both from LDS. A chunk stages at most kChunk
+// winners: offsets in buf[0, kChunk), lengths in buf[kChunk, 2 kChunk). Every lane of the calling
+// wave must call it.
+__device__ __forceinline__ void emit_push_row(Emit& e, uint32_t* buf, bool win, uint32_t off, uint32_t len) {
+    const unsigned long long m = __ballot(win);
+    if (!m) return;
+    uint32_t base = 0;
+    if (lane_id() == 0) base = atomicAdd(&e.n, (uint32_t)__popcll(m));
+    base = from_lane0(base);
+    if (win) {
+        const uint32_t idx = base + rank_in(m);
+        buf[idx] = off;
+        buf[kChunk + idx] = len;
+    }
+}
+
 // Block-uniform call. Flushes when at least `at` winners are staged (at = 1: flush anything).
 // Pass 1: every thread's entries (i = tid + k * kBlock) — invalidated bit, row length; one block
 // scan of (entries with rows, edges) and one packed reservation. Pass 2: the entries in the same
@@ -424,23 +451,23 @@ __device__ __forceinline__ void emit_flush(Emit& e, uint32_t* buf, uint32_t at, 
     const uint32_t n = e.n < CAP ? e.n : CAP;
     __syncthreads();   // every thread has read e.n before any wave can push again
     if (n < at || n == 0) return;   // uniform decision
-    constexpr int kPer = CAP / kBlock;
-    // a push chunk stages at most kChunk winners: pass 1 gathers each winner's row offset with its
-    // length and keeps both in the buffer's two halves (pass 2 then writes without a gather)
+    // a push chunk stages each winner's row offset and length (emit_push_row): no gathers here, and
+    // at most kChunk of them
     constexpr bool kStage2 = CAP == kChunkEmitCap;
+    constexpr int kPer = (kStage2 ? kChunk : CAP) / kBlock;
     static_assert(!kStage2 || 2 * kChunk <= CAP, "push winners fit half the buffer");
     uint32_t cnt = 0, lsum = 0;
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
         const uint32_t i = threadIdx.x + k * kBlock;
         if (i < n) {
-            const uint32_t h = buf[i];
-            mark_invalidated(o.inv_bm, h);
-            const uint32_t len = o.row_len[h];
+            uint32_t len;
             if constexpr (kStage2) {
-                const uint32_t off = (uint32_t)o.row_off[h];   // pool positions are < 2^32
-                buf[i] = off;
-                buf[kChunk + i] = len;
+                len = buf[kChunk + i];
+            } else {
+                const uint32_t h = buf[i];
+                mark_invalidated(o.inv_bm, h);
+                len = o.row_len[h];
             }
             cnt += len ? 1u : 0u;
             lsum += len;
@@ -848,12 +875,25 @@ __device__ __forceinline__ void expand_level(int L, uint64_t F, uint64_t T, uint
                 else if (r == 2) ++flagged;
             }
         }
+        // a winner's invalidated bit and its row, requested as soon as its visit has returned (the
+        // flush then needs no gather round trip)
+        uint32_t rl[kEPT], ro[kEPT];
+#pragma unroll
+        for (int j = 0; j < kEPT; ++j) {
+            rl[j] = 0;
+            ro[j] = 0;
+            if ((win_mask >> j) & 1u) {
+                mark_invalidated(o.inv_bm, dst[j]);
+                rl[j] = o.row_len[dst[j]];
+                ro[j] = (uint32_t)o.row_off[dst[j]];   // pool positions are < 2^32
+            }
+        }
         // the chunk's winners (at most cedges) are staged over the chunk map, flushed before the
         // next chunk refills it
         __syncthreads();
         PROBE(L, 6);
 #pragma unroll
-        for (int j = 0; j < kEPT; ++j) emit_push<kChunkEmitCap>(em, eb, (win_mask >> j) & 1u, dst[j], o);
+        for (int j = 0; j < kEPT; ++j) emit_push_row(em, eb, (win_mask >> j) & 1u, ro[j], rl[j]);
         emit_flush<kChunkEmitCap>(em, eb, 1, o);
         PROBE(L, 7);
         if constexpr (PART) msg_flush(me, kMsgCap / 2, ra);
@@ -877,6 +917,8 @@ struct PullArgs {
     const uint32_t* __restrict__ uin_len;
     const uint32_t* __restrict__ uin_src;
     const uint32_t* front_rd;                // invalidated bitmap (multi-GPU: all-gathered, global ids)
+    uint32_t hot_bit0;                       // a hot head's code: hot_bit0 + rank (its snapshot bit)
+    uint32_t hot_lds;                        // hot snapshot words staged into LDS per block (<= kLdsHot)
     uint32_t* inv_bm;                        // this device's invalidated bitmap (owned words |= winners)
     const uint32_t* __restrict__ cls;        // expandable-class bitmap
     uint32_t* wl;                            // per block (at its segment base): expandable winners
@@ -908,6 +950,7 @@ constexpr uint32_t kWaveTailCap = kTailCap / (kBlock / 64);   // queued candidat
 // visits / winners / classes of the owned tiles in LDS: 32-bit words (two lanes of a wave that
 // share a word serialise their atomics; narrower words halve how many do)
 struct PullLds {
+    uint32_t hot[kLdsHot];                          // the hot heads' snapshot (first hot_lds words)
     uint32_t vm[kOwnWords];                         // visits: the level's start, | this level's non-winners
     uint32_t wm[kOwnWords];                         // winners
     uint32_t cs[kOwnWords];                         // expandable class (read only)
@@ -917,7 +960,10 @@ struct PullLds {
 
 // k_level's LDS (32-bit words): push — the chunk map, then the chunk's winners; pull — the tail queue
 // (kTailCap) and PullLds at kChunk + 4
-constexpr uint32_t kLevelLds = std::max<uint32_t>(kChunkEmitCap + 8, kChunk + 4 + (sizeof(PullLds) + 3) / 4);
+// the multi-GPU push's per-owner staging (MsgEmit<true>) follows the push region
+constexpr uint32_t kPushLds = kChunkEmitCap + 8;
+constexpr uint32_t kLevelLds =
+    std::max<uint32_t>(kPushLds + (sizeof(MsgEmit<true>) + 7) / 8 * 2, kChunk + 4 + (sizeof(PullLds) + 3) / 4);
 
 // a thread's winners: count, those with a non-empty row, their row lengths
 struct WinSum {
@@ -928,8 +974,13 @@ struct WinSum {
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // the bitmap word holding a list head's invalidated bit: a hot head's code indexes the snapshot
-// that follows the invalidated bitmap (g->hot_w0), any other head the bitmap itself
-__device__ __forceinline__ const uint32_t* head_word(const PullArgs& p, uint32_t h) { return p.front_rd + (h >> 5); }
+// that follows the invalidated bitmap (g->hot_w0), any other head the bitmap itself. The snapshot's
+// first hot_lds words are read from the block's LDS copy: a random probe of an L2-resident bitmap
+// costs ~4x an L1 hit and ~5x an LDS read (profiles/r5f_probe_rate.txt, r5g_snap_rate.txt)
+__device__ __forceinline__ uint32_t head_bits(const PullArgs& p, const PullLds& s, uint32_t h) {
+    const uint32_t r = (h - p.hot_bit0) >> 5;   // wraps past hot_lds for a cold head
+    return r < p.hot_lds ? s.hot[r] : p.front_rd[h >> 5];
+}
 
 // an entry past the list reads as a dead candidate at the block's first slot
 __device__ __forceinline__ uint4 load_cand(const uint4* p, bool in, uint32_t s_lo) {
@@ -1076,13 +1127,20 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
         const uint64_t w_lo = s_lo >> 5, w_end = ((uint64_t)p.n_slots + 31) >> 5;
         const uint32_t nw = 2 * wp.tpb * kTileWords;
         constexpr uint32_t kPer = kOwnWords / kBlock;
-        uint32_t vv[kPer], cc[kPer];
+        constexpr uint32_t kHotPer = kLdsHot / kBlock;
+        uint32_t vv[kPer], cc[kPer], hh[kHotPer];
 #pragma unroll
         for (uint32_t k = 0; k < kPer; ++k) {
             const uint32_t i = threadIdx.x + k * kBlock;
             const bool in = i < nw && w_lo + i < w_end;
             vv[k] = in ? vis[w_lo + i] : ~0u;
             cc[k] = in ? p.cls[w_lo + i] : 0u;
+        }
+        const uint32_t* hot = p.front_rd + (p.hot_bit0 >> 5);
+#pragma unroll
+        for (uint32_t k = 0; k < kHotPer; ++k) {
+            const uint32_t i = threadIdx.x + k * kBlock;
+            hh[k] = i < p.hot_lds ? hot[i] : 0u;
         }
 #pragma unroll
         for (uint32_t k = 0; k < kPer; ++k) {
@@ -1093,6 +1151,8 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
                 s.wm[i] = 0;
             }
         }
+#pragma unroll
+        for (uint32_t k = 0; k < kHotPer; ++k) s.hot[threadIdx.x + k * kBlock] = hh[k];
     }
     if (threadIdx.x == 0) {
         s.sn = 0;
@@ -1122,8 +1182,8 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
             f0[j] = (lv[j] && (c[j].z & 1)) ? ~0u : 0u;
             f1[j] = 0u;
 #else
-            f0[j] = lv[j] ? *head_word(p, c[j].z) : 0u;
-            f1[j] = (lv[j] && c[j].w != FGI_NONE) ? *head_word(p, c[j].w) : 0u;
+            f0[j] = lv[j] ? head_bits(p, s, c[j].z) : 0u;
+            f1[j] = (lv[j] && c[j].w != FGI_NONE) ? head_bits(p, s, c[j].w) : 0u;
 #endif
         }
         uint4 cn[4];
@@ -1234,19 +1294,17 @@ __device__ __forceinline__ void pull_epilogue(int L, const PullArgs& p, LevelCtr
                                               const unsigned long long (&bs)[3], unsigned long long* s_red) {
     __shared__ unsigned long long s_tot[3];
     const uint64_t G = gridDim.x;
-    // per-thread partial sums -> the block's sums
+    // per-thread partial sums -> the block's sums, one packed word: a block owns at most
+    // kMaxIter * kPullTile = 32,768 slots (winners < 2^16) and its winners' rows hold < 2^32 edges
+    static_assert(kMaxIter * kPullTile < 65536, "pull block sums pack into 16 bits");
     const unsigned long long b0 = block_sum(bs[0], s_red), b1 = block_sum(bs[1], s_red), b2 = block_sum(bs[2], s_red);
-    if (threadIdx.x == 0) {
-        coh_xchg(p.bsum + blockIdx.x, b0);
-        coh_xchg(p.bsum + G + blockIdx.x, b1);
-        coh_xchg(p.bsum + 2 * G + blockIdx.x, b2);
-    }
+    if (threadIdx.x == 0) coh_xchg(p.bsum + blockIdx.x, pack3(b0, b1, b2));
     PROBE(L, 5);
     if (!last_block(done, gridDim.x)) {
         PROBE(L, 6);
         return;
     }
-    prefix_columns(p.bsum, p.bsum + 3 * G, 3, G, s_tot, s_red);
+    prefix_columns(p.bsum, p.bsum + 3 * G, G, s_tot);
     __syncthreads();
     if (threadIdx.x == 0) {
         ln->w = s_tot[0];
@@ -1258,7 +1316,7 @@ __device__ __forceinline__ void pull_epilogue(int L, const PullArgs& p, LevelCtr
 
 // One level's traversal: push (expand) or pull, as decided for the level on the device.
 template <bool PART>
-__global__ __launch_bounds__(kBlock, 5) void k_level(int L, WaveParams wp, ExpandArgs x, PullArgs p,
+__global__ __launch_bounds__(kBlock, kLevelOcc) void k_level(int L, WaveParams wp, ExpandArgs x, PullArgs p,
                                                   const unsigned long long* node, uint32_t* vis, Out o, WaveCtr* ctr,
                                                   unsigned long long* blk, unsigned long long* done, RemoteArgs ra) {
     // push: the chunk map (s_rel, s_base), then the chunk's winners over it; pull: queue + buffers
@@ -1266,10 +1324,11 @@ __global__ __launch_bounds__(kBlock, 5) void k_level(int L, WaveParams wp, Expan
     uint32_t* s_rel = s_x;                    // [kChunk + 1]
     uint32_t* s_base = s_x + kChunk + 4;      // [kChunk + 2], 16-byte aligned
     __shared__ Emit em;
-    __shared__ MsgEmit<PART> me;
+    MsgEmit<PART>& me = *reinterpret_cast<MsgEmit<PART>*>(s_x + kPushLds);   // push levels only
     __shared__ unsigned long long s_st[kBlock / 64][kStats];
     __shared__ unsigned long long s_red[kBlock / 64];
     static_assert(sizeof(PullLds) <= (kLevelLds - kChunk - 4) * 4 && kTailCap <= kChunk, "pull LDS");
+    static_assert(kPushLds % 2 == 0 && (kPushLds + sizeof(MsgEmit<true>) / 4) <= kLevelLds, "push LDS");
     PROBE(L, 0);
     LevelCtr& lc = ctr->lvl[L % kRing];
     o.ln = &ctr->lvl[(L + 1) % kRing];
@@ -1731,12 +1790,12 @@ static_assert(kFinalBlocks <= kLevelGridMax, "epilogue geometry");
 
 }  // namespace
 
-// 5 resident blocks per CU (k_level launch bounds); a pull block owns at most kMaxIter tiles, so a
+// kLevelOcc resident blocks per CU (k_level launch bounds); a pull block owns at most kMaxIter tiles, so a
 // larger graph gets more blocks, up to kLevelGridMax (134M slots per device); beyond that, no pull.
 // FGI_OPT_PULL_TPB fixes the tiles per block instead (tests: every grid takes the same results).
 void pull_geometry(const fgi_graph* g, uint32_t* grid, uint32_t* tpb) {
     const uint64_t n_tiles = ((uint64_t)g->n_slots + kPullTile - 1) / kPullTile;
-    uint64_t G = std::min<uint64_t>((uint64_t)g->n_cu * 5, kLevelGridMax);
+    uint64_t G = std::min<uint64_t>((uint64_t)g->n_cu * kLevelOcc, kLevelGridMax);
     uint64_t t = (n_tiles + G - 1) / G;
     if (g->opt_pull_tpb > 0) {
         t = std::min<uint64_t>((uint64_t)g->opt_pull_tpb, kMaxIter);
@@ -1760,7 +1819,7 @@ WaveParams wave_params(fgi_graph* g, int multi, int direction, uint64_t total_ed
     wp.stay_pull_f = g->opt_pull_beta > 0 ? n_beta / (uint64_t)g->opt_pull_beta : ~0ull;
     pull_geometry(g, &wp.grid, &wp.tpb);
     if (wp.grid == 0) {   // no pull levels: the traversal grid of a push level
-        wp.grid = std::min<uint32_t>((uint32_t)g->n_cu * 5, kLevelGridMax);
+        wp.grid = std::min<uint32_t>((uint32_t)g->n_cu * kLevelOcc, kLevelGridMax);
         wp.tpb = 0;
         if (wp.direction != 1) wp.direction = 1;
     }
@@ -1809,6 +1868,8 @@ PullArgs pull_args(fgi_graph* g, uint32_t n_slots, const uint32_t* front_rd) {
     p.uin_len = g->uin_len;
     p.uin_src = g->uin_src;
     p.front_rd = front_rd;
+    p.hot_bit0 = (uint32_t)(g->hot_w0 * 32);
+    p.hot_lds = std::min<uint32_t>(g->n_hot / 32, kLdsHot);
     p.inv_bm = g->inv_bm;
     p.wl = g->wl;
     p.cls = g->cls_bm;
