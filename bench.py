@@ -355,6 +355,9 @@ def main():
         "gteps": gteps,
         "v_inv_per_step": st.v_inv // args.steps,
         "e_trav_per_step": st.e_trav // args.steps,
+        "e_trav_semantics": ("sum of |_usedBy| over the invalidated nodes at wave start; rows keep RemoveUsedBy'd "
+                             "entries until the next prune, so later waves of a mutated graph count them. Here every "
+                             "timed wave runs on the freshly built graph (restore only), which has none"),
         "levels_per_step": st.levels / args.steps,
         "wave_kernel_ms": st.kernel_ms / args.steps,
         "wave_alg_gbs": wave_gbs,
@@ -401,8 +404,15 @@ def main():
         result["e2e"] = e2e
     try:
         rv, rpath = pkg.fgi.rccl_info()
-        result["rccl"] = {"version": rv, "path": rpath}
+        # libfgi links /opt/rocm's librccl (csrc/Makefile); a process that loaded torch first resolves
+        # the nccl symbols to torch's bundled copy instead
+        linked = "/opt/rocm"
+        differs = not os.path.realpath(rpath).startswith(os.path.realpath(linked))
+        result["rccl"] = {"version": rv, "path": rpath, "linked": linked + "/lib/librccl.so", "differs_from_linked": differs}
         log(f"[rank {rank}] libfgi RCCL: ncclGetVersion {rv} from {rpath}")
+        if differs:
+            log(f"[rank {rank}] WARNING: libfgi is bound to {rpath}, not the librccl it links ({linked}/lib); "
+                "a host that does not load torch first runs /opt/rocm's RCCL")
     except Exception as e:  # informational only
         result["rccl"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu and cfg["kind"] == "rmat":

@@ -1077,26 +1077,67 @@ __global__ void k_hot_pick(uint32_t k_max, uint32_t n_hot, const uint64_t* __res
     hot_rank[(uint32_t)key] = k;
 }
 
-// a list head as the pull level probes it: its bit in the invalidated bitmap, or, for a hot head, its
-// bit in the snapshot that follows the bitmap (bit hot_bit0 + rank)
-__device__ __forceinline__ uint32_t head_code(uint32_t h, const uint32_t* hot_rank, uint32_t hot_bit0) {
+// the cold heads (heads that are not hot) of handles [64 w, 64 w + 64): one word per wave
+__global__ void k_ch_mask(uint32_t n, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ hot_rank,
+                          unsigned long long* mask, uint32_t* pop) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool c = u < n && cnt[u] != 0 && (FGI_HEAD_FREQ || hot_rank[u] == FGI_NONE);
+    const unsigned long long m = __ballot(c);
+    if ((threadIdx.x & 63) == 0 && u < ((n + 63u) & ~63u)) {
+        mask[u >> 6] = m;
+        pop[u >> 6] = (uint32_t)__popcll(m);
+    }
+}
+
+// a list head as the pull level probes it: for a hot head, its bit in the snapshot that follows the
+// bitmap (bit hot_bit0 + rank); for a cold head (ch_mask), its bit in the cold-head bitmap (bit
+// ch_bit0 + its rank among the cold heads); otherwise (partitions) its bit in the bitmap itself
+__device__ __forceinline__ uint32_t head_code(uint32_t h, const uint32_t* hot_rank, uint32_t hot_bit0,
+                                              const unsigned long long* ch_mask, const uint32_t* ch_base,
+                                              uint32_t ch_bit0, const uint32_t* ch_rank) {
     if (h == FGI_NONE || !hot_rank) return h;
+    if (ch_rank && ch_mask) {   // FGI_HEAD_FREQ: every head by its rank
+        const unsigned long long m = ch_mask[h >> 6];
+        const uint32_t b = h & 63;
+        if (!((m >> b) & 1ull)) return h;
+        return hot_bit0 + ch_rank[ch_base[h >> 6] + (uint32_t)__popcll(m & ((1ull << b) - 1ull))];
+    }
     const uint32_t r = hot_rank[h];
-    return r != FGI_NONE ? (hot_bit0 + r) : h;
+    if (r != FGI_NONE) return hot_bit0 + r;
+    if (!ch_mask) return h;
+    const unsigned long long m = ch_mask[h >> 6];
+    const uint32_t b = h & 63;
+    if (!((m >> b) & 1ull)) return h;
+    return ch_bit0 + ch_base[h >> 6] + (uint32_t)__popcll(m & ((1ull << b) - 1ull));
 }
 
 __global__ void k_cand_fill(uint32_t n, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos,
                             const uint64_t* __restrict__ uin_head, const uint32_t* __restrict__ uin_len,
                             const uint32_t* __restrict__ row_len, const uint32_t* __restrict__ hot_rank,
-                            uint32_t hot_bit0, uint4* cand, unsigned long long* too_long) {
+                            uint32_t hot_bit0, const unsigned long long* __restrict__ ch_mask,
+                            const uint32_t* __restrict__ ch_base, uint32_t ch_bit0,
+                            const uint32_t* __restrict__ ch_rank, uint4* cand, unsigned long long* too_long) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= n || !flag[d]) return;
     const uint32_t p = pos[d], rl = row_len[d];
     if (rl >> 31) atomicAdd(too_long, 1ull);
     const uint64_t h = uin_head[d];
     cand[p] = make_uint4(d, (rl & 0x7FFFFFFFu) | (uin_len[d] > 2 ? 0x80000000u : 0u),
-                         head_code((uint32_t)h, hot_rank, hot_bit0), head_code((uint32_t)(h >> 32), hot_rank, hot_bit0));
+                         head_code((uint32_t)h, hot_rank, hot_bit0, ch_mask, ch_base, ch_bit0, ch_rank),
+                         head_code((uint32_t)(h >> 32), hot_rank, hot_bit0, ch_mask, ch_base, ch_bit0, ch_rank));
 }
+
+#if FGI_HEAD_FREQ
+// FGI_HEAD_FREQ: the rank (by head count, descending) of every head, indexed by its order among the heads
+__global__ void k_rank_fill(uint32_t n_heads, const uint64_t* __restrict__ sorted, const unsigned long long* __restrict__ mask,
+                            const uint32_t* __restrict__ base, uint32_t* rank) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_heads) return;
+    const uint32_t h = (uint32_t)sorted[k];
+    const unsigned long long m = mask[h >> 6];
+    rank[base[h >> 6] + (uint32_t)__popcll(m & ((1ull << (h & 63)) - 1ull))] = k;
+}
+#endif
 
 // segment base of pull block b: the candidates before its first slot b * tpb * kPullTile
 __global__ void k_cand_seg(uint32_t G, uint64_t span, uint32_t n, const uint32_t* __restrict__ pos, uint32_t total,
@@ -1345,6 +1386,7 @@ uint32_t hot_count(uint64_t n) {
 
 fgi_status build_candidates(fgi_graph* g) {
     g->cand_grid = 0;
+    g->ch_words = 0;
     uint32_t G = 0, tpb = 0;
     pull_geometry(g, &G, &tpb);
     if (G == 0) return FGI_OK;
@@ -1411,12 +1453,41 @@ fgi_status build_candidates(fgi_graph* g) {
         const uint32_t n_hot = hot_count(NH);
         hipLaunchKernelGGL(k_hot_pick, dim3(n_hot / 256), dim3(256), 0, s, NH, n_hot, k1, g->hot_id, hot_rank);
         FGI_HIP(g, hipGetLastError());
+        // cold heads (single engine): ranked in handle order, their bits past the snapshot
+        if (!part) {
+            const uint64_t NW = ((uint64_t)NH + 63) / 64;
+            if (!g->ch_mask) {
+                FGI_TRY(dmalloc(g, &g->ch_mask, g->bm_words / 2));
+                FGI_TRY(dmalloc(g, &g->ch_base, g->bm_words / 2 + 1));
+            }
+            Tmp tpp, tcs;
+            uint32_t* pop;
+            FGI_TRY(tmalloc(g, tpp, &pop, NW + 1));
+            FGI_HIP(g, hipMemsetAsync(pop + NW, 0, 4, s));
+            hipLaunchKernelGGL(k_ch_mask, dim3(nblk(NW * 64)), dim3(256), 0, s, NH, cnt, hot_rank, g->ch_mask, pop);
+            size_t cb = 0;
+            FGI_HIP(g, rocprim::exclusive_scan(nullptr, cb, pop, g->ch_base, 0u, (size_t)NW + 1, rocprim::plus<uint32_t>(), s));
+            char* ct;
+            FGI_TRY(tmalloc(g, tcs, &ct, cb));
+            FGI_HIP(g, rocprim::exclusive_scan(ct, cb, pop, g->ch_base, 0u, (size_t)NW + 1, rocprim::plus<uint32_t>(), s));
+            uint32_t n_cold = 0;
+            FGI_TRY(d2h(g, &n_cold, g->ch_base + NW, 1));
+#if FGI_HEAD_FREQ
+            // every head (n_cold counts them all): ranked by count, bits from the snapshot's first word
+            g->ch_w0 = g->hot_w0;
+            if (!g->ch_rank) FGI_TRY(dmalloc(g, &g->ch_rank, (size_t)g->bm_words * 32));
+            if (n_cold) hipLaunchKernelGGL(k_rank_fill, dim3(nblk(n_cold)), dim3(256), 0, s, n_cold, k1, g->ch_mask, g->ch_base, g->ch_rank);
+            g->n_heads = n_cold;
+#endif
+            if (g->ch_w0 * 32 + n_cold < (uint64_t)FGI_NONE) g->ch_words = ((uint64_t)n_cold + 63) / 64 * 2;
+        }
         FGI_HIP(g, hipStreamSynchronize(s));
-        g->n_hot = n_hot;
+        g->n_hot = (FGI_HEAD_FREQ && !part) ? 0u : n_hot;   // FGI_HEAD_FREQ: no snapshot to gather
     }
     FGI_HIP(g, hipMemsetAsync(g->misc_dev + 15, 0, sizeof(unsigned long long), s));
     hipLaunchKernelGGL(k_cand_fill, dim3(nblk(N)), dim3(256), 0, s, N, flag, pos, g->uin_head, g->uin_len, g->row_len,
-                       hot_rank, (uint32_t)(g->hot_w0 * 32), g->cand, g->misc_dev + 15);
+                       hot_rank, (uint32_t)(g->hot_w0 * 32), g->ch_words ? g->ch_mask : nullptr, g->ch_base,
+                       (uint32_t)(g->ch_w0 * 32), FGI_HEAD_FREQ ? g->ch_rank : nullptr, g->cand, g->misc_dev + 15);
     hipLaunchKernelGGL(k_cand_seg, dim3(nblk(G + 1)), dim3(256), 0, s, G, (uint64_t)tpb * kPullTile, N, pos, total,
                        g->cand_seg);
     FGI_HIP(g, hipGetLastError());
@@ -1547,8 +1618,10 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
         dmalloc(g, &g->uin_head, g->n_slots + 1))
         return fail(FGI_ENOMEM);
     g->bm_words = (H + 63) / 64 * 2 + 2;
-    // the invalidated bitmap carries the hot heads' snapshot past its end (build_candidates)
-    if (dmalloc(g, &g->vis_bm, g->bm_words) || dmalloc(g, &g->inv_bm, g->bm_words + kHot / 32) ||
+    // the invalidated bitmap carries the hot heads' snapshot past its end, then the cold heads' bits
+    // (at most one per handle; build_candidates)
+    g->ch_w0 = g->bm_words + kHot / 32;
+    if (dmalloc(g, &g->vis_bm, g->bm_words) || dmalloc(g, &g->inv_bm, g->ch_w0 + g->bm_words) ||
         dmalloc(g, &g->cls_bm, g->bm_words) || dmalloc(g, &g->uin_more, g->bm_words))
         return fail(FGI_ENOMEM);
     hipMemset(g->done, 0, (size_t)(kDoneGroups + 1) * kDoneStride * sizeof(unsigned long long));
@@ -1607,6 +1680,9 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->wl);
     dfree(g->cand_seg);
     dfree(g->hot_id);
+    dfree(g->ch_mask);
+    dfree(g->ch_base);
+    dfree(g->ch_rank);
     for (int k = 0; k < 2; ++k) {
         dfree(g->sv[k]);
         dfree(g->sv_cnt[k]);
