@@ -315,7 +315,11 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *   FGI_OPT_FRONT_EXCHANGE [0] partitions, before a pull level: 0 per level whichever moves fewer
  *                            bytes, 1 all-gather of the whole invalidated bitmap, 2 only the words
  *                            that changed since the previous exchange (8 B each, to every rank);
- *                            all ranks of a partition must set the same value */
+ *                            all ranks of a partition must set the same value
+ *   FGI_OPT_HOT_HEADS   [0]  most list heads a pull level probes through the hot snapshot: 0 sizes
+ *                            it from the graph (65,536-262,144); n > 0 caps it at n rounded up to 256,
+ *                            so the other heads probe the cold-head bitmap (tests pin that path on
+ *                            small graphs; results never depend on it) */
 #define FGI_OPT_DEAD_FILTER 1
 #define FGI_OPT_DIRECTION 2
 #define FGI_OPT_PULL_ALPHA 3
@@ -325,6 +329,7 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
 #define FGI_OPT_PART_COLLECTIVES 7
 #define FGI_OPT_PULL_TPB 8
 #define FGI_OPT_FRONT_EXCHANGE 9
+#define FGI_OPT_HOT_HEADS 10
 fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value);
 
 /* ---- multi-GPU (1-D vertex-range partition, RCCL all-to-all frontier exchange) --------------- */

@@ -329,6 +329,7 @@ struct fgi_graph {
     int opt_direction = 0;
     int opt_pull_alpha = 28;           // profiles/r2y_direction_sweep.jsonl: 28 beats 14 on configs[0] (-6%) and [1] (-1%)
     int opt_pull_tpb = 0;             // pull tiles per block (0: from the CU count; tests)
+    int opt_hot_heads = 0;            // FGI_OPT_HOT_HEADS: cap on the hot heads (0: by graph size)
     int opt_pull_beta = 24;           // after a pull, pull again while the frontier exceeds n / beta
     int opt_level_timing = 1;         // HIP events around each level's k_level launch (statistics)
 

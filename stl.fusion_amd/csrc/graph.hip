@@ -1450,7 +1450,9 @@ fgi_status build_candidates(fgi_graph* g) {
         char* st;
         FGI_TRY(tmalloc(g, tt, &st, sb));
         FGI_HIP(g, rocprim::radix_sort_keys_desc(st, sb, k0, k1, (size_t)NH, 0, 64, s));
-        const uint32_t n_hot = hot_count(NH);
+        uint32_t n_hot = hot_count(NH);
+        if (g->opt_hot_heads > 0)   // tests: most heads cold
+            n_hot = std::min<uint32_t>(n_hot, (uint32_t)(g->opt_hot_heads + 255) / 256 * 256);
         hipLaunchKernelGGL(k_hot_pick, dim3(n_hot / 256), dim3(256), 0, s, NH, n_hot, k1, g->hot_id, hot_rank);
         FGI_HIP(g, hipGetLastError());
         // cold heads (single engine): ranked in handle order, their bits past the snapshot
@@ -2006,6 +2008,17 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
         // the candidate lists are segmented per pull block: rebuilt for the new grid. A partition's
         // dependency lists come from its load (part_build_in_lists), which a wave never redoes, so its
         // candidates are re-segmented here over the lists it has.
+        if (!g->part) {
+            g->uin_epoch = 0;
+        } else if (g->uin_src && g->uin_epoch == g->mut_epoch) {
+            hipSetDevice(g->device);
+            return build_candidates(g);
+        }
+        return FGI_OK;
+    case FGI_OPT_HOT_HEADS:
+        if (value < 0 || value > (int64_t)kHot) return set_err(g, FGI_EINVAL, "hot heads must be 0..%u", kHot);
+        g->opt_hot_heads = (int)value;
+        // the candidates' head codes depend on the hot set: rebuilt (as for FGI_OPT_PULL_TPB)
         if (!g->part) {
             g->uin_epoch = 0;
         } else if (g->uin_src && g->uin_epoch == g->mut_epoch) {

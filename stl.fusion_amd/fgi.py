@@ -23,6 +23,7 @@ OPT_DEAD_FILTER, OPT_DIRECTION, OPT_PULL_ALPHA, OPT_LEVEL_TIMING, OPT_PULL_BETA,
 OPT_PART_COLLECTIVES = 7
 OPT_PULL_TPB = 8
 OPT_FRONT_EXCHANGE = 9
+OPT_HOT_HEADS = 10
 DIR_AUTO, DIR_PUSH, DIR_PULL = 0, 1, 2
 NONE = 0xFFFFFFFF
 COMPUTING, CONSISTENT, INVALIDATED = 0, 1, 2

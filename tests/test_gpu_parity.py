@@ -91,7 +91,9 @@ def test_wave_layered_config1_shape(pkg, gpu_available):
 
 
 PATHS = {  # name -> (direction, dead filter)
-    "push_nofilter": (1, 0), "push": (1, 1), "pull": (2, 1), "auto": (0, 1), "auto_alpha2": (0, 1)}
+    "push_nofilter": (1, 0), "push": (1, 1), "pull": (2, 1), "auto": (0, 1), "auto_alpha2": (0, 1),
+    # 256 hot heads at most: on these small graphs most list heads are cold (head-only bitmap probes)
+    "pull_cold": (2, 1), "auto_cold": (0, 1)}
 
 
 def _set_path(g, name):
@@ -100,6 +102,8 @@ def _set_path(g, name):
     g.set_option(1, f)
     if name == "auto_alpha2":
         g.set_option(3, 2)
+    if name.endswith("_cold"):
+        g.set_option(10, 256)   # FGI_OPT_HOT_HEADS
 
 
 @pytest.mark.parametrize("path", list(PATHS))
@@ -123,7 +127,7 @@ def test_wave_rmat(pkg, gpu_available, stale, path):
     assert len(ids2) == 0
 
 
-@pytest.mark.parametrize("path", ["push_nofilter", "push", "pull"])
+@pytest.mark.parametrize("path", ["push_nofilter", "push", "pull", "pull_cold"])
 def test_wave_mixed_states_and_immediately(pkg, gpu_available, path):
     rng = np.random.default_rng(7)
     n = 5000
@@ -158,7 +162,7 @@ def test_hub_row_spans_many_chunks(pkg, gpu_available, path):
     _compare_wave(g, o, n, np.array([0], np.uint32))
 
 
-@pytest.mark.parametrize("path", ["push", "pull"])
+@pytest.mark.parametrize("path", ["push", "pull", "pull_cold"])
 def test_cycles_and_self_loops(pkg, gpu_available, path):
     n = 1000
     versions = O.version_of(5, np.arange(n))
@@ -245,7 +249,7 @@ class Pair:
         return self.o.last(slot)
 
 
-@pytest.mark.parametrize("path", ["auto", "pull"])
+@pytest.mark.parametrize("path", ["auto", "pull", "pull_cold"])
 def test_compute_method_lifecycle_random(pkg, gpu_available, path):
     """Random begin_compute / add_used / set_output / invalidate sequences (streaming-mix shape).
     Under "pull" every level is bottom-up, so the dependency-list cache is rebuilt after each
