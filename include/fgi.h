@@ -318,8 +318,8 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *                            all ranks of a partition must set the same value
  *   FGI_OPT_HOT_HEADS   [0]  most list heads a pull level probes through the hot snapshot: 0 sizes
  *                            it from the graph (65,536-262,144); n > 0 caps it at n rounded up to 256,
- *                            so the other heads probe the cold-head bitmap (tests pin that path on
- *                            small graphs; results never depend on it) */
+ *                            so the other heads are probed in the invalidated bitmap itself (tests pin
+ *                            that path on small graphs; results never depend on it) */
 #define FGI_OPT_DEAD_FILTER 1
 #define FGI_OPT_DIRECTION 2
 #define FGI_OPT_PULL_ALPHA 3

@@ -129,9 +129,6 @@ constexpr uint32_t kFinalBlocks = 1024; // grid of the final collect (invalidate
 #ifndef FGI_HOT
 #define FGI_HOT 262144                  // measurement builds: make variant-hot HOT=<n> (a multiple of 256)
 #endif
-#ifndef FGI_HEAD_FREQ
-#define FGI_HEAD_FREQ 0                 // measurement builds: make variant-headfreq (fgi_graph::ch_rank)
-#endif
 constexpr uint32_t kHot = FGI_HOT;      // most hot list heads (pull probes through a snapshot of kHot / 8 B)
 #ifndef FGI_LDS_HOT
 #define FGI_LDS_HOT 2048                // measurement builds: make variant-ldshot LDSHOT=<words>
@@ -279,6 +276,14 @@ struct fgi_graph {
                                        // dependencies of each entry, the ones a wave reaches earliest
     uint32_t* uin_more = nullptr;      // bitmap: the list has more than two entries
     uint64_t uin_cap = 0;
+    // Per pool position: the entry was live (tag == its dependant's version) when the dependency lists
+    // were built. Versions change only through mutations (mut_epoch) and entries move only through
+    // compaction (pool_epoch), so while both are unchanged an entry is live iff its bit is set and its
+    // dependant is current: fgi_prune then reads this bitmap and a bitmap of current nodes (2 MB at 16 M
+    // slots, L2-resident) instead of gathering every dependant's 8-byte node word.
+    unsigned long long* pool_live = nullptr;
+    uint64_t pool_live_cap = 0;              // positions covered
+    uint64_t pl_mut_epoch = 0, pl_pool_epoch = ~0ull;
     // Pull candidates: the slots with a non-empty dependency list, grouped by the
     // pull block owning their tile range (segment [cand_seg[b], cand_seg[b + 1]), slot order), as
     // (slot, list heads, row length | more-than-two-entries bit << 31). A pull level reads the
@@ -296,20 +301,6 @@ struct fgi_graph {
     uint64_t hot_w0 = 0;               // the snapshot's first word in the bitmap a pull level probes
                                        // (inv_bm, or a partition's front_global): kHot / 32 words
                                        // allocated past its end; a hot head's code is 32 * hot_w0 + rank
-    // Cold heads (single engine): the list heads that are not hot, ranked in handle order. A cold
-    // head's code is 32 * ch_w0 + rank: its bit lives past the hot snapshot in inv_bm (a head-only
-    // bitmap, ~1/15 of the handles at R-MAT 24, so the cold probes stay in a few hundred KB instead of
-    // the whole invalidated bitmap) and is set wherever the head's invalidated bit is. ch_mask[w]: the
-    // cold heads among handles [64 w, 64 w + 64); ch_base[w]: the rank of the first of them.
-    unsigned long long* ch_mask = nullptr;   // [bm_words / 2]
-    uint32_t* ch_base = nullptr;             // [bm_words / 2 + 1]
-    uint64_t ch_w0 = 0;                      // first 32-bit word of the cold-head bits in inv_bm
-    uint64_t ch_words = 0;                   // 32-bit words of cold-head bits (0: heads keep handle codes)
-    // FGI_HEAD_FREQ builds (measurement): every head (hot or cold) ranked by how many lists it heads,
-    // its bit at hot_w0 + rank maintained where its invalidated bit is (no snapshot gather);
-    // ch_rank[i]: the rank of the i-th head in handle order (ch_mask / ch_base then cover all heads)
-    uint32_t* ch_rank = nullptr;
-    uint32_t n_heads = 0;
     uint4* sv[2] = {nullptr, nullptr};
     uint32_t* sv_cnt[2] = {nullptr, nullptr};   // [pull grid] survivors per block
     uint64_t cand_cap = 0;

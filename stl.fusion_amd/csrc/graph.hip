@@ -685,7 +685,18 @@ struct PruneArgs {
     uint64_t* chunk_map;        // chunk -> handle | first chunk of its row << 32
     uint32_t* chunk_st;         // zeroed; kChunkDone | kept entries once a chunk has loaded
     unsigned long long* st;     // kPrN counters
+    // fast path (fgi_graph::pool_live valid, else null): liveness at list build per pool position,
+    // and the handles whose node is current
+    const unsigned long long* live_bm;
+    const uint32_t* cur_bm;
 };
+
+// Computed.cs:412-413 for the entry at pool position pos: through the two bitmaps on the fast path,
+// else from the dependant's node word
+__device__ __forceinline__ bool entry_live(const PruneArgs& a, uint64_t pos, uint32_t dst, uint64_t tag) {
+    if (a.live_bm) return ((a.live_bm[pos >> 6] >> (pos & 63)) & 1ull) && ((a.cur_bm[dst >> 5] >> (dst & 31)) & 1u);
+    return edge_live(a.node, dst, tag);
+}
 
 // the chunk map entries of one long row (nch chunks from cb), by the calling threads
 __device__ __forceinline__ void prune_map_row(uint64_t* map, uint32_t h, uint32_t cb, uint32_t nch, uint32_t t,
@@ -763,7 +774,10 @@ __device__ void prune_short_rows(const PruneArgs& a, uint32_t* s_lh, uint32_t* s
                 tag[q] = f < total ? pr_ld(a.pool_tag + ro[q] + k) : 0ull;
             }
 #pragma unroll
-            for (int q = 0; q < kShortPer; ++q) keep[q] = (s0 + 64 * q + lane < total) && edge_live(a.node, col[q], tag[q]);
+            for (int q = 0; q < kShortPer; ++q) {
+                const uint32_t f = s0 + 64 * q + lane;
+                keep[q] = f < total && entry_live(a, ro[q] + (f - s_pre[wid][rr[q]]), col[q], tag[q]);
+            }
 #pragma unroll
             for (int q = 0; q < kShortPer; ++q) {
                 const uint32_t sq = s0 + 64 * q;
@@ -819,7 +833,7 @@ __device__ void prune_chunk(const PruneArgs& a, uint32_t c, uint32_t* s_w, uint3
 #pragma unroll
     for (int j = 0; j < kChunkPer; ++j) {
         const uint32_t k = base + threadIdx.x * kChunkPer + j;
-        keep |= (k < len && edge_live(a.node, col[j], tag[j])) ? (1u << j) : 0u;
+        keep |= (k < len && entry_live(a, o + k, col[j], tag[j])) ? (1u << j) : 0u;
     }
     const uint32_t cnt = (uint32_t)__popc(keep);
     uint32_t x = cnt;
@@ -872,6 +886,17 @@ __device__ void prune_chunk(const PruneArgs& a, uint32_t c, uint32_t* s_w, uint3
 }
 
 __global__ void k_coop_warm(uint32_t) {}
+
+// bit h: handle h's node is current (not Invalidated, not empty) — the prune's fast path
+__global__ void k_build_cur(uint32_t n, const unsigned long long* __restrict__ node, unsigned long long* cur64) {
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t lim = ((uint64_t)n + 63) / 64 * 64;
+    for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < lim; h += nthr) {
+        const bool c = h < n && word_is_current(node[h]);
+        const unsigned long long m = __ballot(c);
+        if ((threadIdx.x & 63) == 0) cur64[h >> 6] = m;
+    }
+}
 
 }  // namespace
 
@@ -987,7 +1012,7 @@ __global__ void k_in_pairs(uint32_t n, uint32_t n_slots, const unsigned long lon
                            const uint64_t* __restrict__ row_off, const uint32_t* __restrict__ row_len,
                            const uint32_t* __restrict__ pool_col, const uint64_t* __restrict__ pool_tag,
                            const uint32_t* __restrict__ weight, uint32_t wbits, uint32_t wmax, uint32_t top,
-                           uint64_t* keys, uint32_t* vals) {
+                           uint64_t* keys, uint32_t* vals, unsigned long long* live_bm) {
     const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
@@ -996,12 +1021,24 @@ __global__ void k_in_pairs(uint32_t n, uint32_t n_slots, const unsigned long lon
         const uint32_t len = row_len[u];
         const uint64_t o = row_off[u];
         const uint64_t wk = (uint64_t)(wmax - (u < n_slots ? weight[u] : 0u));
-        for (uint32_t k = lane; k < len; k += 64) {
-            const uint32_t d = pool_col[o + k];
-            const uint64_t t = pool_tag[o + k];
-            const bool live = t != 0 && (node[d] & kVMask) == t;
-            keys[o + k] = live ? (((uint64_t)d << wbits) | wk) : dead;
-            vals[o + k] = (uint32_t)u;
+        for (uint32_t k0 = 0; k0 < len; k0 += 64) {   // wave-uniform
+            const uint32_t k = k0 + lane;
+            bool live = false;
+            if (k < len) {
+                const uint32_t d = pool_col[o + k];
+                const uint64_t t = pool_tag[o + k];
+                live = t != 0 && (node[d] & kVMask) == t;
+                keys[o + k] = live ? (((uint64_t)d << wbits) | wk) : dead;
+                vals[o + k] = (uint32_t)u;
+            }
+            // positions o + k0 .. + 63: at most two words of the liveness bitmap (rows share words)
+            const unsigned long long m = __ballot(live);
+            if (live_bm && lane == 0 && m) {
+                const uint64_t p0 = o + k0;
+                const uint32_t sh = (uint32_t)(p0 & 63);
+                atomicOr(live_bm + (p0 >> 6), m << sh);
+                if (sh && (m >> (64 - sh))) atomicOr(live_bm + (p0 >> 6) + 1, m >> (64 - sh));
+            }
         }
     }
 }
@@ -1077,67 +1114,26 @@ __global__ void k_hot_pick(uint32_t k_max, uint32_t n_hot, const uint64_t* __res
     hot_rank[(uint32_t)key] = k;
 }
 
-// the cold heads (heads that are not hot) of handles [64 w, 64 w + 64): one word per wave
-__global__ void k_ch_mask(uint32_t n, const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ hot_rank,
-                          unsigned long long* mask, uint32_t* pop) {
-    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-    const bool c = u < n && cnt[u] != 0 && (FGI_HEAD_FREQ || hot_rank[u] == FGI_NONE);
-    const unsigned long long m = __ballot(c);
-    if ((threadIdx.x & 63) == 0 && u < ((n + 63u) & ~63u)) {
-        mask[u >> 6] = m;
-        pop[u >> 6] = (uint32_t)__popcll(m);
-    }
-}
-
-// a list head as the pull level probes it: for a hot head, its bit in the snapshot that follows the
-// bitmap (bit hot_bit0 + rank); for a cold head (ch_mask), its bit in the cold-head bitmap (bit
-// ch_bit0 + its rank among the cold heads); otherwise (partitions) its bit in the bitmap itself
-__device__ __forceinline__ uint32_t head_code(uint32_t h, const uint32_t* hot_rank, uint32_t hot_bit0,
-                                              const unsigned long long* ch_mask, const uint32_t* ch_base,
-                                              uint32_t ch_bit0, const uint32_t* ch_rank) {
+// a list head as the pull level probes it: its bit in the invalidated bitmap, or, for a hot head, its
+// bit in the snapshot that follows the bitmap (bit hot_bit0 + rank)
+__device__ __forceinline__ uint32_t head_code(uint32_t h, const uint32_t* hot_rank, uint32_t hot_bit0) {
     if (h == FGI_NONE || !hot_rank) return h;
-    if (ch_rank && ch_mask) {   // FGI_HEAD_FREQ: every head by its rank
-        const unsigned long long m = ch_mask[h >> 6];
-        const uint32_t b = h & 63;
-        if (!((m >> b) & 1ull)) return h;
-        return hot_bit0 + ch_rank[ch_base[h >> 6] + (uint32_t)__popcll(m & ((1ull << b) - 1ull))];
-    }
     const uint32_t r = hot_rank[h];
-    if (r != FGI_NONE) return hot_bit0 + r;
-    if (!ch_mask) return h;
-    const unsigned long long m = ch_mask[h >> 6];
-    const uint32_t b = h & 63;
-    if (!((m >> b) & 1ull)) return h;
-    return ch_bit0 + ch_base[h >> 6] + (uint32_t)__popcll(m & ((1ull << b) - 1ull));
+    return r != FGI_NONE ? (hot_bit0 + r) : h;
 }
 
 __global__ void k_cand_fill(uint32_t n, const uint32_t* __restrict__ flag, const uint32_t* __restrict__ pos,
                             const uint64_t* __restrict__ uin_head, const uint32_t* __restrict__ uin_len,
                             const uint32_t* __restrict__ row_len, const uint32_t* __restrict__ hot_rank,
-                            uint32_t hot_bit0, const unsigned long long* __restrict__ ch_mask,
-                            const uint32_t* __restrict__ ch_base, uint32_t ch_bit0,
-                            const uint32_t* __restrict__ ch_rank, uint4* cand, unsigned long long* too_long) {
+                            uint32_t hot_bit0, uint4* cand, unsigned long long* too_long) {
     const uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
     if (d >= n || !flag[d]) return;
     const uint32_t p = pos[d], rl = row_len[d];
     if (rl >> 31) atomicAdd(too_long, 1ull);
     const uint64_t h = uin_head[d];
     cand[p] = make_uint4(d, (rl & 0x7FFFFFFFu) | (uin_len[d] > 2 ? 0x80000000u : 0u),
-                         head_code((uint32_t)h, hot_rank, hot_bit0, ch_mask, ch_base, ch_bit0, ch_rank),
-                         head_code((uint32_t)(h >> 32), hot_rank, hot_bit0, ch_mask, ch_base, ch_bit0, ch_rank));
+                         head_code((uint32_t)h, hot_rank, hot_bit0), head_code((uint32_t)(h >> 32), hot_rank, hot_bit0));
 }
-
-#if FGI_HEAD_FREQ
-// FGI_HEAD_FREQ: the rank (by head count, descending) of every head, indexed by its order among the heads
-__global__ void k_rank_fill(uint32_t n_heads, const uint64_t* __restrict__ sorted, const unsigned long long* __restrict__ mask,
-                            const uint32_t* __restrict__ base, uint32_t* rank) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_heads) return;
-    const uint32_t h = (uint32_t)sorted[k];
-    const unsigned long long m = mask[h >> 6];
-    rank[base[h >> 6] + (uint32_t)__popcll(m & ((1ull << (h & 63)) - 1ull))] = k;
-}
-#endif
 
 // segment base of pull block b: the candidates before its first slot b * tpb * kPullTile
 __global__ void k_cand_seg(uint32_t G, uint64_t span, uint32_t n, const uint32_t* __restrict__ pos, uint32_t total,
@@ -1304,9 +1300,18 @@ fgi_status ensure_in_lists(fgi_graph* g) {
         FGI_TRY(tmalloc(g, tv0, &v0, P));
         FGI_TRY(tmalloc(g, tv1, &v1, P));
         FGI_HIP(g, hipMemsetAsync(k0, 0xFF, P * sizeof(uint64_t), s));   // row slack: dead keys
+        // the pool's liveness bitmap (fgi_prune's fast path) comes with the lists
+        const uint64_t lw = (P + 63) / 64 + 1;
+        if (g->pool_live_cap < lw * 64) {
+            dfree(g->pool_live);
+            g->pool_live_cap = 0;
+            FGI_TRY(dmalloc(g, &g->pool_live, lw + lw / 8));
+            g->pool_live_cap = (lw + lw / 8) * 64;
+        }
+        FGI_HIP(g, hipMemsetAsync(g->pool_live, 0, lw * 8, s));
         hipLaunchKernelGGL(k_in_pairs, dim3(grid), dim3(256), 0, s, H, N,
                            reinterpret_cast<const unsigned long long*>(g->node), g->row_off, g->row_len, g->pool_col,
-                           g->pool_tag, g->uin_len, wbits, wmax, top, k0, v0);
+                           g->pool_tag, g->uin_len, wbits, wmax, top, k0, v0, g->pool_live);
         FGI_HIP(g, hipGetLastError());
         size_t sb = 0;
         FGI_HIP(g, rocprim::radix_sort_pairs(nullptr, sb, k0, k1, v0, v1, (size_t)P, 0, top + 1, s));
@@ -1319,6 +1324,8 @@ fgi_status ensure_in_lists(fgi_graph* g) {
     FGI_TRY(build_in_heads(g));
     FGI_HIP(g, hipStreamSynchronize(s));
     g->uin_epoch = g->mut_epoch;
+    g->pl_mut_epoch = (total && P) ? g->mut_epoch : 0;
+    g->pl_pool_epoch = g->pool_epoch;
     return FGI_OK;
 }
 
@@ -1386,7 +1393,6 @@ uint32_t hot_count(uint64_t n) {
 
 fgi_status build_candidates(fgi_graph* g) {
     g->cand_grid = 0;
-    g->ch_words = 0;
     uint32_t G = 0, tpb = 0;
     pull_geometry(g, &G, &tpb);
     if (G == 0) return FGI_OK;
@@ -1451,45 +1457,16 @@ fgi_status build_candidates(fgi_graph* g) {
         FGI_TRY(tmalloc(g, tt, &st, sb));
         FGI_HIP(g, rocprim::radix_sort_keys_desc(st, sb, k0, k1, (size_t)NH, 0, 64, s));
         uint32_t n_hot = hot_count(NH);
-        if (g->opt_hot_heads > 0)   // tests: most heads cold
+        if (g->opt_hot_heads > 0)   // tests: most heads probed in the invalidated bitmap itself
             n_hot = std::min<uint32_t>(n_hot, (uint32_t)(g->opt_hot_heads + 255) / 256 * 256);
         hipLaunchKernelGGL(k_hot_pick, dim3(n_hot / 256), dim3(256), 0, s, NH, n_hot, k1, g->hot_id, hot_rank);
         FGI_HIP(g, hipGetLastError());
-        // cold heads (single engine): ranked in handle order, their bits past the snapshot
-        if (!part) {
-            const uint64_t NW = ((uint64_t)NH + 63) / 64;
-            if (!g->ch_mask) {
-                FGI_TRY(dmalloc(g, &g->ch_mask, g->bm_words / 2));
-                FGI_TRY(dmalloc(g, &g->ch_base, g->bm_words / 2 + 1));
-            }
-            Tmp tpp, tcs;
-            uint32_t* pop;
-            FGI_TRY(tmalloc(g, tpp, &pop, NW + 1));
-            FGI_HIP(g, hipMemsetAsync(pop + NW, 0, 4, s));
-            hipLaunchKernelGGL(k_ch_mask, dim3(nblk(NW * 64)), dim3(256), 0, s, NH, cnt, hot_rank, g->ch_mask, pop);
-            size_t cb = 0;
-            FGI_HIP(g, rocprim::exclusive_scan(nullptr, cb, pop, g->ch_base, 0u, (size_t)NW + 1, rocprim::plus<uint32_t>(), s));
-            char* ct;
-            FGI_TRY(tmalloc(g, tcs, &ct, cb));
-            FGI_HIP(g, rocprim::exclusive_scan(ct, cb, pop, g->ch_base, 0u, (size_t)NW + 1, rocprim::plus<uint32_t>(), s));
-            uint32_t n_cold = 0;
-            FGI_TRY(d2h(g, &n_cold, g->ch_base + NW, 1));
-#if FGI_HEAD_FREQ
-            // every head (n_cold counts them all): ranked by count, bits from the snapshot's first word
-            g->ch_w0 = g->hot_w0;
-            if (!g->ch_rank) FGI_TRY(dmalloc(g, &g->ch_rank, (size_t)g->bm_words * 32));
-            if (n_cold) hipLaunchKernelGGL(k_rank_fill, dim3(nblk(n_cold)), dim3(256), 0, s, n_cold, k1, g->ch_mask, g->ch_base, g->ch_rank);
-            g->n_heads = n_cold;
-#endif
-            if (g->ch_w0 * 32 + n_cold < (uint64_t)FGI_NONE) g->ch_words = ((uint64_t)n_cold + 63) / 64 * 2;
-        }
         FGI_HIP(g, hipStreamSynchronize(s));
-        g->n_hot = (FGI_HEAD_FREQ && !part) ? 0u : n_hot;   // FGI_HEAD_FREQ: no snapshot to gather
+        g->n_hot = n_hot;
     }
     FGI_HIP(g, hipMemsetAsync(g->misc_dev + 15, 0, sizeof(unsigned long long), s));
     hipLaunchKernelGGL(k_cand_fill, dim3(nblk(N)), dim3(256), 0, s, N, flag, pos, g->uin_head, g->uin_len, g->row_len,
-                       hot_rank, (uint32_t)(g->hot_w0 * 32), g->ch_words ? g->ch_mask : nullptr, g->ch_base,
-                       (uint32_t)(g->ch_w0 * 32), FGI_HEAD_FREQ ? g->ch_rank : nullptr, g->cand, g->misc_dev + 15);
+                       hot_rank, (uint32_t)(g->hot_w0 * 32), g->cand, g->misc_dev + 15);
     hipLaunchKernelGGL(k_cand_seg, dim3(nblk(G + 1)), dim3(256), 0, s, G, (uint64_t)tpb * kPullTile, N, pos, total,
                        g->cand_seg);
     FGI_HIP(g, hipGetLastError());
@@ -1620,10 +1597,8 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
         dmalloc(g, &g->uin_head, g->n_slots + 1))
         return fail(FGI_ENOMEM);
     g->bm_words = (H + 63) / 64 * 2 + 2;
-    // the invalidated bitmap carries the hot heads' snapshot past its end, then the cold heads' bits
-    // (at most one per handle; build_candidates)
-    g->ch_w0 = g->bm_words + kHot / 32;
-    if (dmalloc(g, &g->vis_bm, g->bm_words) || dmalloc(g, &g->inv_bm, g->ch_w0 + g->bm_words) ||
+    // the invalidated bitmap carries the hot heads' snapshot past its end (build_candidates)
+    if (dmalloc(g, &g->vis_bm, g->bm_words) || dmalloc(g, &g->inv_bm, g->bm_words + kHot / 32) ||
         dmalloc(g, &g->cls_bm, g->bm_words) || dmalloc(g, &g->uin_more, g->bm_words))
         return fail(FGI_ENOMEM);
     hipMemset(g->done, 0, (size_t)(kDoneGroups + 1) * kDoneStride * sizeof(unsigned long long));
@@ -1678,13 +1653,11 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->uin_len);
     dfree(g->uin_src);
     dfree(g->uin_head);
+    dfree(g->pool_live);
     dfree(g->cand);
     dfree(g->wl);
     dfree(g->cand_seg);
     dfree(g->hot_id);
-    dfree(g->ch_mask);
-    dfree(g->ch_base);
-    dfree(g->ch_rank);
     for (int k = 0; k < 2; ++k) {
         dfree(g->sv[k]);
         dfree(g->sv_cnt[k]);
@@ -2680,7 +2653,7 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
 // counters land in st[kPrN].
 // e0 (nullable) is recorded right before the launch: the temporaries, their clearing and the first
 // occupancy query (which loads the kernel's code object) stay outside the timed span
-static fgi_status prune_range_launch(fgi_graph* g, uint32_t lo, uint32_t hi, Tmp& tmap, Tmp& tcst,
+static fgi_status prune_range_launch(fgi_graph* g, uint32_t lo, uint32_t hi, Tmp& tmap, Tmp& tcst, Tmp& tcur,
                                      unsigned long long* st, hipEvent_t e0) {
     hipStream_t s = g->stream;
     // every chunk holds more than kPruneLong / 2 entries of a row: the pool bounds their number
@@ -2704,6 +2677,17 @@ static fgi_status prune_range_launch(fgi_graph* g, uint32_t lo, uint32_t hi, Tmp
     a.pool_col = g->pool_col;
     a.pool_tag = g->pool_tag;
     a.st = st;
+    // fast path: the entries' liveness at list build still holds (no mutation, no compaction since)
+    if (g->pool_live && g->pl_mut_epoch == g->mut_epoch && g->pl_pool_epoch == g->pool_epoch &&
+        g->pool_top <= g->pool_live_cap && !getenv("FGI_PRUNE_GATHER")) {
+        uint32_t* cur;
+        FGI_TRY(tmalloc(g, tcur, &cur, g->bm_words));
+        const uint32_t H = g->n_handles;
+        hipLaunchKernelGGL(k_build_cur, dim3(std::min<uint32_t>((H + 255) / 256 + 1, 8192)), dim3(256), 0, s, H,
+                           a.node, reinterpret_cast<unsigned long long*>(cur));
+        a.live_bm = g->pool_live;
+        a.cur_bm = cur;
+    }
     if (getenv("FGI_TRACE")) fprintf(stderr, "[fgi] prune [%u, %u): %u blocks (%d per CU)\n", lo, hi, grid, per_cu);
     void* args[] = {&a};
     if (e0) FGI_HIP(g, hipEventRecord(e0, s));
@@ -2767,8 +2751,8 @@ static fgi_status prune_rows(fgi_graph* g, uint32_t lo, uint32_t hi, bool allow_
     unsigned long long* st = g->misc_dev;
     FGI_HIP(g, hipMemsetAsync(st, 0, kPrN * sizeof(unsigned long long), s));
     hipEvent_t e0 = g->ev_w0, e1 = g->ev_w1;
-    Tmp tmap, tcst;
-    if (hi > lo) FGI_TRY(prune_range_launch(g, lo, hi, tmap, tcst, st, e0));
+    Tmp tmap, tcst, tcur;
+    if (hi > lo) FGI_TRY(prune_range_launch(g, lo, hi, tmap, tcst, tcur, st, e0));
     else FGI_HIP(g, hipEventRecord(e0, s));
     FGI_HIP(g, hipEventRecord(e1, s));
     unsigned long long c[kPrN];

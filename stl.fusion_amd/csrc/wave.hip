@@ -316,11 +316,6 @@ struct Out {
     uint64_t* __restrict__ nescan;
     uint32_t* __restrict__ ncstart;
     LevelCtr* ln;
-    // cold heads (single engine, else null): their bits past the hot snapshot (fgi_graph::ch_mask)
-    const unsigned long long* __restrict__ ch_mask;
-    const uint32_t* __restrict__ ch_base;
-    unsigned long long* ch_bm;
-    const uint32_t* __restrict__ ch_rank;   // FGI_HEAD_FREQ: ranks of all heads (else null)
 };
 
 // A frontier entry: its row (offset, length) and exclusive edge offset es, and the chunk map entries
@@ -372,48 +367,13 @@ __device__ __forceinline__ void write_entry_wave(const Out& o, bool has, uint64_
     write_span(o.ncstart, has, (uint32_t)idx, es, len);
 }
 
-// The cold-head bits of the handles won in word w (won: bit b = handle 64 w + b invalidated): their ranks
-// are consecutive from ch_base[w], so they span at most two 64-bit words; returnless ORs.
-__device__ __forceinline__ void mark_cold_heads(const unsigned long long* __restrict__ ch_mask,
-                                                const uint32_t* __restrict__ ch_base, unsigned long long* ch_bm,
-                                                const uint32_t* __restrict__ ch_rank, uint64_t w,
-                                                unsigned long long won) {
-    const unsigned long long hm = ch_mask[w];
-    unsigned long long x = hm & won;
-    if (!x) return;
-    const uint32_t base = ch_base[w], sh = base & 63u;
-    if (ch_rank) {   // FGI_HEAD_FREQ: one bit per head, at its rank
-        uint32_t* bm32 = reinterpret_cast<uint32_t*>(ch_bm);
-        for (; x; x &= x - 1) {
-            const uint32_t b = (uint32_t)__builtin_ctzll(x);
-            const uint32_t r = ch_rank[base + (uint32_t)__popcll(hm & ((1ull << b) - 1ull))];
-            __hip_atomic_fetch_or(bm32 + (r >> 5), 1u << (r & 31), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return;
-    }
-    unsigned long long lo = 0, hi = 0;
-    for (; x; x &= x - 1) {
-        const uint32_t b = (uint32_t)__builtin_ctzll(x);
-        const uint32_t r = sh + (uint32_t)__popcll(hm & ((1ull << b) - 1ull));   // < 128
-        if (r < 64) lo |= 1ull << r;
-        else hi |= 1ull << (r - 64);
-    }
-    unsigned long long* q = ch_bm + (base >> 6);
-    if (lo) __hip_atomic_fetch_or(q, lo, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (hi) __hip_atomic_fetch_or(q + 1, hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// a winner's invalidated bit (and its cold-head bit)
-__device__ __forceinline__ void mark_invalidated(const Out& o, uint32_t h) {
-    atomicOr(o.inv_bm + (h >> 5), 1u << (h & 31));
-    if (o.ch_bm) mark_cold_heads(o.ch_mask, o.ch_base, o.ch_bm, o.ch_rank, h >> 6, 1ull << (h & 63));
-}
+__device__ __forceinline__ void mark_invalidated(uint32_t* inv_bm, uint32_t h) { atomicOr(inv_bm + (h >> 5), 1u << (h & 31)); }
 
 // One (possibly absent) winner per lane. Every lane of the wave must call it.
 __device__ __forceinline__ void emit_one(bool win, uint32_t h, const Out& o) {
     const uint32_t len = win ? o.row_len[h] : 0u;
     const uint32_t off = win ? (uint32_t)o.row_off[h] : 0u;   // requested with the length
-    if (win) mark_invalidated(o, h);
+    if (win) mark_invalidated(o.inv_bm, h);
     const unsigned long long mine = (win && len) ? ((1ull << 32) | len) : 0ull;
     unsigned long long tot;
     const unsigned long long ex = wave_excl_scan64(mine, tot);
@@ -454,7 +414,7 @@ __device__ __forceinline__ void emit_push(Emit& e, uint32_t* buf, bool win, uint
         if (idx < CAP) {
             buf[idx] = h;
         } else {
-            mark_invalidated(o, h);
+            mark_invalidated(o.inv_bm, h);
             const uint32_t len = o.row_len[h];
             if (len) {
                 const unsigned long long r = atomicAdd(&o.ln->ft, (1ull << 32) | len);
@@ -506,7 +466,7 @@ __device__ __forceinline__ void emit_flush(Emit& e, uint32_t* buf, uint32_t at, 
                 len = buf[kChunk + i];
             } else {
                 const uint32_t h = buf[i];
-                mark_invalidated(o, h);
+                mark_invalidated(o.inv_bm, h);
                 len = o.row_len[h];
             }
             cnt += len ? 1u : 0u;
@@ -923,7 +883,7 @@ __device__ __forceinline__ void expand_level(int L, uint64_t F, uint64_t T, uint
             rl[j] = 0;
             ro[j] = 0;
             if ((win_mask >> j) & 1u) {
-                mark_invalidated(o, dst[j]);
+                mark_invalidated(o.inv_bm, dst[j]);
                 rl[j] = o.row_len[dst[j]];
                 ro[j] = (uint32_t)o.row_off[dst[j]];   // pool positions are < 2^32
             }
@@ -960,10 +920,6 @@ struct PullArgs {
     uint32_t hot_bit0;                       // a hot head's code: hot_bit0 + rank (its snapshot bit)
     uint32_t hot_lds;                        // hot snapshot words staged into LDS per block (<= kLdsHot)
     uint32_t* inv_bm;                        // this device's invalidated bitmap (owned words |= winners)
-    const unsigned long long* __restrict__ ch_mask;   // cold heads (null: none)
-    const uint32_t* __restrict__ ch_base;
-    unsigned long long* ch_bm;
-    const uint32_t* __restrict__ ch_rank;
     const uint32_t* __restrict__ cls;        // expandable-class bitmap
     uint32_t* wl;                            // per block (at its segment base): expandable winners
     unsigned long long* bsum;                // [3][grid] per-block sums, then [3][grid] prefixes
@@ -990,7 +946,6 @@ constexpr uint32_t kOwnWords = 2 * kMaxIter * kTileWords;   // owned 32-bit bitm
 constexpr uint32_t kCandBatch = 4 * kBlock; // candidates per block step (4 per lane)
 constexpr uint32_t kWaveBatch = 4 * 64;     // a wave's run per step
 constexpr uint32_t kWaveTailCap = kTailCap / (kBlock / 64);   // queued candidates per wave
-constexpr uint32_t kHotStageMin = 1024;    // candidates of a block that pay for staging the hot snapshot
 
 // visits / winners / classes of the owned tiles in LDS: 32-bit words (two lanes of a wave that
 // share a word serialise their atomics; narrower words halve how many do)
@@ -999,7 +954,6 @@ struct PullLds {
     uint32_t vm[kOwnWords];                         // visits: the level's start, | this level's non-winners
     uint32_t wm[kOwnWords];                         // winners
     uint32_t cs[kOwnWords];                         // expandable class (read only)
-    uint32_t dirty[kOwnWords / 64];                 // owned 64-bit words whose visits changed without a winner
     uint32_t sn;                                    // survivors written
     uint32_t wn;                                    // expandable winners listed
 };
@@ -1023,15 +977,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // that follows the invalidated bitmap (g->hot_w0), any other head the bitmap itself. The snapshot's
 // first hot_lds words are read from the block's LDS copy: a random probe of an L2-resident bitmap
 // costs ~4x an L1 hit and ~5x an LDS read (profiles/r5f_probe_rate.txt, r5g_snap_rate.txt)
-__device__ __forceinline__ uint32_t head_bits(const PullArgs& p, const PullLds& s, uint32_t hot_lds, uint32_t h) {
+__device__ __forceinline__ uint32_t head_bits(const PullArgs& p, const PullLds& s, uint32_t h) {
     const uint32_t r = (h - p.hot_bit0) >> 5;   // wraps past hot_lds for a cold head
-    return r < hot_lds ? s.hot[r] : p.front_rd[h >> 5];
-}
-
-// a visit that does not win changes an owned visit word the winners' word does not show
-__device__ __forceinline__ void visit_nonwinner(PullLds& s, uint32_t rel, uint32_t bit) {
-    atomicOr(&s.vm[rel >> 5], bit);
-    atomicOr(&s.dirty[rel >> 11], 1u << ((rel >> 6) & 31));
+    return r < p.hot_lds ? s.hot[r] : p.front_rd[h >> 5];
 }
 
 // an entry past the list reads as a dead candidate at the block's first slot
@@ -1056,7 +1004,7 @@ __device__ __forceinline__ void pull_hit(const PullArgs& p, PullLds& s, uint64_t
             p.wl[seg + atomicAdd(&s.wn, 1u)] = d;
         }
     } else {
-        visit_nonwinner(s, rel, bit);
+        atomicOr(&s.vm[rel >> 5], bit);
     }
 }
 
@@ -1165,8 +1113,6 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
     const uint32_t cnt = npull == 0 ? seg_n : min(p.sv_cnt[sid - 1][b], seg_n);
     uint4* const sv_out = p.sv[dst] + seg;     // this level's survivors (the block's segment)
     uint32_t* const wl_out = p.wl + seg;       // this level's expandable winners
-    // a block with few candidates probes the hot snapshot through L1 instead of staging 8 KB of it
-    const uint32_t hot_lds = cnt >= kHotStageMin ? p.hot_lds : 0u;
     // the first batch's entries are requested before the owned words are staged
     // (FGI_PULL_PREFETCH=0 builds the variant without the look-ahead, for measurement)
     uint4 c[4];
@@ -1194,7 +1140,7 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
 #pragma unroll
         for (uint32_t k = 0; k < kHotPer; ++k) {
             const uint32_t i = threadIdx.x + k * kBlock;
-            hh[k] = i < hot_lds ? hot[i] : 0u;
+            hh[k] = i < p.hot_lds ? hot[i] : 0u;
         }
 #pragma unroll
         for (uint32_t k = 0; k < kPer; ++k) {
@@ -1205,12 +1151,9 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
                 s.wm[i] = 0;
             }
         }
-        if (hot_lds) {
 #pragma unroll
-            for (uint32_t k = 0; k < kHotPer; ++k) s.hot[threadIdx.x + k * kBlock] = hh[k];
-        }
+        for (uint32_t k = 0; k < kHotPer; ++k) s.hot[threadIdx.x + k * kBlock] = hh[k];
     }
-    if (threadIdx.x < kOwnWords / 64) s.dirty[threadIdx.x] = 0;
     if (threadIdx.x == 0) {
         s.sn = 0;
         s.wn = 0;
@@ -1239,8 +1182,8 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
             f0[j] = (lv[j] && (c[j].z & 1)) ? ~0u : 0u;
             f1[j] = 0u;
 #else
-            f0[j] = lv[j] ? head_bits(p, s, hot_lds, c[j].z) : 0u;
-            f1[j] = (lv[j] && c[j].w != FGI_NONE) ? head_bits(p, s, hot_lds, c[j].w) : 0u;
+            f0[j] = lv[j] ? head_bits(p, s, c[j].z) : 0u;
+            f1[j] = (lv[j] && c[j].w != FGI_NONE) ? head_bits(p, s, c[j].w) : 0u;
 #endif
         }
         uint4 cn[4];
@@ -1276,7 +1219,7 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
                     ws.e += rl ? 1u : 0u;
                     ws.l += rl;
                 } else {
-                    visit_nonwinner(s, rel, bit);
+                    atomicOr(&s.vm[rel >> 5], bit);
                     flagged += first_visit(node[d]) == 2 ? 1u : 0u;
                 }
             }
@@ -1322,19 +1265,16 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
     PROBE(L, 2);
     __syncthreads();
     PROBE(L, 3);
-    // write back the owned words that changed (visits before this level | this level's)
+    // write back the owned words (visits before this level | this level's)
     unsigned long long* vis64 = reinterpret_cast<unsigned long long*>(vis);
     unsigned long long* inv64 = reinterpret_cast<unsigned long long*>(p.inv_bm);
     for (uint32_t i = threadIdx.x; i < wp.tpb * kTileWords; i += blockDim.x) {
         const uint64_t sl = s_lo + (uint64_t)i * 64;
-        const unsigned long long wm = s.wm[2 * i] | ((unsigned long long)s.wm[2 * i + 1] << 32);
-        if (sl < p.n_slots && (wm || ((s.dirty[i >> 5] >> (i & 31)) & 1u))) {
+        if (sl < p.n_slots) {
+            const unsigned long long wm = s.wm[2 * i] | ((unsigned long long)s.wm[2 * i + 1] << 32);
             vis64[sl >> 6] = wm | s.vm[2 * i] | ((unsigned long long)s.vm[2 * i + 1] << 32);
             // returnless: the word's earlier bits need not be read back (nothing in this launch reads it)
-            if (wm) {
-                __hip_atomic_fetch_or(inv64 + (sl >> 6), wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (p.ch_bm) mark_cold_heads(p.ch_mask, p.ch_base, p.ch_bm, p.ch_rank, sl >> 6, wm);
-            }
+            if (wm) __hip_atomic_fetch_or(inv64 + (sl >> 6), wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
     bs[0] = ws.w;
@@ -1752,8 +1692,7 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
 }
 
 __global__ __launch_bounds__(kBlock) void k_wave_init(WaveCtr* ctr, unsigned long long* blk, uint32_t* inv_bm,
-                                                      uint32_t* vis_bm, uint64_t bm_words, uint32_t* ch_bm,
-                                                      uint64_t ch_words) {
+                                                      uint32_t* vis_bm, uint64_t bm_words) {
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
     unsigned long long* c = reinterpret_cast<unsigned long long*>(ctr);
@@ -1762,7 +1701,6 @@ __global__ __launch_bounds__(kBlock) void k_wave_init(WaveCtr* ctr, unsigned lon
     uint4* f4 = reinterpret_cast<uint4*>(inv_bm);
     for (uint64_t i = tid; i < bm_words / 4; i += nthr) f4[i] = make_uint4(0u, 0u, 0u, 0u);
     for (uint64_t i = bm_words / 4 * 4 + tid; i < bm_words; i += nthr) inv_bm[i] = 0u;
-    for (uint64_t i = tid; i < ch_words; i += nthr) ch_bm[i] = 0u;   // cold-head bits
     if (vis_bm) {   // fgi_restore's deferred clear
         uint4* v4 = reinterpret_cast<uint4*>(vis_bm);
         for (uint64_t i = tid; i < bm_words / 4; i += nthr) v4[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -1894,11 +1832,7 @@ bool pull_ready(const fgi_graph* g, const WaveParams& wp) {
 }
 
 Out out_for(fgi_graph* g, int buf, LevelCtr* ln) {
-    const bool ch = g->ch_words != 0;
-    return Out{g->row_off,   g->row_len,     g->inv_bm, g->fr_off[buf], g->fr_len[buf], g->escan[buf], g->cstart[buf], ln,
-               ch ? g->ch_mask : nullptr, ch ? g->ch_base : nullptr,
-               ch ? reinterpret_cast<unsigned long long*>(g->inv_bm + g->ch_w0) : nullptr,
-               (ch && FGI_HEAD_FREQ) ? g->ch_rank : nullptr};
+    return Out{g->row_off, g->row_len, g->inv_bm, g->fr_off[buf], g->fr_len[buf], g->escan[buf], g->cstart[buf], ln};
 }
 
 CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, const WaveParams& wp, int buf) {
@@ -1937,12 +1871,6 @@ PullArgs pull_args(fgi_graph* g, uint32_t n_slots, const uint32_t* front_rd) {
     p.hot_bit0 = (uint32_t)(g->hot_w0 * 32);
     p.hot_lds = std::min<uint32_t>(g->n_hot / 32, kLdsHot);
     p.inv_bm = g->inv_bm;
-    const bool ch = g->ch_words != 0 && front_rd == g->inv_bm;
-    p.ch_mask = ch ? g->ch_mask : nullptr;
-    p.ch_base = ch ? g->ch_base : nullptr;
-    p.ch_bm = ch ? reinterpret_cast<unsigned long long*>(g->inv_bm + g->ch_w0) : nullptr;
-    p.ch_rank = (ch && FGI_HEAD_FREQ) ? g->ch_rank : nullptr;
-    if (ch && FGI_HEAD_FREQ) p.hot_lds = std::min<uint32_t>((g->n_heads + 31) / 32, kLdsHot);
     p.wl = g->wl;
     p.cls = g->cls_bm;
     p.bsum = g->bsum;
@@ -2030,7 +1958,7 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
     FGI_TRY(coop_warm(g));
     if (!g->coop_clean)
         hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
-                           (uint32_t*)nullptr, (uint64_t)g->bm_words, g->inv_bm + g->ch_w0, g->ch_words);
+                           (uint32_t*)nullptr, (uint64_t)g->bm_words);
     CoopArgs a{};
     a.roots = roots_dev;
     a.imm = imm_dev;
@@ -2123,8 +2051,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     bool allow_pull = wp0.direction != 1 && pull_ready(g, wp0);
     static_assert(sizeof(WaveCtr) % 8 == 0, "WaveCtr is cleared as 64-bit words");
     hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
-                       g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words, g->inv_bm + g->ch_w0,
-                       g->ch_words);
+                       g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
     g->vis_stale = false;
     g->coop_clean = false;
 #if FGI_PROBE
@@ -2314,8 +2241,7 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     if (coll) FGI_HIP(g, hipMemsetAsync(pv.sent_bm, 0, pv.sent_words * 4, s));
     if (coll) FGI_TRY(part_front_reset(g));
     hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
-                       g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words, g->inv_bm + g->ch_w0,
-                       g->ch_words);
+                       g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
     g->vis_stale = false;
     g->coop_clean = false;
     while (g->ev.size() < 2) {

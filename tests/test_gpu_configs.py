@@ -79,8 +79,13 @@ def _oracle_edges(o):
     return canon_edges(*o.export_used_by())
 
 
-@pytest.mark.parametrize("mode", ["prune", "prune_range"])
-def test_configs3_scale20_prune_parity(pkg, gpu_available, mode):
+@pytest.mark.parametrize("mode", ["prune", "prune_gather", "prune_range"])
+def test_configs3_scale20_prune_parity(pkg, gpu_available, mode, monkeypatch):
+    """The first wave builds the dependency lists, so "prune" runs the fast path (liveness recorded at
+    list build + a bitmap of current nodes); "prune_gather" pins the node-word gathers; "prune_range"
+    runs its first batch on the fast path and the later ones (after the first compaction) on gathers."""
+    if mode == "prune_gather":
+        monkeypatch.setenv("FGI_PRUNE_GATHER", "1")
     scale, ef, seed, sseed, rseed = 20, 16, 0x5EED0024, 0x5EED00C0, 0x5EED1024
     n = 1 << scale
     O.set_threads(THREADS)
@@ -99,7 +104,7 @@ def test_configs3_scale20_prune_parity(pkg, gpu_available, mode):
     ids = g.invalidate(roots, stats=ws)
     assert np.array_equal(np.sort(ids), np.sort(o.inv_log())) and (ws.v_inv, ws.e_trav) == (st.v_inv, st.e_trav)
     o.clear_log()
-    if mode == "prune":
+    if mode in ("prune", "prune_gather"):
         ps = g.prune()
         oe, ne = o.prune()
         assert ps.new_edges == ne and ps.old_edges >= oe, (ps.old_edges, ps.new_edges, oe, ne)

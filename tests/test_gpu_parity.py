@@ -92,7 +92,8 @@ def test_wave_layered_config1_shape(pkg, gpu_available):
 
 PATHS = {  # name -> (direction, dead filter)
     "push_nofilter": (1, 0), "push": (1, 1), "pull": (2, 1), "auto": (0, 1), "auto_alpha2": (0, 1),
-    # 256 hot heads at most: on these small graphs most list heads are cold (head-only bitmap probes)
+    # 256 hot heads at most: on these small graphs most list heads are then probed in the invalidated
+    # bitmap itself instead of the hot snapshot
     "pull_cold": (2, 1), "auto_cold": (0, 1)}
 
 
