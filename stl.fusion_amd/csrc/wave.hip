@@ -946,6 +946,7 @@ constexpr uint32_t kOwnWords = 2 * kMaxIter * kTileWords;   // owned 32-bit bitm
 constexpr uint32_t kCandBatch = 4 * kBlock; // candidates per block step (4 per lane)
 constexpr uint32_t kWaveBatch = 4 * 64;     // a wave's run per step
 constexpr uint32_t kWaveTailCap = kTailCap / (kBlock / 64);   // queued candidates per wave
+constexpr uint32_t kLaneTail = 12;          // lists a lane scans alone in a tail pass (entries 4..11)
 
 // visits / winners / classes of the owned tiles in LDS: 32-bit words (two lanes of a wave that
 // share a word serialise their atomics; narrower words halve how many do)
@@ -1009,10 +1010,12 @@ __device__ __forceinline__ void pull_hit(const PullArgs& p, PullLds& s, uint64_t
 }
 
 // A wave's queued candidates (both heads missed, the list goes on). Pass 1: one lane per candidate
-// probes entries 2 and 3 (both in flight together) — most queued candidates settle here. Pass 2:
-// the ones whose list goes past entry 3 without a hit, 8 lanes per candidate over entries 4.. in
-// steps of 8 (early exit); the next candidate's list is located while the current one is scanned.
-// q (the wave's queue of candidate indices) is reused for pass 2's list.
+// probes entries 2 and 3 (both in flight together) — most queued candidates settle here. Pass 2a:
+// lists of at most kLaneTail entries that go past entry 3 without a hit, one lane per candidate with
+// all of entries 4.. in flight (configs[0]'s 8-entry lists of nodes two levels ahead: 64 per step
+// instead of 8). Pass 2b: the longer lists, 8 lanes per candidate over entries 4.. in steps of 8
+// (early exit); the next candidate's list is located while the current one is scanned. q (the wave's
+// queue of candidate indices) is reused for pass 2's lists (bit 31: longer than kLaneTail).
 __device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, uint4* sv_out, const unsigned long long* node,
                                            uint64_t s_lo, uint64_t seg, uint32_t* q, uint32_t nq, PullLds& s,
                                            uint32_t& flagged, uint32_t& examined, uint32_t& tails, WinSum& ws) {
@@ -1036,7 +1039,7 @@ __device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, 
         examined += (u2 != FGI_NONE ? 1u : 0u) + (u3 != FGI_NONE ? 1u : 0u);
         const bool more = in && !hit && len > 4;
         const unsigned long long mm = __ballot(more);
-        if (more) q[nlong + rank_in(mm)] = qi;   // below every entry still unread
+        if (more) q[nlong + rank_in(mm)] = qi | (len > kLaneTail ? 0x80000000u : 0u);   // below every entry still unread
         nlong += (uint32_t)__popcll(mm);
         if (in && hit) {
             const uint32_t d = c.x, rel = (uint32_t)(d - s_lo);
@@ -1054,6 +1057,51 @@ __device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, 
         }
         tails += in ? 1u : 0u;
     }
+    __builtin_amdgcn_wave_barrier();
+    // pass 2a: the short lists, one lane each; the long ones compacted to the queue's front
+    uint32_t nl2 = 0;
+    for (uint32_t r0 = 0; r0 < nlong; r0 += 64) {   // wave-uniform
+        const uint32_t e = r0 + lane;
+        const uint32_t v = e < nlong ? q[e] : 0u;
+        const bool in = e < nlong && !(v >> 31);
+        const bool lng = e < nlong && (v >> 31);
+        const unsigned long long lm = __ballot(lng);
+        if (lng) q[nl2 + rank_in(lm)] = v & 0x7FFFFFFFu;   // below every entry still unread
+        nl2 += (uint32_t)__popcll(lm);
+        uint4 c = make_uint4(0u, 0u, 0u, 0u);
+        uint32_t len = 0;
+        uint64_t off = 0;
+        if (in) {
+            c = src[seg + v];
+            len = p.uin_len[c.x];
+            off = p.uin_off[c.x];
+        }
+        uint32_t u[kLaneTail - 4];
+#pragma unroll
+        for (uint32_t k = 0; k < kLaneTail - 4; ++k) u[k] = (in && 4 + k < len) ? p.uin_src[off + 4 + k] : FGI_NONE;
+        bool found = false;
+#pragma unroll
+        for (uint32_t k = 0; k < kLaneTail - 4; ++k)
+            if (u[k] != FGI_NONE) {
+                found |= bit_of(p.front_rd, u[k]);
+                ++examined;
+            }
+        if (in && found) {
+            const uint32_t d = c.x, rel = (uint32_t)(d - s_lo);
+            const bool win = (s.cs[rel >> 5] >> (d & 31)) & 1u;
+            pull_hit(p, s, s_lo, seg, d, win, c.y, ws);
+            if (!win) flagged += first_visit(node[d]) == 2 ? 1u : 0u;
+        }
+        const bool surv = in && !found;
+        const unsigned long long sm = __ballot(surv);
+        if (sm) {
+            uint32_t sb = 0;
+            if (lane == 0) sb = atomicAdd(&s.sn, (uint32_t)__popcll(sm));
+            sb = from_lane0(sb);
+            if (surv) sv_out[sb + rank_in(sm)] = c;
+        }
+    }
+    nlong = nl2;
     __builtin_amdgcn_wave_barrier();
     const uint32_t sub = lane & 7, grp = lane >> 3;
     constexpr uint32_t G8 = 8;
