@@ -262,7 +262,10 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
 /* ---- graph maintenance ---------------------------------------------------------------------- */
 /* One ComputedGraphPruner pass (Internal/ComputedGraphPruner.cs:79-94): PruneUsedBy on every
  * registered Consistent node (Computed.cs:400-419) — keep (slot, tag) iff the slot's current node
- * exists with version == tag — then compact the edge pool. */
+ * exists with version == tag — then compact the edge pool. While no mutation and no compaction has
+ * happened since the pull dependency lists were built, the version half of that test is read from the
+ * liveness the list build recorded per pool entry, and only "current" from a bitmap of the node words
+ * (same result, no per-entry gather of the dependant's node word). */
 fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats);
 /* The same PruneUsedBy pass over the rows of handles [first, first + count) only (one batch of
  * ComputedGraphPruner's walk, ComputedGraphPruner.cs:79-94). Rows are compacted in place: their
