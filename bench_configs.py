@@ -42,13 +42,16 @@ def timed_waves(g, pkg, d_roots, n_roots, steps, warmup):
         g.restore()
         g.invalidate_dev(n_roots, d_roots.data_ptr(), 0, pkg.WaveStats())
     st = pkg.WaveStats()
+    g.set_option(pkg.fgi.OPT_LEVEL_TIMING, 0)   # as bench.py's headline: no per-level events in the stream
     torch.cuda.synchronize()
     t = time.perf_counter()
     for _ in range(steps):
         g.restore()
         g.invalidate_dev(n_roots, d_roots.data_ptr(), 0, st)
     torch.cuda.synchronize()
-    return (time.perf_counter() - t) / steps, st
+    dt = (time.perf_counter() - t) / steps
+    g.set_option(pkg.fgi.OPT_LEVEL_TIMING, 1)
+    return dt, st
 
 
 def cpu_oracle_layered(cfg, roots, threads, runs=3):
