@@ -66,7 +66,10 @@ def test_batched_prune_sequence_matches_pruner(pkg, gpu_available, batch):
     o.close()
 
 
-def test_long_rows_compact_in_place(pkg, gpu_available):
+@pytest.mark.parametrize("lists", [False, True])
+def test_long_rows_compact_in_place(pkg, gpu_available, lists):
+    """lists=True: a pull-only wave first builds the dependency lists, so the prune reads the entries'
+    liveness recorded at that build (fgi_prune's fast path) instead of gathering node words."""
     n = 20000
     rng = np.random.default_rng(31)
     versions = O.version_of(5, np.arange(n))
@@ -81,6 +84,9 @@ def test_long_rows_compact_in_place(pkg, gpu_available):
     tags = versions[dst].copy()
     tags[rng.random(len(tags)) < 0.6] += np.uint64(2)
     g, o = build_pair(pkg, n, versions, flags, src, dst, tags)
+    if lists:   # slot 5 has no row: the wave invalidates it alone
+        g.set_option(2, 2)
+        _compare_wave(g, o, n, np.array([5], np.uint32))
     before = [g.used_by(hub) for hub in (0, 1, 2)]
     ps = g.prune()
     oe, ne = o.prune()
@@ -170,3 +176,52 @@ def test_restore_after_in_place_prune(pkg, gpu_available):
         return
     o.restore()
     _compare_wave(g, o, n, rng.integers(0, n, 60).astype(np.uint32))
+
+
+def test_prune_after_recompute_sees_new_versions(pkg, gpu_available):
+    """Lists built by a pull wave, then some nodes recomputed (new versions: the entries that captured
+    their old versions go stale) before the prune: the liveness recorded at the list build no longer
+    holds, so the prune must check the current versions (mut_epoch moved) and drop those entries."""
+    from test_gpu_parity import Pair
+    rng = np.random.default_rng(41)
+    n = 3000
+    p = Pair(pkg, n)
+    ver = O.version_of(91, np.arange(n))
+    slots = np.arange(n, dtype=np.uint32)
+    p.begin(slots, ver, np.zeros(n, np.uint8))
+    p.g.set_output(slots)
+    for s_ in slots:
+        p.o.set_output(p.node(int(s_)))
+    # dependencies: every node uses a few others (AddUsed while Computing: recompute a batch first)
+    batch = rng.choice(n, 1500, replace=False).astype(np.uint32)
+    ver[batch] += np.uint64(1000)
+    p.begin(batch, ver[batch], np.zeros(len(batch), np.uint8))
+    dep = np.repeat(batch, 4)
+    use = rng.integers(0, n, len(dep)).astype(np.uint32)
+    res = p.g.add_used(dep, use)
+    assert list(res) == [p.o.add_used(p.node(int(d)), p.node(int(u))) for d, u in zip(dep, use)]
+    p.g.set_output(batch)
+    for s_ in batch:
+        p.o.set_output(p.node(int(s_)))
+    # a pull-only wave builds the lists (and the pool's liveness bits)
+    p.g.set_option(2, 2)
+    roots = rng.integers(0, n, 3).astype(np.uint32)
+    p.o.clear_log()
+    p.o.invalidate_slots(roots)
+    gids = p.g.invalidate(roots)
+    assert np.array_equal(np.sort(gids), np.sort(p.o.inv_log()))
+    # recompute nodes other rows point at: their old-version entries go stale
+    used = np.unique(use)
+    again = used[rng.random(len(used)) < 0.5].astype(np.uint32)
+    ver[again] += np.uint64(7)
+    p.begin(again, ver[again], np.zeros(len(again), np.uint8))
+    p.g.set_output(again)
+    for s_ in again:
+        p.o.set_output(p.node(int(s_)))
+    ps = p.g.prune()
+    oe, ne = p.o.prune()
+    assert ps.new_edges == ne, (ps.new_edges, ne)
+    u, d, t = p.g.export_edges()
+    ge = canon_edges(u, d, t)
+    ge = ge[ge[:, 0] < n] if len(ge) else ge
+    assert np.array_equal(ge, oracle_edges(p.o, n))
