@@ -345,7 +345,8 @@ struct AuArgs {
     unsigned long long* cnt;   // [0] candidates [1] pending [2] overflow rows [3] entries the overflow rows need
 };
 
-__device__ __forceinline__ void au_classify(uint32_t i, const AuArgs& a) {
+// one pair: its result code; true (and *out) if it is a new `_usedBy` entry to append
+__device__ __forceinline__ bool au_classify_pair(uint32_t i, const AuArgs& a, Cand* out) {
     const uint32_t* dep = a.dep;
     const uint32_t* used = a.used;
     const uint32_t n_slots = a.n_slots;
@@ -359,23 +360,21 @@ __device__ __forceinline__ void au_classify(uint32_t i, const AuArgs& a) {
     unsigned long long* hset = a.hset;
     const uint64_t hmask = a.hmask;
     uint32_t* result = a.result;
-    Cand* cand = a.cand;
-    unsigned long long* ncand = a.cnt;
     const uint32_t d = dep[i], u = used[i];
     const unsigned long long wd = node[d];
     if ((wd & kVMask) == 0 || word_state(wd) != FGI_COMPUTING) {   // Computed.cs:351-364
         result[i] = FGI_USED_DROPPED;
-        return;
+        return false;
     }
     const unsigned long long wu = node[u];
     if ((wu & kVMask) == 0 || word_state(wu) == FGI_INVALIDATED) {  // Computed.cs:376-378
         atomicOr(node + d, kW_IOSO);
         result[i] = FGI_USED_INVALIDATED;
-        return;
+        return false;
     }
     if (word_state(wu) == FGI_COMPUTING) {                           // Computed.cs:374-375
         result[i] = FGI_USED_ESTATE;
-        return;
+        return false;
     }
     result[i] = FGI_USED_ADDED;                                      // Computed.cs:381-383
     // set semantics: (u, d) within this batch ...
@@ -384,7 +383,7 @@ __device__ __forceinline__ void au_classify(uint32_t i, const AuArgs& a) {
     while (true) {
         const unsigned long long prev = atomicCAS(hset + p, ~0ull, key);
         if (prev == ~0ull) break;
-        if (prev == key) return;
+        if (prev == key) return false;
         p = (p + 1) & hmask;
     }
     const uint32_t ds = home_of(d, n_slots, home);
@@ -394,18 +393,46 @@ __device__ __forceinline__ void au_classify(uint32_t i, const AuArgs& a) {
         const uint64_t o = row_off[u];
         const uint32_t len = row_len[u];
         for (uint32_t k = 0; k < len; ++k)
-            if (pool_col[o + k] == ds && pool_tag[o + k] == tag) return;
+            if (pool_col[o + k] == ds && pool_tag[o + k] == tag) return false;
     }
-    const unsigned long long c = atomicAdd(ncand, 1ull);
-    cand[c] = Cand{u, d, ds, 0, tag};
+    *out = Cand{u, d, ds, 0, tag};
+    return true;
+}
+
+// Pairs [blockIdx.x * blockDim.x, ...): block-uniform call. The block's new candidates are appended
+// with one reservation per block (a single counter word serialises ~88 atomics per microsecond).
+__device__ __forceinline__ void au_classify_block(uint32_t i, bool valid, const AuArgs& a) {
+    __shared__ uint32_t s_w[8];
+    __shared__ unsigned long long s_base;
+    Cand cd{};
+    const bool want = valid && au_classify_pair(i, a, &cd);
+    const unsigned long long m = __ballot(want);
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if (lane == 0) s_w[wid] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (uint32_t w = 0; w < nw; ++w) {
+        before += w < wid ? s_w[w] : 0u;
+        total += s_w[w];
+    }
+    if (threadIdx.x == 0) s_base = total ? atomicAdd(a.cnt, (unsigned long long)total) : 0ull;
+    __syncthreads();
+    if (want) {
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        a.cand[s_base + before + r] = cd;
+    }
 }
 
 __global__ void k_au_classify(uint32_t n, AuArgs a) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) au_classify(i, a);
+    au_classify_block(i, i < n, a);
 }
 
-__device__ __forceinline__ void au_reserve(uint64_t i, const AuArgs& a) {
+// Candidate i (valid) per lane; every lane of the wave calls it. Consecutive candidates with the same
+// used node (a hub's dependants, appended by one batch) reserve their row slots with one atomic per
+// run of equal keys in the wave instead of one each (the row-length word of a hub otherwise takes
+// a thousand serialised atomics).
+__device__ __forceinline__ void au_reserve(uint64_t i, bool valid, const AuArgs& a) {
     const uint64_t* row_off = a.row_off;
     uint32_t* row_len = a.row_len;
     const uint32_t* row_cap = a.row_cap;
@@ -415,8 +442,21 @@ __device__ __forceinline__ void au_reserve(uint64_t i, const AuArgs& a) {
     uint32_t* pend_pos = a.pend_pos;
     uint32_t* ovf_rows = a.ovf_rows;
     unsigned long long* cnt = a.cnt + 1;
-    const Cand c = a.cand[i];
-    const uint32_t pos = atomicAdd(&row_len[c.used], 1u);
+    const uint32_t lane = threadIdx.x & 63;
+    const Cand c = valid ? a.cand[i] : Cand{FGI_NONE, 0u, 0u, 0u, 0ull};
+    const uint32_t prev = __shfl_up(c.used, 1, 64);
+    const bool head = valid && (lane == 0 || prev != c.used);
+    const unsigned long long heads = __ballot(head), vm = __ballot(valid);
+    // this lane's run: from the nearest head at or below it to the next head (or the last valid lane)
+    const unsigned long long below = heads & (lane == 63 ? ~0ull : ((2ull << lane) - 1ull));
+    const uint32_t start = below ? 63u - (uint32_t)__builtin_clzll(below) : 0u;
+    const unsigned long long above = heads & ~((2ull << lane) - 1ull) & (lane == 63 ? 0ull : ~0ull);
+    const uint32_t end = above ? (uint32_t)__builtin_ctzll(above) : 64u - (uint32_t)__builtin_clzll(vm | 1ull);
+    uint32_t base = 0;
+    if (head) base = atomicAdd(&row_len[c.used], end - start);
+    base = __shfl(base, start, 64);
+    if (!valid) return;
+    const uint32_t pos = base + (lane - start);
     const uint32_t cap = row_cap[c.used];
     atomicAdd(&used_cnt[c.dep_handle], 1u);                          // dependant._used.Add (365-366)
     if (pos < cap) {
@@ -432,7 +472,7 @@ __device__ __forceinline__ void au_reserve(uint64_t i, const AuArgs& a) {
 
 __global__ void k_au_reserve(uint64_t nc, AuArgs a) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nc) au_reserve(i, a);
+    au_reserve(i, i < nc, a);
 }
 
 __device__ __forceinline__ uint32_t grow_cap(uint32_t need) {
@@ -553,13 +593,14 @@ __global__ void kb_bc_install(const unsigned long long* ab, uint32_t n, InstallA
 __global__ void kb_au_classify(const unsigned long long* ab, uint32_t n, AuArgs a) {
     if (batch_aborted(ab)) return;
     const uint64_t i = grid_tid();
-    if (i < n) au_classify((uint32_t)i, a);
+    au_classify_block((uint32_t)i, i < n, a);
 }
 
 __global__ void kb_au_reserve(const unsigned long long* ab, AuArgs a) {
     if (batch_aborted(ab)) return;
     const uint64_t nc = a.cnt[0];
-    for (uint64_t i = grid_tid(); i < nc; i += grid_threads()) au_reserve(i, a);
+    for (uint64_t i0 = grid_tid() - (threadIdx.x & 63); i0 < nc; i0 += grid_threads())   // wave-uniform
+        au_reserve(i0 + (threadIdx.x & 63), i0 + (threadIdx.x & 63) < nc, a);
 }
 
 __global__ void kb_au_size(const unsigned long long* ab, AuArgs a) {

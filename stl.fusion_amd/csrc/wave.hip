@@ -1715,17 +1715,39 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
     CPROBE(8);
     unsigned long long* vis64 = reinterpret_cast<unsigned long long*>(a.vis);
     unsigned long long* invw = reinterpret_cast<unsigned long long*>(a.inv_bm);
-    for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x) {
-        unsigned long long v = vis64[w];
-        if (v) {
-            vis64[w] = 0ull;
-            for (; v; v &= v - 1) {
-                const uint64_t h = w * 64 + (uint64_t)(__ffsll((long long)v) - 1);
-                a.node[h] = visited_word(a.node[h]);
+    // Visits folded into the node words. The final collect does not read visit or node words, so
+    // the fold needs no barrier and spreads over the whole grid: each wave takes runs of 64 visit words
+    // (one per lane), then folds its non-zero words one lane per handle, eight words' node words in
+    // flight at a time. (A block folding its own range bit by bit serialised tens of thousands of
+    // read-modify-writes in the few blocks that own a hub's consecutive dependants.)
+    {
+        const uint32_t W = blockDim.x >> 6;
+        const uint64_t step = (uint64_t)gridDim.x * W * 64;
+        for (uint64_t w0 = ((uint64_t)blockIdx.x * W + wid) * 64; w0 < words; w0 += step) {   // wave-uniform
+            const uint64_t w = w0 + lane;
+            const unsigned long long mine = w < words ? vis64[w] : 0ull;
+            if (mine) vis64[w] = 0ull;
+            unsigned long long nz = __ballot(mine != 0ull);
+            while (nz) {   // wave-uniform
+                uint32_t idx[8];
+                bool m[8];
+                unsigned long long nv[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    idx[j] = nz ? (uint32_t)__builtin_ctzll(nz) : 64u;
+                    nz &= nz ? nz - 1 : 0ull;
+                    const unsigned long long wj = idx[j] < 64u ? __shfl(mine, (int)idx[j], 64) : 0ull;
+                    m[j] = (wj >> lane) & 1ull;
+                    nv[j] = m[j] ? a.node[(w0 + idx[j]) * 64 + lane] : 0ull;
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    if (m[j]) a.node[(w0 + idx[j]) * 64 + lane] = visited_word(nv[j]);
             }
         }
-        if (w - lo >= kFinalStage || s_words[w - lo]) invw[w] = 0ull;
     }
+    for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x)
+        if (w - lo >= kFinalStage || s_words[w - lo]) invw[w] = 0ull;
     if (threadIdx.x < (uint32_t)kStats) a.blk[(uint64_t)threadIdx.x * kStatBlocks + blockIdx.x] = 0ull;
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) {
