@@ -1647,7 +1647,9 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
                                            &ctr->pull_live, &ctr->pull_win,  &ctr->pull_tail, &ctr->pull_scan};
         const unsigned long long* col = a.blk + (uint64_t)k * kStatBlocks;
         unsigned long long x = 0;
-        for (uint32_t q = threadIdx.x; q < kStatBlocks; q += blockDim.x) x += col[q];
+        // only this grid's rows are written (the others were cleared by k_wave_init or by the previous
+        // cooperative wave's own blocks): one load per thread instead of a 16-deep chain of loads
+        for (uint32_t q = threadIdx.x; q < gridDim.x; q += blockDim.x) x += col[q];
         x = block_sum(x, s_red);
         if (threadIdx.x == 0) {
             const unsigned long long v = x + (k == kStFlagged ? ctr->root_flagged : 0ull);
