@@ -8,6 +8,7 @@
 (c) fgi_prune_step runs only once waves have made enough entries stale, then walks the handles.
 (d) A full prune with and without defragmentation gives the same rows; defragmenting shrinks the
     pool and leaves row slack.
+(e) The walk interleaved with recompute / AddUsed / wave churn, through both prune paths.
 """
 import numpy as np
 import pytest
@@ -221,6 +222,65 @@ def test_prune_after_recompute_sees_new_versions(pkg, gpu_available):
     ps = p.g.prune()
     oe, ne = p.o.prune()
     assert ps.new_edges == ne, (ps.new_edges, ne)
+    u, d, t = p.g.export_edges()
+    ge = canon_edges(u, d, t)
+    ge = ge[ge[:, 0] < n] if len(ge) else ge
+    assert np.array_equal(ge, oracle_edges(p.o, n))
+
+
+@pytest.mark.parametrize("path", ["auto", "pull"])
+def test_prune_windows_interleaved_with_churn(pkg, gpu_available, path):
+    """The pruner's walk interleaved with a compute-method workload: each step recomputes a batch,
+    captures dependencies, finishes most computations, runs a wave, then prunes one window of slots
+    (fgi_prune_range; every third step a whole fgi_prune). Under "pull" every wave rebuilds the
+    dependency lists, so the prunes alternate between the liveness recorded at a list build and the
+    node-word gather (any mutation in between moves mut_epoch). After every prune the window's rows
+    equal the oracle's, and every wave matches the oracle's cascade."""
+    from test_gpu_parity import Pair, _set_path
+    rng = np.random.default_rng(53)
+    n = 2500
+    p = Pair(pkg, n, n_detached=8192)
+    _set_path(p.g, path)
+    ver = O.version_of(17, np.arange(n))
+    slots = np.arange(n, dtype=np.uint32)
+    p.begin(slots, ver, np.zeros(n, np.uint8))
+    p.g.set_output(slots)
+    for s_ in slots:
+        p.o.set_output(p.node(int(s_)))
+    win = 700
+    lo = 0
+    for step in range(18):
+        k = int(rng.integers(50, 400))
+        bs = rng.choice(n, k, replace=False).astype(np.uint32)
+        ver[bs] += np.uint64(1000)
+        p.begin(bs, ver[bs], (rng.random(k) < 0.1).astype(np.uint8))
+        dep = np.repeat(bs, rng.integers(1, 6, k))
+        use = rng.integers(0, n, len(dep)).astype(np.uint32)
+        res = p.g.add_used(dep, use)
+        assert list(res) == [p.o.add_used(p.node(int(d)), p.node(int(u))) for d, u in zip(dep, use)]
+        fin = bs[rng.random(k) < 0.85]
+        p.g.set_output(fin)
+        for s_ in fin:
+            p.o.set_output(p.node(int(s_)))
+        roots = rng.integers(0, n, int(rng.integers(1, 40))).astype(np.uint32)
+        p.o.clear_log()
+        p.o.invalidate_slots(roots)
+        gids = p.g.invalidate(roots)
+        assert np.array_equal(np.sort(gids), np.sort(p.o.inv_log())), step
+        if step % 3 == 2:
+            ps = p.g.prune()
+            oe, ne = p.o.prune()
+            a, b = 0, n
+        else:
+            ps = p.g.prune_range(lo, win)
+            oe, ne = p.o.prune_range(lo, win)
+            a, b = lo, min(lo + win, n)
+            lo = 0 if lo + win >= n else lo + win
+        assert ps.new_edges >= ne and ps.old_edges >= oe, (step, ps.new_edges, ne)
+        assert np.array_equal(_rows_of(p.g, a, b, n), _oracle_rows(p.o, a, b, n)), step
+        assert_states_equal(p.g, p.o, n)
+    p.g.prune()
+    p.o.prune()
     u, d, t = p.g.export_edges()
     ge = canon_edges(u, d, t)
     ge = ge[ge[:, 0] < n] if len(ge) else ge
