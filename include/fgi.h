@@ -240,7 +240,7 @@ typedef struct fgi_batch_stats {
     uint64_t e_match;
     uint64_t n_flagged;
     double kernel_ms;      /* device time from the batch's first launch to its last (HIP events) */
-    double wave_ms;        /* of which the waves' cooperative launches (HIP events) */
+    double wave_ms;        /* of which the cascades' one-launch waves (HIP events) */
     double total_ms;       /* wall time of the call */
     uint32_t host_syncs;   /* times the call waited for the device */
     uint32_t pad;
@@ -250,9 +250,9 @@ typedef struct fgi_batch_stats {
  * exactly as the matching single call would apply it (fgi_invalidate, fgi_begin_compute — its
  * displacement cascade included —, fgi_add_used, fgi_set_output — its InvalidateOnSetOutput cascade
  * included; Computed.cs:141-230, 347-385, ComputedRegistry.cs:83-97), but every count stays on the
- * device and each cascade runs as one cooperative launch: the call uploads the batch once and waits
- * for the device once (once more if an add_used step must grow the edge pool, and once more to copy
- * out_ids). out_ids gets the handles invalidated by the batch's cascades, cascade after cascade
+ * device and each cascade runs as one launch (one block per CU, grid barriers between its levels): the
+ * call uploads the batch once and waits for the device once (once more if an add_used step must grow
+ * the edge pool, and once more to copy out_ids). FGI_EDEVICE if a cascade's grid barrier timed out. out_ids gets the handles invalidated by the batch's cascades, cascade after cascade
  * (each in ascending order); FGI_ECAPACITY with *out_n = the count if cap is too small. If the
  * batch runs out of detached handles, FGI_ECAPACITY names the step: the steps before it are
  * applied, it and the later ones are not. */

@@ -235,6 +235,7 @@ struct fgi_graph {
     unsigned long long* bsum = nullptr;  // [8][kStatBlocks] per-block sums / prefixes of the epilogues
     unsigned long long* done = nullptr;  // completion counters of the last-block epilogues
     fgi::WaveCtr* ctr = nullptr;
+    unsigned long long* gbar = nullptr;   // k_wave_coop's grid-barrier counter (plain launches)
     unsigned long long* blk_stats = nullptr;   // [kStatBlocks][kStatCols] per-block wave statistics
     fgi::WaveCtr* ctr_host = nullptr;  // pinned
     uint32_t* roots_buf = nullptr;     // staging for host roots
@@ -403,13 +404,15 @@ inline void note_words(fgi_graph* g) {
 // mutates node words outside a wave calls it first.
 fgi_status fold(fgi_graph* g);
 fgi_status flush_vis(fgi_graph* g);
+bool coop_launch_mode();                 // FGI_COOP_LAUNCH=1: streaming waves as cooperative launches
 fgi_status coop_warm(fgi_graph* g);   // first cooperative launch of the graph's process, outside timed spans   // fgi_restore's deferred visit-bitmap clear, before any use but a wave's init
 #if FGI_PROBE
 void print_coop_probe();
 #endif
-// A push-only wave in one cooperative launch, without host synchronisation (streaming batches):
+// A push-only wave in one launch (k_wave_coop), without host synchronisation (streaming batches):
 // device-resident roots (n_max, or *n_dev of them), ids appended at out[*out_n ..), totals added to
-// acc[0..6] (waves, levels, invalidated, E_trav, E_match, flagged, frontier entries); nothing
+// acc[0..6] (waves, levels, invalidated, E_trav, E_match, flagged, frontier entries; acc[7] set if a
+// grid barrier timed out); nothing
 // happens if *abort (nullable) is set when the wave starts.
 fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev, const uint8_t* imm_dev,
                          const unsigned long long* n_dev, uint32_t* out, unsigned long long* out_n,

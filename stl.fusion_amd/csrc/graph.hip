@@ -650,7 +650,7 @@ __device__ __forceinline__ int prune_mode(uint32_t h, uint32_t n_slots, unsigned
     return 2;                                          // Computing, or detached (not in the registry)
 }
 
-// measurement variants of k_prune (make variant-pexp PEXP=mask; wrong results): 1 = skip long
+// measurement variants of the prune kernels (make variant-pexp PEXP=mask; wrong results): 1 = skip long
 // rows, 2 / 8 = non-temporal pool loads / stores, 4 = no liveness gathers
 #ifndef FGI_PEXP
 #define FGI_PEXP 0
@@ -696,19 +696,19 @@ __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v, uint32_t& total
     return x - v;
 }
 
-// PruneUsedBy in place, rows of handles [lo, hi), one cooperative launch (k_prune): an Invalidated /
+// PruneUsedBy in place, rows of handles [lo, hi), two launches (k_prune_rows, k_prune_chunks): an Invalidated /
 // empty node's row is dropped (len 0), a registered Consistent node's row keeps the entries whose
 // slot's current node is at the entry's version, every other row is kept whole. Rows keep their
 // offsets and capacities (the freed entries are slack the row grows into).
 //   phase 1: waves take 64 consecutive rows and filter the rows of at most kPruneLong entries as
 //            one flattened sequence; the longer rows are listed as chunks of kChunk entries
 //            (chunk map: handle | first chunk of the row << 32), one atomic per block.
-//   grid barrier
+//   kernel boundary
 //   phase 2: blocks take chunks in index order. A chunk loads and checks its entries, publishes
 //            its kept count, then sums the counts of the row's earlier chunks (each published only
 //            after that chunk's loads, so no store of this chunk can pass an unread entry) and
 //            stores; the row's last chunk sets its length. Chunks wait only on lower chunk
-//            indices, every block is resident: the lowest unfinished chunk always proceeds.
+//            indices, and blocks start in index order: the lowest unfinished chunk always proceeds.
 constexpr uint32_t kPruneLong = 1024;
 constexpr uint32_t kBlockLong = 64;     // long rows a block lists with one atomic
 constexpr int kChunkPer = 8;
@@ -956,9 +956,26 @@ fgi_status coop_warm(fgi_graph* g) {
 
 namespace {
 
-__global__ __launch_bounds__(256) void k_prune(PruneArgs a) {
+// Block-reduced prune counters added to st[] (one atomic per wave and counter).
+__device__ __forceinline__ void prune_flush(const PruneArgs& a, unsigned long long (&acc)[4]) {
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        for (int d = 32; d >= 1; d >>= 1) acc[q] += __shfl_xor(acc[q], d, 64);
+    if (lane == 0) {
+        if (acc[0]) atomicAdd(&a.st[kPrOld], acc[0]);
+        if (acc[1]) atomicAdd(&a.st[kPrNew], acc[1]);
+        if (acc[2]) atomicAdd(&a.st[kPrDropped], acc[2]);
+        if (acc[3]) atomicAdd(&a.st[kPrLive], acc[3]);
+    }
+}
+
+// Phase 1 of a prune: the short rows (one wave each) and, for each long row, its chunks' entries in
+// the chunk map. Phase 2 (k_prune_chunks) runs in the next launch: the kernel boundary is the grid
+// barrier between them (plain launches: a cooperative launch's dispatch gap is ~11.7 us).
+__global__ __launch_bounds__(256) void k_prune_rows(PruneArgs a) {
     __shared__ uint32_t s_lh[kBlockLong], s_lc[kBlockLong];
-    __shared__ uint32_t s_nl, s_cb, s_w[4], s_pfx;
+    __shared__ uint32_t s_nl, s_cb;
     if (threadIdx.x == 0) s_nl = 0;
     __syncthreads();
     unsigned long long acc[4] = {0, 0, 0, 0};   // old, new, dropped, live
@@ -977,19 +994,16 @@ __global__ __launch_bounds__(256) void k_prune(PruneArgs a) {
         prune_map_row(a.chunk_map, s_lh[q], cb, s_lc[q], threadIdx.x, blockDim.x);
         cb += s_lc[q];
     }
-    cooperative_groups::this_grid().sync();
+    prune_flush(a, acc);
+}
+
+// Phase 2: the long rows' chunks, each compacted in place after its row's earlier chunks (chunk_st).
+__global__ __launch_bounds__(256) void k_prune_chunks(PruneArgs a) {
+    __shared__ uint32_t s_w[4], s_pfx;
+    unsigned long long acc[4] = {0, 0, 0, 0};
     const uint32_t n_chunks = (uint32_t)__hip_atomic_load(&a.st[kPrChunks], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     for (uint32_t c = blockIdx.x; c < n_chunks; c += gridDim.x) prune_chunk(a, c, s_w, s_pfx, acc);
-    const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        for (int d = 32; d >= 1; d >>= 1) acc[q] += __shfl_xor(acc[q], d, 64);
-    if (lane == 0) {
-        if (acc[0]) atomicAdd(&a.st[kPrOld], acc[0]);
-        if (acc[1]) atomicAdd(&a.st[kPrNew], acc[1]);
-        if (acc[2]) atomicAdd(&a.st[kPrDropped], acc[2]);
-        if (acc[3]) atomicAdd(&a.st[kPrLive], acc[3]);
-    }
+    prune_flush(a, acc);
 }
 
 // Defragmentation: every row copied to a fresh pool at the exclusive scan of its new capacity
@@ -1632,7 +1646,7 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
         dmalloc(g, &g->inv, H) || dmalloc(g, &g->fr_off[0], H) || dmalloc(g, &g->fr_off[1], H) ||
         dmalloc(g, &g->fr_len[0], H) || dmalloc(g, &g->fr_len[1], H) || dmalloc(g, &g->escan[0], H) ||
         dmalloc(g, &g->escan[1], H) || dmalloc(g, &g->bsum, 8ull * kStatBlocks) ||
-        dmalloc(g, &g->done, (size_t)(kDoneGroups + 1) * kDoneStride) || dmalloc(g, &g->ctr, 1) ||
+        dmalloc(g, &g->done, (size_t)(kDoneGroups + 1) * kDoneStride) || dmalloc(g, &g->ctr, 1) || dmalloc(g, &g->gbar, 2) ||
         dmalloc(g, &g->blk_stats, (size_t)kStatBlocks * kStatCols) || dmalloc(g, &g->misc_dev, 16) ||
         dmalloc(g, &g->pool_top_dev, 1) || dmalloc(g, &g->uin_off, H) || dmalloc(g, &g->uin_len, H) ||
         dmalloc(g, &g->uin_head, g->n_slots + 1))
@@ -1644,6 +1658,7 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
         return fail(FGI_ENOMEM);
     hipMemset(g->done, 0, (size_t)(kDoneGroups + 1) * kDoneStride * sizeof(unsigned long long));
     hipMemset(g->bsum, 0, 8ull * kStatBlocks * sizeof(unsigned long long));
+    hipMemset(g->gbar, 0, 2 * sizeof(unsigned long long));
     hipMemset(g->vis_bm, 0, g->bm_words * 4);
     hipMemset(g->inv_bm, 0, g->bm_words * 4);
     hipMemset(g->uin_more, 0, g->bm_words * 4);
@@ -1710,6 +1725,7 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->bsum);
     dfree(g->done);
     dfree(g->ctr);
+    dfree(g->gbar);
     dfree(g->blk_stats);
     dfree(g->roots_buf);
     dfree(g->imm_buf);
@@ -2447,7 +2463,7 @@ static fgi_status batch_launch(fgi_graph* g, uint32_t from, uint32_t n_steps, co
 fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, uint32_t* out_ids, uint64_t cap,
                          uint64_t* out_n, fgi_batch_stats* stats) {
     if (!g || (n_steps && !steps)) return FGI_EINVAL;
-    FGI_TRY(coop_warm(g));   // once per graph, before the call's timed span
+    if (coop_launch_mode()) FGI_TRY(coop_warm(g));   // once per graph, before the call's timed span
     const auto t0 = std::chrono::steady_clock::now();
     if (out_n) *out_n = 0;
     uint64_t n_waves = 0, n_begin = 0, n_add = 0;
@@ -2644,6 +2660,8 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
         g->free_detached.resize(g->free_detached.size() - (size_t)scr_h[2]);
         return set_err(g, FGI_ECAPACITY, "step %u: out of detached handles (%zu free)", k, g->free_detached.size());
     }
+    if (scr_h[3 + 7])   // acc[kAccBarrier]: a cascade's grid barrier timed out (its results are not trusted)
+        return set_err(g, FGI_EDEVICE, "a cascade's grid barrier timed out: blocks of one grid were not resident together");
     // host bookkeeping: the detached handles taken, the per-step outputs
     g->free_detached.resize(g->free_detached.size() - (size_t)scr_h[2]);
     for (uint32_t k = 0; k < n_steps; ++k) {
@@ -2703,10 +2721,14 @@ static fgi_status prune_range_launch(fgi_graph* g, uint32_t lo, uint32_t hi, Tmp
     FGI_TRY(tmalloc(g, tmap, &a.chunk_map, max_chunks));
     FGI_TRY(tmalloc(g, tcst, &a.chunk_st, max_chunks));
     FGI_HIP(g, hipMemsetAsync(a.chunk_st, 0, max_chunks * sizeof(uint32_t), s));
-    static int per_cu = 0;
-    if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_prune, 256, 0) != hipSuccess || per_cu < 1))
+    // each phase on the blocks the chip holds at once (chunks wait on earlier chunks: a second round
+    // of blocks would leave a tail)
+    static int per_cu = 0, per_cu2 = 0;
+    if (per_cu == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_prune_rows, 256, 0) != hipSuccess || per_cu < 1))
         per_cu = 1;
-    FGI_TRY(coop_warm(g));
+    if (per_cu2 == 0 &&
+        (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu2, k_prune_chunks, 256, 0) != hipSuccess || per_cu2 < 1))
+        per_cu2 = 1;
     const uint64_t resident = (uint64_t)per_cu * (uint64_t)std::max(g->n_cu, 1);
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(resident, nblk((uint64_t)(hi - lo) * 64)));
     a.lo = lo;
@@ -2730,9 +2752,11 @@ static fgi_status prune_range_launch(fgi_graph* g, uint32_t lo, uint32_t hi, Tmp
         a.cur_bm = cur;
     }
     if (getenv("FGI_TRACE")) fprintf(stderr, "[fgi] prune [%u, %u): %u blocks (%d per CU)\n", lo, hi, grid, per_cu);
-    void* args[] = {&a};
     if (e0) FGI_HIP(g, hipEventRecord(e0, s));
-    FGI_HIP(g, hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_prune), dim3(grid), dim3(256), args, 0, s));
+    hipLaunchKernelGGL(k_prune_rows, dim3(grid), dim3(256), 0, s, a);
+    const uint64_t resident2 = (uint64_t)per_cu2 * (uint64_t)std::max(g->n_cu, 1);
+    hipLaunchKernelGGL(k_prune_chunks, dim3((uint32_t)std::min<uint64_t>(resident2, max_chunks)), dim3(256), 0, s, a);
+    FGI_HIP(g, hipGetLastError());
     return FGI_OK;
 }
 

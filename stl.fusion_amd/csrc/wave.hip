@@ -1540,7 +1540,7 @@ constexpr uint32_t kFinalStage = 1024;   // bitmap words a block keeps in LDS (8
 // grid barrier where run_wave has a kernel boundary. The root count may be read from the device
 // (roots produced by an earlier step). The invalidated handles are appended at out[*out_n ..) in
 // ascending order and *out_n advanced; acc accumulates the batch's totals.
-enum : int { kAccWaves, kAccLevels, kAccInv, kAccETrav, kAccEMatch, kAccFlagged, kAccFTotal, kAccN };
+enum : int { kAccWaves, kAccLevels, kAccInv, kAccETrav, kAccEMatch, kAccFlagged, kAccFTotal, kAccBarrier, kAccN };
 static_assert(kAccN <= kAccCount, "batch accumulators");
 
 struct CoopArgs {
@@ -1568,10 +1568,43 @@ struct CoopArgs {
     unsigned long long* out_n;
     unsigned long long* acc;           // [kAccN]
     const unsigned long long* abort;   // nullable: a batch's abort word (set: the wave does nothing)
+    unsigned long long* gbar;          // plain launch: the grid barrier's arrival counter (monotonic)
 };
 
+// Grid barrier of a plain (non-cooperative) launch of k_wave_coop. A cooperative launch goes to the
+// runtime's cooperative queue: ~11.7 us of dispatch gap before each, where plain launches follow
+// each other within 0.1 us (profiles/r6n_stream_kernels.txt), and a streaming round makes six of
+// them, four with no roots. The grid is one block per CU, far below what the chip holds resident,
+// so every block runs at once without the cooperative guarantee. As the device library's barrier:
+// agent-scope fences on both sides; one thread per block arrives on a monotonic counter and waits
+// for the next multiple of the grid size. A wait longer than 2 s (wall clock, 100 MHz) gives up and
+// flags the batch (acc[kAccBarrier]: fgi_run_batch then fails with FGI_EDEVICE) instead of hanging.
+constexpr uint64_t kGridBarTimeout = 200000000ull;
+__device__ __forceinline__ void soft_grid_sync(unsigned long long* cnt, unsigned long long* broken) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long arrived = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long target = (arrived / gridDim.x + 1) * gridDim.x;
+        const uint64_t t0 = wall_clock64();
+        while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if (wall_clock64() - t0 > kGridBarTimeout) {
+                __hip_atomic_store(broken, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+}
+
+template <bool SOFT>
 __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
-    cooperative_groups::grid_group grid = cooperative_groups::this_grid();
+    auto grid_sync = [&]() {
+        if constexpr (SOFT) soft_grid_sync(a.gbar, a.acc + kAccBarrier);
+        else cooperative_groups::this_grid().sync();
+    };
     __shared__ __align__(16) uint32_t s_x[kChunkEmitCap + 8];
     uint32_t* s_rel = s_x;
     uint32_t* s_base = s_x + kChunk + 4;
@@ -1604,14 +1637,14 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
     if (a.imm) {   // Invalidate(true) roots first: their CAS may change node words
         for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gsize)
             root_step<1>(i0 + threadIdx.x, a.roots, a.imm, n, 0u, a.n_handles, a.node, a.vis, o0, ctr);
-        grid.sync();
+        grid_sync();
     }
     for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gsize)
         root_step<0>(i0 + threadIdx.x, a.roots, a.imm, n, 0u, a.n_handles, a.node, a.vis, o0, ctr);
     CPROBE(1);
     uint64_t levels = 0, e_trav = 0, f_total = 0;
     for (int L = 0;; ++L) {
-        grid.sync();   // level L's frontier (and its counter) is complete
+        grid_sync();   // level L's frontier (and its counter) is complete
         if (L < 4) CPROBE(2 + L);
         if (threadIdx.x == 0) s_ft = coh_read(&ctr->lvl[L % kRing].ft);
         __syncthreads();
@@ -1667,7 +1700,7 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
     c = block_sum(c, s_red);
     if (threadIdx.x == 0) coh_xchg(a.cnt + blockIdx.x, c);
     CPROBE(6);
-    grid.sync();
+    grid_sync();
     CPROBE(7);
     unsigned long long part = 0;
     for (uint32_t k = threadIdx.x; k < blockIdx.x; k += blockDim.x) part += coh_read(a.cnt + k);
@@ -2010,7 +2043,18 @@ void print_coop_probe() {
 }
 #endif
 
-// One push-only wave in a single cooperative launch (k_wave_coop): no host synchronisation. The roots
+// FGI_COOP_LAUNCH=1: k_wave_coop as a cooperative launch (grid barriers by the device library)
+// instead of a plain launch with soft_grid_sync. Nothing else launches cooperatively.
+bool coop_launch_mode() {
+    static const bool coop = [] {
+        const char* e = getenv("FGI_COOP_LAUNCH");
+        return e && e[0] == '1';
+    }();
+    return coop;
+}
+
+// One push-only wave in a single launch of k_wave_coop (one block per CU, grid barriers between its
+// phases): no host synchronisation. The roots
 // (n_max, or *n_dev of them) are device-resident; the invalidated handles are appended at
 // out[*out_n ..). The wave folds its visits into the node words itself.
 fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev, const uint8_t* imm_dev,
@@ -2018,16 +2062,19 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
                          unsigned long long* acc, const unsigned long long* abort) {
     hipStream_t s = g->stream;
     FGI_TRY(ensure_cstart(g, std::max<uint64_t>(g->pool_top, g->pool_cap)));
+    const bool coop = coop_launch_mode();
     static int per_cu = 0;
     if (per_cu == 0 &&
-        (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wave_coop, kBlock, 0) != hipSuccess || per_cu < 1))
+        (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, coop ? k_wave_coop<false> : k_wave_coop<true>, kBlock, 0) !=
+             hipSuccess ||
+         per_cu < 1))
         per_cu = 1;
     // one block per CU: enough for the waves this path serves, and a cheaper grid barrier
     const uint32_t G = std::max<uint32_t>((uint32_t)kStats, (uint32_t)std::max(g->n_cu, 1));
     if ((uint64_t)G > (uint64_t)per_cu * (uint64_t)std::max(g->n_cu, 1))
         return set_err(g, FGI_ENOTSUP, "cooperative wave: %u blocks cannot be resident", G);
     FGI_TRY(fold(g));   // visits of a level-launched wave
-    FGI_TRY(coop_warm(g));
+    if (coop) FGI_TRY(coop_warm(g));
     if (!g->coop_clean)
         hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
                            (uint32_t*)nullptr, (uint64_t)g->bm_words);
@@ -2058,8 +2105,14 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
     a.out_n = out_n;
     a.acc = acc;
     a.abort = abort;
-    void* args[] = {&a};
-    FGI_HIP(g, hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_wave_coop), dim3(G), dim3(kBlock), args, 0, s));
+    a.gbar = g->gbar;
+    if (coop) {
+        void* args[] = {&a};
+        FGI_HIP(g, hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_wave_coop<false>), dim3(G), dim3(kBlock), args, 0, s));
+    } else {
+        hipLaunchKernelGGL(k_wave_coop<true>, dim3(G), dim3(kBlock), 0, s, a);
+        FGI_HIP(g, hipGetLastError());
+    }
     g->coop_clean = true;   // the wave folded its visits and cleared what it used
     note_words(g);
     return FGI_OK;
