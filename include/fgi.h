@@ -252,10 +252,11 @@ typedef struct fgi_batch_stats {
  * included; Computed.cs:141-230, 347-385, ComputedRegistry.cs:83-97), but every count stays on the
  * device and each cascade runs as one launch (one block per CU, grid barriers between its levels): the
  * call uploads the batch once and waits for the device once (once more if an add_used step must grow
- * the edge pool, and once more to copy out_ids). FGI_EDEVICE if a cascade's grid barrier timed out. out_ids gets the handles invalidated by the batch's cascades, cascade after cascade
- * (each in ascending order); FGI_ECAPACITY with *out_n = the count if cap is too small. If the
- * batch runs out of detached handles, FGI_ECAPACITY names the step: the steps before it are
- * applied, it and the later ones are not. */
+ * the edge pool, and once more to copy out_ids). out_ids gets the handles invalidated by the batch's
+ * cascades, cascade after cascade (each in ascending order); FGI_ECAPACITY with *out_n = the count if
+ * cap is too small. If the batch runs out of detached handles, FGI_ECAPACITY names the step: the
+ * steps before it are applied, it and the later ones are not. FGI_EINVAL (a bad argument in any step)
+ * applies nothing. FGI_EDEVICE if a cascade's grid barrier timed out. */
 fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, uint32_t* out_ids, uint64_t cap,
                          uint64_t* out_n, fgi_batch_stats* stats);
 

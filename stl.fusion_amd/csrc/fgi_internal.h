@@ -212,6 +212,7 @@ struct fgi_graph {
     uint32_t* home = nullptr;          // [n_detached]: home slot of a detached handle
     std::vector<uint32_t> free_detached;  // host free list of detached handles
     std::vector<uint64_t> seen_bits;      // host scratch bitmap over slots (batch duplicate checks)
+    std::vector<uint8_t> seen_slots;      // host scratch, a byte per slot (fgi_run_batch's duplicate checks)
     // device temporaries of the mutation calls, kept for reuse (same stream, so reuse is ordered
     // after the previous user) instead of a hipMalloc + hipFree (an implicit device sync) per call
     std::vector<std::pair<size_t, void*>> tmp_cache;

@@ -2467,7 +2467,7 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
     const auto t0 = std::chrono::steady_clock::now();
     if (out_n) *out_n = 0;
     uint64_t n_waves = 0, n_begin = 0, n_add = 0;
-    for (uint32_t k = 0; k < n_steps; ++k) {   // the single calls' argument checks
+    for (uint32_t k = 0; k < n_steps; ++k) {   // step kinds and pointers (the elements: while staging)
         const fgi_step& sp = steps[k];
         if (sp.n && !sp.handles) return set_err(g, FGI_EINVAL, "step %u: no handles", k);
         switch (sp.kind) {
@@ -2475,31 +2475,13 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
             case FGI_STEP_SET_OUTPUT:
                 ++n_waves;
                 break;
-            case FGI_STEP_BEGIN_COMPUTE: {
+            case FGI_STEP_BEGIN_COMPUTE:
                 if (sp.n && !sp.version) return set_err(g, FGI_EINVAL, "step %u: no versions", k);
-                std::vector<uint64_t>& seen = g->seen_bits;
-                if (seen.size() < ((size_t)g->n_slots + 63) / 64) seen.assign(((size_t)g->n_slots + 63) / 64, 0);
-                const char* why = nullptr;
-                uint32_t i = 0, bad = 0;
-                for (; i < sp.n; ++i) {
-                    const uint32_t x = sp.handles[i];
-                    if (x >= g->n_slots) { why = "slot out of range"; bad = x; break; }
-                    if (sp.version[i] == 0 || sp.version[i] > kVMask) { why = "bad version"; bad = i; break; }
-                    const uint64_t m = 1ull << (x & 63);
-                    if (seen[x >> 6] & m) { why = "slot repeated in one step"; bad = x; break; }
-                    seen[x >> 6] |= m;
-                }
-                for (uint32_t j = 0; j < i; ++j) seen[sp.handles[j] >> 6] = 0;
-                if (why) return set_err(g, FGI_EINVAL, "step %u: %s (%u)", k, why, bad);
                 ++n_waves;
                 n_begin += sp.n;
                 break;
-            }
             case FGI_STEP_ADD_USED:
                 if (sp.n && !sp.used) return set_err(g, FGI_EINVAL, "step %u: no used handles", k);
-                for (uint32_t i = 0; i < sp.n; ++i)
-                    if (sp.handles[i] >= g->n_handles || sp.used[i] >= g->n_handles)
-                        return set_err(g, FGI_EINVAL, "step %u: handle out of range at %u", k, i);
                 n_add += sp.n;
                 break;
             default:
@@ -2507,6 +2489,7 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
         }
     }
     FGI_TRY(single_only(g, "fgi_run_batch"));
+    const auto t_check = std::chrono::steady_clock::now();
     hipSetDevice(g->device);
     hipStream_t st = g->stream;
     // capacities, before anything is queued: the ids of every cascade, pool headroom for the rows
@@ -2571,29 +2554,84 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
     }
     char* H = g->bst_h;
     char* D = g->bst_d;
-    if (n_take) std::memcpy(H, g->free_detached.data() + (g->free_detached.size() - n_take), n_take * 4);
+    // The single calls' argument checks, made while the inputs are staged (one pass over the caller's
+    // arrays): range and version checks as branch-free reductions beside the copies (they vectorise),
+    // then a slot-repeat test over the staged copy with a byte per slot (independent stores, no
+    // read-modify-write chain through one bitmap word). The first offender is searched for only on
+    // failure. Nothing has been queued yet, so a bad step applies nothing.
     for (uint32_t k = 0; k < n_steps; ++k) {
         const fgi_step& sp = steps[k];
-        const size_t n = sp.n;
-        std::memcpy(H + in_off[4 * k], sp.handles, n * 4);
+        const uint32_t n = sp.n;
+        uint32_t* hh = reinterpret_cast<uint32_t*>(H + in_off[4 * k]);
         bs[k].h = reinterpret_cast<const uint32_t*>(D + in_off[4 * k]);
-        if (sp.kind == FGI_STEP_ADD_USED) {
-            std::memcpy(H + in_off[4 * k + 1], sp.used, n * 4);
-            bs[k].used = reinterpret_cast<const uint32_t*>(D + in_off[4 * k + 1]);
-        }
         if (sp.kind == FGI_STEP_BEGIN_COMPUTE) {
-            std::memcpy(H + in_off[4 * k + 2], sp.version, n * 8);
+            uint64_t* hv = reinterpret_cast<uint64_t*>(H + in_off[4 * k + 2]);
+            uint32_t hmax = 0;
+            uint64_t vbad = 0;
+            for (uint32_t i = 0; i < n; ++i) {
+                const uint32_t x = sp.handles[i];
+                const uint64_t v = sp.version[i];
+                hh[i] = x;
+                hv[i] = v;
+                hmax = std::max(hmax, x);
+                vbad |= (uint64_t)(v - 1 >= kVMask);   // version 0 or > kVMask
+            }
+            std::vector<uint8_t>& seen = g->seen_slots;
+            if (seen.size() < g->n_slots) seen.assign(g->n_slots, 0);
+            uint32_t dup = 0;
+            if (hmax < g->n_slots && !vbad) {
+                for (uint32_t i = 0; i < n; ++i) {
+                    dup |= seen[hh[i]];
+                    seen[hh[i]] = 1;
+                }
+                for (uint32_t i = 0; i < n; ++i) seen[hh[i]] = 0;
+            }
+            if (hmax >= g->n_slots || vbad || dup) {
+                const char* why = "bad step";
+                uint32_t i = 0, bad = 0;
+                for (; i < n; ++i) {
+                    const uint32_t x = sp.handles[i];
+                    if (x >= g->n_slots) { why = "slot out of range"; bad = x; break; }
+                    if (sp.version[i] == 0 || sp.version[i] > kVMask) { why = "bad version"; bad = i; break; }
+                    if (seen[x]) { why = "slot repeated in one step"; bad = x; break; }
+                    seen[x] = 1;
+                }
+                for (uint32_t j = 0; j < i; ++j) seen[sp.handles[j]] = 0;
+                return set_err(g, FGI_EINVAL, "step %u: %s (%u)", k, why, bad);
+            }
             bs[k].ver = reinterpret_cast<const uint64_t*>(D + in_off[4 * k + 2]);
+        } else if (sp.kind == FGI_STEP_ADD_USED) {
+            uint32_t* hu = reinterpret_cast<uint32_t*>(H + in_off[4 * k + 1]);
+            uint32_t hmax = 0;
+            for (uint32_t i = 0; i < n; ++i) {
+                const uint32_t d = sp.handles[i], u = sp.used[i];
+                hh[i] = d;
+                hu[i] = u;
+                hmax = std::max(hmax, std::max(d, u));
+            }
+            if (n && hmax >= g->n_handles)
+                for (uint32_t i = 0; i < n; ++i)
+                    if (sp.handles[i] >= g->n_handles || sp.used[i] >= g->n_handles)
+                        return set_err(g, FGI_EINVAL, "step %u: handle out of range at %u", k, i);
+            bs[k].used = reinterpret_cast<const uint32_t*>(D + in_off[4 * k + 1]);
+        } else {
+            std::memcpy(hh, sp.handles, (size_t)n * 4);
         }
         if (in_off[4 * k + 3]) {
             std::memcpy(H + in_off[4 * k + 3], sp.flags, n);
             bs[k].flags = reinterpret_cast<const uint8_t*>(D + in_off[4 * k + 3]);
         }
     }
+    if (n_take) std::memcpy(H, g->free_detached.data() + (g->free_detached.size() - n_take), n_take * 4);
     unsigned long long* scr = reinterpret_cast<unsigned long long*>(D + in_bytes);
     unsigned long long* scr_h = reinterpret_cast<unsigned long long*>(H + in_bytes);
     std::memset(scr_h, 0, scr_words * 8);
     hipEvent_t b0 = g->ev_w0, b1 = g->ev_w1;
+    // FGI_BATCH_TIMES=1: the call's host phases on stderr (staging, enqueue, wait, unpacking; us)
+    static const bool times = getenv("FGI_BATCH_TIMES") != nullptr;
+    using clk = std::chrono::steady_clock;
+    const clk::time_point t_pack = times ? clk::now() : t0;
+    clk::time_point t_enq = t_pack, t_wait = t_pack;
     FGI_HIP(g, hipEventRecord(b0, st));
     FGI_HIP(g, hipMemcpyAsync(D, H, in_bytes + scr_words * 8, hipMemcpyHostToDevice, st));   // one upload
     // per-step device temporaries
@@ -2641,7 +2679,9 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
         FGI_HIP(g, hipMemcpyAsync(H + in_bytes, D + in_bytes, scr_bytes + out_bytes, hipMemcpyDeviceToHost, st));
         if (spec) FGI_HIP(g, hipMemcpyAsync(H + ids_off, g->bout, spec * 4, hipMemcpyDeviceToHost, st));
         FGI_HIP(g, hipEventRecord(b1, st));
+        if (times) t_enq = clk::now();
         FGI_HIP(g, hipStreamSynchronize(st));
+        if (times) t_wait = clk::now();
         ++syncs;
         g->pool_top = scr_h[ptop_word];
         const unsigned long long ab = scr_h[0];
@@ -2689,6 +2729,13 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
             FGI_HIP(g, hipStreamSynchronize(st));
             ++syncs;
         }
+    }
+    if (times) {
+        const clk::time_point t_end = clk::now();
+        auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        fprintf(stderr, "[fgi] batch check %.1f pack %.1f enqueue %.1f wait %.1f unpack %.1f total %.1f us (%u steps)\n",
+                us(t0, t_check), us(t_check, t_pack),
+                us(t_pack, t_enq), us(t_enq, t_wait), us(t_wait, t_end), us(t0, t_end), n_steps);
     }
     if (stats) {
         const unsigned long long* acc = scr_h + 3;

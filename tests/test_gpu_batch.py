@@ -8,6 +8,8 @@
     one-step batch (displacement and InvalidateOnSetOutput cascades included).
 (c) A batch whose add_used step outgrows the pool headroom (the call grows the pool and resumes).
 (d) A batch that runs out of detached handles: FGI_ECAPACITY, the steps before it applied.
+(e) A batch with a bad argument in any step (a slot repeated in one begin_compute step, a slot or a
+    handle out of range, a bad version): FGI_EINVAL, nothing applied.
 """
 import functools
 
@@ -141,3 +143,47 @@ def test_batch_out_of_detached_handles(pkg, gpu_available):
     assert (f[0] & 3) == 1                  # step 0 applied
     assert (f[1] & 3) == 0 and v[1] == 1    # step 1 not
     g.close()
+
+
+@pytest.mark.parametrize("bad", ["repeat", "slot_range", "version0", "version_big", "used_range", "dep_range"])
+def test_batch_bad_argument_applies_nothing(pkg, gpu_available, bad):
+    rng = np.random.default_rng(61)
+    n = 2000
+    from harness import random_states
+    from test_gpu_parity import _edges_from_live
+    versions, flags = random_states(n, rng, p_delay=0.0)
+    src, dst, tags = _edges_from_live(versions, flags, rng, 8000, n, stale_p=0.2)
+    g, o = build_pair(pkg, n, versions, flags, src, dst, tags)
+    before = g.dump_states()
+    edges = g.export_edges()
+    slots = rng.choice(n, 500, replace=False).astype(np.uint32)
+    ver = (versions[slots] + np.uint64(5)).astype(np.uint64)
+    dep = slots[:300].copy()
+    use = rng.integers(0, n, 300).astype(np.uint32)
+    if bad == "repeat":
+        slots[400] = slots[17]
+    elif bad == "slot_range":
+        slots[250] = n + 3
+    elif bad == "version0":
+        ver[99] = 0
+    elif bad == "version_big":
+        ver[499] = np.uint64(1) << np.uint64(60)
+    elif bad == "used_range":
+        use[123] = g.n_handles
+    elif bad == "dep_range":
+        dep[299] = g.n_handles + 7
+    steps = [("invalidate", rng.integers(0, n, 20).astype(np.uint32)),
+             ("begin_compute", slots, ver),
+             ("add_used", dep, use),
+             ("set_output", slots[:100])]
+    with pytest.raises(pkg.FgiError) as e:
+        g.run_batch(steps)
+    assert e.value.status == pkg.fgi.EINVAL
+    after = g.dump_states()
+    assert all(np.array_equal(a, b) for a, b in zip(before, after))
+    assert all(np.array_equal(a, b) for a, b in zip(edges, g.export_edges()))
+    # the graph still takes a good batch (the scratch the checks used is clean again)
+    slots2 = np.unique(slots[slots < n])[:200].astype(np.uint32)
+    g.run_batch([("begin_compute", slots2, (versions[slots2] + np.uint64(9)).astype(np.uint64))])
+    g.close()
+    o.close()
