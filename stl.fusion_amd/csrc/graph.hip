@@ -2700,8 +2700,12 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
         g->free_detached.resize(g->free_detached.size() - (size_t)scr_h[2]);
         return set_err(g, FGI_ECAPACITY, "step %u: out of detached handles (%zu free)", k, g->free_detached.size());
     }
-    if (scr_h[3 + 7])   // acc[kAccBarrier]: a cascade's grid barrier timed out (its results are not trusted)
+    if (scr_h[3 + 7]) {   // acc[kAccBarrier]: a cascade's grid barrier timed out (its results are not trusted)
+        // the arrival counter may no longer be a multiple of the grid size: start it again
+        FGI_HIP(g, hipMemsetAsync(g->gbar, 0, 2 * sizeof(unsigned long long), st));
+        FGI_HIP(g, hipStreamSynchronize(st));
         return set_err(g, FGI_EDEVICE, "a cascade's grid barrier timed out: blocks of one grid were not resident together");
+    }
     // host bookkeeping: the detached handles taken, the per-step outputs
     g->free_detached.resize(g->free_detached.size() - (size_t)scr_h[2]);
     for (uint32_t k = 0; k < n_steps; ++k) {
