@@ -350,16 +350,16 @@ class Graph:
                     f = _u8(sp[3])
                     keep.append(f)
                     st.flags = f.ctypes.data
-                out = np.zeros(len(h), np.uint32)
+                out = np.empty(len(h), np.uint32)   # every element is written
             elif kind == "add_used":
                 st.kind = STEP_ADD_USED
                 u = _u32(sp[2])
                 keep.append(u)
                 st.used = u.ctypes.data
-                out = np.zeros(len(h), np.uint32)
+                out = np.empty(len(h), np.uint32)   # every element is written
             elif kind == "set_output":
                 st.kind = STEP_SET_OUTPUT
-                out = np.zeros(len(h), np.uint8)
+                out = np.empty(len(h), np.uint8)
             else:
                 raise ValueError(kind)
             if out is not None:
