@@ -10,7 +10,7 @@ python - <<PY
 import json, re, statistics as st
 rows = [l for l in open('$out/stream.err') if l.startswith('[fgi] batch')]
 print(len(rows), 'batches')
-keys = ['check', 'pack', 'enqueue', 'wait', 'unpack', 'total']
+keys = ['check', 'cap', 'stage', 'pack', 'enqueue', 'wait', 'unpack', 'total']
 vals = {k: [] for k in keys}
 for l in rows[len(rows) // 4:]:
     for k in keys:

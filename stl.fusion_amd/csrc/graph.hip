@@ -2503,6 +2503,7 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
     }
     if (n_add) FGI_TRY(ensure_pool(g, g->pool_top + std::max<uint64_t>(1ull << 20, 4 * n_add)));
     FGI_TRY(ensure_cstart(g, std::max<uint64_t>(g->pool_top, g->pool_cap)));
+    const auto t_cap = std::chrono::steady_clock::now();
     // detached handles the begin_compute steps may take (top of the free list)
     const uint64_t n_take = std::min<uint64_t>(n_begin, g->free_detached.size());
     // staging: inputs (uploaded once) | the detached-handle list | outputs (downloaded once)
@@ -2623,6 +2624,7 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
         }
     }
     if (n_take) std::memcpy(H, g->free_detached.data() + (g->free_detached.size() - n_take), n_take * 4);
+    const auto t_stage = std::chrono::steady_clock::now();
     unsigned long long* scr = reinterpret_cast<unsigned long long*>(D + in_bytes);
     unsigned long long* scr_h = reinterpret_cast<unsigned long long*>(H + in_bytes);
     std::memset(scr_h, 0, scr_words * 8);
@@ -2737,8 +2739,8 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
     if (times) {
         const clk::time_point t_end = clk::now();
         auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-        fprintf(stderr, "[fgi] batch check %.1f pack %.1f enqueue %.1f wait %.1f unpack %.1f total %.1f us (%u steps)\n",
-                us(t0, t_check), us(t_check, t_pack),
+        fprintf(stderr, "[fgi] batch check %.1f cap %.1f stage %.1f pack %.1f enqueue %.1f wait %.1f unpack %.1f total %.1f us (%u steps)\n",
+                us(t0, t_check), us(t_check, t_cap), us(t_cap, t_stage), us(t_check, t_pack),
                 us(t_pack, t_enq), us(t_enq, t_wait), us(t_wait, t_end), us(t0, t_end), n_steps);
     }
     if (stats) {
