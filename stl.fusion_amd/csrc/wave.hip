@@ -678,6 +678,17 @@ __device__ __forceinline__ uint32_t level_mult(uint64_t T, uint32_t grid) {
     return m;
 }
 
+// A cascade's grid (k_wave_coop) is one block per CU and its levels are small: the largest chunks
+// that still leave every chunk its own block, so a level is one round of chunks (each chunk is a chain
+// of dependent round trips; a second round doubles the level). A 100-hub wave's leaf level (100 k
+// edges) takes 196 chunks of 512 edges instead of 391 of 256 over 256 blocks.
+__device__ __forceinline__ uint32_t level_mult_one_round(uint64_t T, uint32_t grid) {
+    const uint64_t nfine = (T + kFine - 1) / kFine;
+    uint32_t m = 1;
+    while (m < (uint32_t)kEPT && (nfine + m - 1) / m > grid) m <<= 1;
+    return m;
+}
+
 // ---- collect: a pull level's winners lists -> the next level's frontier list ------------------
 // Pull block b listed its expandable winners at wl[seg[b] ..); the pull's last block left the
 // exclusive prefixes of the per-block (winners, expandable winners, row lengths) sums in pre[].
@@ -1569,6 +1580,7 @@ struct CoopArgs {
     unsigned long long* acc;           // [kAccN]
     const unsigned long long* abort;   // nullable: a batch's abort word (set: the wave does nothing)
     unsigned long long* gbar;          // plain launch: the grid barrier's arrival counter (monotonic)
+    int one_round;                     // chunk size by level_mult_one_round (FGI_COOP_CHUNKS=0: level_mult)
 };
 
 // Grid barrier of a plain (non-cooperative) launch of k_wave_coop. A cooperative launch goes to the
@@ -1665,7 +1677,8 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
         const Out o{a.row_off, a.row_len,        a.inv_bm, a.fr_off[buf ^ 1], a.fr_len[buf ^ 1],
                     a.escan[buf ^ 1], a.cstart[buf ^ 1], &ctr->lvl[(L + 1) % kRing]};
         emit_init(em);
-        expand_level<false>(kProbeLevelsOff, F, T, level_mult(T, gridDim.x), x, a.node, a.vis, o, em, s_x, me, s_rel, s_base, a.blk,
+        const uint32_t mult = a.one_round ? level_mult_one_round(T, gridDim.x) : level_mult(T, gridDim.x);
+        expand_level<false>(kProbeLevelsOff, F, T, mult, x, a.node, a.vis, o, em, s_x, me, s_rel, s_base, a.blk,
                             s_st, RemoteArgs{});
     }
     // final collect (as k_final, with a grid barrier instead of waiting on status words)
@@ -2106,6 +2119,11 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
     a.acc = acc;
     a.abort = abort;
     a.gbar = g->gbar;
+    static const int one_round = [] {
+        const char* e = getenv("FGI_COOP_CHUNKS");
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    a.one_round = one_round;
     if (coop) {
         void* args[] = {&a};
         FGI_HIP(g, hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_wave_coop<false>), dim3(G), dim3(kBlock), args, 0, s));
