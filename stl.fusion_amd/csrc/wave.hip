@@ -2082,12 +2082,13 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
              hipSuccess ||
          per_cu < 1))
         per_cu = 1;
-    // one block per CU: enough for the waves this path serves, and a cheaper grid barrier
     static const uint32_t g_env = [] {   // FGI_COOP_BLOCKS: measurement knob (grid size)
         const char* e = getenv("FGI_COOP_BLOCKS");
         return e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
     }();
-    const uint32_t G = std::max<uint32_t>((uint32_t)kStats, g_env ? g_env : (uint32_t)std::max(g->n_cu, 1));
+    // one block per two CUs: with the software barrier a grid of 128 runs a configs[4] round's cascades
+    // in 0.24 ms of kernels against 0.32 ms with 256 blocks (profiles/r6zl_coop_blocks.txt)
+    const uint32_t G = std::max<uint32_t>((uint32_t)kStats, g_env ? g_env : (uint32_t)std::max(g->n_cu / 2, 1));
     if ((uint64_t)G > (uint64_t)per_cu * (uint64_t)std::max(g->n_cu, 1))
         return set_err(g, FGI_ENOTSUP, "cooperative wave: %u blocks cannot be resident", G);
     FGI_TRY(fold(g));   // visits of a level-launched wave
