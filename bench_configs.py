@@ -168,7 +168,7 @@ def run_stream(pkg, W, args):
         bst = pkg.fgi.BatchStats()
         # the application's batches (the synthetic schedule) are built before the timed loop
         tb = time.perf_counter()
-        batches = []
+        batches, expect = [], []
         R = p["rounds"]
         R_prof = max(10, R // 5)   # instrumented rounds after the timed ones: the cascades' share
         for r in range(1, R + R_prof + 1):
@@ -181,6 +181,11 @@ def run_stream(pkg, W, args):
                       ("begin_compute", ls, mix.new_versions(ls).copy(), mix.has_delay[ls]),
                       ("add_used", ls, mix.hub_of(ls)), ("set_output", ls), ("invalidate", roots)]
             batches.append(steps)
+            # the round's cascades, in step order: the timers' roots (each a delayed leaf whose delay
+            # the previous wave started: Invalidate(true) invalidates it), then the wave, which is
+            # the root hubs plus their undelayed leaves (Computed.cs:186-198: delayed ones only start)
+            ch = mix.children(roots)
+            expect.append(np.concatenate([np.sort(timers), np.sort(np.concatenate([roots, ch[mix.has_delay[ch] == 0]]))]))
             e_edges += len(ls)
             prev = roots
         build_s = time.perf_counter() - tb
@@ -188,11 +193,16 @@ def run_stream(pkg, W, args):
         # process's one-time cooperative-launch setup is paid by an empty batch first (like the load)
         g.set_option(pkg.fgi.OPT_LEVEL_TIMING, 0)
         g.run_batch([])
+        got = []
         t0 = time.perf_counter()
         for steps in batches[:R]:
             ids, _ = g.run_batch(steps, stats=bst)
+            got.append(ids)
             v_inv += len(ids)
         total = time.perf_counter() - t0
+        # every timed round's ids against the schedule's closed form (after the clock stops)
+        bad = [r for r, (a, b) in enumerate(zip(got, expect)) if not np.array_equal(a, b.astype(a.dtype))]
+        del got
         # instrumented rounds: every cascade between HIP events
         g.set_option(pkg.fgi.OPT_LEVEL_TIMING, 1)
         pst = pkg.fgi.BatchStats()
@@ -215,8 +225,13 @@ def run_stream(pkg, W, args):
                "host_syncs_per_round": bst.host_syncs / R, "cascades_per_round": bst.waves / R,
                "run_batch_call_ms_per_round": bst.total_ms / R, "schedule_build_ms_per_round": build_s / R * 1e3,
                "initial_load_s": load_s,
-               "note": "host arrays cross the C-ABI once per round (one pinned upload, one download of the ids)"}
+               "checked_rounds": R, "rounds_with_wrong_ids": bad,
+               "note": "host arrays cross the C-ABI once per round (one pinned upload, one download of the ids); "
+                       "every timed round's ids checked against the schedule's closed form (timer roots, then "
+                       "the wave's hubs and undelayed leaves); node words are checked against the oracle at "
+                       "this size in tests/test_gpu_full_size.py"}
         g.close()
+        assert not bad, f"configs[4]: rounds {bad[:8]} returned ids other than the schedule's"
         return out
     t0 = time.perf_counter()
     for r in range(1, p["rounds"] + 1):

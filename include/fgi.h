@@ -256,7 +256,15 @@ typedef struct fgi_batch_stats {
  * cascades, cascade after cascade (each in ascending order); FGI_ECAPACITY with *out_n = the count if
  * cap is too small. If the batch runs out of detached handles, FGI_ECAPACITY names the step: the
  * steps before it are applied, it and the later ones are not. FGI_EINVAL (a bad argument in any step)
- * applies nothing. FGI_EDEVICE if a cascade's grid barrier timed out. */
+ * applies nothing.
+ * FGI_EDEVICE if a cascade's grid barrier timed out (blocks of one cascade's grid were not resident
+ * together, e.g. other work held the device). The batch is then half-applied: the steps before the
+ * failed cascade are, the cascade may have been partly folded into node words, the later steps are
+ * not. The graph is poisoned: every later call but fgi_restore, fgi_destroy, fgi_last_error and
+ * fgi_set_option returns FGI_ESTATE until fgi_restore brings back the last snapshot (node words, rows,
+ * detached handles); without a snapshot, only fgi_destroy remains. This mirrors the reference's
+ * "Invalidate never throws" (Computed.cs:200-229) as far as a device fault allows: the failure is
+ * reported once and nothing later runs on an undefined registry. */
 fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, uint32_t* out_ids, uint64_t cap,
                          uint64_t* out_n, fgi_batch_stats* stats);
 
@@ -285,7 +293,9 @@ fgi_status fgi_release(fgi_graph* g, uint32_t n, const uint32_t* handle);
 /* ---- bench / test support ------------------------------------------------------------------- */
 /* Save / restore node states and row lengths on the device (reset from a pristine copy).
  * fgi_restore is stream-ordered: it may return before the device copies finish; every later call
- * on the graph runs after them. */
+ * on the graph runs after them. On a poisoned graph (a failed fgi_run_batch, FGI_EDEVICE) fgi_restore
+ * copies back every saved table, clears the wave bitmaps and the detached-handle list to the
+ * snapshot's, and makes the graph usable again. */
 fgi_status fgi_snapshot(fgi_graph* g);
 fgi_status fgi_restore(fgi_graph* g);
 /* Device-side synthetic workloads. All nodes Consistent with
@@ -323,7 +333,12 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *   FGI_OPT_HOT_HEADS   [0]  most list heads a pull level probes through the hot snapshot: 0 sizes
  *                            it from the graph (65,536-262,144); n > 0 caps it at n rounded up to 256,
  *                            so the other heads are probed in the invalidated bitmap itself (tests pin
- *                            that path on small graphs; results never depend on it) */
+ *                            that path on small graphs; results never depend on it)
+ *   FGI_OPT_FAULT_INJECT [0] tests only: value (k << 16) | b, b > 0: in the (k+1)-th streaming
+ *                            cascade launched from now (fgi_run_batch), block b - 1 leaves at its first
+ *                            grid barrier without arriving, and that cascade's barrier times out after
+ *                            20 ms: the failure path runs deterministically (FGI_EDEVICE, then the
+ *                            poisoned graph) */
 #define FGI_OPT_DEAD_FILTER 1
 #define FGI_OPT_DIRECTION 2
 #define FGI_OPT_PULL_ALPHA 3
@@ -334,6 +349,7 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
 #define FGI_OPT_PULL_TPB 8
 #define FGI_OPT_FRONT_EXCHANGE 9
 #define FGI_OPT_HOT_HEADS 10
+#define FGI_OPT_FAULT_INJECT 11
 fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value);
 
 /* ---- multi-GPU (1-D vertex-range partition, RCCL all-to-all frontier exchange) --------------- */

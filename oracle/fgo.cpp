@@ -548,6 +548,29 @@ uint32_t fgo_add_used(fgo* o, uint32_t dependant_h, uint32_t used_h, fgo_stats* 
     return result;
 }
 
+// Batches of the three calls above over slots (each slot's most recent node), applied one by one
+// in order: the same calls a test would make per element, without a foreign call per element.
+int fgo_begin_compute_n(fgo* o, uint32_t n, const uint32_t* slots, const uint64_t* versions,
+                        const uint8_t* has_delay, fgo_stats* st) {
+    for (uint32_t i = 0; i < n; ++i)
+        if (fgo_begin_compute(o, slots[i], versions[i], has_delay ? has_delay[i] : 0, nullptr, nullptr, st)) return 1;
+    return 0;
+}
+
+uint32_t fgo_set_output_n(fgo* o, uint32_t n, const uint32_t* slots, fgo_stats* st) {
+    uint32_t set = 0;
+    for (uint32_t i = 0; i < n; ++i) set += (uint32_t)fgo_set_output(o, fgo_last(o, slots[i]), st);
+    return set;
+}
+
+void fgo_add_used_n(fgo* o, uint32_t n, const uint32_t* dependant_slots, const uint32_t* used_slots,
+                    uint32_t* out_codes, fgo_stats* st) {
+    for (uint32_t i = 0; i < n; ++i) {
+        const uint32_t r = fgo_add_used(o, fgo_last(o, dependant_slots[i]), fgo_last(o, used_slots[i]), st);
+        if (out_codes) out_codes[i] = r;
+    }
+}
+
 int fgo_invalidate_slots(fgo* o, uint32_t n, const uint32_t* slots, const uint8_t* immediately,
                          uint32_t n_threads, fgo_stats* st) {
     o->wave++;

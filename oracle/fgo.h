@@ -92,6 +92,13 @@ int fgo_begin_compute(fgo* o, uint32_t slot, uint64_t version, int has_delay,
 int fgo_set_output(fgo* o, uint32_t h, fgo_stats* st);
 /* dependant.AddUsed(used) (Computed.cs:347-368): returns an FGO_USED_* code. */
 uint32_t fgo_add_used(fgo* o, uint32_t dependant_h, uint32_t used_h, fgo_stats* st);
+/* The three calls above over slots (each resolved to fgo_last(slot)), one by one in order.
+ * has_delay and out_codes may be NULL. fgo_set_output_n returns how many nodes were Computing. */
+int fgo_begin_compute_n(fgo* o, uint32_t n, const uint32_t* slots, const uint64_t* versions,
+                        const uint8_t* has_delay, fgo_stats* st);
+uint32_t fgo_set_output_n(fgo* o, uint32_t n, const uint32_t* slots, fgo_stats* st);
+void fgo_add_used_n(fgo* o, uint32_t n, const uint32_t* dependant_slots, const uint32_t* used_slots,
+                    uint32_t* out_codes, fgo_stats* st);
 
 /* `using (Computed.Invalidate()) svc.Get(slot)` for each root slot in order
  * (Internal/ComputedExt.cs:29-35 -> Computed.cs:162-230). immediately may be NULL.

@@ -43,7 +43,10 @@ _SIG = {
     "fgo_begin_compute": ([_O, C.c_uint32, C.c_uint64, C.c_int, _u32p, _u32p, C.POINTER(Stats)], C.c_int),
     "fgo_set_output": ([_O, C.c_uint32, C.POINTER(Stats)], C.c_int),
     "fgo_add_used": ([_O, C.c_uint32, C.c_uint32, C.POINTER(Stats)], C.c_uint32),
-    "fgo_invalidate_slots": ([_O, C.c_uint32, _u32p, _u8p, C.c_uint32, C.POINTER(Stats)], C.c_int),
+    "fgo_begin_compute_n": ([_O, C.c_uint32, _u32p, _u64p, _u8p, C.POINTER(Stats)], C.c_int),
+    "fgo_set_output_n": ([_O, C.c_uint32, _u32p, C.POINTER(Stats)], C.c_uint32),
+    "fgo_add_used_n": ([_O, C.c_uint32, _u32p, _u32p, _u32p, C.POINTER(Stats)], None),
+    "fgo_invalidate_slots":([_O, C.c_uint32, _u32p, _u8p, C.c_uint32, C.POINTER(Stats)], C.c_int),
     "fgo_invalidate_nodes": ([_O, C.c_uint32, _u32p, _u8p, C.POINTER(Stats)], C.c_int),
     "fgo_invalidate_everything": ([_O, C.POINTER(Stats)], C.c_int),
     "fgo_prune": ([_O, _u64p, _u64p], C.c_int),
@@ -195,6 +198,22 @@ class Oracle:
 
     def add_used(self, dependant_h, used_h):
         return self.l.fgo_add_used(self.o, dependant_h, used_h, None)
+
+    def begin_compute_slots(self, slots, versions, has_delay=None):
+        s, v = u32(slots), u64(versions)
+        d = None if has_delay is None else np.ascontiguousarray(np.asarray(has_delay, np.uint8))
+        assert self.l.fgo_begin_compute_n(self.o, len(s), _p(s, C.c_uint32), _p(v, C.c_uint64), _p(d, C.c_uint8),
+                                          None) == 0
+
+    def set_output_slots(self, slots):
+        s = u32(slots)
+        return self.l.fgo_set_output_n(self.o, len(s), _p(s, C.c_uint32), None)
+
+    def add_used_slots(self, dependant_slots, used_slots):
+        d, u = u32(dependant_slots), u32(used_slots)
+        out = np.zeros(len(d), np.uint32)
+        self.l.fgo_add_used_n(self.o, len(d), _p(d, C.c_uint32), _p(u, C.c_uint32), _p(out, C.c_uint32), None)
+        return out
 
     def invalidate_slots(self, slots, immediately=None, threads=1, stats=None):
         s = u32(slots)

@@ -139,6 +139,10 @@ constexpr uint32_t kHotMin = kLdsHot * 32 > 65536 ? kLdsHot * 32 : 65536;
 // resident k_level blocks per CU: LDS-bound once the LDS snapshot passes 8 KB (160 KB per CU)
 constexpr uint32_t kLevelOcc = kLdsHot <= 2048 ? 5 : kLdsHot <= 4096 ? 4 : 3;
 constexpr int kAccCount = 8;            // batch accumulators (fgi_run_batch; run_wave_coop's acc)
+// A batch's abort word (fgi_run_batch): reason << 32 | (step + 1). kAbortBarrier: a cascade's grid
+// barrier timed out (no step index; the graph is poisoned until fgi_restore).
+constexpr unsigned long long kAbortDetach = 1, kAbortPool = 2, kAbortBarrier = 3;
+constexpr int kAccBarrierIdx = 7;       // acc[7]: a cascade's grid barrier timed out
 
 // Per-level counters. The producers of level L's frontier (roots, push emits, received targets)
 // reserve list space with ONE packed 64-bit atomic on `ft` (frontier entries << 32 | edges): the
@@ -339,6 +343,16 @@ struct fgi_graph {
     uint32_t* snap_row_cap = nullptr;
     uint32_t* snap_used = nullptr;
     uint64_t snap_epoch = ~0ull;
+    uint32_t* snap_home = nullptr;           // [n_detached]
+    std::vector<uint32_t> snap_free_detached;
+
+    // A failed streaming batch (a cascade's grid barrier timed out) left the graph half-applied: every
+    // entry point but fgi_restore / fgi_destroy / fgi_last_error / fgi_set_option returns FGI_ESTATE
+    // until fgi_restore brings back the snapshot (graph.hip, usable()).
+    bool failed = false;
+    int coop_per_cu = 0;                     // resident k_wave_coop blocks per CU on this graph's device
+    uint32_t fault_block = 0;                // FGI_OPT_FAULT_INJECT: block + 1 of a cascade that skips a barrier
+    uint32_t fault_skip = 0;                 // ... after this many more cascade launches
 
     // timing
     std::vector<hipEvent_t> ev;        // pairs around expand launches
@@ -417,7 +431,7 @@ void print_coop_probe();
 // happens if *abort (nullable) is set when the wave starts.
 fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev, const uint8_t* imm_dev,
                          const unsigned long long* n_dev, uint32_t* out, unsigned long long* out_n,
-                         unsigned long long* acc, const unsigned long long* abort);
+                         unsigned long long* acc, unsigned long long* abort);
 // Rebuild the expandable-class bitmap if node words changed (wave.hip).
 fgi_status ensure_cls(fgi_graph* g);
 // Pull tiles of a level over n slots with `grid` blocks.

@@ -560,8 +560,7 @@ __global__ void k_set_output(uint32_t n, const uint32_t* __restrict__ h, uint32_
 // ---- streaming batches (fgi_run_batch) ------------------------------------------------------------
 // A batch's kernels read their item counts from the device and do nothing once the batch's abort
 // word is set (a step that cannot complete here: the host finishes it, or reports it, after its one
-// synchronisation). Abort word: reason << 32 | (step + 1).
-constexpr unsigned long long kAbortDetach = 1, kAbortPool = 2;
+// synchronisation). Abort word: reason << 32 | (step + 1) (kAbort*, fgi_internal.h).
 
 __device__ __forceinline__ bool batch_aborted(const unsigned long long* ab) {
     return __hip_atomic_load(ab, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
@@ -1610,6 +1609,13 @@ fgi_status load_rows(fgi_graph* g, uint64_t m, const uint64_t* host_keys, const 
 using namespace fgi;
 
 static fgi_status single_only(fgi_graph* g, const char* what);
+// A graph a failed batch poisoned (fgi_run_batch, FGI_EDEVICE) takes no call but fgi_restore,
+// fgi_destroy, fgi_last_error and fgi_set_option.
+static fgi_status usable(fgi_graph* g) {
+    return g->failed ? set_err(g, FGI_ESTATE, "a streaming batch failed on the device (%s); fgi_restore or fgi_destroy",
+                               "grid barrier timeout")
+                     : FGI_OK;
+}
 
 extern "C" {
 
@@ -1735,6 +1741,7 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->snap_row_len);
     dfree(g->snap_row_cap);
     dfree(g->snap_used);
+    dfree(g->snap_home);
     if (g->scratch) hipFree(g->scratch);
     if (g->ctr_host) hipHostFree(g->ctr_host);
     if (g->misc_host) hipHostFree(g->misc_host);
@@ -1806,6 +1813,7 @@ fgi_status fgi_load_edges(fgi_graph* g, uint64_t m, const uint32_t* used, const 
 
 fgi_status fgi_get_state(fgi_graph* g, uint32_t n, const uint32_t* handle, uint64_t* version, uint32_t* state_flags) {
     if (!g || (n && !handle)) return FGI_EINVAL;
+    FGI_TRY(usable(g));
     for (uint32_t i = 0; i < n; ++i)
         if (handle[i] >= g->n_handles) return set_err(g, FGI_EINVAL, "handle %u out of range", handle[i]);
     if (n == 0) return FGI_OK;
@@ -1830,6 +1838,7 @@ fgi_status fgi_get_state(fgi_graph* g, uint32_t n, const uint32_t* handle, uint6
 
 fgi_status fgi_dump_states(fgi_graph* g, uint64_t* version, uint32_t* state_flags) {
     if (!g) return FGI_EINVAL;
+    FGI_TRY(usable(g));
     hipSetDevice(g->device);
     FGI_TRY(fold(g));
     std::vector<uint64_t> w(g->n_handles);
@@ -1870,6 +1879,7 @@ __global__ void k_used_by_live(uint32_t len, const uint32_t* __restrict__ col, c
 
 fgi_status fgi_get_used_by(fgi_graph* g, uint32_t handle, uint32_t* dep, uint64_t* tag, uint64_t cap, uint64_t* out_n) {
     if (!g || handle >= g->n_handles) return FGI_EINVAL;
+    FGI_TRY(usable(g));
     hipSetDevice(g->device);
     FGI_TRY(fold(g));
     uint64_t w = 0, off = 0;
@@ -1908,6 +1918,7 @@ fgi_status fgi_get_used_by(fgi_graph* g, uint32_t handle, uint32_t* dep, uint64_
 
 fgi_status fgi_get_used_count(fgi_graph* g, uint32_t handle, uint32_t* out) {
     if (!g || !out || handle >= g->n_handles) return FGI_EINVAL;
+    FGI_TRY(usable(g));
     hipSetDevice(g->device);
     FGI_TRY(fold(g));
     uint64_t w = 0;
@@ -1920,6 +1931,7 @@ fgi_status fgi_get_used_count(fgi_graph* g, uint32_t handle, uint32_t* out) {
 
 fgi_status fgi_get_degrees(fgi_graph* g, uint32_t* degree, uint64_t* total) {
     if (!g) return FGI_EINVAL;
+    FGI_TRY(usable(g));
     hipSetDevice(g->device);
     FGI_TRY(fold(g));
     const uint32_t H = g->n_handles;
@@ -1939,6 +1951,7 @@ fgi_status fgi_get_degrees(fgi_graph* g, uint32_t* degree, uint64_t* total) {
 
 fgi_status fgi_export_edges(fgi_graph* g, uint32_t* used, uint32_t* dep, uint64_t* tag, uint64_t cap, uint64_t* out_n) {
     if (!g) return FGI_EINVAL;
+    FGI_TRY(usable(g));
     hipSetDevice(g->device);
     FGI_TRY(fold(g));
     Tmp tk, tt;
@@ -1958,6 +1971,7 @@ fgi_status fgi_export_edges(fgi_graph* g, uint32_t* used, uint32_t* dep, uint64_
 
 fgi_status fgi_snapshot(fgi_graph* g) {
     if (!g) return FGI_EINVAL;
+    FGI_TRY(usable(g));
     hipSetDevice(g->device);
     const size_t H = g->n_handles;
     if (!g->snap_node) {
@@ -1972,6 +1986,11 @@ fgi_status fgi_snapshot(fgi_graph* g) {
     FGI_HIP(g, hipMemcpyAsync(g->snap_row_len, g->row_len, H * 4, hipMemcpyDeviceToDevice, s));
     FGI_HIP(g, hipMemcpyAsync(g->snap_row_cap, g->row_cap, H * 4, hipMemcpyDeviceToDevice, s));
     FGI_HIP(g, hipMemcpyAsync(g->snap_used, g->used_cnt, H * 4, hipMemcpyDeviceToDevice, s));
+    if (g->n_detached) {
+        if (!g->snap_home && dmalloc(g, &g->snap_home, g->n_detached)) return FGI_ENOMEM;
+        FGI_HIP(g, hipMemcpyAsync(g->snap_home, g->home, (size_t)g->n_detached * 4, hipMemcpyDeviceToDevice, s));
+    }
+    g->snap_free_detached = g->free_detached;
     FGI_HIP(g, hipStreamSynchronize(s));
     g->snap_epoch = g->pool_epoch;
     g->snap_mut_epoch = g->mut_epoch;
@@ -1985,11 +2004,27 @@ fgi_status fgi_snapshot(fgi_graph* g) {
 // snapshot's and clearing the bitmap restores every node; words are copied back only if something
 // else (a fold, a mutation, an immediate root) changed them.
 fgi_status fgi_restore(fgi_graph* g) {
-    if (!g || !g->snap_node) return FGI_EINVAL;
+    if (!g) return FGI_EINVAL;
+    if (!g->snap_node) return g->failed ? usable(g) : FGI_EINVAL;
     if (g->snap_epoch != g->pool_epoch) return set_err(g, FGI_ESTATE, "edge pool was rebuilt since the snapshot");
     hipSetDevice(g->device);
     const size_t H = g->n_handles;
     hipStream_t s = g->stream;
+    if (g->failed) {
+        // a failed batch: words, visit / invalidated bits and the wave counters are undefined. Every
+        // saved table is copied back and the wave state cleared before the graph is usable again.
+        FGI_HIP(g, hipMemcpyAsync(g->node, g->snap_node, H * 8, hipMemcpyDeviceToDevice, s));
+        FGI_HIP(g, hipMemsetAsync(g->vis_bm, 0, g->bm_words * 4, s));
+        FGI_HIP(g, hipMemsetAsync(g->inv_bm, 0, g->bm_words * 4, s));
+        FGI_HIP(g, hipMemsetAsync(g->gbar, 0, 2 * sizeof(unsigned long long), s));
+        g->words_dirty = false;
+        g->cls_valid = false;
+        g->v_dirty = false;
+        g->vis_stale = false;
+        g->coop_clean = false;   // the next cascade re-initialises the wave counters
+        g->ids_valid = false;
+        g->mut_epoch = ~0ull;    // forces the row tables' copy below
+    }
     if (g->words_dirty) {
         FGI_HIP(g, hipMemcpyAsync(g->node, g->snap_node, H * 8, hipMemcpyDeviceToDevice, s));
         g->words_dirty = false;
@@ -2008,8 +2043,14 @@ fgi_status fgi_restore(fgi_graph* g) {
     FGI_HIP(g, hipMemcpyAsync(g->row_len, g->snap_row_len, H * 4, hipMemcpyDeviceToDevice, s));
     FGI_HIP(g, hipMemcpyAsync(g->row_cap, g->snap_row_cap, H * 4, hipMemcpyDeviceToDevice, s));
     FGI_HIP(g, hipMemcpyAsync(g->used_cnt, g->snap_used, H * 4, hipMemcpyDeviceToDevice, s));
+    // the detached handles the mutations since the snapshot took are free again (their words and rows
+    // are the snapshot's)
+    if (g->n_detached && g->snap_home)
+        FGI_HIP(g, hipMemcpyAsync(g->home, g->snap_home, (size_t)g->n_detached * 4, hipMemcpyDeviceToDevice, s));
+    g->free_detached = g->snap_free_detached;
     FGI_HIP(g, hipStreamSynchronize(s));
     g->mut_epoch = g->snap_mut_epoch;   // rows and versions are those of the snapshot again
+    g->failed = false;
     return FGI_OK;
 }
 
@@ -2060,6 +2101,12 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
         if (value < 0) return set_err(g, FGI_EINVAL, "beta must be >= 0");
         g->opt_pull_beta = (int)value;
         return FGI_OK;
+    case FGI_OPT_FAULT_INJECT:
+        if (value < 0 || ((value & 0xFFFF) == 0 && value != 0) || value >= (1ll << 32))
+            return set_err(g, FGI_EINVAL, "fault injection: (launches to skip << 16) | (block + 1), block + 1 > 0");
+        g->fault_block = (uint32_t)(value & 0xFFFF);
+        g->fault_skip = (uint32_t)(value >> 16);
+        return FGI_OK;
     default: return set_err(g, FGI_EINVAL, "unknown option %d", option);
     }
 }
@@ -2068,6 +2115,7 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
 // The single-device wave and mutation entry points address rows whose entries are local handles; a
 // partitioned graph's rows hold global dependant ids (part.hip), so they must go through fgi_part_*.
 static fgi_status single_only(fgi_graph* g, const char* what) {
+    FGI_TRY(usable(g));
     return g->part ? set_err(g, FGI_ESTATE, "%s: partitioned graph, use the fgi_part_* entry points", what) : FGI_OK;
 }
 static fgi_status stage_roots(fgi_graph* g, uint64_t n) {
@@ -2153,6 +2201,7 @@ fgi_status fgi_free_pinned(void* p) {
 
 fgi_status fgi_wave_ids_dev(fgi_graph* g, const uint32_t** ids_dev, uint64_t* n) {
     if (!g || !ids_dev) return FGI_EINVAL;
+    FGI_TRY(usable(g));
     hipSetDevice(g->device);
     if (!g->part) FGI_TRY(ensure_ids(g));
     *ids_dev = g->inv;
@@ -2162,6 +2211,7 @@ fgi_status fgi_wave_ids_dev(fgi_graph* g, const uint32_t** ids_dev, uint64_t* n)
 
 fgi_status fgi_last_wave_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n) {
     if (!g) return FGI_EINVAL;
+    FGI_TRY(usable(g));
     hipSetDevice(g->device);
     return copy_ids(g, out_ids, cap, out_n);
 }
@@ -2687,6 +2737,21 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
         ++syncs;
         g->pool_top = scr_h[ptop_word];
         const unsigned long long ab = scr_h[0];
+        if (scr_h[3 + kAccBarrierIdx] || (ab >> 32) == kAbortBarrier) {
+            // a cascade's grid barrier timed out: its blocks left without finishing, the batch's later
+            // kernels did nothing. The detached handles the device consumed are accounted for, the
+            // barrier counter restarts, and the graph is poisoned until fgi_restore (fgi.h).
+            g->free_detached.resize(g->free_detached.size() - (size_t)std::min<uint64_t>(scr_h[2], n_take));
+            FGI_HIP(g, hipMemsetAsync(g->gbar, 0, 2 * sizeof(unsigned long long), st));
+            FGI_HIP(g, hipStreamSynchronize(st));
+            g->failed = true;
+            g->coop_clean = false;
+            note_words(g);
+            touch(g);
+            return set_err(g, FGI_EDEVICE,
+                           "a cascade's grid barrier timed out (blocks of one grid were not resident together); "
+                           "the batch is half-applied and the graph unusable until fgi_restore");
+        }
         if (!ab) break;
         const uint32_t k = (uint32_t)(ab & 0xFFFFFFFFull) - 1;
         if ((ab >> 32) == kAbortPool) {   // grow the pool, then finish step k and run the rest
@@ -2701,12 +2766,6 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
         // out of detached handles at step k: steps before it are applied
         g->free_detached.resize(g->free_detached.size() - (size_t)scr_h[2]);
         return set_err(g, FGI_ECAPACITY, "step %u: out of detached handles (%zu free)", k, g->free_detached.size());
-    }
-    if (scr_h[3 + 7]) {   // acc[kAccBarrier]: a cascade's grid barrier timed out (its results are not trusted)
-        // the arrival counter may no longer be a multiple of the grid size: start it again
-        FGI_HIP(g, hipMemsetAsync(g->gbar, 0, 2 * sizeof(unsigned long long), st));
-        FGI_HIP(g, hipStreamSynchronize(st));
-        return set_err(g, FGI_EDEVICE, "a cascade's grid barrier timed out: blocks of one grid were not resident together");
     }
     // host bookkeeping: the detached handles taken, the per-step outputs
     g->free_detached.resize(g->free_detached.size() - (size_t)scr_h[2]);
@@ -2904,12 +2963,14 @@ static fgi_status prune_rows(fgi_graph* g, uint32_t lo, uint32_t hi, bool allow_
 
 fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats) {
     if (!g) return FGI_EINVAL;
+    FGI_TRY(usable(g));
     if (stats) *stats = fgi_prune_stats{};
     return prune_rows(g, 0, g->n_handles, true, stats);
 }
 
 fgi_status fgi_prune_range(fgi_graph* g, uint32_t first, uint32_t count, fgi_prune_stats* stats) {
     if (!g) return FGI_EINVAL;
+    FGI_TRY(usable(g));
     if (stats) *stats = fgi_prune_stats{};
     if (first > g->n_handles) return set_err(g, FGI_EINVAL, "first handle %u out of range", first);
     const uint32_t hi = (uint32_t)std::min<uint64_t>((uint64_t)first + count, g->n_handles);
@@ -2918,6 +2979,7 @@ fgi_status fgi_prune_range(fgi_graph* g, uint32_t first, uint32_t count, fgi_pru
 
 fgi_status fgi_prune_step(fgi_graph* g, uint32_t batch, uint32_t stale_pct, fgi_prune_stats* stats) {
     if (!g || batch == 0) return FGI_EINVAL;
+    FGI_TRY(usable(g));
     if (stats) *stats = fgi_prune_stats{};
     // ComputedGraphPruner (Internal/ComputedGraphPruner.cs:50-110) walks the registry in batches;
     // here a batch runs only while the estimated stale entries exceed stale_pct of the pool
@@ -2935,6 +2997,7 @@ fgi_status fgi_prune_step(fgi_graph* g, uint32_t batch, uint32_t stale_pct, fgi_
 
 fgi_status fgi_release(fgi_graph* g, uint32_t n, const uint32_t* handle) {
     if (!g || (n && !handle)) return FGI_EINVAL;
+    FGI_TRY(usable(g));
     hipSetDevice(g->device);
     FGI_TRY(fold(g));
     if (n) note_words(g);

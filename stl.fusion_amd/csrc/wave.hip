@@ -1552,7 +1552,7 @@ constexpr uint32_t kFinalStage = 1024;   // bitmap words a block keeps in LDS (8
 // (roots produced by an earlier step). The invalidated handles are appended at out[*out_n ..) in
 // ascending order and *out_n advanced; acc accumulates the batch's totals.
 enum : int { kAccWaves, kAccLevels, kAccInv, kAccETrav, kAccEMatch, kAccFlagged, kAccFTotal, kAccBarrier, kAccN };
-static_assert(kAccN <= kAccCount, "batch accumulators");
+static_assert(kAccN <= kAccCount && kAccBarrier == kAccBarrierIdx, "batch accumulators");
 
 struct CoopArgs {
     const uint32_t* roots;
@@ -1579,6 +1579,9 @@ struct CoopArgs {
     unsigned long long* out_n;
     unsigned long long* acc;           // [kAccN]
     const unsigned long long* abort;   // nullable: a batch's abort word (set: the wave does nothing)
+    unsigned long long* abort_w;       // the same word, set (kAbortBarrier) when a grid barrier times out
+    uint64_t bar_timeout;              // grid barrier timeout, 100 MHz ticks
+    uint32_t fault_block;              // fault injection: block fault_block - 1 skips its first barrier
     unsigned long long* gbar;          // plain launch: the grid barrier's arrival counter (monotonic)
     int one_round;                     // chunk size by level_mult_one_round (FGI_COOP_CHUNKS=0: level_mult)
 };
@@ -1586,36 +1589,64 @@ struct CoopArgs {
 // Grid barrier of a plain (non-cooperative) launch of k_wave_coop. A cooperative launch goes to the
 // runtime's cooperative queue: ~11.7 us of dispatch gap before each, where plain launches follow
 // each other within 0.1 us (profiles/r6n_stream_kernels.txt), and a streaming round makes six of
-// them, four with no roots. The grid is one block per CU, far below what the chip holds resident,
-// so every block runs at once without the cooperative guarantee. As the device library's barrier:
-// agent-scope fences on both sides; one thread per block arrives on a monotonic counter and waits
-// for the next multiple of the grid size. A wait longer than 2 s (wall clock, 100 MHz) gives up and
-// flags the batch (acc[kAccBarrier]: fgi_run_batch then fails with FGI_EDEVICE) instead of hanging.
+// them, four with no roots. The grid is one block per two CUs, far below what the chip holds
+// resident, so every block runs at once without the cooperative guarantee. As the device library's
+// barrier: agent-scope fences on both sides; one thread per block arrives on a monotonic counter and
+// waits for the next multiple of the grid size.
+// Failure is defined, never a hang or a half-synchronised grid: a wait longer than the timeout (2 s
+// of the 100 MHz wall clock) marks the grid broken (acc[kAccBarrier]) and sets the batch's abort word
+// (kAbortBarrier: the batch's later kernels and cascades do nothing); a block waiting at a barrier
+// leaves as soon as it sees the broken mark. Returns false in every block that did not see the
+// barrier complete: the caller returns at once, writing nothing more. A block that did see it
+// complete went on with complete data; it leaves at its next barrier. fgi_run_batch then fails with
+// FGI_EDEVICE and poisons the graph until fgi_restore (graph.hip).
+// skip (fault injection, FGI_OPT_FAULT_INJECT): this block leaves without arriving, as a block that
+// is never resident would never arrive.
 constexpr uint64_t kGridBarTimeout = 200000000ull;
-__device__ __forceinline__ void soft_grid_sync(unsigned long long* cnt, unsigned long long* broken) {
+__device__ __forceinline__ bool soft_grid_sync(unsigned long long* cnt, unsigned long long* broken,
+                                               unsigned long long* abort_w, uint64_t timeout, bool skip) {
+    __shared__ int s_ok;
+    if (skip) return false;   // block-uniform
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned long long arrived = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long target = (arrived / gridDim.x + 1) * gridDim.x;
         const uint64_t t0 = wall_clock64();
+        int ok = 1;
         while (__hip_atomic_load(cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            if (__hip_atomic_load(broken, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
+                ok = 0;
+                break;
+            }
             __builtin_amdgcn_s_sleep(1);
-            if (wall_clock64() - t0 > kGridBarTimeout) {
+            if (wall_clock64() - t0 > timeout) {
                 __hip_atomic_store(broken, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (abort_w) atomicCAS(abort_w, 0ull, kAbortBarrier << 32);
+                ok = 0;
                 break;
             }
         }
+        s_ok = ok;
     }
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    return s_ok != 0;
 }
 
 template <bool SOFT>
 __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
-    auto grid_sync = [&]() {
-        if constexpr (SOFT) soft_grid_sync(a.gbar, a.acc + kAccBarrier);
-        else cooperative_groups::this_grid().sync();
+    // false: the grid is broken (soft barrier only); the block returns at once
+    int n_sync = 0;
+    auto grid_sync = [&]() -> bool {
+        if constexpr (SOFT) {
+            const bool skip = a.fault_block != 0 && n_sync == 0 && blockIdx.x + 1 == a.fault_block;
+            ++n_sync;
+            return soft_grid_sync(a.gbar, a.acc + kAccBarrier, a.abort_w, a.bar_timeout, skip);
+        } else {
+            cooperative_groups::this_grid().sync();
+            return true;
+        }
     };
     __shared__ __align__(16) uint32_t s_x[kChunkEmitCap + 8];
     uint32_t* s_rel = s_x;
@@ -1649,14 +1680,14 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
     if (a.imm) {   // Invalidate(true) roots first: their CAS may change node words
         for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gsize)
             root_step<1>(i0 + threadIdx.x, a.roots, a.imm, n, 0u, a.n_handles, a.node, a.vis, o0, ctr);
-        grid_sync();
+        if (!grid_sync()) return;
     }
     for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < n; i0 += gsize)
         root_step<0>(i0 + threadIdx.x, a.roots, a.imm, n, 0u, a.n_handles, a.node, a.vis, o0, ctr);
     CPROBE(1);
     uint64_t levels = 0, e_trav = 0, f_total = 0;
     for (int L = 0;; ++L) {
-        grid_sync();   // level L's frontier (and its counter) is complete
+        if (!grid_sync()) return;   // level L's frontier (and its counter) is complete
         if (L < 4) CPROBE(2 + L);
         if (threadIdx.x == 0) s_ft = coh_read(&ctr->lvl[L % kRing].ft);
         __syncthreads();
@@ -1713,7 +1744,7 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
     c = block_sum(c, s_red);
     if (threadIdx.x == 0) coh_xchg(a.cnt + blockIdx.x, c);
     CPROBE(6);
-    grid_sync();
+    if (!grid_sync()) return;
     CPROBE(7);
     unsigned long long part = 0;
     for (uint32_t k = threadIdx.x; k < blockIdx.x; k += blockDim.x) part += coh_read(a.cnt + k);
@@ -2072,11 +2103,15 @@ bool coop_launch_mode() {
 // out[*out_n ..). The wave folds its visits into the node words itself.
 fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev, const uint8_t* imm_dev,
                          const unsigned long long* n_dev, uint32_t* out, unsigned long long* out_n,
-                         unsigned long long* acc, const unsigned long long* abort) {
+                         unsigned long long* acc, unsigned long long* abort) {
     hipStream_t s = g->stream;
     FGI_TRY(ensure_cstart(g, std::max<uint64_t>(g->pool_top, g->pool_cap)));
     const bool coop = coop_launch_mode();
-    static int per_cu = 0;
+    // resident blocks per CU, per graph (its device): the launch-time residency bound below. The grid
+    // is half the CUs, a quarter of what the kernel's resources allow, so other work on the device
+    // would have to hold most of it for blocks to wait on each other; if it does, the barrier's timeout
+    // fails the batch cleanly (soft_grid_sync) instead of hanging.
+    int& per_cu = g->coop_per_cu;
     if (per_cu == 0 &&
         (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, coop ? k_wave_coop<false> : k_wave_coop<true>, kBlock, 0) !=
              hipSuccess ||
@@ -2123,7 +2158,21 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
     a.out_n = out_n;
     a.acc = acc;
     a.abort = abort;
+    a.abort_w = abort;
     a.gbar = g->gbar;
+    // fault injection (FGI_OPT_FAULT_INJECT, tests): after fault_skip more cascade launches, one block
+    // of the cascade leaves at its first barrier without arriving; the others give up after 20 ms
+    uint32_t fb = 0;
+    if (g->fault_block) {
+        if (g->fault_skip == 0) {
+            fb = g->fault_block;
+            g->fault_block = 0;
+        } else {
+            --g->fault_skip;
+        }
+    }
+    a.fault_block = fb;
+    a.bar_timeout = fb ? 2000000ull : kGridBarTimeout;
     static const int one_round = [] {
         const char* e = getenv("FGI_COOP_CHUNKS");
         return e && e[0] == '0' ? 0 : 1;

@@ -24,6 +24,7 @@ OPT_PART_COLLECTIVES = 7
 OPT_PULL_TPB = 8
 OPT_FRONT_EXCHANGE = 9
 OPT_HOT_HEADS = 10
+OPT_FAULT_INJECT = 11
 DIR_AUTO, DIR_PUSH, DIR_PULL = 0, 1, 2
 NONE = 0xFFFFFFFF
 COMPUTING, CONSISTENT, INVALIDATED = 0, 1, 2

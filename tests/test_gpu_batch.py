@@ -187,3 +187,80 @@ def test_batch_bad_argument_applies_nothing(pkg, gpu_available, bad):
     g.run_batch([("begin_compute", slots2, (versions[slots2] + np.uint64(9)).astype(np.uint64))])
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("skip,block", [(1, 1), (1, 128), (0, 7)])
+def test_batch_barrier_timeout_poisons_until_restore(pkg, gpu_available, skip, block):
+    """A cascade whose grid barrier times out (FGI_OPT_FAULT_INJECT: one block leaves without arriving)
+    fails the batch with FGI_EDEVICE; the graph then refuses every call with FGI_ESTATE until
+    fgi_restore, after which the same batch (detached handles included) matches the oracle, and so
+    does a second one. skip = 1: the fault is in the batch's second cascade (the first, a displacement
+    cascade, has completed and detached the delayed leaves it displaced)."""
+    fgi = pkg.fgi
+    mix = _mix(pkg, 48, 120, 6, 20, 0x5EED00E0)
+    n = mix.n
+    used, dep, tag = mix.initial_edges()
+    g, o = build_pair(pkg, n, mix.version.copy(), mix.state_flags(), used, dep, tag, n_detached=512)
+    g.snapshot()
+    hubs = mix.roots(0)
+    leaves = mix.children(hubs[:2])
+    delayed = leaves[mix.has_delay[leaves] != 0]
+    assert len(delayed) > 0
+    vd = (mix.version[delayed] + np.uint64(2)).astype(np.uint64)
+    roots = hubs[2:]
+    steps = [("begin_compute", delayed, vd, np.ones(len(delayed), np.uint8)),   # displaced + detached
+             ("invalidate", roots),
+             ("set_output", delayed)]
+    g.set_option(fgi.OPT_FAULT_INJECT, (skip << 16) | block)
+    with pytest.raises(fgi.FgiError) as e:
+        g.run_batch(steps)
+    assert e.value.status == fgi.EDEVICE, e.value
+    for call in (lambda: g.get_state([0]), lambda: g.dump_states(), lambda: g.invalidate(roots),
+                 lambda: g.run_batch([("invalidate", roots)]), lambda: g.prune(), lambda: g.snapshot()):
+        with pytest.raises(fgi.FgiError) as e2:
+            call()
+        assert e2.value.status == fgi.ESTATE
+    g.restore()
+    assert_states_equal(g, o, n)            # the snapshot's states again
+    ids, outs = g.run_batch(steps)
+    o.clear_log()
+    for s_, v in zip(delayed, vd):
+        o.begin_compute(int(s_), int(v), True)
+    disp = o.inv_log()
+    assert len(disp) == 0                   # displaced delayed nodes only start their delay
+    o.invalidate_slots(roots)
+    w = o.inv_log()
+    for s_ in delayed:
+        assert o.set_output(o.last(int(s_))) == 1
+    assert np.array_equal(ids, np.sort(w).astype(np.uint32))
+    assert np.all(outs[0] != fgi.NONE)      # every displaced delayed leaf was detached
+    assert np.all(outs[2] == 1)
+    assert_states_equal(g, o, n)
+    # a second batch on the recovered graph
+    r2 = mix.roots(1)
+    ids2, _ = g.run_batch([("invalidate", r2)])
+    o.clear_log()
+    o.invalidate_slots(r2)
+    assert np.array_equal(ids2, np.sort(o.inv_log()).astype(np.uint32))
+    assert_states_equal(g, o, n)
+    g.close()
+    o.close()
+
+
+def test_restore_without_snapshot_keeps_the_graph_poisoned(pkg, gpu_available):
+    fgi = pkg.fgi
+    mix = _mix(pkg, 8, 50, 2, 0, 0x5EED00E0)
+    used, dep, tag = mix.initial_edges()
+    g, o = build_pair(pkg, mix.n, mix.version.copy(), mix.state_flags(), used, dep, tag)
+    o.close()
+    g.set_option(fgi.OPT_FAULT_INJECT, 1)
+    with pytest.raises(fgi.FgiError) as e:
+        g.run_batch([("invalidate", mix.roots(0))])
+    assert e.value.status == fgi.EDEVICE
+    with pytest.raises(fgi.FgiError) as e:
+        g.restore()
+    assert e.value.status == fgi.ESTATE
+    with pytest.raises(fgi.FgiError) as e:
+        g.invalidate(mix.roots(0))
+    assert e.value.status == fgi.ESTATE
+    g.close()
