@@ -107,6 +107,13 @@ typedef struct fgi_wave_stats {
     double pull_ms;            /* device time of the k_pull launches (HIP events) */
     uint64_t pull_bytes;       /* algorithmic bytes of the k_pull launches */
     uint64_t pull_launches;    /* k_pull launches (every level of a wave that may pull) */
+    /* fused waves: the head and tail launches that run the roots, the small push levels,
+       the collect after a pull level and the final count inside one persistent grid each */
+    uint64_t fused_launches;   /* head / tail launches */
+    double fused_ms;           /* their summed device time (HIP events, FGI_OPT_LEVEL_TIMING) */
+    uint64_t fused_push_bytes; /* algorithmic bytes of the push levels they ran (20 B per edge + 40 B
+                                  per frontier entry, as a k_level push) */
+    uint64_t host_syncs;       /* times the wave waited for the device */
 } fgi_wave_stats;
 
 typedef struct fgi_prune_stats {
@@ -334,6 +341,14 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *                            it from the graph (65,536-262,144); n > 0 caps it at n rounded up to 256,
  *                            so the other heads are probed in the invalidated bitmap itself (tests pin
  *                            that path on small graphs; results never depend on it)
+ *   FGI_OPT_FUSED       [1]  waves whose directions are settled (pull lists ready, or push only) run
+ *                            their roots and small push levels inside two persistent launches and only
+ *                            the pull levels (and push levels over one round of the fused grid) as
+ *                            separate launches, with one host synchronisation; 0 runs
+ *                            every level as launches in groups. Tests add 2 (no prediction of the
+ *                            launches: extra rounds), 4 (every push level as its own launch) or 8
+ *                            (every push level in the fused grid); the environment's FGI_FUSED=0
+ *                            makes 0 the default
  *   FGI_OPT_FAULT_INJECT [0] tests only: value (k << 16) | b, b > 0: in the (k+1)-th streaming
  *                            cascade launched from now (fgi_run_batch), block b - 1 leaves at its first
  *                            grid barrier without arriving, and that cascade's barrier times out after
@@ -350,6 +365,7 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
 #define FGI_OPT_FRONT_EXCHANGE 9
 #define FGI_OPT_HOT_HEADS 10
 #define FGI_OPT_FAULT_INJECT 11
+#define FGI_OPT_FUSED 12
 fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value);
 
 /* ---- multi-GPU (1-D vertex-range partition, RCCL all-to-all frontier exchange) --------------- */

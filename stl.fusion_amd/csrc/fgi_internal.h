@@ -16,6 +16,7 @@
 #include <stdint.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <string>
 #include <utility>
 #include <vector>
@@ -143,6 +144,9 @@ constexpr int kAccCount = 8;            // batch accumulators (fgi_run_batch; ru
 // barrier timed out (no step index; the graph is poisoned until fgi_restore).
 constexpr unsigned long long kAbortDetach = 1, kAbortPool = 2, kAbortBarrier = 3;
 constexpr int kAccBarrierIdx = 7;       // acc[7]: a cascade's grid barrier timed out
+// grid-barrier arrival counters (g->gbar, monotonic, a multiple of the grid size between launches):
+// word 0 k_wave_coop's (streaming cascades), word kGbarFused k_wave_fused's (their grids differ)
+constexpr int kGbarWords = 32, kGbarFused = 16;
 
 // Per-level counters. The producers of level L's frontier (roots, push emits, received targets)
 // reserve list space with ONE packed 64-bit atomic on `ft` (frontier entries << 32 | edges): the
@@ -179,9 +183,28 @@ struct WaveCtr {
     unsigned long long pull_scan;   // pull: slots scanned (bitmap reads), summed over pull levels
     unsigned long long pull_tail;   // pull: candidates whose head dependency missed (list scanned)
     unsigned long long root_flagged;  // flag-only visits of the roots kernel
-    unsigned long long pad[5];
+    // fused waves (run_wave): the head / tail kernels run the small push levels inside
+    // one launch each; k_level launches in between run the pull levels (and push levels too large for
+    // the fused grid), each reading its level from here
+    unsigned long long cur;         // the next level to run
+    unsigned long long mid_base;    // the level of the round's first k_level launch (mid index 0)
+    unsigned long long phase;       // kPhaseDone once the final count has run
+    unsigned long long broken;      // a fused kernel's grid barrier timed out
+    unsigned long long n_levels;    // device-side totals of the wave: non-empty levels,
+    unsigned long long e_trav;      //   their frontier edges (E_trav),
+    unsigned long long f_total;     //   their frontier entries,
+    unsigned long long n_pull;      //   pull levels,
+    unsigned long long push_edges;  //   edges / entries of the push levels run inside the fused kernels
+    unsigned long long push_f;
+    unsigned long long n_mid;       //   levels run by k_level launches
+    unsigned long long mid_kind[16];  // per k_level launch of the round (mid index): 0 nothing, 1 push, 2 pull
+    unsigned long long mid_push_edges;  // edges / entries of the push levels run by k_level launches
+    unsigned long long mid_push_f;
+    unsigned long long pad2[3];
     LevelCtr lvl[kRing];
 };
+constexpr unsigned long long kPhaseDone = 1;
+constexpr int kMidMax = 16;         // k_level launches per round of a fused wave
 
 // per-wave accounting of a partitioned wave
 struct PartWave {
@@ -191,6 +214,15 @@ struct PartWave {
     double expand_ms = 0, pull_ms = 0;
     bool pulled = false;
 };
+
+// FGI_OPT_FUSED bits: fused waves on; tests: no mid-pair prediction (every k_level level found by an
+// extra round), every push level as a k_level launch, every push level in the fused grid
+constexpr int kFusedOn = 1, kFusedNoPredict = 2, kFusedMidPush = 4, kFusedTailPush = 8;
+// FGI_FUSED=0 in the environment: waves as level groups by default (measurement of the older path)
+inline int fused_default() {
+    const char* e = getenv("FGI_FUSED");
+    return (e && e[0] == '0') ? 0 : kFusedOn;
+}
 
 // ---- host-side graph object -------------------------------------------------------------------
 struct DevBuf {
@@ -240,7 +272,7 @@ struct fgi_graph {
     unsigned long long* bsum = nullptr;  // [8][kStatBlocks] per-block sums / prefixes of the epilogues
     unsigned long long* done = nullptr;  // completion counters of the last-block epilogues
     fgi::WaveCtr* ctr = nullptr;
-    unsigned long long* gbar = nullptr;   // k_wave_coop's grid-barrier counter (plain launches)
+    unsigned long long* gbar = nullptr;   // [kGbarWords] grid-barrier counters (k_wave_coop, k_wave_fused)
     unsigned long long* blk_stats = nullptr;   // [kStatBlocks][kStatCols] per-block wave statistics
     fgi::WaveCtr* ctr_host = nullptr;  // pinned
     uint32_t* roots_buf = nullptr;     // staging for host roots
@@ -250,6 +282,8 @@ struct fgi_graph {
     bool want_ids = true;              // run_wave writes the invalidated list (false: bitmap and count only)
     bool ids_valid = false;            // inv holds the last wave's list (else ensure_ids rebuilds it)
     int last_levels = 4;               // non-empty levels of the last wave (sizes the first level group)
+    int last_mid = 3;                  // k_level launches the last fused wave needed (its mid pairs)
+    int fused_per_cu = 0;              // resident k_wave_fused blocks per CU (0: not queried yet)
     bool coop_warm = false;            // a cooperative launch has run (coop_warm)
 
     // Visit bitmap over handles: bit h set = node h was visited by a wave since the
@@ -329,6 +363,7 @@ struct fgi_graph {
     int opt_hot_heads = 0;            // FGI_OPT_HOT_HEADS: cap on the hot heads (0: by graph size)
     int opt_pull_beta = 24;           // after a pull, pull again while the frontier exceeds n / beta
     int opt_level_timing = 1;         // HIP events around each level's k_level launch (statistics)
+    int opt_fused = fgi::fused_default();  // FGI_OPT_FUSED (kFused* bits)
 
     // generic scratch (sorts, batches)
     void* scratch = nullptr;

@@ -1652,7 +1652,7 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
         dmalloc(g, &g->inv, H) || dmalloc(g, &g->fr_off[0], H) || dmalloc(g, &g->fr_off[1], H) ||
         dmalloc(g, &g->fr_len[0], H) || dmalloc(g, &g->fr_len[1], H) || dmalloc(g, &g->escan[0], H) ||
         dmalloc(g, &g->escan[1], H) || dmalloc(g, &g->bsum, 8ull * kStatBlocks) ||
-        dmalloc(g, &g->done, (size_t)(kDoneGroups + 1) * kDoneStride) || dmalloc(g, &g->ctr, 1) || dmalloc(g, &g->gbar, 2) ||
+        dmalloc(g, &g->done, (size_t)(kDoneGroups + 1) * kDoneStride) || dmalloc(g, &g->ctr, 1) || dmalloc(g, &g->gbar, kGbarWords) ||
         dmalloc(g, &g->blk_stats, (size_t)kStatBlocks * kStatCols) || dmalloc(g, &g->misc_dev, 16) ||
         dmalloc(g, &g->pool_top_dev, 1) || dmalloc(g, &g->uin_off, H) || dmalloc(g, &g->uin_len, H) ||
         dmalloc(g, &g->uin_head, g->n_slots + 1))
@@ -1664,7 +1664,7 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
         return fail(FGI_ENOMEM);
     hipMemset(g->done, 0, (size_t)(kDoneGroups + 1) * kDoneStride * sizeof(unsigned long long));
     hipMemset(g->bsum, 0, 8ull * kStatBlocks * sizeof(unsigned long long));
-    hipMemset(g->gbar, 0, 2 * sizeof(unsigned long long));
+    hipMemset(g->gbar, 0, kGbarWords * sizeof(unsigned long long));
     hipMemset(g->vis_bm, 0, g->bm_words * 4);
     hipMemset(g->inv_bm, 0, g->bm_words * 4);
     hipMemset(g->uin_more, 0, g->bm_words * 4);
@@ -2016,7 +2016,7 @@ fgi_status fgi_restore(fgi_graph* g) {
         FGI_HIP(g, hipMemcpyAsync(g->node, g->snap_node, H * 8, hipMemcpyDeviceToDevice, s));
         FGI_HIP(g, hipMemsetAsync(g->vis_bm, 0, g->bm_words * 4, s));
         FGI_HIP(g, hipMemsetAsync(g->inv_bm, 0, g->bm_words * 4, s));
-        FGI_HIP(g, hipMemsetAsync(g->gbar, 0, 2 * sizeof(unsigned long long), s));
+        FGI_HIP(g, hipMemsetAsync(g->gbar, 0, kGbarWords * sizeof(unsigned long long), s));
         g->words_dirty = false;
         g->cls_valid = false;
         g->v_dirty = false;
@@ -2100,6 +2100,10 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
     case FGI_OPT_PULL_BETA:
         if (value < 0) return set_err(g, FGI_EINVAL, "beta must be >= 0");
         g->opt_pull_beta = (int)value;
+        return FGI_OK;
+    case FGI_OPT_FUSED:
+        if (value < 0 || value > 15) return set_err(g, FGI_EINVAL, "fused-wave bits must be 0..15");
+        g->opt_fused = (int)value;
         return FGI_OK;
     case FGI_OPT_FAULT_INJECT:
         if (value < 0 || ((value & 0xFFFF) == 0 && value != 0) || value >= (1ll << 32))
@@ -2742,7 +2746,7 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
             // kernels did nothing. The detached handles the device consumed are accounted for, the
             // barrier counter restarts, and the graph is poisoned until fgi_restore (fgi.h).
             g->free_detached.resize(g->free_detached.size() - (size_t)std::min<uint64_t>(scr_h[2], n_take));
-            FGI_HIP(g, hipMemsetAsync(g->gbar, 0, 2 * sizeof(unsigned long long), st));
+            FGI_HIP(g, hipMemsetAsync(g->gbar, 0, kGbarWords * sizeof(unsigned long long), st));
             FGI_HIP(g, hipStreamSynchronize(st));
             g->failed = true;
             g->coop_clean = false;

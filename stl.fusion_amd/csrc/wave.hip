@@ -660,14 +660,16 @@ struct WaveParams {
 };
 
 // Beamer's two rules, as a pure function of the counters (every block decides the same).
-__device__ __forceinline__ bool level_pulls(const WaveCtr* ctr, int L, const WaveParams& wp) {
-    const LevelCtr& lc = ctr->lvl[L % kRing];
-    if (wp.multi) return lc.pull != 0;
-    const uint64_t F = lvl_F(lc), T = lvl_T(lc);
+__device__ __forceinline__ bool level_pulls(const WaveCtr* ctr, int L, const WaveParams& wp, uint64_t F, uint64_t T) {
     if (F == 0 || wp.direction == 1) return false;
     if (wp.direction == 2) return true;
     const bool prev_pull = L > 0 && ctr->lvl[(L + kRing - 1) % kRing].pull != 0;
     return T > wp.pull_threshold || (prev_pull && F > wp.stay_pull_f);
+}
+__device__ __forceinline__ bool level_pulls(const WaveCtr* ctr, int L, const WaveParams& wp) {
+    const LevelCtr& lc = ctr->lvl[L % kRing];
+    if (wp.multi) return lc.pull != 0;
+    return level_pulls(ctr, L, wp, lvl_F(lc), lvl_T(lc));
 }
 
 // fine chunks per expand chunk: as large as kEPT allows while every block still gets two chunks
@@ -714,26 +716,23 @@ struct CollectArgs {
 
 constexpr int kCollectThreads = 256;
 
-// Level L's frontier list when level L-1 pulled and level L pushes; before a pull level, the hot
-// heads' snapshot; otherwise nothing to do.
-__global__ __launch_bounds__(kCollectThreads) void k_collect(int L, WaveCtr* ctr, WaveParams wp, CollectArgs c) {
-    const LevelCtr& lc = ctr->lvl[L % kRing];
-    if (lvl_F(lc) == 0) return;
-    if (level_pulls(ctr, L, wp)) {
-        // one entry per lane, 64 bits per wave (n_hot and the grid stride are multiples of 64)
-        unsigned long long* hot64 = reinterpret_cast<unsigned long long*>(c.hot_bm);
-        for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < c.n_hot; k += gridDim.x * blockDim.x) {
-            const uint32_t u = c.hot_id[k];
-            const unsigned long long m = __ballot(u != FGI_NONE && bit_of(c.inv, u));
-            if (lane_id() == 0) hot64[k >> 6] = m;
-        }
-        return;
+// The hot heads' snapshot before a pull level: one entry per lane, 64 bits per wave (n_hot and the
+// thread stride are multiples of 64).
+__device__ __forceinline__ void collect_hot(const CollectArgs& c, uint64_t tid, uint64_t stride) {
+    unsigned long long* hot64 = reinterpret_cast<unsigned long long*>(c.hot_bm);
+    for (uint64_t k = tid; k < c.n_hot; k += stride) {
+        const uint32_t u = c.hot_id[k];
+        const unsigned long long m = __ballot(u != FGI_NONE && bit_of(c.inv, u));
+        if (lane_id() == 0) hot64[k >> 6] = m;
     }
-    if (L == 0 || !ctr->lvl[(L + kRing - 1) % kRing].pull) return;
-    const uint64_t G = wp.grid;   // the pull grid
+}
+
+// Push level L's frontier list from pull level L-1's per-block winners lists: one wave per pull block
+// (waves w0, w0 + W, ... of the caller's grid).
+__device__ __forceinline__ void collect_front(const LevelCtr& lc, uint64_t G, const CollectArgs& c, uint64_t w0,
+                                              uint64_t W) {
     const uint32_t lane = lane_id();
-    const uint64_t W = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t b = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); b < G; b += W) {   // wave-uniform
+    for (uint64_t b = w0; b < G; b += W) {   // wave-uniform
         const uint64_t e0 = c.pre[G + b], e1 = b + 1 < G ? c.pre[G + b + 1] : lvl_F(lc);
         uint64_t es = c.pre[2 * G + b];
         const uint64_t base = c.seg[b];
@@ -755,6 +754,39 @@ __global__ __launch_bounds__(kCollectThreads) void k_collect(int L, WaveCtr* ctr
             es += tot;
         }
     }
+}
+
+// A fused wave's k_collect / k_level launch with mid index i (passed as L = -1 - i): its level is
+// mid_base + i, run only while it is still the wave's current level (a launch past the levels that
+// need one, or a block reading `cur` after its own launch advanced it, finds another level and does
+// nothing). Returns -1 if there is nothing to do.
+__device__ __forceinline__ int mid_level(const WaveCtr* ctr, int L) {
+    if (L >= 0) return L;
+    if (ctr->phase == kPhaseDone || ctr->broken) return -1;
+    const uint64_t want = ctr->mid_base + (uint64_t)(-1 - L);
+    return ctr->cur == want ? (int)want : -1;
+}
+
+// Level L's frontier list when level L-1 pulled and level L pushes; before a pull level, the hot
+// heads' snapshot; otherwise nothing to do. Fused waves (L < 0, mid index): only for the levels the
+// k_level launch will run (pull, or a push of more than big_push edges); the small push levels and
+// their collect run in the fused tail kernel.
+__global__ __launch_bounds__(kCollectThreads) void k_collect(int L, WaveCtr* ctr, WaveParams wp, CollectArgs c,
+                                                             CollectArgs c1, uint64_t big_push) {
+    const bool fused = L < 0;
+    L = mid_level(ctr, L);
+    if (L < 0) return;
+    if (fused && (L & 1)) c = c1;   // a fused wave's level is known on the device only: odd levels, buffer 1
+    const LevelCtr& lc = ctr->lvl[L % kRing];
+    if (lvl_F(lc) == 0) return;
+    if (level_pulls(ctr, L, wp)) {
+        collect_hot(c, (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, (uint64_t)gridDim.x * blockDim.x);
+        return;
+    }
+    if (fused && lvl_T(lc) <= big_push) return;
+    if (L == 0 || !ctr->lvl[(L + kRing - 1) % kRing].pull) return;
+    collect_front(lc, wp.grid, c, (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6),
+                  (uint64_t)gridDim.x * (blockDim.x >> 6));
 }
 
 // ---- push: edge-parallel expansion ------------------------------------------------------------
@@ -1350,7 +1382,8 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
 // The last block of a pull level: prefixes of the per-block (winners, expandable winners, row
 // lengths) for a possible collect, and level L+1's frontier totals.
 __device__ __forceinline__ void pull_epilogue(int L, const PullArgs& p, LevelCtr* ln, unsigned long long* done,
-                                              const unsigned long long (&bs)[3], unsigned long long* s_red) {
+                                              const unsigned long long (&bs)[3], unsigned long long* s_red,
+                                              unsigned long long* cur = nullptr) {
     __shared__ unsigned long long s_tot[3];
     const uint64_t G = gridDim.x;
     // per-thread partial sums -> the block's sums, one packed word: a block owns at most
@@ -1369,15 +1402,22 @@ __device__ __forceinline__ void pull_epilogue(int L, const PullArgs& p, LevelCtr
         ln->w = s_tot[0];
         ln->F = s_tot[1];
         ln->T = s_tot[2];
+        if (cur) *cur = (unsigned long long)L + 1;   // a fused wave's next level (every block has finished)
     }
     PROBE(L, 6);
 }
 
 // One level's traversal: push (expand) or pull, as decided for the level on the device.
+// Larg >= 0: level Larg (run_wave's level groups, the partitioned wave). Larg < 0: a fused wave's
+// launch with mid index -1 - Larg (mid_level): it runs its level if that level pulls or pushes more
+// than big_push edges (the fused tail kernel runs the smaller push levels), adds the level to the
+// wave's device-side totals and, from its last block, advances the wave's current level. The
+// frontier buffers alternate with the level's parity: x / o serve even levels, x1 / o1 odd ones.
 template <bool PART>
-__global__ __launch_bounds__(kBlock, kLevelOcc) void k_level(int L, WaveParams wp, ExpandArgs x, PullArgs p,
-                                                  const unsigned long long* node, uint32_t* vis, Out o, WaveCtr* ctr,
-                                                  unsigned long long* blk, unsigned long long* done, RemoteArgs ra) {
+__global__ __launch_bounds__(kBlock, kLevelOcc) void k_level(int Larg, WaveParams wp, ExpandArgs x, ExpandArgs x1, PullArgs p,
+                                                  const unsigned long long* node, uint32_t* vis, Out o, Out o1, WaveCtr* ctr,
+                                                  unsigned long long* blk, unsigned long long* done, RemoteArgs ra,
+                                                  uint64_t big_push) {
     // push: the chunk map (s_rel, s_base), then the chunk's winners over it; pull: queue + buffers
     __shared__ __align__(16) uint32_t s_x[kLevelLds];
     uint32_t* s_rel = s_x;                    // [kChunk + 1]
@@ -1388,23 +1428,44 @@ __global__ __launch_bounds__(kBlock, kLevelOcc) void k_level(int L, WaveParams w
     __shared__ unsigned long long s_red[kBlock / 64];
     static_assert(sizeof(PullLds) <= (kLevelLds - kChunk - 4) * 4 && kTailCap <= kChunk, "pull LDS");
     static_assert(kPushLds % 2 == 0 && (kPushLds + sizeof(MsgEmit<true>) / 4) <= kLevelLds, "push LDS");
+    const bool fused = !PART && Larg < 0;
+    const int L = mid_level(ctr, Larg);
+    if (L < 0) return;
+    if (fused && (L & 1)) {
+        x = x1;
+        o = o1;
+    }
     PROBE(L, 0);
     LevelCtr& lc = ctr->lvl[L % kRing];
     o.ln = &ctr->lvl[(L + 1) % kRing];
+    if (fused && lvl_F(lc) == 0) return;   // the wave is done: the tail kernel runs the final count
+    const bool pull = level_pulls(ctr, L, wp);
+    if (fused && !pull && lvl_T(lc) <= big_push) return;   // the tail kernel's
     if (blockIdx.x == 0 && threadIdx.x < sizeof(LevelCtr) / 8)
         reinterpret_cast<unsigned long long*>(&ctr->lvl[(L + 2) % kRing])[threadIdx.x] = 0ull;
-    const bool pull = level_pulls(ctr, L, wp);
     const uint64_t npull = lc.npull;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         if (!PART) lc.pull = pull ? 1ull : 0ull;
         o.ln->npull = npull + (pull ? 1 : 0);
+        if (fused) {
+            ctr->n_levels += 1;
+            ctr->e_trav += lvl_T(lc);
+            ctr->f_total += lvl_F(lc);
+            ctr->n_pull += pull ? 1 : 0;
+            ctr->n_mid += 1;
+            ctr->mid_kind[(-1 - Larg) % kMidMax] = pull ? 2 : 1;
+            if (!pull) {
+                ctr->mid_push_edges += lvl_T(lc);
+                ctr->mid_push_f += lvl_F(lc);
+            }
+        }
     }
     // multi-GPU pull levels run on every rank (parents may be remote); otherwise no frontier, no work
     if (pull) {
         unsigned long long bs[3] = {0, 0, 0};
         pull_level(L, p, wp, npull, node, vis, s_rel, *reinterpret_cast<PullLds*>(s_base), blk, s_st, bs);
         PROBE(L, 4);
-        pull_epilogue(L, p, o.ln, done, bs, s_red);
+        pull_epilogue(L, p, o.ln, done, bs, s_red, fused ? &ctr->cur : nullptr);
         return;
     }
     const uint64_t F = lvl_F(lc), T = lvl_T(lc);
@@ -1420,6 +1481,7 @@ __global__ __launch_bounds__(kBlock, kLevelOcc) void k_level(int L, WaveParams w
     expand_level<PART>(L, F, T, mult, x, node, vis, o, em, s_x, me, s_rel, s_base, blk, s_st, ra);
     PROBE(L, 2);
     if constexpr (PART) publish_ft(o.ln, done, active);   // the host all-reduces F / T
+    else if (fused && last_block(done, active) && threadIdx.x == 0) ctr->cur = (unsigned long long)L + 1;
     PROBE(L, 3);
 }
 
@@ -1502,7 +1564,8 @@ __global__ __launch_bounds__(kBlock) void k_final_count(const unsigned long long
 
 __global__ __launch_bounds__(kBlock) void k_final_write(const unsigned long long* __restrict__ inv64, uint64_t words,
                                                         uint64_t wpb, const unsigned long long* __restrict__ status,
-                                                        WaveCtr* ctr, uint32_t* out) {
+                                                        WaveCtr* ctr, uint32_t* out, int need_done) {
+    if (need_done && ctr->phase != kPhaseDone) return;   // a fused wave whose tail stopped early: not yet
     __shared__ unsigned long long s_red[kBlock / 64];
     __shared__ unsigned long long s_wbase[kBlock / 64];
     __shared__ uint32_t s_stage[kBlock / 64][kPullTile];
@@ -1840,6 +1903,183 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
     CPROBE(9);
 }
 
+// ---- fused waves: the small push levels of a wave inside two persistent launches -----------------
+// run_wave's launch sequence is: k_wave_fused<false> (head) — the wave's counters, bitmaps and
+// statistics cleared, the roots, then push levels while they are small; k_collect + k_level pairs
+// (mid launches) — the pull levels, and push levels of more than big_push edges; k_wave_fused<true>
+// (tail) — the collect of a push level that follows a pull level, the remaining small push levels and
+// the final count (V_inv, the per-block counts k_final_write lists the ids from). A small push level
+// is a chain of dependent round trips over a few thousand edges: inside a persistent grid (one block
+// per CU) its cost is one software grid barrier instead of a kernel launch and a collect launch each
+// (DESIGN.md §3). The head and the tail each stop at the first level that needs a k_level launch
+// (the wave's current level, ctr->cur); the host launches a predicted number of mid pairs (the previous
+// wave's), then the tail, and synchronises once; a tail that stopped early (more mid levels than
+// predicted) is followed by another round.
+struct FusedArgs {
+    const uint32_t* roots;
+    const uint8_t* imm;
+    uint32_t n_roots;
+    uint32_t n_handles;
+    unsigned long long* node;
+    uint32_t* vis;
+    uint32_t* inv_bm;
+    const uint64_t* row_off;
+    const uint32_t* row_len;
+    uint32_t* fr_off[2];
+    uint32_t* fr_len[2];
+    uint64_t* escan[2];
+    uint32_t* cstart[2];
+    const uint32_t* pool_col;
+    const uint64_t* pool_tag;
+    int dead_filter;
+    int clear_vis;                     // fgi_restore's deferred clear of the visit bitmap
+    uint64_t bm_words;
+    WaveCtr* ctr;
+    unsigned long long* blk;
+    unsigned long long* gbar;          // grid-barrier arrival counter (monotonic; g->gbar + kGbarFused)
+    unsigned long long* done;          // completion counters (last_block)
+    uint64_t bar_timeout;
+    WaveParams wp;
+    CollectArgs col;
+    uint64_t big_push;                 // push levels with more edges run as k_level launches
+    unsigned long long* status;        // [fin_G] per-block invalidated counts for k_final_write
+    uint32_t fin_G;
+    uint64_t fin_wpb;
+};
+
+template <bool TAIL>
+__global__ __launch_bounds__(kBlock) void k_wave_fused(FusedArgs a) {
+    __shared__ __align__(16) uint32_t s_x[kChunkEmitCap + 8];
+    uint32_t* s_rel = s_x;
+    uint32_t* s_base = s_x + kChunk + 4;
+    __shared__ Emit em;
+    __shared__ MsgEmit<false> me;
+    __shared__ unsigned long long s_st[kBlock / 64][kStats];
+    __shared__ unsigned long long s_red[kBlock / 64];
+    __shared__ unsigned long long s_ft;
+    WaveCtr* ctr = a.ctr;
+    auto grid_sync = [&]() -> bool { return soft_grid_sync(a.gbar, &ctr->broken, nullptr, a.bar_timeout, false); };
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
+    int L = 0;
+    if constexpr (!TAIL) {
+        // the wave's counters (broken too: nothing can have set it before the first barrier), the
+        // per-block statistics, the invalidated bitmap and the hot snapshot past it, the visit bitmap
+        unsigned long long* c64 = reinterpret_cast<unsigned long long*>(ctr);
+        for (uint64_t i = tid; i < sizeof(WaveCtr) / 8; i += nthr) c64[i] = 0ull;
+        for (uint64_t i = tid; i < (uint64_t)kStatBlocks * kStatCols; i += nthr) a.blk[i] = 0ull;
+        uint4* f4 = reinterpret_cast<uint4*>(a.inv_bm);
+        for (uint64_t i = tid; i < a.bm_words / 4; i += nthr) f4[i] = make_uint4(0u, 0u, 0u, 0u);
+        for (uint64_t i = a.bm_words / 4 * 4 + tid; i < a.bm_words; i += nthr) a.inv_bm[i] = 0u;
+        if (a.clear_vis) {
+            uint4* v4 = reinterpret_cast<uint4*>(a.vis);
+            for (uint64_t i = tid; i < a.bm_words / 4; i += nthr) v4[i] = make_uint4(0u, 0u, 0u, 0u);
+            for (uint64_t i = a.bm_words / 4 * 4 + tid; i < a.bm_words; i += nthr) a.vis[i] = 0u;
+        }
+        if (!grid_sync()) return;
+        const Out o0{a.row_off, a.row_len, a.inv_bm, a.fr_off[0], a.fr_len[0], a.escan[0], a.cstart[0], &ctr->lvl[0]};
+        const uint32_t gsize = gridDim.x * blockDim.x;
+        if (a.imm) {   // Invalidate(true) roots first: their CAS may change node words
+            for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < a.n_roots; i0 += gsize)
+                root_step<1>(i0 + threadIdx.x, a.roots, a.imm, a.n_roots, 0u, a.n_handles, a.node, a.vis, o0, ctr);
+            if (!grid_sync()) return;
+        }
+        for (uint32_t i0 = blockIdx.x * blockDim.x; i0 < a.n_roots; i0 += gsize)
+            root_step<0>(i0 + threadIdx.x, a.roots, a.imm, a.n_roots, 0u, a.n_handles, a.node, a.vis, o0, ctr);
+        if (!grid_sync()) return;
+    } else {
+        // uniform: written by earlier launches only
+        if (ctr->phase == kPhaseDone || ctr->broken) return;
+        L = (int)ctr->cur;
+        const LevelCtr& lc = ctr->lvl[L % kRing];
+        const uint64_t F = lvl_F(lc), T = lvl_T(lc);
+        if (F != 0) {
+            if (level_pulls(ctr, L, a.wp, F, T) || T > a.big_push) {   // a mid level: the host runs another round
+                if (blockIdx.x == 0 && threadIdx.x == 0) ctr->mid_base = (unsigned long long)L;
+                return;
+            }
+            if (L > 0 && ctr->lvl[(L + kRing - 1) % kRing].pull) {   // after a pull level: its frontier list
+                CollectArgs c = a.col;
+                const int buf = L & 1;
+                c.fr_off = a.fr_off[buf];
+                c.fr_len = a.fr_len[buf];
+                c.escan = a.escan[buf];
+                c.cstart = a.cstart[buf];
+                collect_front(lc, a.wp.grid, c, (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6),
+                              (uint64_t)gridDim.x * (blockDim.x >> 6));
+                if (!grid_sync()) return;
+            }
+        }
+    }
+    // the push levels while they are small (level L's frontier and counters are complete here)
+    for (;; ++L) {
+        LevelCtr& lc = ctr->lvl[L % kRing];
+        if (threadIdx.x == 0) s_ft = coh_read(&lc.ft);
+        __syncthreads();
+        const uint64_t F = lc.F ? lc.F : (s_ft >> 32), T = lc.F ? lc.T : (s_ft & 0xFFFFFFFFull);
+        if (F == 0) break;
+        if (level_pulls(ctr, L, a.wp, F, T) || T > a.big_push) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) {
+                ctr->cur = (unsigned long long)L;
+                ctr->mid_base = (unsigned long long)L;
+            }
+            return;
+        }
+        if (blockIdx.x == 0) {
+            if (threadIdx.x == 0) {
+                ctr->lvl[(L + 1) % kRing].npull = lc.npull;
+                ctr->n_levels += 1;
+                ctr->e_trav += T;
+                ctr->f_total += F;
+                ctr->push_edges += T;
+                ctr->push_f += F;
+            }
+            // level L + 1's counter accumulates during this level; L + 2's is cleared for the next one
+            if (threadIdx.x < sizeof(LevelCtr) / 8)
+                reinterpret_cast<unsigned long long*>(&ctr->lvl[(L + 2) % kRing])[threadIdx.x] = 0ull;
+        }
+        const int buf = L & 1;
+        const ExpandArgs x{a.fr_off[buf], a.escan[buf], a.cstart[buf], a.pool_col, a.pool_tag, a.dead_filter};
+        const Out o{a.row_off,          a.row_len,         a.inv_bm, a.fr_off[buf ^ 1], a.fr_len[buf ^ 1],
+                    a.escan[buf ^ 1], a.cstart[buf ^ 1], &ctr->lvl[(L + 1) % kRing]};
+        emit_init(em);
+        expand_level<false>(kProbeLevelsOff, F, T, level_mult_one_round(T, gridDim.x), x, a.node, a.vis, o, em, s_x, me,
+                            s_rel, s_base, a.blk, s_st, RemoteArgs{});
+        if (!grid_sync()) return;
+    }
+    // the wave is done: statistics folded into the wave counters, the per-block counts of the final
+    // collect (k_final_write's geometry), V_inv by the last block
+    if (blockIdx.x < (uint32_t)kStats) {
+        const int k = blockIdx.x;
+        unsigned long long* dst[kStats] = {&ctr->e_match,   &ctr->n_flagged, &ctr->pull_surv, &ctr->pull_edges,
+                                           &ctr->pull_live, &ctr->pull_win,  &ctr->pull_tail, &ctr->pull_scan};
+        const unsigned long long* col = a.blk + (uint64_t)k * kStatBlocks;
+        unsigned long long x = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < kStatBlocks / kBlock; ++q) x += col[q * kBlock + threadIdx.x];
+        x = block_sum(x, s_red);
+        if (threadIdx.x == 0) *dst[k] = x + (k == kStFlagged ? ctr->root_flagged : 0ull);
+    }
+    const uint64_t words = ((uint64_t)a.n_handles + 63) / 64;
+    const unsigned long long* inv64 = reinterpret_cast<const unsigned long long*>(a.inv_bm);
+    for (uint32_t t = blockIdx.x; t < a.fin_G; t += gridDim.x) {   // block-uniform
+        const uint64_t lo = t * a.fin_wpb, hi = std::min<uint64_t>(words, lo + a.fin_wpb);
+        unsigned long long c = 0;
+        for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x) c += (unsigned long long)__popcll(inv64[w]);
+        c = block_sum(c, s_red);
+        if (threadIdx.x == 0) coh_xchg(a.status + t, c);
+    }
+    if (!last_block(a.done, gridDim.x)) return;
+    unsigned long long all = 0;
+    for (uint32_t k = threadIdx.x; k < a.fin_G; k += blockDim.x) all += coh_read(a.status + k);
+    all = block_sum(all, s_red);
+    if (threadIdx.x == 0) {
+        ctr->inv = all;
+        ctr->cur = (unsigned long long)L;
+        ctr->phase = kPhaseDone;
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void k_wave_init(WaveCtr* ctr, unsigned long long* blk, uint32_t* inv_bm,
                                                       uint32_t* vis_bm, uint64_t bm_words) {
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -2049,7 +2289,7 @@ hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true) {
                        (const unsigned long long*)g->blk_stats, ids ? 0 : 1, g->done);
     if (ids)
         hipLaunchKernelGGL(k_final_write, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb,
-                           (const unsigned long long*)st, g->ctr, g->inv);
+                           (const unsigned long long*)st, g->ctr, g->inv, 0);
     return hipGetLastError();
 }
 
@@ -2230,6 +2470,208 @@ void print_probe(fgi_graph* g, int L0, int L1) {
 }
 #endif
 
+namespace {
+
+// FGI_FUSED_BLOCKS: the fused kernels' grid (default one block per CU; measurement)
+
+uint32_t fused_grid(const fgi_graph* g) {
+    static const uint32_t env = [] {
+        const char* e = getenv("FGI_FUSED_BLOCKS");
+        return e ? (uint32_t)strtoul(e, nullptr, 10) : 0u;
+    }();
+    return std::max<uint32_t>((uint32_t)kStats, env ? env : (uint32_t)std::max(g->n_cu, 1));
+}
+
+hipError_t ensure_events(fgi_graph* g, size_t n) {
+    while (g->ev.size() < n) {
+        hipEvent_t e;
+        const hipError_t r = hipEventCreateWithFlags(&e, event_flags());
+        if (r != hipSuccess) return r;
+        g->ev.push_back(e);
+    }
+    return hipSuccess;
+}
+
+}  // namespace
+
+// A wave as fused launches (k_wave_fused head, k_collect + k_level mid pairs, k_wave_fused tail; see
+// above): one host synchronisation when the predicted number of mid pairs suffices. Returns
+// FGI_ENOTSUP (nothing launched) if the fused grid cannot be resident on this device.
+static fgi_status run_wave_fused(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
+                                 fgi_wave_stats* stats, WaveParams wp, bool timing,
+                                 std::chrono::steady_clock::time_point t0) {
+    hipStream_t s = g->stream;
+    const uint32_t G = fused_grid(g);
+    if (g->fused_per_cu == 0) {
+        int a = 0, b = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&a, k_wave_fused<false>, kBlock, 0) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, k_wave_fused<true>, kBlock, 0) != hipSuccess)
+            a = b = 0;
+        g->fused_per_cu = std::max(1, std::min(a, b));
+    }
+    if ((uint64_t)G > (uint64_t)g->fused_per_cu * (uint64_t)std::max(g->n_cu, 1)) return FGI_ENOTSUP;
+    FusedArgs a{};
+    a.roots = roots_dev;
+    a.imm = imm_dev;
+    a.n_roots = n_roots;
+    a.n_handles = g->n_handles;
+    a.node = reinterpret_cast<unsigned long long*>(g->node);
+    a.vis = g->vis_bm;
+    a.inv_bm = g->inv_bm;
+    a.row_off = g->row_off;
+    a.row_len = g->row_len;
+    for (int k = 0; k < 2; ++k) {
+        a.fr_off[k] = g->fr_off[k];
+        a.fr_len[k] = g->fr_len[k];
+        a.escan[k] = g->escan[k];
+        a.cstart[k] = g->cstart[k];
+    }
+    a.pool_col = g->pool_col;
+    a.pool_tag = g->pool_tag;
+    a.dead_filter = g->opt_dead_filter;
+    a.clear_vis = g->vis_stale ? 1 : 0;
+    a.bm_words = g->bm_words;
+    a.ctr = g->ctr;
+    a.blk = g->blk_stats;
+    a.gbar = g->gbar + kGbarFused;
+    a.done = g->done;
+    a.bar_timeout = kGridBarTimeout;
+    a.wp = wp;
+    a.col = collect_args(g, g->n_slots, wp, 0);   // frontier buffers chosen per level on the device
+    a.big_push = (uint64_t)G * kChunk;            // one round of the largest chunks over the grid
+    if (g->opt_fused & kFusedMidPush) a.big_push = 0;          // tests: every push level as a k_level launch
+    if (g->opt_fused & kFusedTailPush) a.big_push = ~0ull;     // tests: every push level in the fused grid
+    const uint64_t words = ((uint64_t)g->n_handles + 63) / 64;
+    a.fin_G = (uint32_t)std::min<uint64_t>(kFinalBlocks, std::max<uint64_t>(kStats, (words + 255) / 256));
+    a.fin_wpb = (words + a.fin_G - 1) / a.fin_G;
+    a.status = g->bsum + 6ull * kStatBlocks;
+    g->vis_stale = false;
+    g->coop_clean = false;
+    if (n_roots) g->v_dirty = true;
+    const auto* node = reinterpret_cast<const unsigned long long*>(g->node);
+    FGI_HIP(g, ensure_events(g, 2 * (size_t)kMidMax + 4));
+    hipEvent_t* ev = g->ev.data();
+    const size_t eh = 2 * (size_t)kMidMax;   // the head's / tail's event pair
+    if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
+    if (timing) FGI_HIP(g, hipEventRecord(ev[eh], s));
+    hipLaunchKernelGGL(k_wave_fused<false>, dim3(G), dim3(kBlock), 0, s, a);
+    if (timing) FGI_HIP(g, hipEventRecord(ev[eh + 1], s));
+    FGI_HIP(g, hipGetLastError());
+    const ExpandArgs x0 = expand_args(g, 0), x1 = expand_args(g, 1);
+    const Out o0 = out_for(g, 1, nullptr), o1 = out_for(g, 0, nullptr);
+    const PullArgs pa = pull_args(g, g->n_slots, g->inv_bm);
+    const CollectArgs c0 = collect_args(g, g->n_slots, wp, 0), c1 = collect_args(g, g->n_slots, wp, 1);
+    int P = (g->opt_fused & kFusedNoPredict) ? 0 : std::min(kMidMax, std::max(0, g->last_mid));
+    double pull_ms = 0, expand_ms = 0, fused_ms = 0;
+    uint64_t pull_launches = 0, expand_launches = 0, fused_launches = 1, syncs = 0;
+    float ms = 0;
+    for (int round = 0;; ++round) {
+        if (round > 0) FGI_HIP(g, hipMemsetAsync(g->ctr->mid_kind, 0, sizeof(g->ctr->mid_kind), s));
+        for (int i = 0; i < P; ++i) {
+            // the level (mid_base + i) is known on the device only: its parity picks the buffers there
+            hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, -1 - i, g->ctr, wp,
+                               c0, c1, a.big_push);
+            if (timing) FGI_HIP(g, hipEventRecord(ev[2 * i], s));
+            hipLaunchKernelGGL(k_level<false>, dim3(wp.grid), dim3(kBlock), 0, s, -1 - i, wp, x0, x1, pa, node, g->vis_bm,
+                               o0, o1, g->ctr, g->blk_stats, g->done, RemoteArgs{}, a.big_push);
+            if (timing) FGI_HIP(g, hipEventRecord(ev[2 * i + 1], s));
+        }
+        if (timing) FGI_HIP(g, hipEventRecord(ev[eh + 2], s));
+        hipLaunchKernelGGL(k_wave_fused<true>, dim3(G), dim3(kBlock), 0, s, a);
+        if (timing) FGI_HIP(g, hipEventRecord(ev[eh + 3], s));
+        ++fused_launches;
+        if (g->want_ids) {
+            const auto* inv64 = reinterpret_cast<const unsigned long long*>(g->inv_bm);
+            hipLaunchKernelGGL(k_final_write, dim3(a.fin_G), dim3(kBlock), 0, s, inv64, words, a.fin_wpb,
+                               (const unsigned long long*)a.status, g->ctr, g->inv, 1);
+        }
+        FGI_HIP(g, hipGetLastError());
+        FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
+        FGI_HIP(g, hipStreamSynchronize(s));
+        ++syncs;
+        const WaveCtr& c = *g->ctr_host;
+        if (timing) {
+            if (round == 0 && hipEventElapsedTime(&ms, ev[eh], ev[eh + 1]) == hipSuccess) fused_ms += ms;
+            if (hipEventElapsedTime(&ms, ev[eh + 2], ev[eh + 3]) == hipSuccess) fused_ms += ms;
+            for (int i = 0; i < P; ++i) {
+                const unsigned long long kind = c.mid_kind[i];
+                if (!kind || hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1]) != hipSuccess) continue;
+                if (kind == 2) {
+                    pull_ms += ms;
+                    ++pull_launches;
+                } else {
+                    expand_ms += ms;
+                    ++expand_launches;
+                }
+            }
+        } else {
+            for (int i = 0; i < P; ++i) {
+                pull_launches += c.mid_kind[i] == 2;
+                expand_launches += c.mid_kind[i] == 1;
+            }
+        }
+        if (c.broken) {
+            g->failed = true;
+            FGI_HIP(g, hipMemsetAsync(g->gbar, 0, kGbarWords * sizeof(unsigned long long), s));
+            FGI_HIP(g, hipStreamSynchronize(s));
+            return set_err(g, FGI_EDEVICE, "a fused wave's grid barrier timed out; the graph is unusable until fgi_restore");
+        }
+        if (c.phase == kPhaseDone) break;
+        if (round > 4096) return set_err(g, FGI_EDEVICE, "fused wave: no progress");
+        P = (g->opt_fused & kFusedNoPredict) ? 1 : kMidMax;   // more mid levels than predicted
+    }
+    const WaveCtr& c = *g->ctr_host;
+    if (timing || stats) {
+        FGI_HIP(g, hipEventRecord(g->ev_w1, s));
+        FGI_HIP(g, hipEventSynchronize(g->ev_w1));
+    }
+    g->last_mid = (int)c.n_mid;
+    if (imm_dev && n_roots) note_words(g);   // immediate roots changed node words
+    g->last_wave_n = c.inv;
+    g->ids_valid = g->want_ids;
+    g->stale_est += c.e_trav + c.e_match;
+    if (n_roots) g->last_levels = (int)std::max<uint64_t>(c.n_levels, 1);
+    static const bool trace = getenv("FGI_TRACE") != nullptr;
+    if (trace)
+        fprintf(stderr,
+                "[fgi] fused wave: %llu invalidated, %llu levels (%llu pull, %llu by k_level), %llu edges; push levels "
+                "in the fused grid: %llu entries / %llu edges; %llu host syncs; head+tail %.3f ms, pull %.3f ms\n",
+                (unsigned long long)c.inv, (unsigned long long)c.n_levels, (unsigned long long)c.n_pull,
+                (unsigned long long)c.n_mid, (unsigned long long)c.e_trav, (unsigned long long)c.push_f,
+                (unsigned long long)c.push_edges, (unsigned long long)syncs, fused_ms, pull_ms);
+    if (stats) {
+        const uint64_t v = c.inv;
+        stats->roots += n_roots;
+        stats->levels += c.n_levels;
+        stats->v_inv += v;
+        stats->e_trav += c.e_trav;
+        stats->e_match += c.e_match;
+        stats->n_flagged += c.n_flagged;
+        stats->pull_levels += c.n_pull;
+        stats->pull_edges += c.pull_edges;
+        const uint64_t pull_b = pull_level_bytes(c);
+        const uint64_t mid_push_b = 20 * c.mid_push_edges + 40 * c.mid_push_f;
+        const uint64_t fused_push_b = 20 * c.push_edges + 40 * c.push_f;
+        stats->alg_bytes += mid_push_b + fused_push_b + pull_b + 4 * v + 5ull * n_roots;
+        float wave_ms = 0;
+        hipEventElapsedTime(&wave_ms, g->ev_w0, g->ev_w1);
+        stats->kernel_ms += wave_ms;
+        stats->expand_ms += expand_ms;
+        stats->pull_ms += pull_ms;
+        stats->expand_launches += expand_launches;
+        stats->expand_bytes += mid_push_b;
+        stats->pull_bytes += pull_b;
+        stats->pull_launches += pull_launches;
+        stats->f_total += c.f_total;
+        stats->fused_launches += fused_launches;
+        stats->fused_ms += fused_ms;
+        stats->fused_push_bytes += fused_push_b;
+        stats->host_syncs += syncs;
+        stats->total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return FGI_OK;
+}
+
 fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                     fgi_wave_stats* stats) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -2247,6 +2689,14 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     if (wp0.direction == 2 && n_roots) FGI_TRY(ensure_in_lists(g));
     bool allow_pull = wp0.direction != 1 && pull_ready(g, wp0);
     static_assert(sizeof(WaveCtr) % 8 == 0, "WaveCtr is cleared as 64-bit words");
+    // fused launches when the wave's directions are settled (lists ready, or push only); a wave that
+    // may still have to build the dependency lists part-way runs as level groups below
+    if ((g->opt_fused & kFusedOn) && (allow_pull || wp0.direction == 1)) {
+        WaveParams wp = wp0;
+        if (!allow_pull) wp.direction = 1;
+        const fgi_status r = run_wave_fused(g, n_roots, roots_dev, imm_dev, stats, wp, timing, t0);
+        if (r != FGI_ENOTSUP) return r;
+    }
     hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
                        g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
     g->vis_stale = false;
@@ -2281,7 +2731,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         for (int k = 0; k < group; ++k, ++L) {
             const int buf = L & 1;
             hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp,
-                               collect_args(g, g->n_slots, wp, buf));
+                               collect_args(g, g->n_slots, wp, buf), collect_args(g, g->n_slots, wp, buf), ~0ull);
             if (timing) {
                 while (g->ev.size() < 2 * (size_t)(L + 1) + 2) {
                     hipEvent_t e;
@@ -2291,8 +2741,9 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                 FGI_HIP(g, hipEventRecord(g->ev[2 * L], s));
             }
             hipLaunchKernelGGL(k_level<false>, dim3(wp.grid), dim3(kBlock), 0, s, L, wp, expand_args(g, buf),
-                               pull_args(g, g->n_slots, g->inv_bm), node, g->vis_bm,
-                               out_for(g, buf ^ 1, nullptr), g->ctr, g->blk_stats, g->done, RemoteArgs{});
+                               expand_args(g, buf), pull_args(g, g->n_slots, g->inv_bm), node, g->vis_bm,
+                               out_for(g, buf ^ 1, nullptr), out_for(g, buf ^ 1, nullptr), g->ctr, g->blk_stats,
+                               g->done, RemoteArgs{}, ~0ull);
             if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L + 1], s));
         }
         FGI_HIP(g, launch_final(g, g->n_handles, g->want_ids));   // idempotent: repeated if the wave goes on
@@ -2493,11 +2944,12 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
         CollectArgs ca = collect_args(g, pv.n_local, wp, buf);
         ca.inv = front;   // hot heads are global ids
         ca.hot_bm = pv.front_global + g->hot_w0;
-        hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp, ca);
+        hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp, ca, ca, ~0ull);
         if (g->opt_level_timing) FGI_HIP(g, hipEventRecord(g->ev[0], s));
         hipLaunchKernelGGL(k_level<true>, dim3(wp.grid), dim3(kBlock), 0, s, L, wp, expand_args(g, buf),
-                           pull_args(g, g->n_slots, front), node, g->vis_bm, out_for(g, buf ^ 1, nullptr),
-                           g->ctr, g->blk_stats, g->done, ra);
+                           expand_args(g, buf), pull_args(g, g->n_slots, front), node, g->vis_bm,
+                           out_for(g, buf ^ 1, nullptr), out_for(g, buf ^ 1, nullptr), g->ctr, g->blk_stats, g->done,
+                           ra, ~0ull);
         if (g->opt_level_timing) FGI_HIP(g, hipEventRecord(g->ev[1], s));
         FGI_HIP(g, hipGetLastError());
         uint64_t n_recv = 0, n_sent = 0, glob[3] = {0, 0, 0};

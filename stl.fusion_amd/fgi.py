@@ -25,6 +25,7 @@ OPT_PULL_TPB = 8
 OPT_FRONT_EXCHANGE = 9
 OPT_HOT_HEADS = 10
 OPT_FAULT_INJECT = 11
+OPT_FUSED = 12
 DIR_AUTO, DIR_PUSH, DIR_PULL = 0, 1, 2
 NONE = 0xFFFFFFFF
 COMPUTING, CONSISTENT, INVALIDATED = 0, 1, 2
@@ -54,7 +55,8 @@ class WaveStats(C.Structure):
                 ("remote_msgs", C.c_uint64), ("f_total", C.c_uint64), ("expand_launches", C.c_uint64),
                 ("expand_ms", C.c_double), ("expand_bytes", C.c_uint64), ("pull_levels", C.c_uint64),
                 ("pull_edges", C.c_uint64), ("pull_ms", C.c_double), ("pull_bytes", C.c_uint64),
-                ("pull_launches", C.c_uint64)]
+                ("pull_launches", C.c_uint64), ("fused_launches", C.c_uint64), ("fused_ms", C.c_double),
+                ("fused_push_bytes", C.c_uint64), ("host_syncs", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
