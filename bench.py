@@ -65,12 +65,14 @@ def peak_rss_gb():
     return None
 
 
-def cpu_baseline(threads: int, cfg: dict, scale: int, gpu_roots=None):
+def cpu_baseline(threads: int, cfg: dict, scale: int, gpu_roots=None, gpu_ids=None, runs=5, single=False):
     """Time the oracle (reference-faithful CPU cascade: per-node mutex, HashSetSlim3 `_usedBy`,
     hash registry; oracle/fgo.cpp restating Computed.cs:162-230) parallel over roots. At the
     workload's own scale it builds the IDENTICAL graph and root batch (same generator and seeds;
     the roots are checked equal to the GPU's); a smaller --cpu-scale gives a labelled sample.
-    One timed wave at T = `threads`, then (after a restore) one at T = 1."""
+    SURVEY.md §8(d): one warm-up wave, then `runs` timed waves, each from a restored pristine copy; the
+    median is reported. The oracle's invalidated set is compared with the GPU's (gpu_ids) as a set.
+    single: one more timed wave at T = 1 (a minute at configs[1]; off by default)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import fgo  # test infrastructure: the CPU restatement, used here only as the baseline
     fgo.set_threads(threads)
@@ -90,20 +92,31 @@ def cpu_baseline(threads: int, cfg: dict, scale: int, gpu_roots=None):
     build_s = time.time() - t0
 
     def timed(th):
+        o.restore()
         st = fgo.Stats()
+        o.clear_log()
         t = time.perf_counter()
         o.invalidate_slots(r, None, threads=th, stats=st)
         return time.perf_counter() - t, st
 
     out = {}
-    for k, th in enumerate(sorted({threads, 1}, reverse=True)):
+    times = []
+    st = None
+    for k in range(runs + 1):   # run 0 is the warm-up
+        dt, st = timed(threads)
         if k:
-            o.restore()
-        dt, st = timed(th)
-        out[th] = dict(s=dt, v_inv=st.v_inv, e_trav=st.e_trav)
-        log(f"cpu baseline T={th}: {dt:.2f} s, {st.v_inv} nodes, {st.e_trav} edges")
+            times.append(dt)
+        log(f"cpu baseline T={threads} run {k}{' (warm-up)' if k == 0 else ''}: {dt:.2f} s, {st.v_inv} nodes")
+    same_set = None
+    if gpu_ids is not None and scale == cfg["scale"]:
+        same_set = bool(np.array_equal(np.sort(o.inv_log()), np.sort(gpu_ids)))
+    out[threads] = dict(s=statistics.median(times), runs=times, v_inv=st.v_inv, e_trav=st.e_trav)
+    if single and threads != 1:
+        dt, st1 = timed(1)
+        out[1] = dict(s=dt, runs=[dt], v_inv=st1.v_inv, e_trav=st1.e_trav)
+        log(f"cpu baseline T=1: {dt:.2f} s")
     o.close()
-    return out, build_s, m, len(r), identical_roots
+    return out, build_s, m, len(r), identical_roots, same_set
 
 
 def profiled_traffic(kname, config_scale, live_avg_ms):
@@ -157,6 +170,8 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host roots -> host ids) leg")
     ap.add_argument("--partition", action="store_true",
                     help="use the partitioned RCCL engine even at N=1 (it is always used for N>1)")
+    ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU waves after one warm-up (median reported)")
+    ap.add_argument("--cpu-single", action="store_true", help="also time the CPU oracle single-threaded")
     args = ap.parse_args()
 
     import torch
@@ -261,6 +276,7 @@ def main():
     # end-to-end leg (SURVEY.md §8(d)'s t: root H2D -> wave -> V_inv D2H complete): fgi_invalidate
     # with the roots in host memory and the invalidated ids copied into a pinned host buffer
     e2e = None
+    ids_host = None
     if not partitioned and not args.no_e2e:
         out_host = torch.empty(g.n_handles, dtype=torch.int32).pin_memory()
         g.set_option(pkg.fgi.OPT_LEVEL_TIMING, 0)
@@ -280,6 +296,7 @@ def main():
         ids_leg = {"ms_per_step": e2e_s / args.steps * 1e3, "value": st_e.v_inv / e2e_s,
                    "ids_copied_per_step": n_out, "d2h_bytes_per_step": 4 * n_out,
                    "note": "restore + fgi_invalidate(host roots -> pinned host id list)"}
+        ids_host = out_host[:n_out].numpy().astype(np.uint32).copy()
         del out_host
         # the same with the invalidated set returned as a bitmap over handles (fgi_invalidate_bits):
         # n_handles / 8 bytes cross PCIe instead of 4 B per invalidated node
@@ -298,15 +315,20 @@ def main():
         torch.cuda.synchronize()
         b_s = time.perf_counter() - t_b
         g.set_option(pkg.fgi.OPT_LEVEL_TIMING, 1)
-        n_bits = int(np.unpackbits(pin.array.view(np.uint8)).sum())
+        bit_ids = np.nonzero(np.unpackbits(pin.array.view(np.uint8), bitorder="little"))[0]
         pin.close()
         e2e = {"ms_per_step": b_s / args.steps * 1e3, "value": st_b.v_inv / b_s,
-               "output": "bitmap", "d2h_bytes_per_step": 8 * words, "bits_set": n_bits,
-               "same_set_size_as_ids": n_bits == n_out,
-               "note": "restore + fgi_invalidate_bits(host roots -> pinned host bitmap over handles); "
-                       "PCIe-inclusive, never `value`",
+               "gteps": st_b.e_trav / b_s / 1e9,
+               "output": "bitmap", "d2h_bytes_per_step": 8 * words, "bits_set": int(len(bit_ids)),
+               "same_set_as_ids": bool(np.array_equal(bit_ids, np.sort(ids_host))),
+               "note": "SURVEY.md §8(d)'s t: restore + fgi_invalidate_bits (roots H2D from host memory, wave, "
+                       "invalidated set D2H into a pinned host bitmap over handles); PCIe-inclusive, so never "
+                       "`value` (the bench contract: inputs resident in HBM)",
                "ids_output": ids_leg}
 
+    if e2e is None and not partitioned:
+        g.restore()
+        ids_host = np.asarray(g.invalidate(roots), np.uint32)
     v_inv, e_trav, e_match_all = st.v_inv, st.e_trav, st.e_match
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
@@ -359,6 +381,7 @@ def main():
                              "entries until the next prune, so later waves of a mutated graph count them. Here every "
                              "timed wave runs on the freshly built graph (restore only), which has none"),
         "levels_per_step": st.levels / args.steps,
+        "host_syncs_per_step": st.host_syncs / args.steps,
         "wave_kernel_ms": st.kernel_ms / args.steps,
         "wave_alg_gbs": wave_gbs,
         "pull_levels_per_step": st.pull_levels / args.steps,
@@ -380,7 +403,16 @@ def main():
             "timing_pass_ms_per_step": instrumented_ms,
             "push_levels": {"ms_per_step": st_k.expand_ms / args.steps,
                             "launches_per_step": st_k.expand_launches / args.steps,
-                            "gbs": (st_k.expand_bytes / (st_k.expand_ms * 1e-3) / 1e9) if st_k.expand_ms > 0 else 0.0},
+                            "gbs": (st_k.expand_bytes / (st_k.expand_ms * 1e-3) / 1e9) if st_k.expand_ms > 0 else 0.0,
+                            "note": "push levels run as their own k_level launches (more edges than one round "
+                                    "of the fused grid)"},
+            "fused": {"ms_per_step": st_k.fused_ms / args.steps,
+                      "launches_per_step": st_k.fused_launches / args.steps,
+                      "push_bytes_per_step": st_k.fused_push_bytes / args.steps,
+                      "gbs": (st_k.fused_push_bytes / (st_k.fused_ms * 1e-3) / 1e9) if st_k.fused_ms > 0 else 0.0,
+                      "note": "k_wave_fused head + tail: wave init, roots, every push level of at most one "
+                              "round of the grid, the collect after the pull levels and the final count; gbs "
+                              "counts only the push levels' bytes over the whole time of both launches"},
             "pull_levels": {"ms_per_step": st_k.pull_ms / args.steps,
                             "launches_per_step": st_k.pull_launches / args.steps,
                             "gbs": (st_k.pull_bytes / (st_k.pull_ms * 1e-3) / 1e9) if st_k.pull_ms > 0 else 0.0},
@@ -420,7 +452,8 @@ def main():
         threads = info["nproc"]
         cscale = args.cpu_scale or cfg["scale"]
         try:
-            cpu, cbuild, cm, cr, same_roots = cpu_baseline(threads, cfg, cscale, roots)
+            cpu, cbuild, cm, cr, same_roots, same_set = cpu_baseline(threads, cfg, cscale, roots, ids_host,
+                                                                      args.cpu_runs, args.cpu_single)
             best = cpu[threads]
             same = cscale == cfg["scale"]
             result["cpu_baseline"] = {
@@ -433,14 +466,17 @@ def main():
                            + (f"the identical {args.config} graph and {cr}-root batch (BASELINE.json configs[1]: R-MAT "
                               f"scale {cscale}, {cm} edges; roots equal to the GPU's: {same_roots})" if same else
                               f"a labelled sample: R-MAT scale {cscale} ({cm} edges), {cr} roots")
-                           + f", parallel over roots at T = nproc = {threads}; one timed wave per thread count, "
+                           + f", parallel over roots at T = nproc = {threads}; median of {len(best['runs'])} timed "
+                             f"waves after a warm-up, each from a restored pristine copy; "
                              f"{best['v_inv']} nodes / {best['e_trav']} edges per wave"),
                 "gteps": best["e_trav"] / best["s"] / 1e9,
                 "wave_s": best["s"],
-                "single_thread_value": cpu[1]["v_inv"] / cpu[1]["s"],
-                "single_thread_wave_s": cpu[1]["s"],
-                "same_result_as_gpu": bool(same and best["v_inv"] == st.v_inv // args.steps
+                "wave_s_runs": best["runs"],
+                "single_thread_value": (cpu[1]["v_inv"] / cpu[1]["s"]) if 1 in cpu else None,
+                "single_thread_wave_s": cpu[1]["s"] if 1 in cpu else None,
+                "same_result_as_gpu": bool(same and same_set and best["v_inv"] == st.v_inv // args.steps
                                            and best["e_trav"] == st.e_trav // args.steps),
+                "same_set_as_gpu": same_set,
                 "host": info,
                 "build_s": cbuild,
                 "peak_rss_gb": peak_rss_gb(),
