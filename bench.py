@@ -436,15 +436,15 @@ def main():
         result["e2e"] = e2e
     try:
         rv, rpath = pkg.fgi.rccl_info()
-        # libfgi links /opt/rocm's librccl (csrc/Makefile); a process that loaded torch first resolves
-        # the nccl symbols to torch's bundled copy instead
+        # libfgi resolves RCCL from /opt/rocm's librccl.so.1 at run time (RTLD_LOCAL, part.hip rccl()),
+        # so torch's bundled librccl, loaded first in this process, does not take its place
         linked = "/opt/rocm"
         differs = not os.path.realpath(rpath).startswith(os.path.realpath(linked))
-        result["rccl"] = {"version": rv, "path": rpath, "linked": linked + "/lib/librccl.so", "differs_from_linked": differs}
+        result["rccl"] = {"version": rv, "path": rpath, "linked": linked + "/lib/librccl.so.1",
+                          "differs_from_linked": differs, "torch_loaded_first": True}
         log(f"[rank {rank}] libfgi RCCL: ncclGetVersion {rv} from {rpath}")
         if differs:
-            log(f"[rank {rank}] WARNING: libfgi is bound to {rpath}, not the librccl it links ({linked}/lib); "
-                "a host that does not load torch first runs /opt/rocm's RCCL")
+            log(f"[rank {rank}] WARNING: libfgi is bound to {rpath}, not {linked}/lib/librccl.so.1")
     except Exception as e:  # informational only
         result["rccl"] = {"error": repr(e)}
     if rank == 0 and world == 1 and not args.no_cpu and cfg["kind"] == "rmat":

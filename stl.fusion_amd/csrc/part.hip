@@ -28,7 +28,9 @@
 #include <cstring>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include <rocprim/device/device_radix_sort.hpp>
@@ -85,6 +87,70 @@ struct PartState {
 
 static PartState* ps(fgi_graph* g) { return reinterpret_cast<PartState*>(g->part); }
 
+// ---- the RCCL the engine binds to ----------------------------------------------------------------
+// libfgi does not link librccl: a process that loaded another librccl with the same soname first
+// (torch's bundled copy) would otherwise bind the engine's collectives to that one. The entry points
+// are resolved from /opt/rocm's librccl (the one the engine is built against, FGI_RCCL_LIBRARY
+// overrides the path), opened RTLD_LOCAL, once per process: every collective below goes through
+// this table.
+struct RcclApi {
+    void* lib = nullptr;
+    std::string path;
+    decltype(&ncclGetVersion) GetVersion = nullptr;
+    decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
+    decltype(&ncclCommInitRank) CommInitRank = nullptr;
+    decltype(&ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&ncclGetErrorString) GetErrorString = nullptr;
+    decltype(&ncclAllReduce) AllReduce = nullptr;
+    decltype(&ncclAllGather) AllGather = nullptr;
+    decltype(&ncclSend) Send = nullptr;
+    decltype(&ncclRecv) Recv = nullptr;
+    decltype(&ncclGroupStart) GroupStart = nullptr;
+    decltype(&ncclGroupEnd) GroupEnd = nullptr;
+    std::string err;
+};
+
+static const RcclApi& rccl() {
+    static const RcclApi api = [] {
+        RcclApi a;
+        const char* env = getenv("FGI_RCCL_LIBRARY");
+        a.path = env && *env ? env : "/opt/rocm/lib/librccl.so.1";
+        a.lib = dlopen(a.path.c_str(), RTLD_NOW | RTLD_LOCAL);
+        if (!a.lib) {
+            const char* e = dlerror();
+            a.err = e ? e : "dlopen failed";
+            return a;
+        }
+        bool ok = true;
+        auto sym = [&](auto& fn, const char* name) {
+            fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(a.lib, name));
+            if (!fn) {
+                ok = false;
+                a.err = std::string("missing ") + name;
+            }
+        };
+        sym(a.GetVersion, "ncclGetVersion");
+        sym(a.GetUniqueId, "ncclGetUniqueId");
+        sym(a.CommInitRank, "ncclCommInitRank");
+        sym(a.CommDestroy, "ncclCommDestroy");
+        sym(a.GetErrorString, "ncclGetErrorString");
+        sym(a.AllReduce, "ncclAllReduce");
+        sym(a.AllGather, "ncclAllGather");
+        sym(a.Send, "ncclSend");
+        sym(a.Recv, "ncclRecv");
+        sym(a.GroupStart, "ncclGroupStart");
+        sym(a.GroupEnd, "ncclGroupEnd");
+        if (!ok) {
+            dlclose(a.lib);
+            a.lib = nullptr;
+        }
+        return a;
+    }();
+    return api;
+}
+
+static bool rccl_ok() { return rccl().lib != nullptr; }
+
 // c: [W][W + 2] all-gathered counts (targets sent by q to r, then q's next-level F, T)
 template <typename C>
 static void sum_counts(const C* c, uint32_t W, uint64_t* glob) {
@@ -102,7 +168,7 @@ fgi_status part_destroy(fgi_graph* g) {
     PartState* p = ps(g);
     if (!p) return FGI_OK;
     p->ops.reset();
-    if (p->comm) ncclCommDestroy(p->comm);
+    if (p->comm) rccl().CommDestroy(p->comm);
     hipFree(p->v.ver_all);
     hipFree(p->v.sent_bm);
     hipFree(p->v.send_buf);
@@ -134,7 +200,7 @@ bool part_view(fgi_graph* g, PartView* v) {
 
 static fgi_status nccl_check(fgi_graph* g, ncclResult_t r, const char* what) {
     if (r == ncclSuccess) return FGI_OK;
-    return set_err(g, FGI_EDEVICE, "%s: %s", what, ncclGetErrorString(r));
+    return set_err(g, FGI_EDEVICE, "%s: %s", what, rccl().GetErrorString(r));
 }
 #define FGI_NCCL(g, call)                                                  \
     do {                                                                   \
@@ -148,7 +214,7 @@ struct RcclComm final : PartComm {
         PartState* p = ps(g);
         hipStream_t s = g->stream;
         if (p->v.world > 1 || g->opt_part_coll) {
-            FGI_NCCL(g, ncclAllReduce(dev_val, p->scalar, count, ncclUint64, ncclSum, p->comm, s));
+            FGI_NCCL(g, rccl().AllReduce(dev_val, p->scalar, count, ncclUint64, ncclSum, p->comm, s));
             FGI_HIP(g, hipMemcpyAsync(p->scalar_host, p->scalar, 8 * count, hipMemcpyDeviceToHost, s));
         } else {   // one rank: the sum is the value
             FGI_HIP(g, hipMemcpyAsync(p->scalar_host, dev_val, 8 * count, hipMemcpyDeviceToHost, s));
@@ -161,30 +227,30 @@ struct RcclComm final : PartComm {
         PartState* p = ps(g);
         const uint32_t W = p->v.world, R = p->v.rank, S = W + 2;
         hipStream_t s = g->stream;
-        FGI_NCCL(g, ncclAllGather(p->v.send_cnt, p->all_cnt, S, ncclUint64, p->comm, s));
+        FGI_NCCL(g, rccl().AllGather(p->v.send_cnt, p->all_cnt, S, ncclUint64, p->comm, s));
         FGI_HIP(g, hipMemcpyAsync(p->all_cnt_host, p->all_cnt, (size_t)W * S * 8, hipMemcpyDeviceToHost, s));
         FGI_HIP(g, hipStreamSynchronize(s));
         const unsigned long long* c = p->all_cnt_host;   // c[q * S + r]: sent by q to r; c[q * S + W + i]: q's F, T
         sum_counts(c, W, glob);
         uint64_t recv = 0, sent = 0;
-        FGI_NCCL(g, ncclGroupStart());
+        FGI_NCCL(g, rccl().GroupStart());
         for (uint32_t q = 0; q < W; ++q) {
             if (q == R) continue;
             const uint64_t to_q = c[R * S + q], from_q = c[q * S + R];
             if (to_q)
-                FGI_NCCL(g, ncclSend(p->v.send_buf + (uint64_t)q * p->v.block, to_q, ncclUint32, (int)q, p->comm, s));
-            if (from_q) FGI_NCCL(g, ncclRecv(p->v.recv_buf + recv, from_q, ncclUint32, (int)q, p->comm, s));
+                FGI_NCCL(g, rccl().Send(p->v.send_buf + (uint64_t)q * p->v.block, to_q, ncclUint32, (int)q, p->comm, s));
+            if (from_q) FGI_NCCL(g, rccl().Recv(p->v.recv_buf + recv, from_q, ncclUint32, (int)q, p->comm, s));
             recv += from_q;
             sent += to_q;
         }
-        FGI_NCCL(g, ncclGroupEnd());
+        FGI_NCCL(g, rccl().GroupEnd());
         *n_recv = recv;
         *n_sent = sent;
         return FGI_OK;
     }
     fgi_status allgather_front(fgi_graph* g) override {
         PartState* p = ps(g);
-        FGI_NCCL(g, ncclAllGather(g->inv_bm, p->v.front_global, p->v.block / 32, ncclUint32, p->comm, g->stream));
+        FGI_NCCL(g, rccl().AllGather(g->inv_bm, p->v.front_global, p->v.block / 32, ncclUint32, p->comm, g->stream));
         return FGI_OK;
     }
     fgi_status allgather_count(fgi_graph* g, uint64_t mine, uint64_t* all) override {
@@ -192,7 +258,7 @@ struct RcclComm final : PartComm {
         const uint32_t W = p->v.world;
         p->scalar_host[0] = mine;
         FGI_HIP(g, hipMemcpyAsync(p->scalar, p->scalar_host, 8, hipMemcpyHostToDevice, g->stream));
-        FGI_NCCL(g, ncclAllGather(p->scalar, p->all_cnt, 1, ncclUint64, p->comm, g->stream));
+        FGI_NCCL(g, rccl().AllGather(p->scalar, p->all_cnt, 1, ncclUint64, p->comm, g->stream));
         FGI_HIP(g, hipMemcpyAsync(p->all_cnt_host, p->all_cnt, (size_t)W * 8, hipMemcpyDeviceToHost, g->stream));
         FGI_HIP(g, hipStreamSynchronize(g->stream));
         for (uint32_t q = 0; q < W; ++q) all[q] = p->all_cnt_host[q];
@@ -202,14 +268,14 @@ struct RcclComm final : PartComm {
         PartState* p = ps(g);
         const uint32_t W = p->v.world, R = p->v.rank;
         uint64_t recv = 0;
-        FGI_NCCL(g, ncclGroupStart());
+        FGI_NCCL(g, rccl().GroupStart());
         for (uint32_t q = 0; q < W; ++q) {
             if (q == R) continue;
-            if (cnt[R]) FGI_NCCL(g, ncclSend(p->dbuf, cnt[R], ncclUint64, (int)q, p->comm, g->stream));
-            if (cnt[q]) FGI_NCCL(g, ncclRecv(p->rbuf + recv, cnt[q], ncclUint64, (int)q, p->comm, g->stream));
+            if (cnt[R]) FGI_NCCL(g, rccl().Send(p->dbuf, cnt[R], ncclUint64, (int)q, p->comm, g->stream));
+            if (cnt[q]) FGI_NCCL(g, rccl().Recv(p->rbuf + recv, cnt[q], ncclUint64, (int)q, p->comm, g->stream));
             recv += cnt[q];
         }
-        FGI_NCCL(g, ncclGroupEnd());
+        FGI_NCCL(g, rccl().GroupEnd());
         *n_recv = recv;
         return FGI_OK;
     }
@@ -752,8 +818,9 @@ extern "C" {
 
 fgi_status fgi_part_unique_id(uint8_t* id128) {
     if (!id128) return FGI_EINVAL;
+    if (!rccl_ok()) return FGI_ENOTSUP;
     ncclUniqueId id;
-    if (ncclGetUniqueId(&id) != ncclSuccess) return FGI_EDEVICE;
+    if (rccl().GetUniqueId(&id) != ncclSuccess) return FGI_EDEVICE;
     std::memcpy(id128, id.internal, NCCL_UNIQUE_ID_BYTES);
     return FGI_OK;
 }
@@ -763,27 +830,18 @@ static fgi_status part_alloc(fgi_graph* g, uint32_t n_global);
 fgi_status fgi_part_init(fgi_graph* g, uint32_t n_global, const uint8_t* id128) {
     if (!g || !id128) return FGI_EINVAL;
     if (g->part) return set_err(g, FGI_ESTATE, "partition already initialised");
+    if (!rccl_ok())
+        return set_err(g, FGI_ENOTSUP, "RCCL not available (%s: %s)", rccl().path.c_str(), rccl().err.c_str());
     FGI_TRY(part_alloc(g, n_global));
     PartState* p = ps(g);
     ncclUniqueId id;
     std::memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
-    ncclResult_t r = ncclCommInitRank(&p->comm, (int)p->v.world, id, g->rank);
+    ncclResult_t r = rccl().CommInitRank(&p->comm, (int)p->v.world, id, g->rank);
     if (r != ncclSuccess) {
         part_destroy(g);
-        return set_err(g, FGI_EDEVICE, "ncclCommInitRank: %s", ncclGetErrorString(r));
+        return set_err(g, FGI_EDEVICE, "ncclCommInitRank: %s", rccl().GetErrorString(r));
     }
     p->ops.reset(new RcclComm());
-    // the engine is built against /opt/rocm's RCCL headers; a process that loaded another librccl
-    // with the same soname first (e.g. torch's) binds the engine to that one: say so once
-    static bool warned = false;
-    int v = 0;
-    if (!warned && ncclGetVersion(&v) == ncclSuccess && v != NCCL_VERSION_CODE) {
-        Dl_info info{};
-        const char* f = (dladdr(reinterpret_cast<void*>(&ncclGetVersion), &info) && info.dli_fname) ? info.dli_fname : "?";
-        fprintf(stderr, "[fgi] warning: collectives bound to RCCL %d (%s), not the RCCL %d libfgi was built against\n", v,
-                f, (int)NCCL_VERSION_CODE);
-        warned = true;
-    }
     return FGI_OK;
 }
 
@@ -887,15 +945,17 @@ fgi_status fgi_part_local_invalidate(fgi_graph* const* gs, uint32_t P, uint32_t 
     return FGI_OK;
 }
 
-// The RCCL library the engine's collectives bound to (libfgi links librccl; a process that has
-// already loaded another RCCL with the same soname, e.g. torch's, shares that one).
+// The RCCL library the engine's collectives bind to: the file its entry points were resolved from
+// (rccl(): /opt/rocm's librccl, opened privately, whatever other RCCL the process has loaded).
 fgi_status fgi_rccl_info(int* version, char* path, uint64_t cap) {
+    if (!rccl_ok()) return FGI_ENOTSUP;
     int v = 0;
-    if (ncclGetVersion(&v) != ncclSuccess) return FGI_EDEVICE;
+    if (rccl().GetVersion(&v) != ncclSuccess) return FGI_EDEVICE;
     if (version) *version = v;
     if (path && cap) {
         Dl_info info{};
-        const char* f = (dladdr(reinterpret_cast<void*>(&ncclGetVersion), &info) && info.dli_fname) ? info.dli_fname : "";
+        const char* f = (dladdr(reinterpret_cast<void*>(rccl().GetVersion), &info) && info.dli_fname) ? info.dli_fname
+                                                                                                      : rccl().path.c_str();
         std::strncpy(path, f, cap - 1);
         path[cap - 1] = 0;
     }

@@ -65,7 +65,10 @@ def test_bad_config_rejected(pkg):
 
 
 def test_rccl_info_reports_the_bound_library(pkg):
-    """fgi_rccl_info names the RCCL the engine's collectives bind to (two RCCLs can be present in
-    one process: torch's and /opt/rocm's; they share a soname, so the first one loaded wins)."""
+    """fgi_rccl_info names the RCCL the engine's collectives bind to. libfgi does not link librccl: it
+    resolves the entry points from /opt/rocm's librccl.so.1 (RTLD_LOCAL), so torch's bundled librccl —
+    the same soname, loaded first by any process that imports torch — cannot take its place."""
+    import torch  # noqa: F401  (loads torch's librccl into this process first)
     v, path = pkg.fgi.rccl_info()
-    assert v >= 22000 and "rccl" in os.path.basename(path)
+    assert v >= 22700 and "rccl" in os.path.basename(path)
+    assert os.path.realpath(path).startswith(os.path.realpath("/opt/rocm")), path
