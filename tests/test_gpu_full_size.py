@@ -11,13 +11,13 @@ configs[4]  the streaming mix at BASELINE.json's size: 10,000 hubs x 1,000 leave
             size a cascade's leaf level (100,000 edges) is split into multi-fine chunks over the
             cascade grid, and the final collect owns more bitmap words per block than it stages in
             LDS — the paths the small mixes of test_gpu_batch.py never reach.
-configs[3]  R-MAT 24 with 50% stale edges at full size: a wave, then fgi_prune. PruneUsedBy
-            (Computed.cs:400-419) on every registered Consistent node, reached by the pruner's walk
-            (ComputedGraphPruner.cs:79-94), keeps an entry iff the dependant's current node exists
-            with the entry's version. Checked exactly over the exported edge sets: the kept entries
-            are the pre-prune entries of Consistent nodes whose dependant is registered (not
-            Invalidated) at the entry's tag, and PruneStats.new_edges is their count; then a second
-            wave on the pruned graph against the independent least closure (tests/closure_check.py).
+configs[3]  R-MAT 24 with 50% stale edges at full size (263.4 M entries). PruneUsedBy (Computed.cs:400-419)
+            on every registered Consistent node, reached by the pruner's walk (ComputedGraphPruner.cs:
+            79-94), keeps an entry iff the dependant's current node exists with the entry's version.
+            Checked exactly over the exported edge sets, twice: bench_configs.py's prune (restored
+            graph, the fast path) and a prune after a wave (the gather path); the kept entries are
+            exactly the live pre-prune ones and PruneStats.new_edges is their count. Then a wave on the
+            pruned graph against the independent least closure (tests/closure_check.py).
 """
 import numpy as np
 import pytest
@@ -108,8 +108,37 @@ def _sorted_keys(u, d):
     return torch.sort(k).values
 
 
-def test_configs3_full_size_prune_keeps_exactly_the_live_entries(pkg, gpu_available):
+def _live_keys(g, n, v, st):
+    """The exported entries PruneUsedBy keeps (Computed.cs:400-419): rows of Consistent nodes (the
+    export holds the rows of current nodes), dependant registered (not Invalidated) at the entry's tag;
+    as sorted (used << 32 | dependant) keys, and the export's size."""
+    u, d, t = g.export_edges()
+    keep = (u < n) & (d < n)
+    keep[keep] &= st[u[keep]] == CONSISTENT
+    keep[keep] &= st[d[keep]] != INVALIDATED
+    keep[keep] &= t[keep] == v[d[keep]]
+    return _sorted_keys(u[keep], d[keep]), len(u)
+
+
+def _check_prune(g, n, want, old_export):
     import torch
+    ps = g.prune()
+    assert ps.new_edges == len(want), (ps.new_edges, len(want))
+    assert ps.new_edges < old_export, (ps.new_edges, old_export)
+    v, _ = g.dump_states()
+    u1, d1, t1 = g.export_edges()
+    assert len(u1) == len(want)
+    assert np.all(t1 == v[:n][d1]), "a kept entry's tag differs from its dependant's version"
+    assert torch.equal(_sorted_keys(u1, d1), want), "the kept entries differ from the live pre-prune entries"
+    return u1, d1, t1
+
+
+def test_configs3_full_size_prune_keeps_exactly_the_live_entries(pkg, gpu_available):
+    """(a) bench_configs.py's flow: a wave (it builds the pull lists), fgi_restore, fgi_prune on the fast
+    path — every node Consistent, so exactly the entries whose tag is their dependant's version stay
+    (131.7 M of 263.4 M); (b) a wave, then a second prune (the gather path, after (a)'s compaction) —
+    the rows of invalidated nodes are dropped and entries pointing at them too; (c) a third wave on the
+    twice-pruned graph against the independent least closure over the kept entries."""
     from closure_check import DeviceEdges
     from stl_fusion_amd import workloads as W
     cfg = W.CONFIGS["rmat24_churn"]
@@ -119,33 +148,31 @@ def test_configs3_full_size_prune_keeps_exactly_the_live_entries(pkg, gpu_availa
     roots = W.roots_for(g, cfg)
     deg, _ = g.degrees()
     roots2 = O.gen_roots(4096, n, cfg["roots_seed"] + 1, deg[:n])
+    g.snapshot()
     ws = pkg.WaveStats()
-    ids = g.invalidate(roots, stats=ws)          # builds the pull lists (the prune's fast path)
+    g.invalidate(roots, stats=ws)
     assert ws.v_inv > 5_000_000
+    g.restore()
+    # (a)
     v, f = g.dump_states()
     v, st = v[:n], f[:n] & 3
-    u0, d0, t0 = g.export_edges()
-    assert len(u0) == 263_432_932
-    keep = (u0 < n) & (d0 < n)
-    keep[keep] &= st[u0[keep]] == CONSISTENT           # PruneUsedBy runs on Consistent nodes only
-    keep[keep] &= st[d0[keep]] != INVALIDATED          # an Invalidated node is unregistered
-    keep[keep] &= t0[keep] == v[d0[keep]]              # ... at the entry's version
-    want = _sorted_keys(u0[keep], d0[keep])
-    del u0, d0, t0, keep
-    ps = g.prune()
-    assert ps.new_edges == len(want), (ps.new_edges, len(want))
-    assert 10_000_000 < ps.new_edges < ps.old_edges, (ps.new_edges, ps.old_edges)
-    u1, d1, t1 = g.export_edges()
-    assert len(u1) == len(want)
-    assert np.all(t1 == v[d1]), "a kept entry's tag differs from its dependant's version"
-    got = _sorted_keys(u1, d1)
-    assert torch.equal(got, want), "the kept entries differ from the live pre-prune entries"
-    del got, want
-    # a second wave on the pruned graph. The pruned rows hold only entries of Consistent nodes to
-    # registered dependants at their versions, so the least closure over them from the roots that
-    # are still Consistent is exactly the second wave
-    ver_now = v.copy()
-    edges = DeviceEdges(n, u1, d1, t1, ver_now)
+    assert np.all(st == CONSISTENT)
+    want, m0 = _live_keys(g, n, v, st)
+    assert m0 == 263_432_932 and 0.49 < len(want) / m0 < 0.51, (m0, len(want))
+    _check_prune(g, n, want, m0)
+    del want
+    # (b)
+    g.snapshot()
+    ws = pkg.WaveStats()
+    ids = g.invalidate(roots, stats=ws)
+    v, f = g.dump_states()
+    v, st = v[:n], f[:n] & 3
+    want, m1 = _live_keys(g, n, v, st)
+    u1, d1, t1 = _check_prune(g, n, want, m1 + 1)
+    del want
+    # (c) the pruned rows hold only entries of Consistent nodes to registered dependants at their
+    # versions, so the least closure over them from the roots still Consistent is the wave exactly
+    edges = DeviceEdges(n, u1, d1, t1, v)
     del u1, d1, t1
     fresh = roots2[st[roots2] == CONSISTENT]
     ws2 = pkg.WaveStats()
