@@ -349,6 +349,14 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *                            launches: extra rounds), 4 (every push level as its own launch) or 8
  *                            (every push level in the fused grid); the environment's FGI_FUSED=0
  *                            makes 0 the default
+ *   FGI_OPT_PART_PLAN   [1]  partitions: a wave follows the previous wave's directions (when every
+ *                            rank can) and queues all its levels' collectives at fixed sizes, with one
+ *                            host synchronisation at its end (two with remote ranks: the start's
+ *                            all-reduce too); 0 decides every level on the host after an all-reduce.
+ *                            All ranks must set the same value
+ *   FGI_OPT_PART_BUCKET [0]  partitions, planned waves: words per peer of a push level's bucket (a
+ *                            count, then ids; 0 = the allocated 65,536); smaller buckets only delay
+ *                            ids to later push levels (tests pin that path; results never change)
  *   FGI_OPT_FAULT_INJECT [0] tests only: value (k << 16) | b, b > 0: in the (k+1)-th streaming
  *                            cascade launched from now (fgi_run_batch), block b - 1 leaves at its first
  *                            grid barrier without arriving, and that cascade's barrier times out after
@@ -366,6 +374,8 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
 #define FGI_OPT_HOT_HEADS 10
 #define FGI_OPT_FAULT_INJECT 11
 #define FGI_OPT_FUSED 12
+#define FGI_OPT_PART_PLAN 13
+#define FGI_OPT_PART_BUCKET 14
 fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value);
 
 /* ---- multi-GPU (1-D vertex-range partition, RCCL all-to-all frontier exchange) --------------- */

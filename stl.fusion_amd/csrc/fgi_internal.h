@@ -204,6 +204,7 @@ struct WaveCtr {
     LevelCtr lvl[kRing];
 };
 constexpr unsigned long long kPhaseDone = 1;
+constexpr uint32_t kPlanMax = 48;   // levels of a planned partitioned wave
 constexpr int kMidMax = 16;         // k_level launches per round of a fused wave
 
 // per-wave accounting of a partitioned wave
@@ -404,6 +405,12 @@ struct fgi_graph {
     // multi-GPU
     void* part = nullptr;
     fgi::PartWave pw;
+    // planned partitioned waves (run_part_wave): the directions of the previous wave's levels (1 pull),
+    // the key they were learnt under, and whether the pull lists were ready then
+    std::vector<uint8_t> part_plan;
+    uint64_t part_plan_key = 0;
+    bool part_plan_pull = false;
+    int opt_part_plan = 1;             // FGI_OPT_PART_PLAN
 
     std::string err;
 };
@@ -491,13 +498,29 @@ bool part_view(fgi_graph* g, PartView* v);
 // Exchange this level's messages: counts by all-gather, payload by grouped send/recv over RCCL.
 // Returns the number of target ids received (concatenated at recv_buf) and sent.
 fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent, uint64_t* glob);
-// Sum of count (1..4) device u64 over all ranks, returned on the host.
+// Sum of count (1..kPartRedMax) device u64 over all ranks, returned on the host.
 fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out,
                               uint32_t count = 1);
 // all-gather every rank's local invalidated-bitmap words into front_global (part.hip)
 fgi_status part_allgather_front(fgi_graph* g);
 // zero front_global at a wave's start (the delta exchange's baseline)
 fgi_status part_front_reset(fgi_graph* g);
+// Planned waves (run_part_wave): the full frontier all-gather and the fixed-size bucket all-to-all,
+// stream-ordered (no host synchronisation), and the buffers they move.
+constexpr uint32_t kPartRedMax = 160;   // words of one all-reduce (part_allreduce_sum)
+struct PartBuckets {
+    uint32_t C;                        // words per peer: count, then up to C - 1 target ids
+    uint32_t* send;                    // [world][C]
+    uint32_t* recv;                    // [world][C]
+    unsigned long long* cur;           // [world] the next send_buf id to pack per owner
+    unsigned long long* red;           // [kPartRedMax] device all-reduce source
+};
+fgi_status part_allgather_front_async(fgi_graph* g);
+uint64_t part_plan_key(const fgi_graph* g);
+fgi_status part_alltoall_async(fgi_graph* g);
+PartBuckets part_buckets(fgi_graph* g);
+// FGI_OPT_PART_BUCKET: words per peer of the planned waves' buckets (0: all that is allocated)
+fgi_status part_set_bucket(fgi_graph* g, int64_t words);
 // frontier exchanges of each kind so far and the bytes this rank received through them
 fgi_status part_front_stats(fgi_graph* g, uint64_t* full, uint64_t* delta, uint64_t* bytes);
 // Rebuild a partition's pull lists from its dependency-entry store if rows or versions changed.

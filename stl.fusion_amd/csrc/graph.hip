@@ -2101,6 +2101,8 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
         if (value < 0) return set_err(g, FGI_EINVAL, "beta must be >= 0");
         g->opt_pull_beta = (int)value;
         return FGI_OK;
+    case FGI_OPT_PART_PLAN: g->opt_part_plan = value ? 1 : 0; return FGI_OK;
+    case FGI_OPT_PART_BUCKET: return part_set_bucket(g, value);
     case FGI_OPT_FUSED:
         if (value < 0 || value > 15) return set_err(g, FGI_EINVAL, "fused-wave bits must be 0..15");
         g->opt_fused = (int)value;

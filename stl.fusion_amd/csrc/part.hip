@@ -58,6 +58,11 @@ struct PartComm {
     // every rank's delta entries dbuf[0, cnt[rank]) (global word << 32 | word) to every other rank:
     // concatenated at rbuf, returns the number received
     virtual fgi_status exchange_delta(fgi_graph* g, const uint64_t* cnt, uint64_t* n_recv) = 0;
+    // Planned waves (no host synchronisation): stream-ordered collectives of fixed size.
+    // allgather_front without waiting for the host (the next kernels on the stream see front_global)
+    virtual fgi_status allgather_front_async(fgi_graph* g) = 0;
+    // a2a_send[q * C, + C) to rank q, into a2a_recv[r * C, + C) from every rank r
+    virtual fgi_status alltoall_async(fgi_graph* g) = 0;
 };
 
 struct PartState {
@@ -83,6 +88,16 @@ struct PartState {
     unsigned long long* dcnt = nullptr;        // device count of dbuf
     uint64_t front_full = 0, front_delta = 0;  // exchanges of each kind (statistics)
     uint64_t front_bytes = 0;                  // bytes received by this rank's frontier exchanges
+    // planned waves (run_part_wave): the targets a push level forwards move in fixed-size buckets,
+    // a2a_C words per peer (count, then up to a2a_C - 1 ids); what does not fit waits in send_buf
+    // (a2a_cur: the next id to pack per owner) for the next push level
+    uint32_t a2a_C = 0;                        // words per peer in use (<= a2a_cap; FGI_OPT_PART_BUCKET)
+    uint32_t a2a_cap = 0;                      // words per peer allocated
+    uint32_t* a2a_send = nullptr;              // [world][a2a_C]
+    uint32_t* a2a_recv = nullptr;              // [world][a2a_C]
+    unsigned long long* a2a_cur = nullptr;     // [world]
+    unsigned long long* red = nullptr;         // [kPartRedMax] device all-reduce buffer (planned waves)
+    unsigned long long* red_host = nullptr;
 };
 
 static PartState* ps(fgi_graph* g) { return reinterpret_cast<PartState*>(g->part); }
@@ -103,6 +118,7 @@ struct RcclApi {
     decltype(&ncclGetErrorString) GetErrorString = nullptr;
     decltype(&ncclAllReduce) AllReduce = nullptr;
     decltype(&ncclAllGather) AllGather = nullptr;
+    decltype(&ncclAllToAll) AllToAll = nullptr;
     decltype(&ncclSend) Send = nullptr;
     decltype(&ncclRecv) Recv = nullptr;
     decltype(&ncclGroupStart) GroupStart = nullptr;
@@ -136,6 +152,7 @@ static const RcclApi& rccl() {
         sym(a.GetErrorString, "ncclGetErrorString");
         sym(a.AllReduce, "ncclAllReduce");
         sym(a.AllGather, "ncclAllGather");
+        sym(a.AllToAll, "ncclAllToAll");
         sym(a.Send, "ncclSend");
         sym(a.Recv, "ncclRecv");
         sym(a.GroupStart, "ncclGroupStart");
@@ -184,6 +201,11 @@ fgi_status part_destroy(fgi_graph* g) {
     hipFree(p->dbuf);
     hipFree(p->rbuf);
     hipFree(p->dcnt);
+    hipFree(p->a2a_send);
+    hipFree(p->a2a_recv);
+    hipFree(p->a2a_cur);
+    hipFree(p->red);
+    if (p->red_host) hipHostFree(p->red_host);
     if (p->all_cnt_host) hipHostFree(p->all_cnt_host);
     if (p->scalar_host) hipHostFree(p->scalar_host);
     delete p;
@@ -213,14 +235,23 @@ struct RcclComm final : PartComm {
     fgi_status allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out, uint32_t count) override {
         PartState* p = ps(g);
         hipStream_t s = g->stream;
+        const bool big = count > 4;
+        unsigned long long* dst = big ? p->red : p->scalar;
+        unsigned long long* host = big ? p->red_host : p->scalar_host;
         if (p->v.world > 1 || g->opt_part_coll) {
-            FGI_NCCL(g, rccl().AllReduce(dev_val, p->scalar, count, ncclUint64, ncclSum, p->comm, s));
-            FGI_HIP(g, hipMemcpyAsync(p->scalar_host, p->scalar, 8 * count, hipMemcpyDeviceToHost, s));
+            FGI_NCCL(g, rccl().AllReduce(dev_val, dst, count, ncclUint64, ncclSum, p->comm, s));
+            FGI_HIP(g, hipMemcpyAsync(host, dst, 8 * count, hipMemcpyDeviceToHost, s));
         } else {   // one rank: the sum is the value
-            FGI_HIP(g, hipMemcpyAsync(p->scalar_host, dev_val, 8 * count, hipMemcpyDeviceToHost, s));
+            FGI_HIP(g, hipMemcpyAsync(host, dev_val, 8 * count, hipMemcpyDeviceToHost, s));
         }
         FGI_HIP(g, hipStreamSynchronize(s));
-        for (uint32_t i = 0; i < count; ++i) out[i] = p->scalar_host[i];
+        for (uint32_t i = 0; i < count; ++i) out[i] = host[i];
+        return FGI_OK;
+    }
+    fgi_status allgather_front_async(fgi_graph* g) override { return allgather_front(g); }   // stream-ordered
+    fgi_status alltoall_async(fgi_graph* g) override {
+        PartState* p = ps(g);
+        FGI_NCCL(g, rccl().AllToAll(p->a2a_send, p->a2a_recv, p->a2a_C, ncclUint32, p->comm, g->stream));
         return FGI_OK;
     }
     fgi_status exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent, uint64_t* glob) override {
@@ -291,12 +322,28 @@ struct LocalGroup {
     uint32_t arrived = 0;
     uint64_t gen = 0;
     bool failed = false;
-    std::vector<uint64_t> vals;   // [P][4] all-reduce contributions
+    std::vector<uint64_t> vals;   // [P][kPartRedMax] all-reduce contributions
     std::vector<uint64_t> cnt;    // [P][P + 2] targets rank r forwards to owner q, then r's F, T
+    // stream-ordered exchanges (planned waves): rank r records ready[r] when its source is final and
+    // done[r] when its copies from the others are queued; the others' streams wait on them
+    std::vector<hipEvent_t> ready, done;
 
     explicit LocalGroup(std::vector<fgi_graph*> g) : gs(std::move(g)) {
-        vals.assign(gs.size() * 4, 0);
+        vals.assign(gs.size() * kPartRedMax, 0);
         cnt.assign(gs.size() * (gs.size() + 2), 0);
+        ready.assign(gs.size(), nullptr);
+        done.assign(gs.size(), nullptr);
+        for (size_t r = 0; r < gs.size(); ++r) {
+            hipSetDevice(gs[r]->device);
+            hipEventCreateWithFlags(&ready[r], hipEventDisableTiming);
+            hipEventCreateWithFlags(&done[r], hipEventDisableTiming);
+        }
+    }
+    ~LocalGroup() {
+        for (hipEvent_t e : ready)
+            if (e) hipEventDestroy(e);
+        for (hipEvent_t e : done)
+            if (e) hipEventDestroy(e);
     }
     bool arrive() {
         std::unique_lock<std::mutex> lk(mu);
@@ -332,16 +379,17 @@ struct LocalComm final : PartComm {
 
     fgi_status allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out, uint32_t count) override {
         PartState* p = ps(g);
-        FGI_HIP(g, hipMemcpyAsync(p->scalar_host, dev_val, 8 * count, hipMemcpyDeviceToHost, g->stream));
+        unsigned long long* host = count > 4 ? p->red_host : p->scalar_host;
+        FGI_HIP(g, hipMemcpyAsync(host, dev_val, 8 * count, hipMemcpyDeviceToHost, g->stream));
         FGI_HIP(g, hipStreamSynchronize(g->stream));
         {
             std::lock_guard<std::mutex> lk(grp->mu);
-            for (uint32_t i = 0; i < count; ++i) grp->vals[(size_t)rank * 4 + i] = p->scalar_host[i];
+            for (uint32_t i = 0; i < count; ++i) grp->vals[(size_t)rank * kPartRedMax + i] = host[i];
         }
         if (!grp->arrive()) return peer_failed(g);
         for (uint32_t i = 0; i < count; ++i) {
             uint64_t t = 0;
-            for (size_t r = 0; r < grp->gs.size(); ++r) t += grp->vals[r * 4 + i];
+            for (size_t r = 0; r < grp->gs.size(); ++r) t += grp->vals[r * kPartRedMax + i];
             out[i] = t;
         }
         if (!grp->arrive()) return peer_failed(g);   // nobody overwrites vals before all have read them
@@ -393,10 +441,10 @@ struct LocalComm final : PartComm {
         const size_t W = grp->gs.size();
         {
             std::lock_guard<std::mutex> lk(grp->mu);
-            grp->vals[(size_t)rank * 4] = mine;
+            grp->vals[(size_t)rank * kPartRedMax] = mine;
         }
         if (!grp->arrive()) return peer_failed(g);
-        for (size_t q = 0; q < W; ++q) all[q] = grp->vals[q * 4];
+        for (size_t q = 0; q < W; ++q) all[q] = grp->vals[q * kPartRedMax];
         if (!grp->arrive()) return peer_failed(g);
         return FGI_OK;
     }
@@ -416,10 +464,69 @@ struct LocalComm final : PartComm {
         *n_recv = recv;
         return FGI_OK;
     }
+    // Stream-ordered copies between the group's graphs, no host wait: this rank's source is marked
+    // ready on its stream; once every rank has queued its mark (a host-thread barrier, no device
+    // synchronisation), each stream waits for the others' marks and copies; then each stream waits
+    // until every rank's copies are queued behind its own marks, so no source is overwritten early.
+    template <class F>
+    fgi_status exchange_async(fgi_graph* g, F copies) {
+        FGI_HIP(g, hipEventRecord(grp->ready[rank], g->stream));
+        if (!grp->arrive()) return peer_failed(g);
+        for (size_t q = 0; q < grp->gs.size(); ++q)
+            if (q != rank) FGI_HIP(g, hipStreamWaitEvent(g->stream, grp->ready[q], 0));
+        FGI_TRY(copies());
+        FGI_HIP(g, hipEventRecord(grp->done[rank], g->stream));
+        if (!grp->arrive()) return peer_failed(g);
+        for (size_t q = 0; q < grp->gs.size(); ++q)
+            if (q != rank) FGI_HIP(g, hipStreamWaitEvent(g->stream, grp->done[q], 0));
+        return FGI_OK;
+    }
+    fgi_status allgather_front_async(fgi_graph* g) override {
+        PartState* p = ps(g);
+        const uint64_t words = p->v.block / 32;
+        return exchange_async(g, [&]() -> fgi_status {
+            for (size_t q = 0; q < grp->gs.size(); ++q)
+                FGI_HIP(g, hipMemcpyAsync(p->v.front_global + q * words, grp->gs[q]->inv_bm, words * 4, hipMemcpyDefault,
+                                          g->stream));
+            return FGI_OK;
+        });
+    }
+    fgi_status alltoall_async(fgi_graph* g) override {
+        PartState* p = ps(g);
+        const uint64_t C = p->a2a_C;
+        return exchange_async(g, [&]() -> fgi_status {
+            for (size_t q = 0; q < grp->gs.size(); ++q)
+                FGI_HIP(g, hipMemcpyAsync(p->a2a_recv + q * C, ps(grp->gs[q])->a2a_send + (uint64_t)rank * C, C * 4,
+                                          hipMemcpyDefault, g->stream));
+            return FGI_OK;
+        });
+    }
 };
 
 fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent, uint64_t* glob) {
     return ps(g)->ops->exchange(g, n_recv, n_sent, glob);
+}
+
+fgi_status part_allgather_front_async(fgi_graph* g) {
+    PartState* p = ps(g);
+    ++p->front_full;
+    p->front_bytes += (uint64_t)(p->v.world - 1) * p->v.block / 8;
+    return p->ops->allgather_front_async(g);
+}
+
+fgi_status part_alltoall_async(fgi_graph* g) { return ps(g)->ops->alltoall_async(g); }
+
+fgi_status part_set_bucket(fgi_graph* g, int64_t words) {
+    PartState* p = ps(g);
+    if (!p) return set_err(g, FGI_ESTATE, "partition not initialised");
+    if (words < 0) return set_err(g, FGI_EINVAL, "bucket words must be >= 0");
+    p->a2a_C = words == 0 ? p->a2a_cap : (uint32_t)std::max<int64_t>(2, std::min<int64_t>(words, p->a2a_cap));
+    return FGI_OK;
+}
+
+PartBuckets part_buckets(fgi_graph* g) {
+    PartState* p = ps(g);
+    return PartBuckets{p->a2a_C, p->a2a_send, p->a2a_recv, p->a2a_cur, p->red};
 }
 
 namespace {
@@ -513,7 +620,7 @@ fgi_status part_front_stats(fgi_graph* g, uint64_t* full, uint64_t* delta, uint6
 }
 
 fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out, uint32_t count) {
-    if (count < 1 || count > 4) return set_err(g, FGI_EINVAL, "part_allreduce_sum: count %u", count);
+    if (count < 1 || count > kPartRedMax) return set_err(g, FGI_EINVAL, "part_allreduce_sum: count %u", count);
     return ps(g)->ops->allreduce_sum(g, dev_val, out, count);
 }
 
@@ -887,6 +994,17 @@ static fgi_status part_alloc(fgi_graph* g, uint32_t n_global) {
     if (hipHostMalloc(reinterpret_cast<void**>(&p->all_cnt_host), (size_t)W * (W + 2) * 8) != hipSuccess)
         return fail("host");
     if (hipHostMalloc(reinterpret_cast<void**>(&p->scalar_host), 32) != hipSuccess) return fail("host");
+    // planned waves: buckets of a2a_C words per peer (a push level's forwarded targets beyond that wait
+    // for the next push level); 64 K ids per peer moves (world - 1) * 256 KB per rank and level
+    p->a2a_C = p->a2a_cap = (uint32_t)std::min<uint64_t>(65536, (uint64_t)block + 1);
+    if (hipMalloc(&p->a2a_send, (size_t)W * p->a2a_C * 4) != hipSuccess ||
+        hipMalloc(&p->a2a_recv, (size_t)W * p->a2a_C * 4) != hipSuccess || hipMalloc(&p->a2a_cur, (size_t)W * 8) != hipSuccess ||
+        hipMalloc(&p->red, (size_t)kPartRedMax * 8) != hipSuccess)
+        return fail("planned-wave buffers");
+    if (hipMemset(p->a2a_send, 0, (size_t)W * p->a2a_C * 4) != hipSuccess ||
+        hipMemset(p->a2a_recv, 0, (size_t)W * p->a2a_C * 4) != hipSuccess)
+        return fail("planned-wave buffers");
+    if (hipHostMalloc(reinterpret_cast<void**>(&p->red_host), (size_t)kPartRedMax * 8) != hipSuccess) return fail("host");
     return FGI_OK;
 }
 

@@ -1486,9 +1486,12 @@ __global__ __launch_bounds__(kBlock, kLevelOcc) void k_level(int Larg, WaveParam
 }
 
 // multi-GPU: apply the targets other ranks forwarded (their versions were checked by the sender)
+// C > 0 (planned waves): recv holds n / (C - 1) buckets of C words, a count then up to C - 1 ids, and
+// entry i is id i % (C - 1) of bucket i / (C - 1), if within its count.
 __global__ __launch_bounds__(kBlock) void k_apply_recv(int L, uint64_t n, const uint32_t* __restrict__ recv, uint32_t base,
                                                        const unsigned long long* node, uint32_t* vis, Out o,
-                                                       WaveCtr* ctr, unsigned long long* blk, unsigned long long* done) {
+                                                       WaveCtr* ctr, unsigned long long* blk, unsigned long long* done,
+                                                       uint32_t C) {
     __shared__ unsigned long long s_st[kBlock / 64][kStats];
     __shared__ Emit em;
     __shared__ uint32_t eb[kEmitCap];
@@ -1501,8 +1504,15 @@ __global__ __launch_bounds__(kBlock) void k_apply_recv(int L, uint64_t n, const 
         const uint64_t i = it * stride + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
         bool win = false;
         uint32_t h = 0;
-        if (i < n) {
-            h = recv[i] - base;
+        bool in = i < n;
+        uint64_t at = i;
+        if (C && in) {
+            const uint64_t q = i / (C - 1), j = i % (C - 1);
+            in = j < recv[q * C];
+            at = q * C + 1 + j;
+        }
+        if (in) {
+            h = recv[at] - base;
             const unsigned long long w = node[h];
             if ((w & kVMask) != 0) {
                 const int r = visit_bit(vis, h, w);
@@ -1517,6 +1527,38 @@ __global__ __launch_bounds__(kBlock) void k_apply_recv(int L, uint64_t n, const 
     const uint32_t v[kStats] = {0, flagged, 0, 0, 0, 0, 0, 0};
     block_stats_add(blk, s_st, v);
     publish_ft(o.ln, done, gridDim.x);
+}
+
+// Planned multi-GPU waves: one block per owner q moves the next ids it forwarded to q (send_buf slice
+// q, cumulative over the wave: each target at most once, sent_bm) into bucket q of the fixed-size
+// all-to-all: the count, then up to C - 1 ids; the rest waits for the next push level's pack.
+__global__ __launch_bounds__(kBlock) void k_a2a_pack(uint32_t R, uint32_t C, const uint32_t* __restrict__ send_buf,
+                                                     uint32_t block, const unsigned long long* send_cnt,
+                                                     unsigned long long* cur, uint32_t* a2a_send) {
+    const uint32_t q = blockIdx.x;
+    const unsigned long long c0 = cur[q], tot = send_cnt[q];
+    const uint32_t n = q == R ? 0u : (uint32_t)std::min<unsigned long long>(tot - c0, (unsigned long long)(C - 1));
+    uint32_t* dst = a2a_send + (uint64_t)q * C;
+    for (uint32_t i = threadIdx.x; i < n; i += blockDim.x) dst[1 + i] = send_buf[(uint64_t)q * block + c0 + i];
+    if (threadIdx.x == 0) {
+        dst[0] = n;
+        cur[q] = c0 + n;
+    }
+}
+
+// The planned wave's closing all-reduce: red[0] the next level's local frontier, red[1] the forwarded
+// ids still waiting in send_buf, red[2 + 2l .. + 1] level l's local {F, T} (the next wave's plan).
+__global__ void k_part_tail(const WaveCtr* ctr, int K, uint32_t W, const unsigned long long* send_cnt,
+                            const unsigned long long* cur, unsigned long long* red) {
+    if (threadIdx.x != 0) return;
+    red[0] = lvl_F(ctr->lvl[K % kRing]);
+    unsigned long long pend = 0;
+    for (uint32_t q = 0; q < W; ++q) pend += send_cnt[q] - cur[q];
+    red[1] = pend;
+    for (int l = 0; l < K && l < kRing; ++l) {
+        red[2 + 2 * l] = lvl_F(ctr->lvl[l]);
+        red[3 + 2 * l] = lvl_T(ctr->lvl[l]);
+    }
 }
 
 // ---- final collect: the invalidated bitmap -> the invalidated list -----------------------------
@@ -2875,6 +2917,172 @@ fgi_status ensure_ids(fgi_graph* g) {
 // forwarded bound the winners they add, so F + sent >= the next frontier (0: the wave is done) and T
 // scales by the local edges per winner — direction is a cost choice, the result does not depend on
 // it. A level whose winners are all remote falls back to the all-reduce (termination is exact).
+// The plan's key: a plan follows the levels of the wave it was learnt from; any mutation or option
+// change since then starts a new one. Every rank computes it from its own calls, which are the same on
+// all ranks (the start all-reduce also checks that every rank can follow its plan).
+uint64_t part_plan_key(const fgi_graph* g) {
+    return (uint64_t)g->mut_epoch * 1000003ull ^ ((uint64_t)g->opt_direction << 56) ^ ((uint64_t)g->opt_pull_alpha << 40) ^
+           ((uint64_t)g->opt_pull_beta << 24) ^ ((uint64_t)g->opt_front_exchange << 20) ^ (uint64_t)g->uin_epoch;
+}
+
+// A planned partitioned wave (every rank follows the previous wave's directions, g->part_plan): the
+// levels' collectives are stream-ordered and fixed in size — a pull level all-gathers the whole
+// invalidated bitmap, a push level moves its forwarded targets in fixed-size buckets (what does not
+// fit waits for the next push level: a later visit of a node changes nothing, so the result is the
+// same) — so the host queues the whole plan and waits once, at a closing all-reduce of the next
+// frontier, the ids still waiting and every level's {F, T}. If that finds work left, push levels
+// follow, planned the same way, until none is left. The direction of a level is a cost choice:
+// results do not depend on the plan.
+static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveParams& wp, const PartBuckets& pb,
+                                   uint32_t n_roots, fgi_wave_stats* stats, std::chrono::steady_clock::time_point t0) {
+    hipStream_t s = g->stream;
+    const bool coll = pv.world > 1 || g->opt_part_coll;
+    const auto* node = reinterpret_cast<const unsigned long long*>(g->node);
+    const RemoteArgs ra{pv.base, pv.n_local, pv.block, pv.world, pv.ver_all, pv.sent_bm, pv.send_buf, pv.send_cnt};
+    const uint32_t* front = pv.front_global;
+    if (coll) {
+        FGI_HIP(g, hipMemsetAsync(pv.send_cnt, 0, (size_t)pv.world * 8, s));
+        FGI_HIP(g, hipMemsetAsync(pb.cur, 0, (size_t)pv.world * 8, s));
+    }
+    std::vector<uint8_t> plan = g->part_plan;
+    const bool timing = g->opt_level_timing != 0;
+    FGI_HIP(g, ensure_events(g, 2 * (size_t)kPlanMax + 2));
+    uint64_t syncs = 0, rounds = 0;
+    int L = 0;
+    std::vector<uint64_t> glob;
+    double pull_ms = 0, expand_ms = 0;
+    uint64_t pull_launches = 0, expand_launches = 0;
+    while (true) {
+        const int L0 = L;
+        for (size_t k = 0; k < plan.size() && L < (int)kPlanMax; ++k, ++L) {
+            const bool pull = plan[k] != 0;
+            const int buf = L & 1;
+            if (pull) {
+                FGI_HIP(g, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&g->ctr->lvl[L % kRing].pull), 1, 1, s));
+                if (coll) FGI_TRY(part_allgather_front_async(g));
+                else FGI_HIP(g, hipMemcpyAsync(pv.front_global, g->inv_bm, (size_t)pv.block / 32 * 4, hipMemcpyDeviceToDevice, s));
+            }
+            CollectArgs ca = collect_args(g, pv.n_local, wp, buf);
+            ca.inv = front;   // hot heads are global ids
+            ca.hot_bm = pv.front_global + g->hot_w0;
+            hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp, ca, ca,
+                               ~0ull);
+            if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L], s));
+            hipLaunchKernelGGL(k_level<true>, dim3(wp.grid), dim3(kBlock), 0, s, L, wp, expand_args(g, buf),
+                               expand_args(g, buf), pull_args(g, g->n_slots, front), node, g->vis_bm,
+                               out_for(g, buf ^ 1, nullptr), out_for(g, buf ^ 1, nullptr), g->ctr, g->blk_stats, g->done,
+                               ra, ~0ull);
+            if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L + 1], s));
+            if (!pull && coll) {
+                hipLaunchKernelGGL(k_a2a_pack, dim3(pv.world), dim3(kBlock), 0, s, pv.rank, pb.C, pv.send_buf, pv.block,
+                                   pv.send_cnt, pb.cur, pb.send);
+                FGI_TRY(part_alltoall_async(g));
+                const uint64_t n = (uint64_t)pv.world * (pb.C - 1);
+                hipLaunchKernelGGL(k_apply_recv, dim3(std::min<uint64_t>((n + kBlock - 1) / kBlock, (uint64_t)g->n_cu * 8)),
+                                   dim3(kBlock), 0, s, L, n, pb.recv, pv.base, node, g->vis_bm, out_for(g, buf ^ 1, nullptr),
+                                   g->ctr, g->blk_stats, g->done, pb.C);
+            }
+            FGI_HIP(g, hipGetLastError());
+        }
+        // the final collect may be repeated if the wave goes on (it only reads the invalidated bitmap)
+        FGI_HIP(g, launch_final(g, pv.n_local));
+        FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
+        const int K = L;
+        const uint32_t cnt = 2 + 2 * (uint32_t)std::min(K, (int)((kPartRedMax - 2) / 2));
+        hipLaunchKernelGGL(k_part_tail, dim3(1), dim3(64), 0, s, g->ctr, K, coll ? pv.world : 0u, pv.send_cnt, pb.cur,
+                           pb.red);
+        glob.assign(cnt, 0);
+        FGI_TRY(part_allreduce_sum(g, pb.red, glob.data(), cnt));   // the wave's one host synchronisation
+        ++syncs;
+        ++rounds;
+        if (timing)
+            for (int l = L0; l < L; ++l) {
+                float ms = 0;
+                if (hipEventElapsedTime(&ms, g->ev[2 * l], g->ev[2 * l + 1]) != hipSuccess) continue;
+                if (g->ctr_host->lvl[l % kRing].pull) {
+                    pull_ms += ms;
+                    ++pull_launches;
+                } else {
+                    expand_ms += ms;
+                    ++expand_launches;
+                }
+            }
+        if (glob[0] == 0 && glob[1] == 0) break;
+        if (L >= (int)kPlanMax || rounds > 64) return set_err(g, FGI_EDEVICE, "planned partitioned wave: no end in sight");
+        plan.assign(2, 0);   // work left (a longer wave than the plan, or ids waiting): push levels
+    }
+    FGI_HIP(g, hipEventRecord(g->ev_w1, s));
+    FGI_HIP(g, hipEventSynchronize(g->ev_w1));
+    // the next wave's plan: Beamer's rules over this wave's global levels (as the host-driven loop
+    // decides them), computed alike on every rank from the all-reduced {F, T}
+    {
+        const int K = std::min(L, (int)((kPartRedMax - 2) / 2));
+        std::vector<uint8_t> next;
+        bool last_pull = false;
+        const bool allow_pull = g->part_plan_pull;
+        for (int l = 0; l < K; ++l) {
+            const uint64_t F = glob[2 + 2 * l], T = glob[3 + 2 * l];
+            if (F == 0) break;
+            const bool pull = allow_pull && T != 0 &&
+                              (wp.direction == 2 ||
+                               (wp.direction == 0 && (T > wp.pull_threshold || (last_pull && F > wp.stay_pull_f))));
+            next.push_back(pull ? 1 : 0);
+            last_pull = pull;
+        }
+        if (!next.empty()) g->part_plan = next;
+    }
+    const WaveCtr& c = *g->ctr_host;
+    g->last_wave_n = c.inv;
+    g->ids_valid = true;
+    if (stats) {
+        uint64_t levels = 0, e_trav = 0, f_total = 0, push_edges = 0, push_f = 0, pull_levels = 0;
+        for (int l = 0; l < L && l < kRing; ++l) {
+            const LevelCtr& lc = c.lvl[l];
+            const uint64_t F = lvl_F(lc), T = lvl_T(lc);
+            if (lc.pull) ++pull_levels;
+            if (!F) continue;
+            ++levels;
+            e_trav += T;
+            f_total += F;
+            if (!lc.pull) {
+                push_edges += T;
+                push_f += F;
+            }
+        }
+        uint64_t sent_total = 0;
+        if (coll) {
+            std::vector<unsigned long long> sc(pv.world, 0);
+            FGI_HIP(g, hipMemcpy(sc.data(), pv.send_cnt, (size_t)pv.world * 8, hipMemcpyDeviceToHost));
+            for (uint32_t q = 0; q < pv.world; ++q) sent_total += sc[q];
+        }
+        const uint64_t v = c.inv;
+        stats->roots += n_roots;
+        stats->levels += levels;
+        stats->v_inv += v;
+        stats->e_trav += e_trav;
+        stats->e_match += c.e_match;
+        stats->n_flagged += c.n_flagged;
+        stats->remote_msgs += sent_total;
+        const uint64_t pull_b = pull_level_bytes(c);
+        stats->alg_bytes += 20 * push_edges + 40 * push_f + pull_b + 4 * v + 8 * sent_total + 5ull * n_roots;
+        stats->pull_levels += pull_levels;
+        stats->pull_edges += c.pull_edges;
+        stats->pull_ms += pull_ms;
+        stats->pull_bytes += pull_b;
+        stats->pull_launches += pull_launches;
+        float wave_ms = 0;
+        hipEventElapsedTime(&wave_ms, g->ev_w0, g->ev_w1);
+        stats->kernel_ms += wave_ms;
+        stats->expand_ms += expand_ms;
+        stats->expand_launches += expand_launches;
+        stats->expand_bytes += 20 * push_edges + 40 * push_f;
+        stats->f_total += f_total;
+        stats->host_syncs += syncs + (coll ? 1 : 0);   // + the start all-reduce
+        stats->total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return FGI_OK;
+}
+
 fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                          fgi_wave_stats* stats) {
     PartView pv;
@@ -2903,16 +3111,34 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     if (imm_dev && n_roots) note_words(g);
     FGI_HIP(g, hipGetLastError());
     const auto* node = reinterpret_cast<const unsigned long long*>(g->node);
-    // one all-reduce of {local edges, level-0 frontier, its edges, ranks without pull lists}
+    // one all-reduce of {local edges, level-0 frontier, its edges, ranks without pull lists, ranks
+    // that can follow the previous wave's plan}
     const WaveParams wp0 = wave_params(g, 1, g->opt_direction, g->pool_top, pv.n_global);
     const bool can_pull = wp0.direction != 1 && pull_ready(g, wp0);
-    const uint64_t head = g->pool_top, tail = can_pull ? 0ull : 1ull;
-    FGI_HIP(g, hipMemcpyAsync(pv.scratch_u64, &head, 8, hipMemcpyHostToDevice, s));
-    FGI_HIP(g, hipMemcpyAsync(pv.scratch_u64 + 1, &g->ctr->lvl[0].F, 16, hipMemcpyDeviceToDevice, s));
-    FGI_HIP(g, hipMemcpyAsync(pv.scratch_u64 + 3, &tail, 8, hipMemcpyHostToDevice, s));
-    uint64_t sums[4] = {0, 0, 0, 0};
-    FGI_TRY(part_allreduce_sum(g, pv.scratch_u64, sums, 4));
+    const PartBuckets pb = part_buckets(g);
+    const uint64_t key = part_plan_key(g);
+    // (a plan learnt while some rank had no pull lists stays valid only while this rank has none either:
+    // a rank whose lists appeared since votes no, and the wave learns a new plan)
+    const bool plan_ok = g->opt_part_plan && !g->part_plan.empty() && g->opt_front_exchange != 2 &&
+                         g->part_plan_key == key && (can_pull || !g->part_plan_pull);
+    uint64_t sums[5] = {0, 0, 0, 0, 0};
+    if (!coll && plan_ok) {
+        // one rank without collectives: nothing to agree on (the plan is this rank's own)
+        sums[0] = g->pool_top;
+        sums[4] = 1;
+    } else {
+        const uint64_t head[1] = {g->pool_top}, tail[2] = {can_pull ? 0ull : 1ull, plan_ok ? 1ull : 0ull};
+        FGI_HIP(g, hipMemcpyAsync(pb.red, head, 8, hipMemcpyHostToDevice, s));
+        FGI_HIP(g, hipMemcpyAsync(pb.red + 1, &g->ctr->lvl[0].F, 16, hipMemcpyDeviceToDevice, s));
+        FGI_HIP(g, hipMemcpyAsync(pb.red + 3, tail, 16, hipMemcpyHostToDevice, s));
+        FGI_TRY(part_allreduce_sum(g, pb.red, sums, 5));
+    }
     const WaveParams wp = wave_params(g, 1, g->opt_direction, sums[0], pv.n_global);
+    if (sums[4] == pv.world)   // every rank follows the plan: no host synchronisation until the wave's end
+        return run_part_planned(g, pv, wp, pb, n_roots, stats, t0);
+    g->part_plan.clear();      // learnt again by this wave's levels
+    g->part_plan_key = key;
+    g->part_plan_pull = sums[3] == 0;   // every rank's pull lists were ready (the same on all ranks)
     const uint64_t stay_pull_f = wp.stay_pull_f;
     const bool allow_pull = sums[3] == 0;
     const int direction = wp.direction;
@@ -2925,6 +3151,7 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     const double avg_deg = (double)sums[0] / std::max<uint64_t>(1, pv.n_global);
     uint64_t levels = 0, e_trav = 0, f_total = 0, sent_total = 0, push_edges = 0, push_f = 0;
     uint64_t pull_levels = 0, pull_launches = 0, expand_launches = 0;
+    uint64_t syncs = 1;   // the start's all-reduce
     double expand_ms = 0, pull_ms = 0;
     int L = 0;
     bool last_pull = false;
@@ -2932,14 +3159,22 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
         const bool pull = allow_pull && t_global != 0 &&
                           (direction == 2 || (direction == 0 && (t_global > wp.pull_threshold ||
                                                                  (last_pull && f_global > stay_pull_f))));
+        if (g->part_plan.size() < kPlanMax) g->part_plan.push_back(pull ? 1 : 0);
         const int buf = L & 1;
         if (coll) FGI_HIP(g, hipMemsetAsync(pv.send_cnt, 0, (size_t)pv.world * 8, s));
         // the level's direction for its kernels: the flag's high word is zero (the ring slot was
         // cleared two levels ago or at wave start), so a 32-bit device-side set is the whole store
         if (pull) {
             FGI_HIP(g, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&g->ctr->lvl[L % kRing].pull), 1, 1, s));
-            if (coll) FGI_TRY(part_allgather_front(g));
-            else FGI_HIP(g, hipMemcpyAsync(pv.front_global, g->inv_bm, (size_t)pv.block / 32 * 4, hipMemcpyDeviceToDevice, s));
+            if (coll) {
+                uint64_t f0 = 0, d0 = 0, d1 = 0, b = 0;
+                FGI_TRY(part_front_stats(g, &f0, &d0, &b));
+                FGI_TRY(part_allgather_front(g));
+                FGI_TRY(part_front_stats(g, &f0, &d1, &b));
+                syncs += g->opt_front_exchange != 1 ? 1 : 0;   // the delta count's read-back (auto or delta)
+            } else {
+                FGI_HIP(g, hipMemcpyAsync(pv.front_global, g->inv_bm, (size_t)pv.block / 32 * 4, hipMemcpyDeviceToDevice, s));
+            }
         }
         CollectArgs ca = collect_args(g, pv.n_local, wp, buf);
         ca.inv = front;   // hot heads are global ids
@@ -2964,9 +3199,10 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
         if (n_recv)
             hipLaunchKernelGGL(k_apply_recv, dim3(std::min<uint64_t>((n_recv + kBlock - 1) / kBlock, (uint64_t)g->n_cu * 8)),
                                dim3(kBlock), 0, s, L, n_recv, pv.recv_buf, pv.base, node, g->vis_bm,
-                               out_for(g, buf ^ 1, nullptr), g->ctr, g->blk_stats, g->done);
+                               out_for(g, buf ^ 1, nullptr), g->ctr, g->blk_stats, g->done, 0u);
         FGI_HIP(g, hipGetLastError());
         sent_total += n_sent;
+        ++syncs;   // the level's count all-gather or all-reduce
         // every winner remote (the wave's tail): whether the received targets add any is known only
         // after they are applied, so the exact all-reduce decides termination (no empty level)
         if (exch && (glob[0] != 0 || glob[2] == 0)) {
@@ -3017,6 +3253,7 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
         stats->e_match += c.e_match;
         stats->n_flagged += c.n_flagged;
         stats->remote_msgs += sent_total;
+        stats->host_syncs += syncs + 1;   // + the final collect's
         // as run_wave, plus 8 B per forwarded target (written + received)
         const uint64_t pull_b = pull_level_bytes(c);
         stats->alg_bytes += 20 * push_edges + 40 * push_f + pull_b + 4 * v + 8 * sent_total + 5ull * n_roots;

@@ -26,6 +26,8 @@ OPT_FRONT_EXCHANGE = 9
 OPT_HOT_HEADS = 10
 OPT_FAULT_INJECT = 11
 OPT_FUSED = 12
+OPT_PART_PLAN = 13
+OPT_PART_BUCKET = 14
 DIR_AUTO, DIR_PUSH, DIR_PULL = 0, 1, 2
 NONE = 0xFFFFFFFF
 COMPUTING, CONSISTENT, INVALIDATED = 0, 1, 2

@@ -195,7 +195,8 @@ def test_batch_barrier_timeout_poisons_until_restore(pkg, gpu_available, skip, b
     fails the batch with FGI_EDEVICE; the graph then refuses every call with FGI_ESTATE until
     fgi_restore, after which the same batch (detached handles included) matches the oracle, and so
     does a second one. skip = 1: the fault is in the batch's second cascade (the first, a displacement
-    cascade, has completed and detached the delayed leaves it displaced)."""
+    cascade, has completed and detached the delayed leaves it displaced). The invalidated hubs and the
+    displaced leaves lie in disjoint parts of the graph, so the step order does not change the result."""
     fgi = pkg.fgi
     mix = _mix(pkg, 48, 120, 6, 20, 0x5EED00E0)
     n = mix.n
@@ -208,9 +209,12 @@ def test_batch_barrier_timeout_poisons_until_restore(pkg, gpu_available, skip, b
     assert len(delayed) > 0
     vd = (mix.version[delayed] + np.uint64(2)).astype(np.uint64)
     roots = hubs[2:]
-    steps = [("begin_compute", delayed, vd, np.ones(len(delayed), np.uint8)),   # displaced + detached
-             ("invalidate", roots),
-             ("set_output", delayed)]
+    bc = ("begin_compute", delayed, vd, np.ones(len(delayed), np.uint8))   # displaced + detached
+    # skip = 0: the fault hits the batch's first cascade, which must have roots on the host's side (a
+    # displacement cascade of delayed nodes has none: they only start their delay, without a launch)
+    steps = [bc, ("invalidate", roots)] if skip else [("invalidate", roots), bc]
+    steps.append(("set_output", delayed))
+    i_bc = 0 if skip else 1
     g.set_option(fgi.OPT_FAULT_INJECT, (skip << 16) | block)
     with pytest.raises(fgi.FgiError) as e:
         g.run_batch(steps)
@@ -233,7 +237,7 @@ def test_batch_barrier_timeout_poisons_until_restore(pkg, gpu_available, skip, b
     for s_ in delayed:
         assert o.set_output(o.last(int(s_))) == 1
     assert np.array_equal(ids, np.sort(w).astype(np.uint32))
-    assert np.all(outs[0] != fgi.NONE)      # every displaced delayed leaf was detached
+    assert np.all(outs[i_bc] != fgi.NONE)   # every displaced delayed leaf was detached
     assert np.all(outs[2] == 1)
     assert_states_equal(g, o, n)
     # a second batch on the recovered graph
