@@ -1547,17 +1547,18 @@ __global__ __launch_bounds__(kBlock) void k_a2a_pack(uint32_t R, uint32_t C, con
 }
 
 // The planned wave's closing all-reduce: red[0] the next level's local frontier, red[1] the forwarded
-// ids still waiting in send_buf, red[2 + 2l .. + 1] level l's local {F, T} (the next wave's plan).
-__global__ void k_part_tail(const WaveCtr* ctr, int K, uint32_t W, const unsigned long long* send_cnt,
-                            const unsigned long long* cur, unsigned long long* red) {
+// ids still waiting in send_buf, red[2 + 2l .. + 1] level L0 + l's local {F, T}, l < K (the next
+// wave's plan).
+__global__ void k_part_tail(const WaveCtr* ctr, int L0, int L, uint32_t W, const unsigned long long* send_cnt,
+                            const unsigned long long* cur, unsigned long long* red, int K) {
     if (threadIdx.x != 0) return;
-    red[0] = lvl_F(ctr->lvl[K % kRing]);
+    red[0] = lvl_F(ctr->lvl[L % kRing]);
     unsigned long long pend = 0;
     for (uint32_t q = 0; q < W; ++q) pend += send_cnt[q] - cur[q];
     red[1] = pend;
-    for (int l = 0; l < K && l < kRing; ++l) {
-        red[2 + 2 * l] = lvl_F(ctr->lvl[l]);
-        red[3 + 2 * l] = lvl_T(ctr->lvl[l]);
+    for (int l = 0; l < K; ++l) {
+        red[2 + 2 * l] = lvl_F(ctr->lvl[(L0 + l) % kRing]);
+        red[3 + 2 * l] = lvl_T(ctr->lvl[(L0 + l) % kRing]);
     }
 }
 
@@ -2949,14 +2950,16 @@ static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveP
     FGI_HIP(g, ensure_events(g, 2 * (size_t)kPlanMax + 2));
     uint64_t syncs = 0, rounds = 0;
     int L = 0;
-    std::vector<uint64_t> glob;
+    std::vector<uint64_t> glob, plan_ft;
     double pull_ms = 0, expand_ms = 0;
     uint64_t pull_launches = 0, expand_launches = 0;
+    uint64_t levels = 0, e_trav = 0, f_total = 0, push_edges = 0, push_f = 0, pull_levels = 0;
     while (true) {
         const int L0 = L;
-        for (size_t k = 0; k < plan.size() && L < (int)kPlanMax; ++k, ++L) {
+        for (size_t k = 0; k < plan.size(); ++k, ++L) {
             const bool pull = plan[k] != 0;
             const int buf = L & 1;
+            const int e = 2 * (L - L0);
             if (pull) {
                 FGI_HIP(g, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&g->ctr->lvl[L % kRing].pull), 1, 1, s));
                 if (coll) FGI_TRY(part_allgather_front_async(g));
@@ -2967,12 +2970,12 @@ static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveP
             ca.hot_bm = pv.front_global + g->hot_w0;
             hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp, ca, ca,
                                ~0ull);
-            if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L], s));
+            if (timing) FGI_HIP(g, hipEventRecord(g->ev[e], s));
             hipLaunchKernelGGL(k_level<true>, dim3(wp.grid), dim3(kBlock), 0, s, L, wp, expand_args(g, buf),
                                expand_args(g, buf), pull_args(g, g->n_slots, front), node, g->vis_bm,
                                out_for(g, buf ^ 1, nullptr), out_for(g, buf ^ 1, nullptr), g->ctr, g->blk_stats, g->done,
                                ra, ~0ull);
-            if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L + 1], s));
+            if (timing) FGI_HIP(g, hipEventRecord(g->ev[e + 1], s));
             if (!pull && coll) {
                 hipLaunchKernelGGL(k_a2a_pack, dim3(pv.world), dim3(kBlock), 0, s, pv.rank, pb.C, pv.send_buf, pv.block,
                                    pv.send_cnt, pb.cur, pb.send);
@@ -2987,41 +2990,55 @@ static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveP
         // the final collect may be repeated if the wave goes on (it only reads the invalidated bitmap)
         FGI_HIP(g, launch_final(g, pv.n_local));
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
-        const int K = L;
-        const uint32_t cnt = 2 + 2 * (uint32_t)std::min(K, (int)((kPartRedMax - 2) / 2));
-        hipLaunchKernelGGL(k_part_tail, dim3(1), dim3(64), 0, s, g->ctr, K, coll ? pv.world : 0u, pv.send_cnt, pb.cur,
-                           pb.red);
+        // the first round's levels decide the next wave's plan: their {F, T} ride on the all-reduce
+        const int K = rounds == 0 ? L - L0 : 0;
+        const uint32_t cnt = 2 + 2 * (uint32_t)K;
+        hipLaunchKernelGGL(k_part_tail, dim3(1), dim3(64), 0, s, g->ctr, L0, L, coll ? pv.world : 0u, pv.send_cnt, pb.cur,
+                           pb.red, K);
         glob.assign(cnt, 0);
         FGI_TRY(part_allreduce_sum(g, pb.red, glob.data(), cnt));   // the wave's one host synchronisation
+        if (rounds == 0) plan_ft.assign(glob.begin() + 2, glob.end());
         ++syncs;
         ++rounds;
-        if (timing)
-            for (int l = L0; l < L; ++l) {
-                float ms = 0;
-                if (hipEventElapsedTime(&ms, g->ev[2 * l], g->ev[2 * l + 1]) != hipSuccess) continue;
-                if (g->ctr_host->lvl[l % kRing].pull) {
-                    pull_ms += ms;
-                    ++pull_launches;
-                } else {
-                    expand_ms += ms;
-                    ++expand_launches;
+        for (int l = L0; l < L; ++l) {   // the round's levels (a round has at most kPlanMax < kRing)
+            const LevelCtr& lc = g->ctr_host->lvl[l % kRing];
+            const uint64_t F = lvl_F(lc), T = lvl_T(lc);
+            if (lc.pull) ++pull_levels;
+            if (F) {
+                ++levels;
+                e_trav += T;
+                f_total += F;
+                if (!lc.pull) {
+                    push_edges += T;
+                    push_f += F;
                 }
             }
+            float ms = 0;
+            if (!timing || hipEventElapsedTime(&ms, g->ev[2 * (l - L0)], g->ev[2 * (l - L0) + 1]) != hipSuccess) continue;
+            if (lc.pull) {
+                pull_ms += ms;
+                ++pull_launches;
+            } else {
+                expand_ms += ms;
+                ++expand_launches;
+            }
+        }
         if (glob[0] == 0 && glob[1] == 0) break;
-        if (L >= (int)kPlanMax || rounds > 64) return set_err(g, FGI_EDEVICE, "planned partitioned wave: no end in sight");
-        plan.assign(2, 0);   // work left (a longer wave than the plan, or ids waiting): push levels
+        // work left (a longer wave than the plan, or ids waiting in send_buf): push levels; each moves
+        // at least one waiting id per peer, so the wave ends
+        if (rounds > (1u << 20)) return set_err(g, FGI_EDEVICE, "planned partitioned wave: no end in sight");
+        plan.assign(16, 0);
     }
     FGI_HIP(g, hipEventRecord(g->ev_w1, s));
     FGI_HIP(g, hipEventSynchronize(g->ev_w1));
     // the next wave's plan: Beamer's rules over this wave's global levels (as the host-driven loop
     // decides them), computed alike on every rank from the all-reduced {F, T}
     {
-        const int K = std::min(L, (int)((kPartRedMax - 2) / 2));
         std::vector<uint8_t> next;
         bool last_pull = false;
         const bool allow_pull = g->part_plan_pull;
-        for (int l = 0; l < K; ++l) {
-            const uint64_t F = glob[2 + 2 * l], T = glob[3 + 2 * l];
+        for (size_t l = 0; 2 * l + 1 < plan_ft.size() && next.size() < kPlanMax; ++l) {
+            const uint64_t F = plan_ft[2 * l], T = plan_ft[2 * l + 1];
             if (F == 0) break;
             const bool pull = allow_pull && T != 0 &&
                               (wp.direction == 2 ||
@@ -3035,20 +3052,6 @@ static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveP
     g->last_wave_n = c.inv;
     g->ids_valid = true;
     if (stats) {
-        uint64_t levels = 0, e_trav = 0, f_total = 0, push_edges = 0, push_f = 0, pull_levels = 0;
-        for (int l = 0; l < L && l < kRing; ++l) {
-            const LevelCtr& lc = c.lvl[l];
-            const uint64_t F = lvl_F(lc), T = lvl_T(lc);
-            if (lc.pull) ++pull_levels;
-            if (!F) continue;
-            ++levels;
-            e_trav += T;
-            f_total += F;
-            if (!lc.pull) {
-                push_edges += T;
-                push_f += F;
-            }
-        }
         uint64_t sent_total = 0;
         if (coll) {
             std::vector<unsigned long long> sc(pv.world, 0);
