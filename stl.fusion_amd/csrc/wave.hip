@@ -3003,9 +3003,12 @@ static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveP
         for (int l = L0; l < L; ++l) {   // the round's levels (a round has at most kPlanMax < kRing)
             const LevelCtr& lc = g->ctr_host->lvl[l % kRing];
             const uint64_t F = lvl_F(lc), T = lvl_T(lc);
-            if (lc.pull) ++pull_levels;
+            // a level counts as the host-driven loop counts it: if any rank had a frontier (round 0: the
+            // all-reduced F; later rounds, push levels: this rank's); a plan's surplus levels do not
+            const bool ran = rounds == 1 ? plan_ft[2 * (l - L0)] != 0 : F != 0;
+            if (lc.pull && ran) ++pull_levels;
+            if (ran) ++levels;
             if (F) {
-                ++levels;
                 e_trav += T;
                 f_total += F;
                 if (!lc.pull) {
