@@ -341,14 +341,14 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *                            it from the graph (65,536-262,144); n > 0 caps it at n rounded up to 256,
  *                            so the other heads are probed in the invalidated bitmap itself (tests pin
  *                            that path on small graphs; results never depend on it)
- *   FGI_OPT_FUSED       [1]  waves whose directions are settled (pull lists ready, or push only) run
- *                            their roots and small push levels inside two persistent launches and only
- *                            the pull levels (and push levels over one round of the fused grid) as
- *                            separate launches, with one host synchronisation; 0 runs
- *                            every level as launches in groups. Tests add 2 (no prediction of the
- *                            launches: extra rounds), 4 (every push level as its own launch) or 8
- *                            (every push level in the fused grid); the environment's FGI_FUSED=0
- *                            makes 0 the default
+ *   FGI_OPT_FUSED       [0]  1: waves whose directions are settled (pull lists ready, or push only)
+ *                            run their roots and small push levels inside two persistent launches and
+ *                            only the pull levels (and push levels over one round of the fused grid)
+ *                            as separate launches, with one host synchronisation (DESIGN.md §3;
+ *                            measured slower than the default level groups on MI355X). Tests add 2
+ *                            (no prediction of the launches: extra rounds), 4 (every push level as its
+ *                            own launch) or 8 (every push level in the fused grid); the environment's
+ *                            FGI_FUSED=1 makes 1 the default
  *   FGI_OPT_PART_PLAN   [1]  partitions: a wave follows the previous wave's directions (when every
  *                            rank can) and queues all its levels' collectives at fixed sizes, with one
  *                            host synchronisation at its end (two with remote ranks: the start's

@@ -219,10 +219,12 @@ struct PartWave {
 // FGI_OPT_FUSED bits: fused waves on; tests: no mid-pair prediction (every k_level level found by an
 // extra round), every push level as a k_level launch, every push level in the fused grid
 constexpr int kFusedOn = 1, kFusedNoPredict = 2, kFusedMidPush = 4, kFusedTailPush = 8;
-// FGI_FUSED=0 in the environment: waves as level groups by default (measurement of the older path)
+// Fused waves are off by default: on MI355X they measured slower than the level groups (DESIGN.md
+// §3: a grid barrier's cache maintenance costs what a launch does, and the fused grid runs the push
+// levels' dependent round trips with fewer blocks). FGI_FUSED=1 in the environment turns them on.
 inline int fused_default() {
     const char* e = getenv("FGI_FUSED");
-    return (e && e[0] == '0') ? 0 : kFusedOn;
+    return (e && e[0] == '1') ? kFusedOn : 0;
 }
 
 // ---- host-side graph object -------------------------------------------------------------------

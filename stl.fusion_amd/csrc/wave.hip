@@ -1688,6 +1688,7 @@ struct CoopArgs {
     unsigned long long* abort_w;       // the same word, set (kAbortBarrier) when a grid barrier times out
     uint64_t bar_timeout;              // grid barrier timeout, 100 MHz ticks
     uint32_t fault_block;              // fault injection: block fault_block - 1 skips its first barrier
+    int bar_mode;                      // soft_grid_sync's memory ordering (FGI_BAR_MODE)
     unsigned long long* gbar;          // plain launch: the grid barrier's arrival counter (monotonic)
     int one_round;                     // chunk size by level_mult_one_round (FGI_COOP_CHUNKS=0: level_mult)
 };
@@ -1708,14 +1709,19 @@ struct CoopArgs {
 // FGI_EDEVICE and poisons the graph until fgi_restore (graph.hip).
 // skip (fault injection, FGI_OPT_FAULT_INJECT): this block leaves without arriving, as a block that
 // is never resident would never arrive.
+// mode (measurement, FGI_BAR_MODE): 0 every thread fences (agent scope, seq_cst) on both sides; 1 the
+// block's stores are ordered by its block barrier and one wave (thread 0) makes them visible with an
+// agent-scope release fence before it arrives and an acquire fence after its wait (the L2 write-back
+// and invalidate are per XCD and the L1 per CU, so one wave's fences serve the block).
 constexpr uint64_t kGridBarTimeout = 200000000ull;
 __device__ __forceinline__ bool soft_grid_sync(unsigned long long* cnt, unsigned long long* broken,
-                                               unsigned long long* abort_w, uint64_t timeout, bool skip) {
+                                               unsigned long long* abort_w, uint64_t timeout, bool skip, int mode = 0) {
     __shared__ int s_ok;
     if (skip) return false;   // block-uniform
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    if (mode == 0) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
     __syncthreads();
     if (threadIdx.x == 0) {
+        if (mode != 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         const unsigned long long arrived = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned long long target = (arrived / gridDim.x + 1) * gridDim.x;
         const uint64_t t0 = wall_clock64();
@@ -1733,10 +1739,11 @@ __device__ __forceinline__ bool soft_grid_sync(unsigned long long* cnt, unsigned
                 break;
             }
         }
+        if (mode != 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         s_ok = ok;
     }
     __syncthreads();
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    if (mode == 0) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
     return s_ok != 0;
 }
 
@@ -1748,7 +1755,7 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
         if constexpr (SOFT) {
             const bool skip = a.fault_block != 0 && n_sync == 0 && blockIdx.x + 1 == a.fault_block;
             ++n_sync;
-            return soft_grid_sync(a.gbar, a.acc + kAccBarrier, a.abort_w, a.bar_timeout, skip);
+            return soft_grid_sync(a.gbar, a.acc + kAccBarrier, a.abort_w, a.bar_timeout, skip, a.bar_mode);
         } else {
             cooperative_groups::this_grid().sync();
             return true;
@@ -1982,6 +1989,8 @@ struct FusedArgs {
     unsigned long long* gbar;          // grid-barrier arrival counter (monotonic; g->gbar + kGbarFused)
     unsigned long long* done;          // completion counters (last_block)
     uint64_t bar_timeout;
+    int bar_mode;                      // soft_grid_sync's memory ordering (FGI_BAR_MODE)
+    int do_init;                       // the head clears the wave state itself (else k_wave_init ran before)
     WaveParams wp;
     CollectArgs col;
     uint64_t big_push;                 // push levels with more edges run as k_level launches
@@ -2001,11 +2010,14 @@ __global__ __launch_bounds__(kBlock) void k_wave_fused(FusedArgs a) {
     __shared__ unsigned long long s_red[kBlock / 64];
     __shared__ unsigned long long s_ft;
     WaveCtr* ctr = a.ctr;
-    auto grid_sync = [&]() -> bool { return soft_grid_sync(a.gbar, &ctr->broken, nullptr, a.bar_timeout, false); };
+    auto grid_sync = [&]() -> bool {
+        return soft_grid_sync(a.gbar, &ctr->broken, nullptr, a.bar_timeout, false, a.bar_mode);
+    };
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
     int L = 0;
     if constexpr (!TAIL) {
+      if (a.do_init) {
         // the wave's counters (broken too: nothing can have set it before the first barrier), the
         // per-block statistics, the invalidated bitmap and the hot snapshot past it, the visit bitmap
         unsigned long long* c64 = reinterpret_cast<unsigned long long*>(ctr);
@@ -2020,6 +2032,7 @@ __global__ __launch_bounds__(kBlock) void k_wave_fused(FusedArgs a) {
             for (uint64_t i = a.bm_words / 4 * 4 + tid; i < a.bm_words; i += nthr) a.vis[i] = 0u;
         }
         if (!grid_sync()) return;
+      }
         const Out o0{a.row_off, a.row_len, a.inv_bm, a.fr_off[0], a.fr_len[0], a.escan[0], a.cstart[0], &ctr->lvl[0]};
         const uint32_t gsize = gridDim.x * blockDim.x;
         if (a.imm) {   // Invalidate(true) roots first: their CAS may change node words
@@ -2370,6 +2383,15 @@ void print_coop_probe() {
 }
 #endif
 
+// soft_grid_sync's memory ordering (FGI_BAR_MODE, measurement; default 1: one wave per block fences)
+static int bar_mode() {
+    static const int m = [] {
+        const char* e = getenv("FGI_BAR_MODE");
+        return e ? atoi(e) : 1;
+    }();
+    return m;
+}
+
 // FGI_COOP_LAUNCH=1: k_wave_coop as a cooperative launch (grid barriers by the device library)
 // instead of a plain launch with soft_grid_sync. Nothing else launches cooperatively.
 bool coop_launch_mode() {
@@ -2443,6 +2465,7 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
     a.abort = abort;
     a.abort_w = abort;
     a.gbar = g->gbar;
+    a.bar_mode = bar_mode();
     // fault injection (FGI_OPT_FAULT_INJECT, tests): after fault_skip more cascade launches, one block
     // of the cascade leaves at its first barrier without arriving; the others give up after 20 ms
     uint32_t fb = 0;
@@ -2517,6 +2540,14 @@ namespace {
 
 // FGI_FUSED_BLOCKS: the fused kernels' grid (default one block per CU; measurement)
 
+bool fused_init_in_head() {
+    static const bool h = [] {
+        const char* e = getenv("FGI_FUSED_INIT");
+        return e && e[0] == '1';
+    }();
+    return h;
+}
+
 uint32_t fused_grid(const fgi_graph* g) {
     static const uint32_t env = [] {
         const char* e = getenv("FGI_FUSED_BLOCKS");
@@ -2579,6 +2610,8 @@ static fgi_status run_wave_fused(fgi_graph* g, uint32_t n_roots, const uint32_t*
     a.gbar = g->gbar + kGbarFused;
     a.done = g->done;
     a.bar_timeout = kGridBarTimeout;
+    a.bar_mode = bar_mode();
+    a.do_init = fused_init_in_head() ? 1 : 0;
     a.wp = wp;
     a.col = collect_args(g, g->n_slots, wp, 0);   // frontier buffers chosen per level on the device
     a.big_push = (uint64_t)G * kChunk;            // one round of the largest chunks over the grid
@@ -2596,6 +2629,9 @@ static fgi_status run_wave_fused(fgi_graph* g, uint32_t n_roots, const uint32_t*
     hipEvent_t* ev = g->ev.data();
     const size_t eh = 2 * (size_t)kMidMax;   // the head's / tail's event pair
     if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
+    if (!a.do_init)   // the wave state cleared by its own launch: the head's first barrier has no dirty 4 MB
+        hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
+                           a.clear_vis ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
     if (timing) FGI_HIP(g, hipEventRecord(ev[eh], s));
     hipLaunchKernelGGL(k_wave_fused<false>, dim3(G), dim3(kBlock), 0, s, a);
     if (timing) FGI_HIP(g, hipEventRecord(ev[eh + 1], s));
