@@ -2800,7 +2800,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     int L = 0;
     uint64_t levels = 0, e_trav = 0, f_total = 0, pull_levels = 0;
     double expand_ms = 0, pull_ms = 0;
-    uint64_t expand_launches = 0, expand_edges = 0, expand_f = 0, pull_launches = 0;
+    uint64_t expand_launches = 0, expand_edges = 0, expand_f = 0, pull_launches = 0, syncs = 0;
     bool done = (n_roots == 0);
     bool final_done = false;
     while (!done) {
@@ -2830,6 +2830,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
         FGI_HIP(g, hipStreamSynchronize(s));
+        ++syncs;
         for (int l = L0; l < L; ++l) {
             const LevelCtr& lc = g->ctr_host->lvl[l % kRing];
             float ms = 0;
@@ -2929,6 +2930,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         stats->pull_bytes += pull_b;
         stats->pull_launches += pull_launches;
         stats->f_total += f_total;
+        stats->host_syncs += syncs + (final_done ? 0 : 1);
         stats->total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     return FGI_OK;
