@@ -416,11 +416,50 @@ fgi_status fgi_part_export_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, ui
 fgi_status fgi_part_init_local(fgi_graph* const* gs, uint32_t p, uint32_t n_global);
 fgi_status fgi_part_local_invalidate(fgi_graph* const* gs, uint32_t p, uint32_t n_roots, const uint32_t* roots,
                                      const uint8_t* immediately /*nullable*/, fgi_wave_stats* stats /*p entries*/);
+/* ---- mutations, batches and pruning on a partition ----------------
+ * The registry's mutations on a partitioned graph. Every rank makes the same call with the same
+ * arguments — global slot ids, the whole batch — in the same order (the host broadcasts them): each
+ * rank applies the items of the slots it owns, records every listed version in its replica (ver_all),
+ * and joins the call's collectives: the cascades (displacement, InvalidateOnSetOutput, invalidation
+ * steps) run as partitioned waves, and an all-reduce carries a pair's state between the ranks owning
+ * its two ends. Results are those of the single-device call on the whole graph: out_ids gets this
+ * rank's invalidated slots (global ids; cascade after cascade, each ascending).
+ *   fgi_part_begin_compute  fgi_begin_compute; out_detached[i]: the detached local handle on the
+ *                           slot's owner (FGI_NONE on the other ranks). FGI_ECAPACITY on every rank
+ *                           when any rank is out of detached handles (nothing applied)
+ *   fgi_part_add_used       fgi_add_used for pairs of global slots (their current nodes); out_result
+ *                           (FGI_USED_*) on every rank
+ *   fgi_part_set_output     fgi_set_output for global slots; out_set on every rank
+ *   fgi_part_invalidate_all fgi_invalidate_all
+ *   fgi_part_run_batch      fgi_run_batch's steps (handles are global slots) applied in order; each
+ *                           cascade is a partitioned wave
+ *   fgi_part_prune          fgi_prune on this rank's rows (an all-gather of the current-node bitmap
+ *                           decides the entries into other ranks' slots; no other collective)
+ * fgi_part_local_run_batch / fgi_part_local_prune run the same on every rank of an in-process group
+ * (fgi_part_init_local): the out arrays are merged (out_detached from each slot's owner; the results
+ * every rank computes must agree), out_ids gets rank 0's ids, then rank 1's, ...; stats: p entries. */
+fgi_status fgi_part_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, const uint64_t* version,
+                                  const uint8_t* has_delay /*nullable*/, uint32_t* out_detached /*nullable*/,
+                                  uint32_t* out_ids, uint64_t cap, uint64_t* out_n, fgi_wave_stats* stats);
+fgi_status fgi_part_add_used(fgi_graph* g, uint32_t n, const uint32_t* dependant, const uint32_t* used,
+                             uint32_t* out_result /*nullable*/);
+fgi_status fgi_part_set_output(fgi_graph* g, uint32_t n, const uint32_t* slot, uint8_t* out_set /*nullable*/,
+                               uint32_t* out_ids, uint64_t cap, uint64_t* out_n, fgi_wave_stats* stats);
+fgi_status fgi_part_invalidate_all(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n,
+                                   fgi_wave_stats* stats);
+fgi_status fgi_part_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, uint32_t* out_ids, uint64_t cap,
+                              uint64_t* out_n, fgi_batch_stats* stats);
+fgi_status fgi_part_prune(fgi_graph* g, fgi_prune_stats* stats);
+fgi_status fgi_part_local_run_batch(fgi_graph* const* gs, uint32_t p, uint32_t n_steps, const fgi_step* steps,
+                                    uint32_t* out_ids, uint64_t cap, uint64_t* out_n,
+                                    fgi_batch_stats* stats /*p entries*/);
+fgi_status fgi_part_local_prune(fgi_graph* const* gs, uint32_t p, fgi_prune_stats* stats /*p entries*/);
 /* Frontier exchanges of a partition rank so far (full all-gathers, delta exchanges) and the bytes it
  * received through them (FGI_OPT_FRONT_EXCHANGE). */
 fgi_status fgi_part_front_stats(fgi_graph* g, uint64_t* full, uint64_t* delta, uint64_t* bytes);
 /* ncclGetVersion of the RCCL the engine's collectives are bound to, and the file it was loaded
- * from (a process that already loaded another librccl with the same soname shares that one). */
+ * from: /opt/rocm/lib/librccl.so.1 (or $FGI_RCCL_LIBRARY), opened by path with RTLD_LOCAL on first
+ * use, so an RCCL the process loaded before (torch's bundled copy) is not the one bound. */
 fgi_status fgi_rccl_info(int* version, char* path /*nullable*/, uint64_t cap);
 
 #ifdef __cplusplus

@@ -523,6 +523,13 @@ fgi_status part_alltoall_async(fgi_graph* g);
 PartBuckets part_buckets(fgi_graph* g);
 // FGI_OPT_PART_BUCKET: words per peer of the planned waves' buckets (0: all that is allocated)
 fgi_status part_set_bucket(fgi_graph* g, int64_t words);
+// Partitioned mutations (graph.hip): a u32 array summed over the ranks in place (synchronises); the
+// current-node bitmaps of the partitioned prune (this rank's, every rank's all-gathered); the
+// dependency-entry store's append from device arrays.
+fgi_status part_allreduce_u32(fgi_graph* g, uint32_t* dev, uint64_t n);
+fgi_status part_cur_buffers(fgi_graph* g, unsigned long long** local, unsigned long long** all, uint64_t* w64);
+fgi_status part_allgather_cur(fgi_graph* g);
+fgi_status part_store_in_dev(fgi_graph* g, const uint64_t* keys, const uint64_t* tags, uint64_t m);
 // frontier exchanges of each kind so far and the bytes this rank received through them
 fgi_status part_front_stats(fgi_graph* g, uint64_t* full, uint64_t* delta, uint64_t* bytes);
 // Rebuild a partition's pull lists from its dependency-entry store if rows or versions changed.

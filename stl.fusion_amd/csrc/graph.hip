@@ -458,7 +458,8 @@ __device__ __forceinline__ void au_reserve(uint64_t i, bool valid, const AuArgs&
     if (!valid) return;
     const uint32_t pos = base + (lane - start);
     const uint32_t cap = row_cap[c.used];
-    atomicAdd(&used_cnt[c.dep_handle], 1u);                          // dependant._used.Add (365-366)
+    if (used_cnt) atomicAdd(&used_cnt[c.dep_handle], 1u);            // dependant._used.Add (365-366); a
+                                                                     // partition's owner of it counts it
     if (pos < cap) {
         pool_col[row_off[c.used] + pos] = c.dep_slot;
         pool_tag[row_off[c.used] + pos] = c.tag;
@@ -729,11 +730,21 @@ struct PruneArgs {
     // and the handles whose node is current
     const unsigned long long* live_bm;
     const uint32_t* cur_bm;
+    // partitions (rows keep global dependant ids): a dependant is current iff its bit in the
+    // all-gathered current bitmaps (rank q's pw64 words at q * pw64, one per pblock slots) is set, and
+    // its version is the replica's
+    const uint64_t* ver_all;
+    const unsigned long long* cur_all;
+    uint32_t pblock, pw64;
 };
 
 // Computed.cs:412-413 for the entry at pool position pos: through the two bitmaps on the fast path,
 // else from the dependant's node word
 __device__ __forceinline__ bool entry_live(const PruneArgs& a, uint64_t pos, uint32_t dst, uint64_t tag) {
+    if (a.ver_all) {
+        const uint32_t q = dst / a.pblock, l = dst - q * a.pblock;
+        return ((a.cur_all[(uint64_t)q * a.pw64 + (l >> 6)] >> (l & 63)) & 1ull) && a.ver_all[dst] == tag;
+    }
     if (a.live_bm) return ((a.live_bm[pos >> 6] >> (pos & 63)) & 1ull) && ((a.cur_bm[dst >> 5] >> (dst & 31)) & 1u);
     return edge_live(a.node, dst, tag);
 }
@@ -1603,6 +1614,144 @@ fgi_status load_rows(fgi_graph* g, uint64_t m, const uint64_t* host_keys, const 
     FGI_TRY(h2d(g, tags + m0, host_tags, m));
     return build_rows_from_keys(g, m0 + m, keys, tags, 0, 0, 0, src_base, dst_base);
 }
+
+namespace {
+// ---- partitioned mutations (part_* below): the kernels that differ from the single device's -----
+// A partition's rows hold (global dependant, tag); node words, rows and |_used| counts are its own
+// slots' (local handles), and every rank keeps a replica of all versions (ver_all).
+
+__global__ void k_add_base(uint32_t n, uint32_t* a, uint32_t base) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) a[i] += base;
+}
+
+// the recomputed slots' new versions into the replica (every rank, every slot of the call)
+__global__ void k_set_versions(uint32_t n, const uint32_t* __restrict__ slot, const uint64_t* __restrict__ ver,
+                               uint64_t* ver_all) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) ver_all[slot[i]] = ver[i];
+}
+
+// AddUsed, phase A (Computed.cs:350-364), on the ranks owning dependants: 1 if the dependant is
+// Computing, | 2 if it has captured dependencies before (only then can the used row hold the pair)
+__global__ void k_pau_dep(uint32_t n, const uint32_t* __restrict__ dep, uint32_t base, uint32_t n_local,
+                          const unsigned long long* __restrict__ node, const uint32_t* __restrict__ used_cnt, uint32_t* flag) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t d = dep[i] - base;
+    uint32_t f = 0;
+    if (d < n_local) {
+        const unsigned long long w = node[d];
+        if ((w & kVMask) != 0 && word_state(w) == FGI_COMPUTING) f = 1u | (used_cnt[d] ? 2u : 0u);
+    }
+    flag[i] = f;
+}
+
+struct PauArgs {
+    const uint32_t* dep;        // global dependant slots
+    const uint32_t* used;       // global used slots
+    uint32_t base, n_local;
+    const unsigned long long* node;
+    const uint64_t* ver_all;
+    const uint32_t* dflag;      // phase A, all-reduced
+    const uint64_t* row_off;
+    const uint32_t* row_len;
+    const uint32_t* pool_col;
+    const uint64_t* pool_tag;
+    unsigned long long* hset;
+    uint64_t hmask;
+    uint32_t* res;              // (code + 1) | appended << 8 on the used node's owner, else 0
+    Cand* cand;
+    unsigned long long* cnt;
+};
+
+// AddUsed, phase B, on the ranks owning the used nodes: AddUsedBy's rules (Computed.cs:370-385) and
+// the entry (dependant, dependant's version) for the used row, set semantics within the batch and
+// against the row
+__device__ __forceinline__ bool pau_pair(uint32_t i, const PauArgs& a, Cand* out) {
+    const uint32_t u = a.used[i] - a.base;
+    if (u >= a.n_local) {
+        a.res[i] = 0;
+        return false;
+    }
+    const uint32_t d = a.dep[i], f = a.dflag[i];
+    uint32_t code;
+    bool add = false;
+    const unsigned long long wu = a.node[u];
+    if (!(f & 1u)) code = FGI_USED_DROPPED;
+    else if ((wu & kVMask) == 0 || word_state(wu) == FGI_INVALIDATED) code = FGI_USED_INVALIDATED;
+    else if (word_state(wu) == FGI_COMPUTING) code = FGI_USED_ESTATE;
+    else {
+        code = FGI_USED_ADDED;
+        add = true;
+        const unsigned long long key = ((unsigned long long)u << 32) | d;
+        uint64_t p = sm64(key) & a.hmask;
+        while (true) {
+            const unsigned long long prev = atomicCAS(a.hset + p, ~0ull, key);
+            if (prev == ~0ull) break;
+            if (prev == key) {
+                add = false;
+                break;
+            }
+            p = (p + 1) & a.hmask;
+        }
+        const uint64_t tag = a.ver_all[d];
+        if (add && (f & 2u)) {
+            const uint64_t o = a.row_off[u];
+            const uint32_t len = a.row_len[u];
+            for (uint32_t k = 0; k < len && add; ++k)
+                if (a.pool_col[o + k] == d && a.pool_tag[o + k] == tag) add = false;
+        }
+        if (add) *out = Cand{u, FGI_NONE, d, 0, tag};
+    }
+    a.res[i] = (code + 1u) | (add ? 0x100u : 0u);
+    return add;
+}
+
+__global__ void k_pau_classify(uint32_t n, PauArgs a) {
+    __shared__ uint32_t s_w[8];
+    __shared__ unsigned long long s_base;
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    Cand cd{};
+    const bool want = i < n && pau_pair(i, a, &cd);
+    const unsigned long long m = __ballot(want);
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    if (lane == 0) s_w[wid] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, total = 0;
+    for (uint32_t w = 0; w < nw; ++w) {
+        before += w < wid ? s_w[w] : 0u;
+        total += s_w[w];
+    }
+    if (threadIdx.x == 0) s_base = total ? atomicAdd(a.cnt, (unsigned long long)total) : 0ull;
+    __syncthreads();
+    if (want) {
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        a.cand[s_base + before + r] = cd;
+    }
+}
+
+// AddUsed, phase C, on the ranks owning dependants: InvalidateOnSetOutput for a used node found
+// Invalidated (Computed.cs:376-378); for an appended entry, |_used| and the dependency-entry store
+// (the dependant's pull list: used global id at the dependant's version)
+__global__ void k_pau_apply(uint32_t n, const uint32_t* __restrict__ dep, const uint32_t* __restrict__ used,
+                            uint32_t base, uint32_t n_local, const uint32_t* __restrict__ res, unsigned long long* node,
+                            uint32_t* used_cnt, const uint64_t* __restrict__ ver_all, uint64_t* in_keys, uint64_t* in_tags,
+                            unsigned long long* in_cnt) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t d = dep[i] - base;
+    if (d >= n_local) return;
+    const uint32_t r = res[i];
+    if ((r & 0xFFu) == FGI_USED_INVALIDATED + 1u) atomicOr(node + d, kW_IOSO);
+    if (r & 0x100u) {
+        atomicAdd(used_cnt + d, 1u);
+        const unsigned long long k = atomicAdd(in_cnt, 1ull);
+        in_keys[k] = ((uint64_t)d << 32) | used[i];
+        in_tags[k] = ver_all[dep[i]];
+    }
+}
+}  // namespace
 
 }  // namespace fgi
 
@@ -2858,6 +3007,20 @@ static fgi_status prune_range_launch(fgi_graph* g, uint32_t lo, uint32_t hi, Tmp
     a.pool_col = g->pool_col;
     a.pool_tag = g->pool_tag;
     a.st = st;
+    PartView pv;
+    if (part_view(g, &pv)) {   // a partition: the dependants' current bits and versions of every rank
+        unsigned long long *cl, *ca;
+        uint64_t w64 = 0;
+        FGI_TRY(part_cur_buffers(g, &cl, &ca, &w64));
+        FGI_HIP(g, hipMemsetAsync(cl, 0, w64 * 8, s));
+        hipLaunchKernelGGL(k_build_cur, dim3(std::min<uint32_t>((pv.n_local + 255) / 256 + 1, 8192)), dim3(256), 0, s,
+                           pv.n_local, a.node, cl);
+        FGI_TRY(part_allgather_cur(g));
+        a.ver_all = pv.ver_all;
+        a.cur_all = ca;
+        a.pblock = pv.block;
+        a.pw64 = (uint32_t)w64;
+    } else
     // fast path: the entries' liveness at list build still holds (no mutation, no compaction since)
     if (g->pool_live && g->pl_mut_epoch == g->mut_epoch && g->pl_pool_epoch == g->pool_epoch &&
         g->pool_top <= g->pool_live_cap && !getenv("FGI_PRUNE_GATHER")) {
@@ -2925,8 +3088,10 @@ static fgi_status defragment(fgi_graph* g) {
     return ensure_cstart(g, cap);
 }
 
-static fgi_status prune_rows(fgi_graph* g, uint32_t lo, uint32_t hi, bool allow_defrag, fgi_prune_stats* stats) {
-    FGI_TRY(single_only(g, "fgi_prune"));
+static fgi_status prune_rows(fgi_graph* g, uint32_t lo, uint32_t hi, bool allow_defrag, fgi_prune_stats* stats,
+                             bool part_ok = false) {
+    if (part_ok) FGI_TRY(usable(g));
+    else FGI_TRY(single_only(g, "fgi_prune"));
     hipSetDevice(g->device);
     const auto t0 = std::chrono::steady_clock::now();
     FGI_TRY(fold(g));
@@ -3023,6 +3188,431 @@ fgi_status fgi_release(fgi_graph* g, uint32_t n, const uint32_t* handle) {
         touch(g);
     }
     return FGI_OK;
+}
+
+// ---- partitioned mutations, prune and batches ----------------------
+// A partitioned graph takes the registry's mutations too. Every rank makes the same call with the same
+// arguments (global slot ids), in the same order: each applies the items of the slots it owns, writes
+// every listed version into its replica (ver_all), and joins the call's collectives — the cascades
+// (run_part_wave: displacement, InvalidateOnSetOutput, the invalidation steps) and the all-reduces
+// that carry a pair's state between the ranks owning its two ends (AddUsed / AddUsedBy).
+namespace {
+
+fgi_status part_check(fgi_graph* g, PartView* pv, const char* what) {
+    if (!g->part || !part_view(g, pv)) return set_err(g, FGI_ESTATE, "%s: partition not initialised", what);
+    return usable(g);
+}
+
+// this rank's ids of the last partitioned wave (global, ascending) appended to *ids
+fgi_status part_take_ids(fgi_graph* g, const PartView& pv, std::vector<uint32_t>* ids) {
+    if (!ids || g->last_wave_n == 0) return FGI_OK;
+    const size_t at = ids->size();
+    ids->resize(at + g->last_wave_n);
+    FGI_TRY(d2h(g, ids->data() + at, g->inv, g->last_wave_n));
+    for (size_t i = at; i < ids->size(); ++i) (*ids)[i] += pv.base;
+    return FGI_OK;
+}
+
+fgi_status part_check_slots(fgi_graph* g, const PartView& pv, uint32_t n, const uint32_t* slot, bool distinct) {
+    for (uint32_t i = 0; i < n; ++i)
+        if (slot[i] >= pv.n_global) return set_err(g, FGI_EINVAL, "slot %u out of range", slot[i]);
+    if (distinct && n > 1) {
+        std::vector<uint32_t> c(slot, slot + n);
+        std::sort(c.begin(), c.end());
+        for (uint32_t i = 1; i < n; ++i)
+            if (c[i] == c[i - 1]) return set_err(g, FGI_EINVAL, "slot repeated in one batch (%u)", c[i]);
+    }
+    return FGI_OK;
+}
+
+// a cascade from host root slots (global ids; each rank starts the ones it owns), on every rank
+fgi_status part_wave_host(fgi_graph* g, const PartView& pv, uint32_t n, const uint32_t* slots, const uint8_t* imm,
+                          fgi_wave_stats* stats, std::vector<uint32_t>* ids) {
+    (void)pv;
+    Tmp tr, ti;
+    uint32_t* dr = nullptr;
+    uint8_t* di = nullptr;
+    if (n) {
+        FGI_TRY(tmalloc(g, tr, &dr, n));
+        FGI_TRY(h2d(g, dr, slots, n));
+        if (imm) {
+            FGI_TRY(tmalloc(g, ti, &di, n));
+            FGI_TRY(h2d(g, di, imm, n));
+        }
+    }
+    g->last_wave_n = 0;
+    FGI_TRY(run_part_wave(g, n, dr, di, stats));
+    return part_take_ids(g, pv, ids);
+}
+
+// ComputeMethodFunctionBase.Compute + ComputedRegistry.Register with displacement (as
+// fgi_begin_compute) over a partition: out_detached[i] is the detached local handle on the slot's
+// owner (FGI_NONE elsewhere and for nodes not detached)
+fgi_status part_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, const uint64_t* version,
+                              const uint8_t* has_delay, uint32_t* out_detached, fgi_wave_stats* stats,
+                              std::vector<uint32_t>* ids) {
+    PartView pv;
+    FGI_TRY(part_check(g, &pv, "fgi_part_begin_compute"));
+    if (n && (!slot || !version)) return FGI_EINVAL;
+    FGI_TRY(part_check_slots(g, pv, n, slot, true));
+    for (uint32_t i = 0; i < n; ++i)
+        if (version[i] == 0 || version[i] > kVMask) return set_err(g, FGI_EINVAL, "bad version (%u)", i);
+    hipSetDevice(g->device);
+    hipStream_t st = g->stream;
+    std::vector<uint32_t> li, ls;
+    std::vector<uint64_t> lv;
+    std::vector<uint8_t> ld;
+    for (uint32_t i = 0; i < n; ++i)
+        if (slot[i] - pv.base < pv.n_local) {
+            li.push_back(i);
+            ls.push_back(slot[i] - pv.base);
+            lv.push_back(version[i]);
+            ld.push_back(has_delay ? has_delay[i] : 0);
+        }
+    const uint32_t m = (uint32_t)li.size();
+    Tmp ts, tv, td, tc, tr, to, tf, tflag, tall, tallv;
+    uint32_t *ds = nullptr, *droots = nullptr, *dout = nullptr, *dfree_h = nullptr, *dflag = nullptr;
+    uint64_t* dv = nullptr;
+    uint8_t *dd = nullptr, *dcls = nullptr;
+    FGI_TRY(fold(g));
+    FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, 4 * sizeof(unsigned long long), st));
+    if (m) {
+        FGI_TRY(tmalloc(g, ts, &ds, m));
+        FGI_TRY(tmalloc(g, tv, &dv, m));
+        FGI_TRY(tmalloc(g, td, &dd, m));
+        FGI_TRY(tmalloc(g, tc, &dcls, m));
+        FGI_TRY(tmalloc(g, tr, &droots, m));
+        FGI_TRY(tmalloc(g, to, &dout, m));
+        FGI_TRY(h2d(g, ds, ls.data(), m));
+        FGI_TRY(h2d(g, dv, lv.data(), m));
+        FGI_TRY(h2d(g, dd, ld.data(), m));
+        hipLaunchKernelGGL(k_bc_classify, dim3(nblk(m)), dim3(256), 0, st, m, ds,
+                           reinterpret_cast<const unsigned long long*>(g->node), dcls, droots, g->misc_dev);
+    }
+    unsigned long long cnt[2];
+    FGI_TRY(d2h(g, cnt, g->misc_dev, 2));
+    // every rank detaches its displaced survivors, or no rank applies the call
+    FGI_TRY(tmalloc(g, tflag, &dflag, 1));
+    const uint32_t short_h = cnt[1] > g->free_detached.size() ? 1u : 0u;
+    FGI_TRY(h2d(g, dflag, &short_h, 1));
+    FGI_TRY(part_allreduce_u32(g, dflag, 1));
+    uint32_t any_short = 0;
+    FGI_TRY(d2h(g, &any_short, dflag, 1));
+    if (any_short)
+        return set_err(g, FGI_ECAPACITY, "a rank is out of detached handles (this one: %zu free, %llu needed)",
+                       g->free_detached.size(), cnt[1]);
+    // the displacement cascade (ComputedRegistry.cs:91-94) on every rank, then versions and installs
+    if (cnt[0]) hipLaunchKernelGGL(k_add_base, dim3(nblk(cnt[0])), dim3(256), 0, st, (uint32_t)cnt[0], droots, pv.base);
+    g->last_wave_n = 0;
+    FGI_TRY(run_part_wave(g, (uint32_t)cnt[0], droots, nullptr, stats));
+    FGI_TRY(part_take_ids(g, pv, ids));
+    if (n) {
+        uint32_t* as = nullptr;
+        uint64_t* av = nullptr;
+        FGI_TRY(tmalloc(g, tall, &as, n));
+        FGI_TRY(tmalloc(g, tallv, &av, n));
+        FGI_TRY(h2d(g, as, slot, n));
+        FGI_TRY(h2d(g, av, version, n));
+        hipLaunchKernelGGL(k_set_versions, dim3(nblk(n)), dim3(256), 0, st, n, as, av, pv.ver_all);
+    }
+    std::vector<uint32_t> od(m, FGI_NONE);
+    if (m) {
+        std::vector<uint32_t> take(g->free_detached.end() - (ptrdiff_t)cnt[1], g->free_detached.end());
+        FGI_TRY(tmalloc(g, tf, &dfree_h, take.size() + 1));
+        FGI_TRY(h2d(g, dfree_h, take.data(), take.size()));
+        FGI_TRY(fold(g));   // the displacement cascade's visits
+        FGI_HIP(g, hipMemsetAsync(g->misc_dev + 2, 0, sizeof(unsigned long long), st));
+        const InstallArgs ia{ds,         dv,          dd,        dcls,      dfree_h, g->misc_dev + 2, g->n_slots,
+                             reinterpret_cast<unsigned long long*>(g->node), g->row_off, g->row_len, g->row_cap,
+                             g->used_cnt, g->home, dout};
+        hipLaunchKernelGGL(k_bc_install, dim3(nblk(m)), dim3(256), 0, st, m, ia);
+        FGI_HIP(g, hipGetLastError());
+        FGI_TRY(d2h(g, od.data(), dout, m));
+        g->free_detached.resize(g->free_detached.size() - take.size());
+    } else {
+        FGI_HIP(g, hipStreamSynchronize(st));
+    }
+    if (out_detached) {
+        for (uint32_t i = 0; i < n; ++i) out_detached[i] = FGI_NONE;
+        for (uint32_t j = 0; j < m; ++j) out_detached[li[j]] = od[j];
+    }
+    touch(g);
+    note_words(g);
+    return FGI_OK;
+}
+
+// dependant.AddUsed(used) over a partition (Computed.cs:347-385) for pairs of global slots (their
+// current nodes): the dependant's owner says whether it is Computing (all-reduce), the used node's
+// owner applies AddUsedBy's rules and appends the entry to its row, the results are all-reduced, and
+// the dependant's owner applies InvalidateOnSetOutput / counts the new dependency and records it
+// for its pull lists. out_result (every pair, every rank): FGI_USED_*
+fgi_status part_add_used(fgi_graph* g, uint32_t n, const uint32_t* dep, const uint32_t* used, uint32_t* out_result) {
+    PartView pv;
+    FGI_TRY(part_check(g, &pv, "fgi_part_add_used"));
+    if (n && (!dep || !used)) return FGI_EINVAL;
+    FGI_TRY(part_check_slots(g, pv, n, dep, false));
+    FGI_TRY(part_check_slots(g, pv, n, used, false));
+    if (n == 0) return FGI_OK;
+    hipSetDevice(g->device);
+    hipStream_t st = g->stream;
+    uint64_t hcap = 64;
+    while (hcap < 2ull * n) hcap <<= 1;
+    Tmp tdep, tuse, tflag, tres, thash, tcand, tpend, tovf, tik, tit;
+    uint32_t *ddep, *duse, *dflag, *dres, *dpend, *dovf;
+    unsigned long long* dhash;
+    Cand* dcand;
+    uint64_t *ik, *it;
+    FGI_TRY(tmalloc(g, tdep, &ddep, n));
+    FGI_TRY(tmalloc(g, tuse, &duse, n));
+    FGI_TRY(tmalloc(g, tflag, &dflag, n));
+    FGI_TRY(tmalloc(g, tres, &dres, n));
+    FGI_TRY(tmalloc(g, thash, &dhash, hcap));
+    FGI_TRY(tmalloc(g, tcand, &dcand, n));
+    FGI_TRY(tmalloc(g, tpend, &dpend, n));
+    FGI_TRY(tmalloc(g, tovf, &dovf, n));
+    FGI_TRY(tmalloc(g, tik, &ik, n));
+    FGI_TRY(tmalloc(g, tit, &it, n));
+    FGI_TRY(h2d(g, ddep, dep, n));
+    FGI_TRY(h2d(g, duse, used, n));
+    FGI_TRY(fold(g));
+    note_words(g);
+    auto* node = reinterpret_cast<unsigned long long*>(g->node);
+    hipLaunchKernelGGL(k_pau_dep, dim3(nblk(n)), dim3(256), 0, st, n, ddep, pv.base, pv.n_local, node, g->used_cnt, dflag);
+    FGI_TRY(part_allreduce_u32(g, dflag, n));
+    FGI_HIP(g, hipMemsetAsync(dhash, 0xFF, hcap * sizeof(unsigned long long), st));
+    FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, 8 * sizeof(unsigned long long), st));
+    const PauArgs pa{ddep, duse, pv.base, pv.n_local, node, pv.ver_all, dflag, g->row_off, g->row_len, g->pool_col,
+                     g->pool_tag, dhash, hcap - 1, dres, dcand, g->misc_dev};
+    hipLaunchKernelGGL(k_pau_classify, dim3(nblk(n)), dim3(256), 0, st, n, pa);
+    unsigned long long nc = 0;
+    FGI_TRY(d2h(g, &nc, g->misc_dev, 1));
+    if (nc) {
+        touch(g);
+        const AuArgs aa{nullptr,     nullptr,    g->n_slots,  g->home,     node,        g->row_off,
+                        g->row_len,  g->row_cap, nullptr,     g->pool_col, g->pool_tag, dhash,
+                        hcap - 1,    nullptr,    dcand,       dpend,       dovf,        g->misc_dev};
+        hipLaunchKernelGGL(k_au_reserve, dim3(nblk(nc)), dim3(256), 0, st, (uint64_t)nc, aa);
+        unsigned long long c2[2];
+        FGI_TRY(d2h(g, c2, g->misc_dev + 1, 2));
+        if (c2[1]) {   // rows that outgrew their capacity: relocated to the pool top
+            hipLaunchKernelGGL(k_au_size, dim3(nblk(c2[1])), dim3(256), 0, st, (uint64_t)c2[1], dovf, g->row_len,
+                               g->misc_dev + 3);
+            unsigned long long need = 0;
+            FGI_TRY(d2h(g, &need, g->misc_dev + 3, 1));
+            FGI_TRY(ensure_pool(g, g->pool_top + need));
+            FGI_HIP(g, hipMemcpyAsync(g->pool_top_dev, &g->pool_top, sizeof(uint64_t), hipMemcpyHostToDevice, st));
+            hipLaunchKernelGGL(k_au_relocate, dim3(nblk(c2[1] * 64)), dim3(256), 0, st, (uint64_t)c2[1], dovf,
+                               g->row_off, g->row_len, g->row_cap, g->pool_col, g->pool_tag, g->pool_top_dev);
+            hipLaunchKernelGGL(k_au_pending, dim3(nblk(nc)), dim3(256), 0, st, (uint64_t)nc, dcand, dpend, g->row_off,
+                               g->pool_col, g->pool_tag);
+            g->pool_top += need;
+            FGI_TRY(ensure_cstart(g, g->pool_top));
+        }
+    }
+    FGI_TRY(part_allreduce_u32(g, dres, n));
+    FGI_HIP(g, hipMemsetAsync(g->misc_dev + 5, 0, sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_pau_apply, dim3(nblk(n)), dim3(256), 0, st, n, ddep, duse, pv.base, pv.n_local, dres, node,
+                       g->used_cnt, pv.ver_all, ik, it, g->misc_dev + 5);
+    FGI_HIP(g, hipGetLastError());
+    unsigned long long ni = 0;
+    FGI_TRY(d2h(g, &ni, g->misc_dev + 5, 1));
+    if (ni) {
+        FGI_TRY(part_store_in_dev(g, ik, it, ni));
+        touch(g);
+    }
+    std::vector<uint32_t> r(n);
+    FGI_TRY(d2h(g, r.data(), dres, n));
+    if (out_result)
+        for (uint32_t i = 0; i < n; ++i) out_result[i] = (r[i] & 0xFFu) - 1u;
+    return FGI_OK;
+}
+
+// Computed.TrySetOutput (Computed.cs:141-160) over a partition; the nodes flagged
+// InvalidateOnSetOutput are the roots of one cascade on every rank. out_set: every item, every rank
+fgi_status part_set_output(fgi_graph* g, uint32_t n, const uint32_t* slot, uint8_t* out_set, fgi_wave_stats* stats,
+                           std::vector<uint32_t>* ids) {
+    PartView pv;
+    FGI_TRY(part_check(g, &pv, "fgi_part_set_output"));
+    if (n && !slot) return FGI_EINVAL;
+    FGI_TRY(part_check_slots(g, pv, n, slot, false));
+    hipSetDevice(g->device);
+    hipStream_t st = g->stream;
+    std::vector<uint32_t> li, lh;
+    for (uint32_t i = 0; i < n; ++i)
+        if (slot[i] - pv.base < pv.n_local) {
+            li.push_back(i);
+            lh.push_back(slot[i] - pv.base);
+        }
+    const uint32_t m = (uint32_t)li.size();
+    Tmp th, ts, tr, tfl;
+    uint32_t *dh = nullptr, *droots = nullptr, *dfl = nullptr;
+    uint8_t* dset = nullptr;
+    FGI_TRY(fold(g));
+    note_words(g);
+    FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, sizeof(unsigned long long), st));
+    std::vector<uint8_t> set(m, 0);
+    if (m) {
+        FGI_TRY(tmalloc(g, th, &dh, m));
+        FGI_TRY(tmalloc(g, ts, &dset, m));
+        FGI_TRY(tmalloc(g, tr, &droots, m));
+        FGI_TRY(h2d(g, dh, lh.data(), m));
+        hipLaunchKernelGGL(k_set_output, dim3(nblk(m)), dim3(256), 0, st, m, dh, g->n_handles,
+                           reinterpret_cast<unsigned long long*>(g->node), dset, droots, g->misc_dev);
+        FGI_TRY(d2h(g, set.data(), dset, m));
+    }
+    unsigned long long nr = 0;
+    FGI_TRY(d2h(g, &nr, g->misc_dev, 1));
+    if (nr) hipLaunchKernelGGL(k_add_base, dim3(nblk(nr)), dim3(256), 0, st, (uint32_t)nr, droots, pv.base);
+    g->last_wave_n = 0;
+    FGI_TRY(run_part_wave(g, (uint32_t)nr, droots, nullptr, stats));   // Invalidate() (Computed.cs:153-156)
+    FGI_TRY(part_take_ids(g, pv, ids));
+    if (n) {
+        std::vector<uint32_t> all(n, 0);
+        for (uint32_t j = 0; j < m; ++j) all[li[j]] = set[j];
+        FGI_TRY(tmalloc(g, tfl, &dfl, n));
+        FGI_TRY(h2d(g, dfl, all.data(), n));
+        FGI_TRY(part_allreduce_u32(g, dfl, n));
+        FGI_TRY(d2h(g, all.data(), dfl, n));
+        if (out_set)
+            for (uint32_t i = 0; i < n; ++i) out_set[i] = (uint8_t)(all[i] != 0);
+    }
+    return FGI_OK;
+}
+
+// ComputedRegistry.InvalidateEverything (ComputedRegistry.cs:142-147) over a partition: every rank's
+// current nodes are the roots of one cascade
+fgi_status part_invalidate_all(fgi_graph* g, fgi_wave_stats* stats, std::vector<uint32_t>* ids) {
+    PartView pv;
+    FGI_TRY(part_check(g, &pv, "fgi_part_invalidate_all"));
+    hipSetDevice(g->device);
+    hipStream_t st = g->stream;
+    FGI_TRY(fold(g));
+    Tmp tr;
+    uint32_t* roots;
+    FGI_TRY(tmalloc(g, tr, &roots, std::max<uint32_t>(pv.n_local, 1)));
+    FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, sizeof(unsigned long long), st));
+    hipLaunchKernelGGL(k_invalidate_all_roots, dim3(nblk(pv.n_local)), dim3(256), 0, st, pv.n_local,
+                       reinterpret_cast<const unsigned long long*>(g->node), roots, g->misc_dev);
+    unsigned long long nr = 0;
+    FGI_TRY(d2h(g, &nr, g->misc_dev, 1));
+    if (nr) hipLaunchKernelGGL(k_add_base, dim3(nblk(nr)), dim3(256), 0, st, (uint32_t)nr, roots, pv.base);
+    g->last_wave_n = 0;
+    FGI_TRY(run_part_wave(g, (uint32_t)nr, roots, nullptr, stats));
+    return part_take_ids(g, pv, ids);
+}
+
+fgi_status part_copy_ids(fgi_graph* g, const std::vector<uint32_t>& ids, uint32_t* out_ids, uint64_t cap, uint64_t* out_n) {
+    if (out_n) *out_n = ids.size();
+    if (!out_ids) return FGI_OK;
+    if (ids.size() > cap) return FGI_ECAPACITY;
+    std::memcpy(out_ids, ids.data(), ids.size() * 4);
+    (void)g;
+    return FGI_OK;
+}
+
+}  // namespace
+
+fgi_status fgi_part_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, const uint64_t* version,
+                                  const uint8_t* has_delay, uint32_t* out_detached, uint32_t* out_ids, uint64_t cap,
+                                  uint64_t* out_n, fgi_wave_stats* stats) {
+    if (!g) return FGI_EINVAL;
+    std::vector<uint32_t> ids;
+    FGI_TRY(part_begin_compute(g, n, slot, version, has_delay, out_detached, stats, &ids));
+    return part_copy_ids(g, ids, out_ids, cap, out_n);
+}
+
+fgi_status fgi_part_add_used(fgi_graph* g, uint32_t n, const uint32_t* dependant, const uint32_t* used,
+                             uint32_t* out_result) {
+    if (!g) return FGI_EINVAL;
+    return part_add_used(g, n, dependant, used, out_result);
+}
+
+fgi_status fgi_part_set_output(fgi_graph* g, uint32_t n, const uint32_t* slot, uint8_t* out_set, uint32_t* out_ids,
+                               uint64_t cap, uint64_t* out_n, fgi_wave_stats* stats) {
+    if (!g) return FGI_EINVAL;
+    std::vector<uint32_t> ids;
+    FGI_TRY(part_set_output(g, n, slot, out_set, stats, &ids));
+    return part_copy_ids(g, ids, out_ids, cap, out_n);
+}
+
+fgi_status fgi_part_invalidate_all(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64_t* out_n,
+                                   fgi_wave_stats* stats) {
+    if (!g) return FGI_EINVAL;
+    std::vector<uint32_t> ids;
+    FGI_TRY(part_invalidate_all(g, stats, &ids));
+    return part_copy_ids(g, ids, out_ids, cap, out_n);
+}
+
+fgi_status fgi_part_prune(fgi_graph* g, fgi_prune_stats* stats) {
+    PartView pv;
+    if (!g) return FGI_EINVAL;
+    FGI_TRY(part_check(g, &pv, "fgi_part_prune"));
+    if (stats) *stats = fgi_prune_stats{};
+    return prune_rows(g, 0, g->n_handles, true, stats, true);
+}
+
+fgi_status fgi_part_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, uint32_t* out_ids, uint64_t cap,
+                              uint64_t* out_n, fgi_batch_stats* stats) {
+    PartView pv;
+    if (!g || (n_steps && !steps)) return FGI_EINVAL;
+    FGI_TRY(part_check(g, &pv, "fgi_part_run_batch"));
+    const auto t0 = std::chrono::steady_clock::now();
+    if (out_n) *out_n = 0;
+    // a bad argument in any step applies nothing (every rank sees the same batch and refuses it alike)
+    for (uint32_t k = 0; k < n_steps; ++k) {
+        const fgi_step& sp = steps[k];
+        if (sp.kind < FGI_STEP_INVALIDATE || sp.kind > FGI_STEP_SET_OUTPUT)
+            return set_err(g, FGI_EINVAL, "step %u: unknown kind %u", k, sp.kind);
+        if (sp.n && (!sp.handles || (sp.kind == FGI_STEP_ADD_USED && !sp.used) ||
+                     (sp.kind == FGI_STEP_BEGIN_COMPUTE && !sp.version)))
+            return set_err(g, FGI_EINVAL, "step %u: missing arrays", k);
+        FGI_TRY(part_check_slots(g, pv, sp.n, sp.handles, sp.kind == FGI_STEP_BEGIN_COMPUTE));
+        if (sp.kind == FGI_STEP_ADD_USED) FGI_TRY(part_check_slots(g, pv, sp.n, sp.used, false));
+        if (sp.kind == FGI_STEP_BEGIN_COMPUTE)
+            for (uint32_t i = 0; i < sp.n; ++i)
+                if (sp.version[i] == 0 || sp.version[i] > kVMask)
+                    return set_err(g, FGI_EINVAL, "step %u: bad version (%u)", k, i);
+    }
+    std::vector<uint32_t> ids;
+    fgi_wave_stats ws{};
+    for (uint32_t k = 0; k < n_steps; ++k) {
+        const fgi_step& sp = steps[k];
+        if (sp.n && !sp.handles) return set_err(g, FGI_EINVAL, "step %u: no handles", k);
+        const uint64_t before = ws.v_inv;
+        switch (sp.kind) {
+            case FGI_STEP_INVALIDATE: {
+                FGI_TRY(part_check_slots(g, pv, sp.n, sp.handles, false));
+                FGI_TRY(part_wave_host(g, pv, sp.n, sp.handles, sp.flags, &ws, &ids));
+                break;
+            }
+            case FGI_STEP_BEGIN_COMPUTE:
+                FGI_TRY(part_begin_compute(g, sp.n, sp.handles, sp.version, sp.flags, static_cast<uint32_t*>(sp.out), &ws,
+                                           &ids));
+                break;
+            case FGI_STEP_ADD_USED:
+                FGI_TRY(part_add_used(g, sp.n, sp.handles, sp.used, static_cast<uint32_t*>(sp.out)));
+                break;
+            case FGI_STEP_SET_OUTPUT:
+                FGI_TRY(part_set_output(g, sp.n, sp.handles, static_cast<uint8_t*>(sp.out), &ws, &ids));
+                break;
+            default:
+                return set_err(g, FGI_EINVAL, "step %u: unknown kind %u", k, sp.kind);
+        }
+        if (stats && sp.kind != FGI_STEP_ADD_USED) stats->waves += 1;
+        (void)before;
+    }
+    if (stats) {
+        stats->levels += ws.levels;
+        stats->v_inv += ws.v_inv;
+        stats->e_trav += ws.e_trav;
+        stats->e_match += ws.e_match;
+        stats->n_flagged += ws.n_flagged;
+        stats->kernel_ms += ws.kernel_ms;
+        stats->wave_ms += ws.kernel_ms;
+        stats->host_syncs += (uint32_t)ws.host_syncs;
+        stats->total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    return part_copy_ids(g, ids, out_ids, cap, out_n);
 }
 
 }  // extern "C"

@@ -63,6 +63,10 @@ struct PartComm {
     virtual fgi_status allgather_front_async(fgi_graph* g) = 0;
     // a2a_send[q * C, + C) to rank q, into a2a_recv[r * C, + C) from every rank r
     virtual fgi_status alltoall_async(fgi_graph* g) = 0;
+    // Partitioned mutations: the element-wise sum of a device u32 array over all ranks, in place
+    // (synchronises); every rank's cur_local (W64 words) into cur_all[q * W64, + W64) (stream-ordered)
+    virtual fgi_status allreduce_u32(fgi_graph* g, uint32_t* dev, uint64_t n) = 0;
+    virtual fgi_status allgather_cur_async(fgi_graph* g) = 0;
 };
 
 struct PartState {
@@ -98,6 +102,12 @@ struct PartState {
     unsigned long long* a2a_cur = nullptr;     // [world]
     unsigned long long* red = nullptr;         // [kPartRedMax] device all-reduce buffer (planned waves)
     unsigned long long* red_host = nullptr;
+    // partitioned prune: the current-node bits of the owned slots (W64 words, padded per rank) and
+    // every rank's, all-gathered (allocated on first use)
+    uint64_t cur_w64 = 0;
+    unsigned long long* cur_local = nullptr;
+    unsigned long long* cur_all = nullptr;
+    std::vector<uint32_t> u32_host;            // allreduce_u32's host copy (in-process groups)
 };
 
 static PartState* ps(fgi_graph* g) { return reinterpret_cast<PartState*>(g->part); }
@@ -205,6 +215,8 @@ fgi_status part_destroy(fgi_graph* g) {
     hipFree(p->a2a_recv);
     hipFree(p->a2a_cur);
     hipFree(p->red);
+    hipFree(p->cur_local);
+    hipFree(p->cur_all);
     if (p->red_host) hipHostFree(p->red_host);
     if (p->all_cnt_host) hipHostFree(p->all_cnt_host);
     if (p->scalar_host) hipHostFree(p->scalar_host);
@@ -252,6 +264,21 @@ struct RcclComm final : PartComm {
     fgi_status alltoall_async(fgi_graph* g) override {
         PartState* p = ps(g);
         FGI_NCCL(g, rccl().AllToAll(p->a2a_send, p->a2a_recv, p->a2a_C, ncclUint32, p->comm, g->stream));
+        return FGI_OK;
+    }
+    fgi_status allreduce_u32(fgi_graph* g, uint32_t* dev, uint64_t n) override {
+        PartState* p = ps(g);
+        if (n && (p->v.world > 1 || g->opt_part_coll))
+            FGI_NCCL(g, rccl().AllReduce(dev, dev, n, ncclUint32, ncclSum, p->comm, g->stream));
+        FGI_HIP(g, hipStreamSynchronize(g->stream));
+        return FGI_OK;
+    }
+    fgi_status allgather_cur_async(fgi_graph* g) override {
+        PartState* p = ps(g);
+        if (p->v.world > 1 || g->opt_part_coll)
+            FGI_NCCL(g, rccl().AllGather(p->cur_local, p->cur_all, p->cur_w64, ncclUint64, p->comm, g->stream));
+        else
+            FGI_HIP(g, hipMemcpyAsync(p->cur_all, p->cur_local, p->cur_w64 * 8, hipMemcpyDeviceToDevice, g->stream));
         return FGI_OK;
     }
     fgi_status exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent, uint64_t* glob) override {
@@ -501,6 +528,32 @@ struct LocalComm final : PartComm {
             return FGI_OK;
         });
     }
+    fgi_status allgather_cur_async(fgi_graph* g) override {
+        PartState* p = ps(g);
+        const uint64_t W = p->cur_w64;
+        return exchange_async(g, [&]() -> fgi_status {
+            for (size_t q = 0; q < grp->gs.size(); ++q)
+                FGI_HIP(g, hipMemcpyAsync(p->cur_all + q * W, ps(grp->gs[q])->cur_local, W * 8, hipMemcpyDefault, g->stream));
+            return FGI_OK;
+        });
+    }
+    // host-side sum: every rank copies its array out, the group adds them, every rank copies the sum in
+    fgi_status allreduce_u32(fgi_graph* g, uint32_t* dev, uint64_t n) override {
+        PartState* p = ps(g);
+        p->u32_host.resize(n);
+        if (n) FGI_HIP(g, hipMemcpyAsync(p->u32_host.data(), dev, n * 4, hipMemcpyDeviceToHost, g->stream));
+        FGI_HIP(g, hipStreamSynchronize(g->stream));
+        if (!grp->arrive()) return peer_failed(g);
+        std::vector<uint32_t> sum(n, 0);
+        for (size_t q = 0; q < grp->gs.size(); ++q) {
+            const std::vector<uint32_t>& h = ps(grp->gs[q])->u32_host;
+            for (uint64_t i = 0; i < n; ++i) sum[i] += h[i];
+        }
+        if (!grp->arrive()) return peer_failed(g);   // nobody changes its copy before all have read it
+        if (n) FGI_HIP(g, hipMemcpyAsync(dev, sum.data(), n * 4, hipMemcpyHostToDevice, g->stream));
+        FGI_HIP(g, hipStreamSynchronize(g->stream));
+        return FGI_OK;
+    }
 };
 
 fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent, uint64_t* glob) {
@@ -515,6 +568,33 @@ fgi_status part_allgather_front_async(fgi_graph* g) {
 }
 
 fgi_status part_alltoall_async(fgi_graph* g) { return ps(g)->ops->alltoall_async(g); }
+
+fgi_status part_allreduce_u32(fgi_graph* g, uint32_t* dev, uint64_t n) { return ps(g)->ops->allreduce_u32(g, dev, n); }
+
+// every rank's current-node bits (its owned slots: W64 = ceil(block / 64) words each, rank q's at
+// q * W64) into the returned all-gathered array; the caller builds cur_local first (its W64 words)
+fgi_status part_cur_buffers(fgi_graph* g, unsigned long long** local, unsigned long long** all, uint64_t* w64) {
+    PartState* p = ps(g);
+    if (!p->cur_local) {
+        p->cur_w64 = ((uint64_t)p->v.block + 63) / 64;
+        if (hipMalloc(&p->cur_local, p->cur_w64 * 8) != hipSuccess ||
+            hipMalloc(&p->cur_all, p->cur_w64 * 8 * p->v.world) != hipSuccess)
+            return set_err(g, FGI_ENOMEM, "current-node bitmaps");
+    }
+    *local = p->cur_local;
+    *all = p->cur_all;
+    *w64 = p->cur_w64;
+    return FGI_OK;
+}
+
+fgi_status part_allgather_cur(fgi_graph* g) { return ps(g)->ops->allgather_cur_async(g); }
+
+static fgi_status part_store_in(fgi_graph* g, const uint64_t* keys, const uint64_t* tags, uint64_t m);
+
+// device entries (dependant local << 32 | used global, tag) appended to the in-store
+fgi_status part_store_in_dev(fgi_graph* g, const uint64_t* keys, const uint64_t* tags, uint64_t m) {
+    return part_store_in(g, keys, tags, m);
+}
 
 fgi_status part_set_bucket(fgi_graph* g, int64_t words) {
     PartState* p = ps(g);
@@ -1061,6 +1141,102 @@ fgi_status fgi_part_local_invalidate(fgi_graph* const* gs, uint32_t P, uint32_t 
     for (uint32_t r = 0; r < P; ++r)
         if (st[r] != FGI_OK) return st[r];
     return FGI_OK;
+}
+
+// Checks that gs[0..P) is one in-process group, rank by rank; returns its first member's comm.
+static fgi_status local_group(fgi_graph* const* gs, uint32_t P, LocalComm** out) {
+    if (!gs || P == 0) return FGI_EINVAL;
+    LocalComm* c0 = nullptr;
+    for (uint32_t r = 0; r < P; ++r) {
+        if (!gs[r] || !gs[r]->part || ps(gs[r])->v.world != P) return FGI_EINVAL;
+        LocalComm* c = dynamic_cast<LocalComm*>(ps(gs[r])->ops.get());
+        if (!c || c->rank != r) return set_err(gs[r], FGI_EINVAL, "graph is not rank %u of an in-process group", r);
+        if (c0 && c->grp != c0->grp) return set_err(gs[r], FGI_EINVAL, "graphs of different in-process groups");
+        c0 = c;
+    }
+    *out = c0;
+    return FGI_OK;
+}
+
+// Runs fn(rank) on one host thread per rank of an in-process group (the ranks' collectives meet
+// in the group); a failing rank fails the group so that the others leave their collectives.
+extern "C++" template <class F>
+static fgi_status local_run(fgi_graph* const* gs, uint32_t P, LocalComm* c0, F fn) {
+    c0->grp->reset();
+    std::vector<fgi_status> st(P, FGI_OK);
+    std::vector<std::thread> ts;
+    for (uint32_t r = 0; r < P; ++r) {
+        ts.emplace_back([&, r]() {
+            hipSetDevice(gs[r]->device);
+            const fgi_status s = fn(r);
+            if (s != FGI_OK) c0->grp->fail();
+            st[r] = s;
+        });
+    }
+    for (auto& t : ts) t.join();
+    for (uint32_t r = 0; r < P; ++r)
+        if (st[r] != FGI_OK) return st[r];
+    return FGI_OK;
+}
+
+// fgi_part_run_batch on every rank of an in-process group. Each rank writes its step outputs into
+// private buffers; they are merged afterwards: a detached handle comes from the slot's owner, the
+// add_used results and set flags (which every rank computes) must agree across the ranks.
+fgi_status fgi_part_local_run_batch(fgi_graph* const* gs, uint32_t P, uint32_t n_steps, const fgi_step* steps,
+                                    uint32_t* out_ids, uint64_t cap, uint64_t* out_n, fgi_batch_stats* stats) {
+    LocalComm* c0 = nullptr;
+    FGI_TRY(local_group(gs, P, &c0));
+    if (n_steps && !steps) return FGI_EINVAL;
+    std::vector<std::vector<fgi_step>> rs(P, std::vector<fgi_step>(steps, steps + n_steps));
+    std::vector<std::vector<std::vector<uint32_t>>> outs(P, std::vector<std::vector<uint32_t>>(n_steps));
+    for (uint32_t r = 0; r < P; ++r)
+        for (uint32_t k = 0; k < n_steps; ++k)
+            if (steps[k].out) {
+                outs[r][k].assign(steps[k].n, 0);   // u8 flags fit in the first quarter
+                rs[r][k].out = outs[r][k].data();
+            }
+    std::vector<std::vector<uint32_t>> ids(P);
+    std::vector<uint64_t> nid(P, 0);
+    FGI_TRY(local_run(gs, P, c0, [&](uint32_t r) -> fgi_status {
+        fgi_batch_stats* sr = stats ? stats + r : nullptr;
+        if (sr) *sr = fgi_batch_stats{};
+        if (out_ids) ids[r].resize(cap);
+        return fgi_part_run_batch(gs[r], n_steps, rs[r].data(), out_ids ? ids[r].data() : nullptr, cap, &nid[r], sr);
+    }));
+    uint64_t total = 0;
+    for (uint32_t r = 0; r < P; ++r) total += nid[r];
+    if (out_n) *out_n = total;
+    if (out_ids && total > cap) return FGI_ECAPACITY;
+    for (uint32_t r = 0, at = 0; out_ids && r < P; at += (uint32_t)nid[r], ++r)
+        std::memcpy(out_ids + at, ids[r].data(), nid[r] * 4);
+    for (uint32_t k = 0; k < n_steps; ++k) {
+        const fgi_step& sp = steps[k];
+        if (!sp.out) continue;
+        if (sp.kind == FGI_STEP_BEGIN_COMPUTE) {
+            auto* o = static_cast<uint32_t*>(sp.out);
+            for (uint32_t i = 0; i < sp.n; ++i) {
+                o[i] = FGI_NONE;
+                for (uint32_t r = 0; r < P; ++r) {
+                    const PartView& v = ps(gs[r])->v;
+                    if (sp.handles[i] - v.base < v.n_local) o[i] = outs[r][k][i];
+                }
+            }
+        } else {
+            const size_t bytes = sp.kind == FGI_STEP_SET_OUTPUT ? sp.n : (size_t)sp.n * 4;
+            for (uint32_t r = 1; r < P; ++r)
+                if (std::memcmp(outs[r].at(k).data(), outs[0][k].data(), bytes) != 0)
+                    return set_err(gs[r], FGI_ESTATE, "step %u: rank %u's results differ from rank 0's", k, r);
+            std::memcpy(sp.out, outs[0][k].data(), bytes);
+        }
+    }
+    return FGI_OK;
+}
+
+// fgi_part_prune on every rank of an in-process group (stats: P entries, nullable).
+fgi_status fgi_part_local_prune(fgi_graph* const* gs, uint32_t P, fgi_prune_stats* stats) {
+    LocalComm* c0 = nullptr;
+    FGI_TRY(local_group(gs, P, &c0));
+    return local_run(gs, P, c0, [&](uint32_t r) { return fgi_part_prune(gs[r], stats ? stats + r : nullptr); });
 }
 
 // The RCCL library the engine's collectives bind to: the file its entry points were resolved from

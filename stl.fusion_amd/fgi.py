@@ -142,6 +142,16 @@ SIGNATURES = {
     "fgi_part_local_invalidate": [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32, _u32p, _u8p, C.POINTER(WaveStats)],
     "fgi_rccl_info": [C.POINTER(C.c_int), C.c_char_p, C.c_uint64],
     "fgi_run_batch": [_G, C.c_uint32, C.POINTER(Step), _u32p, C.c_uint64, _u64p, C.POINTER(BatchStats)],
+    "fgi_part_begin_compute": [_G, C.c_uint32, _u32p, _u64p, _u8p, _u32p, _u32p, C.c_uint64, _u64p,
+                               C.POINTER(WaveStats)],
+    "fgi_part_add_used": [_G, C.c_uint32, _u32p, _u32p, _u32p],
+    "fgi_part_set_output": [_G, C.c_uint32, _u32p, _u8p, _u32p, C.c_uint64, _u64p, C.POINTER(WaveStats)],
+    "fgi_part_invalidate_all": [_G, _u32p, C.c_uint64, _u64p, C.POINTER(WaveStats)],
+    "fgi_part_run_batch": [_G, C.c_uint32, C.POINTER(Step), _u32p, C.c_uint64, _u64p, C.POINTER(BatchStats)],
+    "fgi_part_prune": [_G, C.POINTER(PruneStats)],
+    "fgi_part_local_run_batch": [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32, C.POINTER(Step), _u32p, C.c_uint64,
+                                 _u64p, C.POINTER(BatchStats)],
+    "fgi_part_local_prune": [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(PruneStats)],
 }
 
 _lib = None
@@ -181,6 +191,52 @@ def _u64(a) -> np.ndarray:
 
 def _u8(a) -> np.ndarray:
     return np.ascontiguousarray(np.asarray(a, dtype=np.uint8))
+
+
+def build_steps(steps):
+    """fgi_step array for fgi_run_batch / fgi_part_run_batch (see Graph.run_batch); returns (array,
+    arrays to keep alive, per-step output arrays or None)."""
+    arr = (Step * len(steps))()
+    keep, outs = [], []
+    for k, sp in enumerate(steps):
+        kind = sp[0]
+        h = _u32(sp[1])
+        keep.append(h)
+        st = arr[k]
+        st.n = len(h)
+        st.handles = h.ctypes.data
+        out = None
+        if kind == "invalidate":
+            st.kind = STEP_INVALIDATE
+            if len(sp) > 2 and sp[2] is not None:
+                f = _u8(sp[2])
+                keep.append(f)
+                st.flags = f.ctypes.data
+        elif kind == "begin_compute":
+            st.kind = STEP_BEGIN_COMPUTE
+            v = _u64(sp[2])
+            keep.append(v)
+            st.version = v.ctypes.data
+            if len(sp) > 3 and sp[3] is not None:
+                f = _u8(sp[3])
+                keep.append(f)
+                st.flags = f.ctypes.data
+            out = np.empty(len(h), np.uint32)   # every element is written
+        elif kind == "add_used":
+            st.kind = STEP_ADD_USED
+            u = _u32(sp[2])
+            keep.append(u)
+            st.used = u.ctypes.data
+            out = np.empty(len(h), np.uint32)   # every element is written
+        elif kind == "set_output":
+            st.kind = STEP_SET_OUTPUT
+            out = np.empty(len(h), np.uint8)
+        else:
+            raise ValueError(kind)
+        if out is not None:
+            st.out = out.ctypes.data
+        outs.append(out)
+    return arr, keep, outs
 
 
 class Graph:
@@ -330,57 +386,21 @@ class Graph:
         ("begin_compute", slots, versions[, has_delay]), ("add_used", dependants, used),
         ("set_output", handles). Returns (ids of every cascade of the batch, per-step outputs: detached
         handles / add_used results / set flags, None for invalidate)."""
-        arr = (Step * len(steps))()
-        keep, outs = [], []
-        for k, sp in enumerate(steps):
-            kind = sp[0]
-            h = _u32(sp[1])
-            keep.append(h)
-            st = arr[k]
-            st.n = len(h)
-            st.handles = h.ctypes.data
-            out = None
-            if kind == "invalidate":
-                st.kind = STEP_INVALIDATE
-                if len(sp) > 2 and sp[2] is not None:
-                    f = _u8(sp[2])
-                    keep.append(f)
-                    st.flags = f.ctypes.data
-            elif kind == "begin_compute":
-                st.kind = STEP_BEGIN_COMPUTE
-                v = _u64(sp[2])
-                keep.append(v)
-                st.version = v.ctypes.data
-                if len(sp) > 3 and sp[3] is not None:
-                    f = _u8(sp[3])
-                    keep.append(f)
-                    st.flags = f.ctypes.data
-                out = np.empty(len(h), np.uint32)   # every element is written
-            elif kind == "add_used":
-                st.kind = STEP_ADD_USED
-                u = _u32(sp[2])
-                keep.append(u)
-                st.used = u.ctypes.data
-                out = np.empty(len(h), np.uint32)   # every element is written
-            elif kind == "set_output":
-                st.kind = STEP_SET_OUTPUT
-                out = np.empty(len(h), np.uint8)
-            else:
-                raise ValueError(kind)
-            if out is not None:
-                st.out = out.ctypes.data
-            outs.append(out)
+        return self._batch(self.lib.fgi_run_batch, "run_batch", steps, stats, want_ids)
+
+    def _batch(self, fn, what, steps, stats, want_ids):
+        arr, keep, outs = build_steps(steps)
         n = C.c_uint64()
         if want_ids:
             cap = max(1, sum(1 for sp in steps if sp[0] != "add_used")) * self.n_handles
             buf = getattr(self, "_ids_buf", None)
             if buf is None or len(buf) < cap:
                 buf = self._ids_buf = np.empty(cap, np.uint32)   # reused across batches
-            self._check(self.lib.fgi_run_batch(self.h, len(steps), arr, _ptr(buf, C.c_uint32), cap, C.byref(n),
-                                               C.byref(stats) if stats is not None else None), "run_batch")
+            self._check(fn(self.h, len(steps), arr, _ptr(buf, C.c_uint32), cap, C.byref(n),
+                           C.byref(stats) if stats is not None else None), what)
             return buf[:n.value].copy(), outs
-        self._check(self.lib.fgi_run_batch(self.h, len(steps), arr, None, 0, C.byref(n),
-                                           C.byref(stats) if stats is not None else None), "run_batch")
+        self._check(fn(self.h, len(steps), arr, None, 0, C.byref(n), C.byref(stats) if stats is not None else None),
+                    what)
         return n.value, outs
 
     def invalidate_into(self, roots, out_ptr: int, cap: int, stats: Optional[WaveStats] = None) -> int:
@@ -497,6 +517,55 @@ class Graph:
                                                  C.byref(stats) if stats is not None else None), "part_invalidate")
         return n.value
 
+    def part_begin_compute(self, slots, versions, has_delay=None, stats: Optional[WaveStats] = None):
+        """fgi_part_begin_compute: (detached local handles on the owner / FGI_NONE, this rank's ids
+        of the displacement cascade)."""
+        s, v = _u32(slots), _u64(versions)
+        hd = None if has_delay is None else _u8(has_delay)
+        out = np.zeros(len(s), np.uint32)
+        ids = np.zeros(self.n_handles, np.uint32)
+        n = C.c_uint64()
+        self._check(self.lib.fgi_part_begin_compute(self.h, len(s), _ptr(s, C.c_uint32), _ptr(v, C.c_uint64),
+                                                    _ptr(hd, C.c_uint8), _ptr(out, C.c_uint32), _ptr(ids, C.c_uint32),
+                                                    len(ids), C.byref(n),
+                                                    C.byref(stats) if stats is not None else None), "part_begin_compute")
+        return out, ids[:n.value].copy()
+
+    def part_add_used(self, dependant, used) -> np.ndarray:
+        d, u = _u32(dependant), _u32(used)
+        out = np.zeros(len(d), np.uint32)
+        self._check(self.lib.fgi_part_add_used(self.h, len(d), _ptr(d, C.c_uint32), _ptr(u, C.c_uint32),
+                                               _ptr(out, C.c_uint32)), "part_add_used")
+        return out
+
+    def part_set_output(self, slots, stats: Optional[WaveStats] = None):
+        h = _u32(slots)
+        out_set = np.zeros(len(h), np.uint8)
+        ids = np.zeros(self.n_handles, np.uint32)
+        n = C.c_uint64()
+        self._check(self.lib.fgi_part_set_output(self.h, len(h), _ptr(h, C.c_uint32), _ptr(out_set, C.c_uint8),
+                                                 _ptr(ids, C.c_uint32), len(ids), C.byref(n),
+                                                 C.byref(stats) if stats is not None else None), "part_set_output")
+        return out_set, ids[:n.value].copy()
+
+    def part_invalidate_all(self, stats: Optional[WaveStats] = None) -> np.ndarray:
+        ids = np.zeros(self.n_handles, np.uint32)
+        n = C.c_uint64()
+        self._check(self.lib.fgi_part_invalidate_all(self.h, _ptr(ids, C.c_uint32), len(ids), C.byref(n),
+                                                     C.byref(stats) if stats is not None else None),
+                    "part_invalidate_all")
+        return ids[:n.value].copy()
+
+    def part_run_batch(self, steps, stats: Optional[BatchStats] = None, want_ids: bool = True):
+        """fgi_part_run_batch: run_batch's steps with global slot ids; every rank passes the same batch.
+        Returns (this rank's ids of the batch's cascades, per-step outputs)."""
+        return self._batch(self.lib.fgi_part_run_batch, "part_run_batch", steps, stats, want_ids)
+
+    def part_prune(self) -> PruneStats:
+        ps = PruneStats()
+        self._check(self.lib.fgi_part_prune(self.h, C.byref(ps)), "part_prune")
+        return ps
+
     def part_front_stats(self):
         """(full all-gathers, delta exchanges, bytes received) of this rank's frontier exchanges."""
         f, d, b = C.c_uint64(), C.c_uint64(), C.c_uint64()
@@ -582,6 +651,38 @@ def part_local_invalidate(graphs, roots, immediately=None):
     st = lib.fgi_part_local_invalidate(arr, len(graphs), len(r), _ptr(r, C.c_uint32), _ptr(imm, C.c_uint8), stats)
     if st != OK:
         raise FgiError(st, "fgi_part_local_invalidate")
+    return list(stats)
+
+
+def _local_error(lib, graphs, st, what):
+    msgs = [(lib.fgi_last_error(g.h) or b"").decode() for g in graphs]
+    raise FgiError(st, what + ": " + "; ".join(m for m in msgs if m))
+
+
+def part_local_run_batch(graphs, steps):
+    """fgi_part_local_run_batch: the batch on every rank of an in-process group. Returns (ids of the
+    batch's cascades, rank 0's then rank 1's ..., merged per-step outputs, per-rank BatchStats)."""
+    lib = load_library()
+    arr_g = (C.c_void_p * len(graphs))(*[g.h.value for g in graphs])
+    arr, keep, outs = build_steps(steps)
+    cap = max(1, sum(1 for sp in steps if sp[0] != "add_used")) * sum(g.n_handles for g in graphs)
+    ids = np.empty(cap, np.uint32)
+    n = C.c_uint64()
+    stats = (BatchStats * len(graphs))()
+    st = lib.fgi_part_local_run_batch(arr_g, len(graphs), len(steps), arr, _ptr(ids, C.c_uint32), cap, C.byref(n),
+                                      stats)
+    if st != OK:
+        _local_error(lib, graphs, st, "fgi_part_local_run_batch")
+    return ids[:n.value].copy(), outs, list(stats)
+
+
+def part_local_prune(graphs):
+    lib = load_library()
+    arr_g = (C.c_void_p * len(graphs))(*[g.h.value for g in graphs])
+    stats = (PruneStats * len(graphs))()
+    st = lib.fgi_part_local_prune(arr_g, len(graphs), stats)
+    if st != OK:
+        _local_error(lib, graphs, st, "fgi_part_local_prune")
     return list(stats)
 
 
