@@ -530,6 +530,9 @@ fgi_status part_allreduce_u32(fgi_graph* g, uint32_t* dev, uint64_t n);
 fgi_status part_cur_buffers(fgi_graph* g, unsigned long long** local, unsigned long long** all, uint64_t* w64);
 fgi_status part_allgather_cur(fgi_graph* g);
 fgi_status part_store_in_dev(fgi_graph* g, const uint64_t* keys, const uint64_t* tags, uint64_t m);
+// the dependency entries whose used end is one of the global slots listed (host, any order) die:
+// their node was displaced while it stayed current (Computing, or a delayed invalidation pending)
+fgi_status part_kill_used(fgi_graph* g, std::vector<uint32_t> slots);
 // frontier exchanges of each kind so far and the bytes this rank received through them
 fgi_status part_front_stats(fgi_graph* g, uint64_t* full, uint64_t* delta, uint64_t* bytes);
 // Rebuild a partition's pull lists from its dependency-entry store if rows or versions changed.

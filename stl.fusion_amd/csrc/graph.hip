@@ -3291,16 +3291,29 @@ fgi_status part_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, co
     }
     unsigned long long cnt[2];
     FGI_TRY(d2h(g, cnt, g->misc_dev, 2));
-    // every rank detaches its displaced survivors, or no rank applies the call
-    FGI_TRY(tmalloc(g, tflag, &dflag, 1));
-    const uint32_t short_h = cnt[1] > g->free_detached.size() ? 1u : 0u;
-    FGI_TRY(h2d(g, dflag, &short_h, 1));
-    FGI_TRY(part_allreduce_u32(g, dflag, 1));
-    uint32_t any_short = 0;
-    FGI_TRY(d2h(g, &any_short, dflag, 1));
-    if (any_short)
+    // one all-reduce: which items each owner detaches (their slots' nodes stay current), and whether
+    // any rank is short of detached handles — then every rank applies the call, or none does
+    std::vector<uint8_t> cls(m);
+    if (m) FGI_TRY(d2h(g, cls.data(), dcls, m));
+    std::vector<uint32_t> fl(n + 1, 0);
+    for (uint32_t j = 0; j < m; ++j) fl[li[j]] = cls[j] == 2 ? 1u : 0u;
+    fl[n] = cnt[1] > g->free_detached.size() ? 1u : 0u;
+    FGI_TRY(tmalloc(g, tflag, &dflag, n + 1));
+    FGI_TRY(h2d(g, dflag, fl.data(), n + 1));
+    FGI_TRY(part_allreduce_u32(g, dflag, n + 1));
+    FGI_TRY(d2h(g, fl.data(), dflag, n + 1));
+    if (fl[n])
         return set_err(g, FGI_ECAPACITY, "a rank is out of detached handles (this one: %zu free, %llu needed)",
                        g->free_detached.size(), cnt[1]);
+    // A detached node keeps its row under a local handle no slot id reaches, so its dependants' entries
+    // must leave their pull lists (push levels start from the slot's new, empty row); this rank's
+    // dependency entries on any rank's detached slots die
+    {
+        std::vector<uint32_t> det;
+        for (uint32_t i = 0; i < n; ++i)
+            if (fl[i]) det.push_back(slot[i]);
+        FGI_TRY(part_kill_used(g, std::move(det)));
+    }
     // the displacement cascade (ComputedRegistry.cs:91-94) on every rank, then versions and installs
     if (cnt[0]) hipLaunchKernelGGL(k_add_base, dim3(nblk(cnt[0])), dim3(256), 0, st, (uint32_t)cnt[0], droots, pv.base);
     g->last_wave_n = 0;

@@ -596,6 +596,40 @@ fgi_status part_store_in_dev(fgi_graph* g, const uint64_t* keys, const uint64_t*
     return part_store_in(g, keys, tags, m);
 }
 
+namespace {
+// entries (dependant local << 32 | used global) whose used end is in the sorted list: tag 0 (a
+// version is never 0, so the list build reads them as dead)
+__global__ void k_in_kill(uint64_t m, const uint64_t* __restrict__ keys, uint64_t* tags, const uint32_t* __restrict__ list,
+                          uint32_t nl) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= m) return;
+    const uint32_t u = (uint32_t)keys[i];
+    uint32_t lo = 0, hi = nl;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (list[mid] < u) lo = mid + 1;
+        else hi = mid;
+    }
+    if (lo < nl && list[lo] == u) tags[i] = 0;
+}
+}  // namespace
+
+fgi_status part_kill_used(fgi_graph* g, std::vector<uint32_t> slots) {
+    PartState* p = ps(g);
+    if (slots.empty() || p->in_n == 0) return FGI_OK;
+    std::sort(slots.begin(), slots.end());
+    slots.erase(std::unique(slots.begin(), slots.end()), slots.end());
+    uint32_t* d = nullptr;
+    if (hipMalloc(&d, slots.size() * 4) != hipSuccess) return set_err(g, FGI_ENOMEM, "displaced-slot list");
+    hipMemcpyAsync(d, slots.data(), slots.size() * 4, hipMemcpyHostToDevice, g->stream);
+    hipLaunchKernelGGL(k_in_kill, dim3((uint32_t)((p->in_n + 255) / 256)), dim3(256), 0, g->stream, p->in_n, p->in_keys, p->in_tags, d,
+                       (uint32_t)slots.size());
+    const hipError_t e = hipStreamSynchronize(g->stream);
+    hipFree(d);
+    FGI_HIP(g, e);
+    return FGI_OK;
+}
+
 fgi_status part_set_bucket(fgi_graph* g, int64_t words) {
     PartState* p = ps(g);
     if (!p) return set_err(g, FGI_ESTATE, "partition not initialised");

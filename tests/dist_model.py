@@ -177,3 +177,141 @@ class RankModel:
         fl = [None] * self.world
         dist.all_gather_object(fl, self.flags.tolist())
         return sorted(x for part in inv for x in part), np.concatenate([np.asarray(f, np.uint32) for f in fl])
+
+
+# ---- the registry's mutations on a partition (part_* in stl.fusion_amd/csrc/graph.hip) -----------
+# Every rank makes the same call with the same global arrays; each applies its own slots. A displaced
+# node leaves the slot (its handle is local and unreachable through slot ids), so the model drops it.
+
+def _own(m, s):
+    return m.lo <= s < m.hi
+
+
+def begin_compute(m, slots, versions, has_delay, direction="auto"):
+    """ComputedRegistry.Register with displacement (ComputedRegistry.cs:83-97): the owners' current
+    Consistent undelayed nodes are the displacement cascade's roots (one partitioned wave); then every
+    rank records the new versions in its replica and the owners install Computing nodes with empty
+    `_usedBy` / `_used`."""
+    roots = []
+    det = torch.zeros(len(slots), dtype=torch.int64)
+    for k, s in enumerate(slots):
+        s = int(s)
+        if _own(m, s):
+            i = s - m.lo
+            f = int(m.flags[i])
+            if m.ver[i] != 0 and (f & 3) == CONSISTENT and not (f & F_HD):
+                roots.append(s)
+            elif m.ver[i] != 0 and (f & 3) != INVALIDATED:
+                det[k] = 1      # displaced while current: detached, out of every slot-addressed path
+    dist.all_reduce(det)
+    gone = {int(s) for k, s in enumerate(slots) if det[k]}
+    for d in m.deps:
+        m.deps[d] -= gone
+    m.wave(roots, direction=direction, alpha=6)
+    for s, v, h in zip(slots, versions, has_delay):
+        s = int(s)
+        m.ver_all[s] = v
+        if _own(m, s):
+            i = s - m.lo
+            m.ver[i] = v
+            m.flags[i] = COMPUTING | (F_HD if h else 0)
+            m.rows[s] = []
+            m.deps.pop(s, None)
+
+
+def add_used(m, dep, used):
+    """AddUsed / AddUsedBy (Computed.cs:347-385) for pairs whose ends may live on different ranks:
+    the dependant's owner says whether it is Computing (all-reduce), the used node's owner applies the
+    rules and appends (dependant, version), the codes are all-reduced, the dependant's owner flags
+    InvalidateOnSetOutput or records the dependency. Returns the FGI_USED_* codes (every rank)."""
+    n = len(dep)
+    comp = torch.zeros(n, dtype=torch.int64)
+    for k in range(n):
+        d = int(dep[k])
+        if _own(m, d):
+            i = d - m.lo
+            comp[k] = int(m.ver[i] != 0 and (int(m.flags[i]) & 3) == COMPUTING)
+    dist.all_reduce(comp)
+    res = torch.zeros(n, dtype=torch.int64)
+    for k in range(n):
+        d, u = int(dep[k]), int(used[k])
+        if not _own(m, u):
+            continue
+        j = u - m.lo
+        st = int(m.flags[j]) & 3
+        if not comp[k]:
+            code = 1                                   # dropped
+        elif m.ver[j] == 0 or st == INVALIDATED:
+            code = 2                                   # invalidated
+        elif st == COMPUTING:
+            code = 3                                   # wrong state
+        else:
+            code = 0
+            e = (d, int(m.ver_all[d]))
+            row = m.rows.setdefault(u, [])
+            if e not in row:
+                row.append(e)
+        res[k] = code + 1
+    dist.all_reduce(res)
+    codes = (res - 1).numpy()
+    for k in range(n):
+        d, u = int(dep[k]), int(used[k])
+        if _own(m, d):
+            if codes[k] == 2:
+                m.flags[d - m.lo] |= F_IOSO
+            elif codes[k] == 0:
+                m.deps.setdefault(d, set()).add(u)
+    return codes
+
+
+def set_output(m, slots, direction="auto"):
+    """TrySetOutput (Computed.cs:141-160): the owners' Computing nodes become Consistent; those flagged
+    InvalidateOnSetOutput are the roots of one partitioned wave. Returns how many were set."""
+    setf = torch.zeros(len(slots), dtype=torch.int64)
+    roots = []
+    for k, s in enumerate(slots):
+        s = int(s)
+        if _own(m, s):
+            i = s - m.lo
+            f = int(m.flags[i])
+            if m.ver[i] != 0 and (f & 3) == COMPUTING:
+                setf[k] = 1
+                m.flags[i] = CONSISTENT | (f & (F_HD | F_DS))
+                if f & F_IOSO:
+                    roots.append(s)
+    m.wave(roots, direction=direction, alpha=6)
+    dist.all_reduce(setf)
+    return int(setf.sum())
+
+
+def prune(m):
+    """PruneUsedBy (Computed.cs:400-419) on the owners' Consistent nodes: an entry stays iff its
+    dependant is registered (current, not Invalidated) at the entry's version; "current" comes from an
+    all-gather of the owners' states (the engine's current-node bitmap), the version from the replica.
+    Returns the entries left on this rank."""
+    cur = np.zeros(m.n, bool)
+    mine = np.zeros(m.hi - m.lo, bool)
+    mine[:] = (m.ver != 0) & ((m.flags & 3) != INVALIDATED)
+    cur[m.lo:m.hi] = mine
+    parts = [torch.zeros(m.n, dtype=torch.bool) for _ in range(m.world)]
+    dist.all_gather(parts, torch.from_numpy(cur))
+    cur = np.logical_or.reduce([p.numpy() for p in parts])
+    left = 0
+    for u, row in m.rows.items():
+        i = u - m.lo
+        if m.ver[i] == 0 or (int(m.flags[i]) & 3) != CONSISTENT:
+            continue
+        m.rows[u] = [(d, t) for d, t in row if cur[d] and m.ver_all[d] == t]
+        left += len(m.rows[u])
+    return left
+
+
+def live_rows(m):
+    """(used, dependant, tag) of the `_usedBy` rows of this rank's registered nodes."""
+    out = []
+    for u, row in m.rows.items():
+        i = u - m.lo
+        if m.ver[i] == 0 or (int(m.flags[i]) & 3) == INVALIDATED:
+            continue
+        out += [(u, d, t) for d, t in row]
+    return out

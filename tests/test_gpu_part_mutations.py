@@ -145,10 +145,14 @@ def _churn_batch(rng, n, present, next_version):
     return steps, next_version + 2 * len(bc)
 
 
+@pytest.mark.parametrize("direction", [0, 2])
 @pytest.mark.parametrize("P", [2, 3, 8])
-def test_random_churn_then_prune_on_partitions(pkg, gpu_available, P):
+def test_random_churn_then_prune_on_partitions(pkg, gpu_available, P, direction):
     """Mixed node states on an R-MAT 12 graph (20% stale entries), eight random batches, then a
-    partitioned prune (prune-after-churn) and a wave on the pruned graph."""
+    partitioned prune (prune-after-churn) and a wave on the pruned graph; auto and pull-only levels
+    (P = 3's ragged ranges have no pull lists: push). The first batch recomputes a delayed node that
+    holds a live entry of an undelayed dependant: the old node is detached, so the wave on the new node
+    must not reach the dependant through the pull lists, which named the used node by its slot."""
     scale, ef, seed, sseed = 12, 8, 7, 0x5EED00C0
     n = 1 << scale
     rng = np.random.default_rng(1000 + P)
@@ -163,6 +167,15 @@ def test_random_churn_then_prune_on_partitions(pkg, gpu_available, P):
     o = O.Oracle(n)
     o.load_graph(versions, flags, s, d, tags)
     _check_states(gs, o, n, block)
+    for g in gs:
+        g.set_option(pkg.fgi.OPT_DIRECTION, direction)
+    st = flags & 3
+    ok = ((st[s] == CONSISTENT) & ((flags[s] & 16) != 0) & (versions[s] != 0) & (st[d] == CONSISTENT) &
+          ((flags[d] & 16) == 0) & (tags == versions[d]))
+    u = int(s[np.nonzero(ok)[0][0]])
+    ids, _, _ = _run_both(pkg, gs, o, [("begin_compute", [u], [(1 << 45) | 1], [0]), ("set_output", [u]),
+                                       ("invalidate", [u])], n, block)
+    assert list(ids) == [u]
     nv = 1 << 40 | 1
     codes = set()
     for b in range(8):
