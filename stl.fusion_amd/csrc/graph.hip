@@ -1450,9 +1450,12 @@ fgi_status build_in_heads(fgi_graph* g) {
 // Hot heads for a graph of n handles: one per 512 handles, a power of two in [kHotMin, kHot]. A/B on
 // one box (profiles/r5e_ab.txt): 64 Ki -> 256 Ki heads took configs[2]'s pull levels from 1.105 to
 // 1.020 ms per wave; on configs[1] a snapshot past 64 Ki costs more to refresh than it saves.
+#ifndef FGI_HOT_DIV
+#define FGI_HOT_DIV 512   // measurement builds: make variant-hot HOT=<n> HOT_DIV=<handles per hot head>
+#endif
 uint32_t hot_count(uint64_t n) {
     uint32_t k = kHotMin;
-    while (k < kHot && k < n / 512) k <<= 1;
+    while (k < kHot && k < n / FGI_HOT_DIV) k <<= 1;
     return k;
 }
 

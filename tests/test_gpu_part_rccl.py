@@ -51,3 +51,61 @@ def test_rccl_partition_world1_matches_oracle(pkg, gpu_available, stale, directi
         v, f = g.dump_states()
         assert np.array_equal(v[:n], ov), wave
         assert np.array_equal(f[:n], of), wave
+
+
+@pytest.mark.parametrize("collectives", [1, 0])
+def test_rccl_partition_world1_mutations_match_oracle(pkg, gpu_available, collectives):
+    """fgi_part_run_batch / fgi_part_invalidate_all / fgi_part_prune through a real RCCL communicator
+    (world size 1): the add_used and begin_compute all-reduces, the cascades and the prune's
+    current-node all-gather. Per batch: the invalidated slots, add_used codes, set flags and every
+    node word against the oracle; then InvalidateEverything."""
+    from harness import canon_edges, random_states
+    from test_gpu_part_mutations import _churn_batch
+    scale, ef, seed, sseed = 11, 8, 3, 0x5EED00C0
+    n = 1 << scale
+    rng = np.random.default_rng(77)
+    versions, flags = random_states(n, rng, seed=seed)
+    s, d = O.gen_rmat(scale, ef, seed)
+    tags = O.gen_tags(s, d, seed, 20, sseed)
+    g = pkg.Graph(n, n_detached=256, rank=0, world=1)
+    g.part_init(n, pkg.fgi.part_unique_id())
+    g.set_option(pkg.fgi.OPT_PART_COLLECTIVES, collectives)
+    present = np.nonzero(versions)[0].astype(np.uint32)
+    g.part_register_nodes(present, versions[present], flags[present])
+    g.part_load_edges(s, d, tags)
+    o = O.Oracle(n)
+    o.load_graph(versions, flags, s, d, tags)
+    nv = (1 << 41) | 1
+    for b in range(4):
+        ov, _ = o.dump_states()
+        steps, nv = _churn_batch(rng, n, ov != 0, nv)
+        ids, outs = g.part_run_batch(steps)
+        o.clear_log()
+        for sp in steps:
+            if sp[0] == "invalidate":
+                o.invalidate_slots(sp[1], sp[2] if len(sp) > 2 else None)
+            elif sp[0] == "begin_compute":
+                o.begin_compute_slots(sp[1], sp[2], sp[3])
+            elif sp[0] == "add_used":
+                assert np.array_equal(outs[2], o.add_used_slots(sp[1], sp[2])), b
+            else:
+                assert int(outs[3].sum()) == o.set_output_slots(sp[1]), b
+        assert np.array_equal(np.sort(ids), np.sort(o.inv_log())), b
+        v, f = g.dump_states()
+        ov, of = o.dump_states()
+        assert np.array_equal(v[:n], ov) and np.array_equal(f[:n], of), b
+    ps = g.part_prune()
+    _, ne = o.prune()
+    assert ps.new_edges == ne
+    u, dd, t = g.export_edges()
+    keep = u < n
+    assert np.array_equal(canon_edges(u[keep], dd[keep], t[keep]), canon_edges(*o.export_used_by()))
+    o.clear_log()
+    ids = g.part_invalidate_all()
+    o.invalidate_everything()
+    assert np.array_equal(np.sort(ids), np.sort(o.inv_log()))
+    v, f = g.dump_states()
+    ov, of = o.dump_states()
+    assert np.array_equal(v[:n], ov) and np.array_equal(f[:n], of)
+    o.close()
+    g.close()
