@@ -227,7 +227,8 @@ def main():
         _, n_edges = g.degrees()
     build_s = time.time() - t0
     for k, v in (("FGI_PULL_ALPHA", "OPT_PULL_ALPHA"), ("FGI_PULL_BETA", "OPT_PULL_BETA"), ("FGI_PULL_TPB", "OPT_PULL_TPB"),
-                 ("FGI_PART_PLAN", "OPT_PART_PLAN")):
+                 ("FGI_PART_PLAN", "OPT_PART_PLAN"), ("FGI_PROBE_SUMMARY", "OPT_PROBE_SUMMARY"),
+                 ("FGI_HOT_HEADS", "OPT_HOT_HEADS")):
         if os.environ.get(k):   # measurement knobs (results never depend on them)
             g.set_option(getattr(pkg.fgi, v), int(os.environ[k]))
     d_roots = torch.from_numpy(roots.astype(np.int32)).to(f"cuda:{local_rank}")

@@ -161,7 +161,7 @@ struct LevelCtr {
     unsigned long long w;       // pull level L-1: its winners (the frontier count before rows)
     unsigned long long mult;    // push: fine chunks per expand chunk
     unsigned long long npull;   // pull levels of the wave before this one (which candidate list to read)
-    unsigned long long pad1;
+    unsigned long long sum;     // pull level: 1 if k_collect built the nonzero-word summary for its probes
 };
 
 // A level's frontier totals: a push producer leaves them packed in ft (the single engine does not
@@ -364,6 +364,11 @@ struct fgi_graph {
     int opt_pull_alpha = 28;           // profiles/r2y_direction_sweep.jsonl: 28 beats 14 on configs[0] (-6%) and [1] (-1%)
     int opt_pull_tpb = 0;             // pull tiles per block (0: from the CU count; tests)
     int opt_hot_heads = 0;            // FGI_OPT_HOT_HEADS: cap on the hot heads (0: by graph size)
+    // probe summary: one bit per 64-bit word of the invalidated bitmap (set iff the word is nonzero),
+    // built before a pull level while few words can be nonzero, so cold head and tail probes that
+    // would miss are answered from an L2-resident table (FGI_OPT_PROBE_SUMMARY)
+    uint32_t* sum_bm = nullptr;
+    int64_t opt_sum_min = 1 << 19;    // fewest 64-bit bitmap words for a summary (-1: never)
     int opt_pull_beta = 24;           // after a pull, pull again while the frontier exceeds n / beta
     int opt_level_timing = 1;         // HIP events around each level's k_level launch (statistics)
     int opt_fused = fgi::fused_default();  // FGI_OPT_FUSED (kFused* bits)

@@ -1812,7 +1812,8 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
     g->bm_words = (H + 63) / 64 * 2 + 2;
     // the invalidated bitmap carries the hot heads' snapshot past its end (build_candidates)
     if (dmalloc(g, &g->vis_bm, g->bm_words) || dmalloc(g, &g->inv_bm, g->bm_words + kHot / 32) ||
-        dmalloc(g, &g->cls_bm, g->bm_words) || dmalloc(g, &g->uin_more, g->bm_words))
+        dmalloc(g, &g->cls_bm, g->bm_words) || dmalloc(g, &g->uin_more, g->bm_words) ||
+        dmalloc(g, &g->sum_bm, ((uint64_t)H + 4095) / 4096 * 2 + 2))
         return fail(FGI_ENOMEM);
     hipMemset(g->done, 0, (size_t)(kDoneGroups + 1) * kDoneStride * sizeof(unsigned long long));
     hipMemset(g->bsum, 0, 8ull * kStatBlocks * sizeof(unsigned long long));
@@ -1879,6 +1880,7 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->vis_bm);
     dfree(g->cls_bm);
     dfree(g->uin_more);
+    dfree(g->sum_bm);
     dfree(g->inv_bm);
     dfree(g->bsum);
     dfree(g->done);
@@ -2255,6 +2257,10 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
         return FGI_OK;
     case FGI_OPT_PART_PLAN: g->opt_part_plan = value ? 1 : 0; return FGI_OK;
     case FGI_OPT_PART_BUCKET: return part_set_bucket(g, value);
+    case FGI_OPT_PROBE_SUMMARY:
+        if (value < -1 || value > (int64_t)FGI_NONE) return set_err(g, FGI_EINVAL, "probe summary: -1 or a word count");
+        g->opt_sum_min = value;
+        return FGI_OK;
     case FGI_OPT_FUSED:
         if (value < 0 || value > 15) return set_err(g, FGI_EINVAL, "fused-wave bits must be 0..15");
         g->opt_fused = (int)value;

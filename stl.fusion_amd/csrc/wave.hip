@@ -712,6 +712,10 @@ struct CollectArgs {
     uint32_t* hot_bm;
     uint32_t n_hot;
     const uint32_t* inv;
+    // probe summary (single engine; null for a partition): one bit per 64-bit word of inv
+    unsigned long long* sum_bm;
+    uint64_t n64;               // 64-bit words of inv the pull levels probe
+    int64_t sum_min;            // fewest words for a summary (< 0: never)
 };
 
 constexpr int kCollectThreads = 256;
@@ -724,6 +728,30 @@ __device__ __forceinline__ void collect_hot(const CollectArgs& c, uint64_t tid, 
         const uint32_t u = c.hot_id[k];
         const unsigned long long m = __ballot(u != FGI_NONE && bit_of(c.inv, u));
         if (lane_id() == 0) hot64[k >> 6] = m;
+    }
+}
+
+// Before pull level L, while few bitmap words can be nonzero (at most the invalidated count so far,
+// estimated from the levels' frontiers: sum * 8 < words), one bit per 64-bit word of the invalidated
+// bitmap, set iff the word is nonzero: a cold probe that would miss (most of them, that early) reads
+// the L2-resident summary instead of a line of a bitmap larger than L2 (R-MAT 27: 16 MB against 4 MB
+// of L2 per XCD). Level L's `sum` word says whether the pull level may use it; every pull level's
+// k_collect writes it. One summary word per wave and step (64 coalesced bitmap words).
+__device__ __forceinline__ void collect_sum(const CollectArgs& c, WaveCtr* ctr, int L, uint64_t wave, uint64_t waves) {
+    bool use = c.sum_bm != nullptr && c.sum_min >= 0 && c.n64 >= (uint64_t)c.sum_min && L < kRing - 4;
+    if (use) {
+        uint64_t S = 0;
+        for (int l = 0; l <= L; ++l) S += lvl_F(ctr->lvl[l]);
+        use = S * 8 < c.n64;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctr->lvl[L % kRing].sum = use ? 1ull : 0ull;
+    if (!use) return;
+    const unsigned long long* inv64 = reinterpret_cast<const unsigned long long*>(c.inv);
+    const uint32_t lane = lane_id();
+    for (uint64_t w = wave; w * 64 < c.n64; w += waves) {   // wave-uniform
+        const uint64_t i = w * 64 + lane;
+        const unsigned long long m = __ballot(i < c.n64 && inv64[i] != 0ull);
+        if (lane == 0) c.sum_bm[w] = m;
     }
 }
 
@@ -781,6 +809,9 @@ __global__ __launch_bounds__(kCollectThreads) void k_collect(int L, WaveCtr* ctr
     if (lvl_F(lc) == 0) return;
     if (level_pulls(ctr, L, wp)) {
         collect_hot(c, (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, (uint64_t)gridDim.x * blockDim.x);
+        if (c.sum_bm)
+            collect_sum(c, ctr, L, (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6),
+                        (uint64_t)gridDim.x * (blockDim.x >> 6));
         return;
     }
     if (fused && lvl_T(lc) <= big_push) return;
@@ -960,6 +991,7 @@ struct PullArgs {
     const uint32_t* __restrict__ uin_len;
     const uint32_t* __restrict__ uin_src;
     const uint32_t* front_rd;                // invalidated bitmap (multi-GPU: all-gathered, global ids)
+    const uint32_t* sum;                     // probe summary of front_rd (null: none; level's `sum` word)
     uint32_t hot_bit0;                       // a hot head's code: hot_bit0 + rank (its snapshot bit)
     uint32_t hot_lds;                        // hot snapshot words staged into LDS per block (<= kLdsHot)
     uint32_t* inv_bm;                        // this device's invalidated bitmap (owned words |= winners)
@@ -1021,9 +1053,18 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 // that follows the invalidated bitmap (g->hot_w0), any other head the bitmap itself. The snapshot's
 // first hot_lds words are read from the block's LDS copy: a random probe of an L2-resident bitmap
 // costs ~4x an L1 hit and ~5x an LDS read (profiles/r5f_probe_rate.txt, r5g_snap_rate.txt)
-__device__ __forceinline__ uint32_t head_bits(const PullArgs& p, const PullLds& s, uint32_t h) {
+__device__ __forceinline__ bool sum_zero(const PullArgs& p, uint32_t h) {
+    return !((p.sum[h >> 11] >> ((h >> 6) & 31)) & 1u);   // h's 64-bit bitmap word is zero
+}
+__device__ __forceinline__ uint32_t head_bits(const PullArgs& p, const PullLds& s, uint32_t h, bool sum) {
     const uint32_t r = (h - p.hot_bit0) >> 5;   // wraps past hot_lds for a cold head
-    return r < p.hot_lds ? s.hot[r] : p.front_rd[h >> 5];
+    if (r < p.hot_lds) return s.hot[r];
+    if (sum && h < p.hot_bit0 && sum_zero(p, h)) return 0u;   // a cold head in a zero word
+    return p.front_rd[h >> 5];
+}
+// a tail entry's invalidated bit (entries are handles, never hot codes)
+__device__ __forceinline__ bool front_bit(const PullArgs& p, uint32_t u, bool sum) {
+    return !(sum && sum_zero(p, u)) && bit_of(p.front_rd, u);
 }
 
 // an entry past the list reads as a dead candidate at the block's first slot
@@ -1061,7 +1102,7 @@ __device__ __forceinline__ void pull_hit(const PullArgs& p, PullLds& s, uint64_t
 // queue of candidate indices) is reused for pass 2's lists (bit 31: longer than kLaneTail).
 __device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, uint4* sv_out, const unsigned long long* node,
                                            uint64_t s_lo, uint64_t seg, uint32_t* q, uint32_t nq, PullLds& s,
-                                           uint32_t& flagged, uint32_t& examined, uint32_t& tails, WinSum& ws) {
+                                           uint32_t& flagged, uint32_t& examined, uint32_t& tails, WinSum& ws, bool sum) {
     const uint32_t lane = lane_id();
     uint32_t nlong = 0;
     for (uint32_t r0 = 0; r0 < nq; r0 += 64) {   // wave-uniform
@@ -1078,7 +1119,7 @@ __device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, 
         }
         const uint32_t u2 = (in && len > 2) ? p.uin_src[off + 2] : FGI_NONE;
         const uint32_t u3 = (in && len > 3) ? p.uin_src[off + 3] : FGI_NONE;
-        const bool hit = (u2 != FGI_NONE && bit_of(p.front_rd, u2)) || (u3 != FGI_NONE && bit_of(p.front_rd, u3));
+        const bool hit = (u2 != FGI_NONE && front_bit(p, u2, sum)) || (u3 != FGI_NONE && front_bit(p, u3, sum));
         examined += (u2 != FGI_NONE ? 1u : 0u) + (u3 != FGI_NONE ? 1u : 0u);
         const bool more = in && !hit && len > 4;
         const unsigned long long mm = __ballot(more);
@@ -1126,7 +1167,7 @@ __device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, 
 #pragma unroll
         for (uint32_t k = 0; k < kLaneTail - 4; ++k)
             if (u[k] != FGI_NONE) {
-                found |= bit_of(p.front_rd, u[k]);
+                found |= front_bit(p, u[k], sum);
                 ++examined;
             }
         if (in && found) {
@@ -1168,7 +1209,7 @@ __device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, 
         bool found = false;
         for (uint32_t r = 4; r < len && !found; r += 8) {   // group-uniform
             const uint32_t k = r + sub;
-            const bool x = k < len && bit_of(p.front_rd, p.uin_src[off + k]);
+            const bool x = k < len && front_bit(p, p.uin_src[off + k], sum);
             examined += (k < len) ? 1u : 0u;
             found = ((__ballot(x) >> (lane & ~7u)) & 0xFFull) != 0;
         }
@@ -1186,7 +1227,7 @@ __device__ __forceinline__ void pull_tails(const PullArgs& p, const uint4* src, 
     }
 }
 
-__device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveParams& wp, uint64_t npull,
+__device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveParams& wp, uint64_t npull, bool sum,
                                            const unsigned long long* node, uint32_t* vis, uint32_t* lds_q, PullLds& s,
                                            unsigned long long* blk, unsigned long long (*s_st)[kStats],
                                            unsigned long long (&bs)[3]) {
@@ -1273,8 +1314,8 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
             f0[j] = (lv[j] && (c[j].z & 1)) ? ~0u : 0u;
             f1[j] = 0u;
 #else
-            f0[j] = lv[j] ? head_bits(p, s, c[j].z) : 0u;
-            f1[j] = (lv[j] && c[j].w != FGI_NONE) ? head_bits(p, s, c[j].w) : 0u;
+            f0[j] = lv[j] ? head_bits(p, s, c[j].z, sum) : 0u;
+            f1[j] = (lv[j] && c[j].w != FGI_NONE) ? head_bits(p, s, c[j].w, sum) : 0u;
 #endif
         }
         uint4 cn[4];
@@ -1339,7 +1380,8 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
         if (base + kCandBatch >= cnt) PROBE(L, 7);
         if (qn > kWaveTailCap - kWaveBatch || base + kCandBatch >= cnt) {
             __builtin_amdgcn_wave_barrier();
-            pull_tails(p, src, sv_out, node, s_lo, seg, wq, (FGI_EXP & 1) ? 0u : qn, s, flagged, examined_tail, tails, ws);
+            pull_tails(p, src, sv_out, node, s_lo, seg, wq, (FGI_EXP & 1) ? 0u : qn, s, flagged, examined_tail, tails, ws,
+                       sum);
             __builtin_amdgcn_wave_barrier();
             qn = 0;
         }
@@ -1463,7 +1505,8 @@ __global__ __launch_bounds__(kBlock, kLevelOcc) void k_level(int Larg, WaveParam
     // multi-GPU pull levels run on every rank (parents may be remote); otherwise no frontier, no work
     if (pull) {
         unsigned long long bs[3] = {0, 0, 0};
-        pull_level(L, p, wp, npull, node, vis, s_rel, *reinterpret_cast<PullLds*>(s_base), blk, s_st, bs);
+        const bool sum = p.sum != nullptr && lc.sum != 0;
+        pull_level(L, p, wp, npull, sum, node, vis, s_rel, *reinterpret_cast<PullLds*>(s_base), blk, s_st, bs);
         PROBE(L, 4);
         pull_epilogue(L, p, o.ln, done, bs, s_red, fused ? &ctr->cur : nullptr);
         return;
@@ -2296,6 +2339,9 @@ CollectArgs collect_args(fgi_graph* g, uint32_t n_slots, const WaveParams& wp, i
     c.hot_bm = g->inv_bm + g->hot_w0;
     c.n_hot = g->n_hot;
     c.inv = g->inv_bm;
+    c.sum_bm = g->part ? nullptr : reinterpret_cast<unsigned long long*>(g->sum_bm);   // over inv_bm only
+    c.n64 = ((uint64_t)g->n_handles + 63) / 64;
+    c.sum_min = g->opt_sum_min;
     return c;
 }
 
@@ -2313,6 +2359,7 @@ PullArgs pull_args(fgi_graph* g, uint32_t n_slots, const uint32_t* front_rd) {
     p.uin_len = g->uin_len;
     p.uin_src = g->uin_src;
     p.front_rd = front_rd;
+    p.sum = (!g->part && front_rd == g->inv_bm) ? g->sum_bm : nullptr;
     p.hot_bit0 = (uint32_t)(g->hot_w0 * 32);
     p.hot_lds = std::min<uint32_t>(g->n_hot / 32, kLdsHot);
     p.inv_bm = g->inv_bm;
