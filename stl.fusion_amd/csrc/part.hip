@@ -1097,6 +1097,10 @@ static fgi_status part_alloc(fgi_graph* g, uint32_t n_global) {
     // even, so the hot heads' snapshot past its end (kHot / 32 words, build_candidates) is 64-bit aligned
     p->v.front_words_global = ((uint64_t)n_global / 32 + 3) & ~1ull;
     if (hipMalloc(&p->v.front_global, (p->v.front_words_global + kHot / 32) * 4) != hipSuccess) return fail("frontier bitmap");
+    // the pull levels' probe summary covers the all-gathered bitmap: one bit per 64-bit word of it
+    hipFree(g->sum_bm);
+    g->sum_bm = nullptr;
+    if (hipMalloc(&g->sum_bm, ((uint64_t)n_global / 4096 + 4) * 8) != hipSuccess) return fail("probe summary");
     if (hipMemset(p->v.front_global, 0, (p->v.front_words_global + kHot / 32) * 4) != hipSuccess) return fail("frontier bitmap");
     if (hipMalloc(&p->v.scratch_u64, 32) != hipSuccess) return fail("scratch");
     if (hipMalloc(&p->weight, (size_t)n_global * 4) != hipSuccess) return fail("list weights");

@@ -2359,7 +2359,9 @@ PullArgs pull_args(fgi_graph* g, uint32_t n_slots, const uint32_t* front_rd) {
     p.uin_len = g->uin_len;
     p.uin_src = g->uin_src;
     p.front_rd = front_rd;
-    p.sum = (!g->part && front_rd == g->inv_bm) ? g->sum_bm : nullptr;
+    // the summary of the bitmap this level probes: inv_bm, or a partition's all-gathered front_global
+    // (used only where the level's k_collect built it: its `sum` word)
+    p.sum = ((g->part != nullptr) == (front_rd != g->inv_bm)) ? g->sum_bm : nullptr;
     p.hot_bit0 = (uint32_t)(g->hot_w0 * 32);
     p.hot_lds = std::min<uint32_t>(g->n_hot / 32, kLdsHot);
     p.inv_bm = g->inv_bm;
@@ -3053,6 +3055,8 @@ static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveP
             CollectArgs ca = collect_args(g, pv.n_local, wp, buf);
             ca.inv = front;   // hot heads are global ids
             ca.hot_bm = pv.front_global + g->hot_w0;
+            ca.sum_bm = reinterpret_cast<unsigned long long*>(g->sum_bm);   // over front_global (part init)
+            ca.n64 = pv.front_words_global / 2;
             hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp, ca, ca,
                                ~0ull);
             if (timing) FGI_HIP(g, hipEventRecord(g->ev[e], s));
@@ -3270,6 +3274,8 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
         CollectArgs ca = collect_args(g, pv.n_local, wp, buf);
         ca.inv = front;   // hot heads are global ids
         ca.hot_bm = pv.front_global + g->hot_w0;
+        ca.sum_bm = reinterpret_cast<unsigned long long*>(g->sum_bm);   // over front_global (part init)
+        ca.n64 = pv.front_words_global / 2;
         hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp, ca, ca, ~0ull);
         if (g->opt_level_timing) FGI_HIP(g, hipEventRecord(g->ev[0], s));
         hipLaunchKernelGGL(k_level<true>, dim3(wp.grid), dim3(kBlock), 0, s, L, wp, expand_args(g, buf),

@@ -92,3 +92,38 @@ def test_summary_after_mutations(pkg, gpu_available):
     assert np.array_equal(v[:n], ov) and np.array_equal(f[:n], of)
     o.close()
     g.close()
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_summary_on_partitions(pkg, gpu_available, P):
+    """A partition's pull levels probe the all-gathered bitmap through the same summary (built over
+    front_global on each rank): planned and host-driven waves match the oracle with it forced on."""
+    scale, ef, seed, stale, sseed = 14, 16, 0x5EED0027, 20, 0x5EED00C0
+    n = 1 << scale
+    block = -(-n // P)
+    gs = [pkg.Graph(block, rank=r, world=P) for r in range(P)]
+    pkg.fgi.part_init_local(gs, n)
+    for g in gs:
+        g.part_synth_rmat(scale, ef, seed, stale, sseed)
+        g.set_option(pkg.fgi.OPT_PROBE_SUMMARY, 0)
+        g.set_option(pkg.fgi.OPT_HOT_HEADS, 256)
+        g.set_option(pkg.fgi.OPT_DIRECTION, 2)
+        g.snapshot()
+    s, d = O.gen_rmat(scale, ef, seed)
+    o = O.Oracle(n)
+    o.load_graph(O.version_of(seed, np.arange(n)), None, s, d, O.gen_tags(s, d, seed, stale, sseed))
+    o.snapshot()
+    roots = O.gen_roots(24, n, 9, np.bincount(s, minlength=n))
+    for rep in range(3):   # learning wave, then planned ones
+        for g in gs:
+            g.restore()
+        o.restore()
+        o.clear_log()
+        st = o.invalidate_slots(roots)
+        stats = pkg.fgi.part_local_invalidate(gs, roots)
+        ids = np.concatenate([g.part_export_ids() for g in gs])
+        assert np.array_equal(np.sort(ids), np.sort(o.inv_log())), rep
+        assert sum(x.v_inv for x in stats) == st.v_inv
+        assert sum(x.e_trav for x in stats) == st.e_trav
+        assert all(x.pull_levels >= 1 for x in stats)
+    o.close()
