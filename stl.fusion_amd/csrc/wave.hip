@@ -806,7 +806,9 @@ __global__ __launch_bounds__(kCollectThreads) void k_collect(int L, WaveCtr* ctr
     if (L < 0) return;
     if (fused && (L & 1)) c = c1;   // a fused wave's level is known on the device only: odd levels, buffer 1
     const LevelCtr& lc = ctr->lvl[L % kRing];
-    if (lvl_F(lc) == 0) return;
+    // a partition's pull level runs on every rank, also on one whose own frontier is empty (its
+    // candidates' parents may be remote): its hot snapshot is needed all the same
+    if (lvl_F(lc) == 0 && !wp.multi) return;
     if (level_pulls(ctr, L, wp)) {
         collect_hot(c, (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, (uint64_t)gridDim.x * blockDim.x);
         if (c.sum_bm)
@@ -814,7 +816,7 @@ __global__ __launch_bounds__(kCollectThreads) void k_collect(int L, WaveCtr* ctr
                         (uint64_t)gridDim.x * (blockDim.x >> 6));
         return;
     }
-    if (fused && lvl_T(lc) <= big_push) return;
+    if (lvl_F(lc) == 0 || (fused && lvl_T(lc) <= big_push)) return;
     if (L == 0 || !ctr->lvl[(L + kRing - 1) % kRing].pull) return;
     collect_front(lc, wp.grid, c, (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6),
                   (uint64_t)gridDim.x * (blockDim.x >> 6));

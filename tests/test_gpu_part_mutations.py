@@ -220,3 +220,32 @@ def test_batch_errors_on_partitions(pkg, gpu_available, P):
     _, f = gs[-1].dump_states()
     assert f[999 - (P - 1) * block] & 3 == COMPUTING
     o.close()
+
+
+@pytest.mark.parametrize("P", [2, 4])
+@pytest.mark.parametrize("direction", [0, 2])
+def test_pull_on_a_rank_without_roots(pkg, gpu_available, P, direction):
+    """Hubs all on rank 0, their leaves spread over every rank: the other ranks start a pull level with
+    an empty local frontier, and must still build their hot-head snapshot and pull (regression: k_collect
+    returned on an empty local frontier, so their leaves were never reached)."""
+    from stl_fusion_amd import workloads as W
+    mix = W.StreamMix(64, 40, 8, 10, 0x5EED00E0)
+    n = mix.n
+    gs, block = _group(pkg, P, n, n_detached=0)
+    used, dep, tag = mix.initial_edges()
+    for g in gs:
+        g.part_register_nodes(np.arange(n, dtype=np.uint32), mix.version, mix.state_flags())
+        g.part_load_edges(used, dep, tag)
+        g.set_option(pkg.fgi.OPT_DIRECTION, direction)
+    o = O.Oracle(n)
+    o.load_graph(mix.version, mix.state_flags(), used, dep, tag)
+    for r in range(3):
+        roots = mix.roots(r)
+        o.clear_log()
+        st = o.invalidate_slots(roots)
+        stats = pkg.fgi.part_local_invalidate(gs, roots)
+        ids = np.concatenate([g.part_export_ids() for g in gs])
+        assert np.array_equal(np.sort(ids), np.sort(o.inv_log())), (r, len(ids), len(o.inv_log()))
+        assert sum(x.v_inv for x in stats) == st.v_inv
+    _check_states(gs, o, n, block)
+    o.close()
