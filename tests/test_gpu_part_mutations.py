@@ -158,7 +158,11 @@ def test_random_churn_then_prune_on_partitions(pkg, gpu_available, P, direction)
     rng = np.random.default_rng(1000 + P)
     versions, flags = random_states(n, rng, seed=seed)
     s, d = O.gen_rmat(scale, ef, seed)
-    tags = O.gen_tags(s, d, seed, 20, sseed)
+    live = (versions[s] != 0) & ((flags[s] & 3) == CONSISTENT)   # only Consistent nodes hold `_usedBy`
+    s, d = s[live], d[live]
+    tags = versions[d].astype(np.uint64).copy()
+    tags[tags == 0] = 7                                            # an entry of an empty slot: never live
+    tags[rng.random(len(s)) < 0.2] += np.uint64(1)                 # 20% stale entries
     gs, block = _group(pkg, P, n)
     present = np.nonzero(versions)[0].astype(np.uint32)
     for g in gs:

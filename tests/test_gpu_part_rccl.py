@@ -66,7 +66,11 @@ def test_rccl_partition_world1_mutations_match_oracle(pkg, gpu_available, collec
     rng = np.random.default_rng(77)
     versions, flags = random_states(n, rng, seed=seed)
     s, d = O.gen_rmat(scale, ef, seed)
-    tags = O.gen_tags(s, d, seed, 20, sseed)
+    live = (versions[s] != 0) & ((flags[s] & 3) == 1)   # only Consistent nodes hold `_usedBy`
+    s, d = s[live], d[live]
+    tags = versions[d].astype(np.uint64).copy()
+    tags[tags == 0] = 7
+    tags[rng.random(len(s)) < 0.2] += np.uint64(1)
     g = pkg.Graph(n, n_detached=256, rank=0, world=1)
     g.part_init(n, pkg.fgi.part_unique_id())
     g.set_option(pkg.fgi.OPT_PART_COLLECTIVES, collectives)
