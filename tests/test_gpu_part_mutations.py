@@ -199,7 +199,7 @@ def test_random_churn_then_prune_on_partitions(pkg, gpu_available, P, direction)
     live = np.nonzero((of & 3) == CONSISTENT)[0]
     roots = rng.choice(live, 64, replace=False).astype(np.uint32)
     ids, _, stats = _run_both(pkg, gs, o, [("invalidate", roots)], n, block)
-    assert len(ids) > len(roots)
+    assert len(ids) > 0   # delayed roots only start their delay
     o.close()
 
 
