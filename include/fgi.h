@@ -357,12 +357,12 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *   FGI_OPT_PART_BUCKET [0]  partitions, planned waves: words per peer of a push level's bucket (a
  *                            count, then ids; 0 = the allocated 65,536); smaller buckets only delay
  *                            ids to later push levels (tests pin that path; results never change)
- *   FGI_OPT_PROBE_SUMMARY [524288] single device: before a pull level while few invalidated-bitmap
- *                            words can be nonzero (the invalidated count so far, by the levels'
- *                            frontiers, under 1/8 of the words), build a one-bit-per-64-bit-word
- *                            summary and answer cold head / tail probes of zero words from it — for
- *                            graphs whose bitmap has at least this many 64-bit words (default 4 MB of
- *                            bitmap: larger than an XCD's L2); 0 on any graph (tests), -1 never
+ *   FGI_OPT_PROBE_SUMMARY [-1] before a pull level while few invalidated-bitmap words can be nonzero
+ *                            (the invalidated count so far, by the levels' frontiers, under 1/8 of the
+ *                            words), build a one-bit-per-64-bit-word summary and answer cold head /
+ *                            tail probes of zero words from it, on graphs whose bitmap has at least
+ *                            this many 64-bit words; 0 on any graph (tests), -1 never (the default:
+ *                            measured slower on configs[2]; results never change)
  *   FGI_OPT_FAULT_INJECT [0] tests only: value (k << 16) | b, b > 0: in the (k+1)-th streaming
  *                            cascade launched from now (fgi_run_batch), block b - 1 leaves at its first
  *                            grid barrier without arriving, and that cascade's barrier times out after
