@@ -128,7 +128,7 @@ constexpr int kDoneGroups = 16;         // two-level completion counters (last-b
 constexpr int kDoneStride = 16;         // 128 B apart
 constexpr uint32_t kFinalBlocks = 1024; // grid of the final collect (invalidated bitmap -> list)
 #ifndef FGI_HOT
-#define FGI_HOT 262144                  // measurement builds: make variant-hot HOT=<n> (a multiple of 256)
+#define FGI_HOT 524288                  // measurement builds: make variant-hot HOT=<n> (a multiple of 256)
 #endif
 constexpr uint32_t kHot = FGI_HOT;      // most hot list heads (pull probes through a snapshot of kHot / 8 B)
 #ifndef FGI_LDS_HOT

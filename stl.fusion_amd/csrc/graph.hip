@@ -1447,11 +1447,14 @@ fgi_status build_in_heads(fgi_graph* g) {
 
 // The pull candidate segments for the graph's pull geometry (see fgi_internal.h). A graph too large
 // to pull on one device, or with a row of 2^31 entries or more, gets none (its waves push).
-// Hot heads for a graph of n handles: one per 512 handles, a power of two in [kHotMin, kHot]. A/B on
+// Hot heads for a graph of n handles: one per 256 handles, a power of two in [kHotMin, kHot]. A/B on
 // one box (profiles/r5e_ab.txt): 64 Ki -> 256 Ki heads took configs[2]'s pull levels from 1.105 to
-// 1.020 ms per wave; on configs[1] a snapshot past 64 Ki costs more to refresh than it saves.
+// 1.020 ms per wave; round 4 (profiles/r8d_hot_ab.txt): 512 Ki heads 0.989 ms (1.202-1.206 ms/step
+// against 1.215-1.221), 1 Mi 0.983 ms of pull levels but no faster a step (the snapshot's refresh),
+// 2 Mi slower; on configs[1] (65,536 heads either way) a snapshot past 64 Ki costs more to refresh
+// than it saves.
 #ifndef FGI_HOT_DIV
-#define FGI_HOT_DIV 512   // measurement builds: make variant-hot HOT=<n> HOT_DIV=<handles per hot head>
+#define FGI_HOT_DIV 256   // measurement builds: make variant-hot HOT=<n> HOT_DIV=<handles per hot head>
 #endif
 uint32_t hot_count(uint64_t n) {
     uint32_t k = kHotMin;
