@@ -3029,7 +3029,12 @@ static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveP
     const bool coll = pv.world > 1 || g->opt_part_coll;
     const auto* node = reinterpret_cast<const unsigned long long*>(g->node);
     const RemoteArgs ra{pv.base, pv.n_local, pv.block, pv.world, pv.ver_all, pv.sent_bm, pv.send_buf, pv.send_cnt};
-    const uint32_t* front = pv.front_global;
+    // one rank without collectives: the pull levels probe the invalidated bitmap itself (no copy into
+    // front_global per pull level) when its hot snapshot sits where the partition's would (the same
+    // word count: no detached handles)
+    const bool alias = !coll && g->hot_w0 == g->bm_words;
+    const uint32_t* front = alias ? g->inv_bm : pv.front_global;
+    uint32_t* const hot_base = alias ? g->inv_bm : pv.front_global;
     if (coll) {
         FGI_HIP(g, hipMemsetAsync(pv.send_cnt, 0, (size_t)pv.world * 8, s));
         FGI_HIP(g, hipMemsetAsync(pb.cur, 0, (size_t)pv.world * 8, s));
@@ -3052,11 +3057,12 @@ static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveP
             if (pull) {
                 FGI_HIP(g, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(&g->ctr->lvl[L % kRing].pull), 1, 1, s));
                 if (coll) FGI_TRY(part_allgather_front_async(g));
-                else FGI_HIP(g, hipMemcpyAsync(pv.front_global, g->inv_bm, (size_t)pv.block / 32 * 4, hipMemcpyDeviceToDevice, s));
+                else if (!alias)
+                    FGI_HIP(g, hipMemcpyAsync(pv.front_global, g->inv_bm, (size_t)pv.block / 32 * 4, hipMemcpyDeviceToDevice, s));
             }
             CollectArgs ca = collect_args(g, pv.n_local, wp, buf);
             ca.inv = front;   // hot heads are global ids
-            ca.hot_bm = pv.front_global + g->hot_w0;
+            ca.hot_bm = hot_base + g->hot_w0;
             ca.sum_bm = reinterpret_cast<unsigned long long*>(g->sum_bm);   // over front_global (part init)
             ca.n64 = pv.front_words_global / 2;
             hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp, ca, ca,
@@ -3243,7 +3249,12 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     // the invalidated bitmap over all slots: all-gathered before pull levels (one rank without
     // collectives: its own words copied in, so the hot snapshot past its end is where the candidates
     // expect it)
-    const uint32_t* front = pv.front_global;
+    // one rank without collectives: the pull levels probe the invalidated bitmap itself (no copy into
+    // front_global per pull level) when its hot snapshot sits where the partition's would (the same
+    // word count: no detached handles)
+    const bool alias = !coll && g->hot_w0 == g->bm_words;
+    const uint32_t* front = alias ? g->inv_bm : pv.front_global;
+    uint32_t* const hot_base = alias ? g->inv_bm : pv.front_global;
     uint64_t f_global = sums[1], t_global = sums[2];
     const double avg_deg = (double)sums[0] / std::max<uint64_t>(1, pv.n_global);
     uint64_t levels = 0, e_trav = 0, f_total = 0, sent_total = 0, push_edges = 0, push_f = 0;
@@ -3269,13 +3280,13 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
                 FGI_TRY(part_allgather_front(g));
                 FGI_TRY(part_front_stats(g, &f0, &d1, &b));
                 syncs += g->opt_front_exchange != 1 ? 1 : 0;   // the delta count's read-back (auto or delta)
-            } else {
+            } else if (!alias) {
                 FGI_HIP(g, hipMemcpyAsync(pv.front_global, g->inv_bm, (size_t)pv.block / 32 * 4, hipMemcpyDeviceToDevice, s));
             }
         }
         CollectArgs ca = collect_args(g, pv.n_local, wp, buf);
         ca.inv = front;   // hot heads are global ids
-        ca.hot_bm = pv.front_global + g->hot_w0;
+        ca.hot_bm = hot_base + g->hot_w0;
         ca.sum_bm = reinterpret_cast<unsigned long long*>(g->sum_bm);   // over front_global (part init)
         ca.n64 = pv.front_words_global / 2;
         hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp, ca, ca, ~0ull);
