@@ -368,7 +368,6 @@ struct fgi_graph {
     // built before a pull level while few words can be nonzero, so cold head and tail probes that
     // would miss are answered from an L2-resident table (FGI_OPT_PROBE_SUMMARY)
     uint32_t* sum_bm = nullptr;
-    uint64_t fin_epoch = 0;           // k_final_one's launch epoch (FGI_FINAL_ONE)
     int64_t opt_sum_min = -1;         // fewest 64-bit bitmap words for a summary (-1: never; measured
                                       // slower on configs[2])
     int opt_pull_beta = 24;           // after a pull, pull again while the frontier exceeds n / beta

@@ -1693,86 +1693,6 @@ __global__ __launch_bounds__(kBlock) void k_final_write(const unsigned long long
     }
 }
 
-// The same final collect in one launch (FGI_FINAL_ONE=1 selects it; measurement): block t counts its
-// words, publishes the count tagged with the launch's epoch, and sums its predecessors' published
-// counts before writing. A block waits only on lower-indexed blocks, which the dispatcher placed
-// before it (each XCD dispatches in order; other kernels' blocks finish on their own), so the waits
-// end; a wait past `timeout` wall-clock ticks marks the wave broken (ctr->broken) and writes nothing.
-__global__ __launch_bounds__(kBlock) void k_final_one(const unsigned long long* __restrict__ inv64, uint64_t words,
-                                                      uint64_t wpb, unsigned long long* status, WaveCtr* ctr,
-                                                      const unsigned long long* __restrict__ blk, uint32_t* out,
-                                                      unsigned long long epoch, uint64_t timeout) {
-    __shared__ unsigned long long s_red[kBlock / 64];
-    __shared__ unsigned long long s_wbase[kBlock / 64];
-    __shared__ uint32_t s_stage[kBlock / 64][kPullTile];
-    __shared__ int s_bad;
-    const uint32_t t = blockIdx.x;
-    const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
-    constexpr uint32_t W = kBlock / 64;
-    constexpr unsigned long long kCnt = (1ull << 40) - 1;
-    if (t < (uint32_t)kStats) {   // the per-block statistics columns, as k_final_count
-        const int k = t;
-        unsigned long long* dst[kStats] = {&ctr->e_match,   &ctr->n_flagged, &ctr->pull_surv, &ctr->pull_edges,
-                                           &ctr->pull_live, &ctr->pull_win,  &ctr->pull_tail, &ctr->pull_scan};
-        const unsigned long long* col = blk + (uint64_t)k * kStatBlocks;
-        unsigned long long x = 0;
-#pragma unroll
-        for (uint32_t q = 0; q < kStatBlocks / kBlock; ++q) x += col[q * kBlock + threadIdx.x];
-        x = block_sum(x, s_red);
-        if (threadIdx.x == 0) *dst[k] = x + (k == kStFlagged ? ctr->root_flagged : 0ull);
-    }
-    const uint64_t lo = t * wpb, hi = std::min<uint64_t>(words, lo + wpb);
-    const uint64_t ww = (wpb + W - 1) / W;
-    const uint64_t wlo = std::min<uint64_t>(hi, lo + wid * ww), whi = std::min<uint64_t>(hi, wlo + ww);
-    uint32_t wc = 0;
-    for (uint64_t x = wlo + lane; x < whi; x += 64) wc += (uint32_t)__popcll(inv64[x]);
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) wc += __shfl_xor(wc, d, 64);
-    if (lane == 0) s_wbase[wid] = wc;
-    if (threadIdx.x == 0) s_bad = 0;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long c = 0;
-        for (uint32_t k = 0; k < W; ++k) c += s_wbase[k];
-        __hip_atomic_store(status + t, (epoch << 40) | c, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // the predecessors' counts, each read until it carries this launch's epoch
-    unsigned long long part = 0;
-    const uint64_t t0 = wall_clock64();
-    for (uint32_t k = threadIdx.x; k < t; k += blockDim.x) {
-        unsigned long long v;
-        while (((v = __hip_atomic_load(status + k, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT)) >> 40) != epoch) {
-            __builtin_amdgcn_s_sleep(1);
-            if (wall_clock64() - t0 > timeout) {
-                s_bad = 1;
-                break;
-            }
-        }
-        part += v & kCnt;
-    }
-    const unsigned long long excl = block_sum(part, s_red);
-    if (s_bad) {
-        if (threadIdx.x == 0) __hip_atomic_store(&ctr->broken, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return;
-    }
-    unsigned long long run = excl;
-    for (uint32_t k = 0; k < wid; ++k) run += s_wbase[k];
-    if (t == gridDim.x - 1 && threadIdx.x == blockDim.x - 1) ctr->inv = run + wc;
-    const uint16_t* bits16 = reinterpret_cast<const uint16_t*>(inv64);
-    for (uint64_t tw = wlo; tw < whi; tw += kTileWords) {   // wave-uniform
-        const uint64_t q = tw * 4 + lane;
-        const uint32_t m = (tw + lane / 4 >= whi) ? 0u : (uint32_t)bits16[q];
-        uint32_t tot;
-        const uint32_t ex = wave_excl_scan((uint32_t)__popc(m), tot);
-        uint32_t o = ex;
-        for (uint32_t mm = m; mm; mm &= mm - 1) s_stage[wid][o++] = (uint32_t)(q * 16 + (uint32_t)(__ffs(mm) - 1));
-        __builtin_amdgcn_wave_barrier();
-        for (uint32_t i = lane; i < tot; i += 64) out[run + i] = s_stage[wid][i];
-        __builtin_amdgcn_wave_barrier();
-        run += tot;
-    }
-}
-
 constexpr uint32_t kFinalStage = 1024;   // bitmap words a block keeps in LDS (8 KB), k_wave_coop
 
 // ---- a whole (push-only) wave in one launch ---------------------------------------------------
@@ -2472,18 +2392,6 @@ hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true) {
     const auto* inv64 = reinterpret_cast<const unsigned long long*>(g->inv_bm);
     // per-block counts apart from the pull prefixes a collect may still read
     unsigned long long* st = g->bsum + 6ull * kStatBlocks;
-    static const bool one = getenv("FGI_FINAL_ONE") && atoi(getenv("FGI_FINAL_ONE")) == 1;
-    if (ids && one) {
-        // the epoch tags this launch's published counts (24 bits, never 0: the words start zeroed)
-        if (g->fin_epoch == 0)   // the status words start zeroed (a count word is epoch << 40 | count)
-            if (hipMemsetAsync(g->bsum + 7ull * kStatBlocks, 0, kStatBlocks * 8, g->stream) != hipSuccess)
-                return hipGetLastError();
-        g->fin_epoch = g->fin_epoch % 0xFFFFFFull + 1;
-        hipLaunchKernelGGL(k_final_one, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb,
-                           g->bsum + 7ull * kStatBlocks, g->ctr, (const unsigned long long*)g->blk_stats,
-                           g->inv, (unsigned long long)g->fin_epoch, (uint64_t)20000000);   // 200 ms
-        return hipGetLastError();
-    }
     hipLaunchKernelGGL(k_final_count, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb, st, g->ctr,
                        (const unsigned long long*)g->blk_stats, ids ? 0 : 1, g->done);
     if (ids)
@@ -3032,7 +2940,6 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         FGI_HIP(g, hipEventRecord(g->ev_w1, s));
         FGI_HIP(g, hipEventSynchronize(g->ev_w1));
     }
-    if (g->ctr_host->broken) return set_err(g, FGI_EDEVICE, "the final collect's blocks waited past the timeout");
     if (imm_dev && n_roots) note_words(g);   // immediate roots changed node words
     g->last_wave_n = g->ctr_host->inv;
     g->ids_valid = g->want_ids;
@@ -3444,7 +3351,6 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
     FGI_HIP(g, hipEventRecord(g->ev_w1, s));
     FGI_HIP(g, hipStreamSynchronize(s));
-    if (g->ctr_host->broken) return set_err(g, FGI_EDEVICE, "the final collect's blocks waited past the timeout");
     g->last_wave_n = g->ctr_host->inv;
     g->ids_valid = true;
     if (stats) {
