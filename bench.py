@@ -184,7 +184,17 @@ def main():
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        # The engine's collectives run over RCCL through libfgi's own communicator (fgi_part_init,
+        # /opt/rocm's librccl). torch's group carries only the bench's bookkeeping — the communicator's
+        # unique id, the barriers around the timed region, the max of the per-rank times, the root
+        # degrees — so it is a gloo group: the process then holds one RCCL instance, the engine's
+        # (FGI_BENCH_TORCH_BACKEND=nccl selects torch's RCCL for it instead).
+        backend = os.environ.get("FGI_BENCH_TORCH_BACKEND", "gloo")
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group(backend)
+    tdev = "cpu" if (dist is not None and dist.get_backend() != "nccl") else f"cuda:{local_rank}"
 
     pkg = _pkg.load()
     from stl_fusion_amd import workloads as W
@@ -210,10 +220,14 @@ def main():
                           cfg.get("stale_seed", 0))
         n_local = min(block, n - rank * block)
         deg_local, _ = g.degrees()
-        deg = torch.zeros(block * world, dtype=torch.int32, device=f"cuda:{local_rank}")
-        mine = torch.zeros(block, dtype=torch.int32, device=f"cuda:{local_rank}")
+        deg = torch.zeros(block * world, dtype=torch.int32, device=tdev)
+        mine = torch.zeros(block, dtype=torch.int32, device=tdev)
         mine[:n_local] = torch.from_numpy(deg_local[:n_local].astype(np.int32)).to(mine.device)
-        if dist:
+        if dist and tdev == "cpu":
+            parts = [torch.zeros(block, dtype=torch.int32) for _ in range(world)]
+            dist.all_gather(parts, mine)
+            deg = torch.cat(parts)
+        elif dist:
             dist.all_gather_into_tensor(deg, mine)
         else:
             deg = mine
@@ -333,10 +347,10 @@ def main():
         ids_host = np.asarray(g.invalidate(roots), np.uint32)
     v_inv, e_trav, e_match_all = st.v_inv, st.e_trav, st.e_match
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local_rank}")
+        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        c = torch.tensor([v_inv, e_trav, e_match_all], dtype=torch.float64, device=f"cuda:{local_rank}")
+        c = torch.tensor([v_inv, e_trav, e_match_all], dtype=torch.float64, device=tdev)
         dist.all_reduce(c, op=dist.ReduceOp.SUM)
         v_inv, e_trav, e_match_all = int(c[0].item()), int(c[1].item()), int(c[2].item())
 
