@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 HEAD (final) on a fresh box, part 1: the GPU suite and the bench line (with the CPU baseline).
 set -u
-out=gpurun_out/r8z
+out=gpurun_out/${1:-r8z}
 mkdir -p "$out"
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --durations=20 --timeout 150 --timeout-method thread > "$out/gpu_tests.log" 2>&1 \
     || { echo "tests rc=$?"; tail -30 "$out/gpu_tests.log"; exit 1; }
