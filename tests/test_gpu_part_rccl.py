@@ -113,3 +113,54 @@ def test_rccl_partition_world1_mutations_match_oracle(pkg, gpu_available, collec
     assert np.array_equal(v[:n], ov) and np.array_equal(f[:n], of)
     o.close()
     g.close()
+
+
+def test_rccl_partition_world1_single_mutation_calls(pkg, gpu_available):
+    """The standalone partition mutation entry points (fgi_part_begin_compute / add_used / set_output /
+    invalidate_all) at world size 1 over RCCL, against the oracle's calls one by one."""
+    from harness import random_states
+    scale, ef, seed = 10, 8, 11
+    n = 1 << scale
+    rng = np.random.default_rng(5)
+    versions, flags = random_states(n, rng, p_empty=0.0, seed=seed)
+    s, d = O.gen_rmat(scale, ef, seed)
+    live = (flags[s] & 3) == 1
+    s, d = s[live], d[live]
+    tags = versions[d].astype(np.uint64).copy()
+    g = pkg.Graph(n, n_detached=128, rank=0, world=1)
+    g.part_init(n, pkg.fgi.part_unique_id())
+    g.set_option(pkg.fgi.OPT_PART_COLLECTIVES, 1)
+    g.part_register_nodes(np.arange(n, dtype=np.uint32), versions, flags)
+    g.part_load_edges(s, d, tags)
+    o = O.Oracle(n)
+    o.load_graph(versions, flags, s, d, tags)
+
+    def same_states():
+        v, f = g.dump_states()
+        ov, of = o.dump_states()
+        return np.array_equal(v[:n], ov) and np.array_equal(f[:n], of)
+
+    bc = rng.choice(n, 40, replace=False).astype(np.uint32)
+    ver = np.arange(1 << 44, (1 << 44) + 2 * len(bc), 2, dtype=np.uint64) | np.uint64(1)
+    hd = (rng.random(len(bc)) < 0.3).astype(np.uint8)
+    o.clear_log()
+    det, ids = g.part_begin_compute(bc, ver, hd)
+    o.begin_compute_slots(bc, ver, hd)
+    assert np.array_equal(np.sort(ids), np.sort(o.inv_log()))
+    assert same_states()
+    dep = rng.choice(bc, 60).astype(np.uint32)
+    use = rng.choice(n, 60).astype(np.uint32)
+    assert np.array_equal(g.part_add_used(dep, use), o.add_used_slots(dep, use))
+    assert same_states()
+    o.clear_log()
+    out_set, ids = g.part_set_output(bc)
+    assert int(out_set.sum()) == o.set_output_slots(bc)
+    assert np.array_equal(np.sort(ids), np.sort(o.inv_log()))
+    assert same_states()
+    o.clear_log()
+    ids = g.part_invalidate_all()
+    o.invalidate_everything()
+    assert np.array_equal(np.sort(ids), np.sort(o.inv_log()))
+    assert same_states()
+    o.close()
+    g.close()
