@@ -126,7 +126,18 @@ constexpr int kStatCols = 8;
 constexpr int kPullTile = 1024;         // slots per pull tile (one block iteration of a pull level)
 constexpr int kDoneGroups = 16;         // two-level completion counters (last-block epilogues)
 constexpr int kDoneStride = 16;         // 128 B apart
-constexpr uint32_t kFinalBlocks = 1024; // grid of the final collect (invalidated bitmap -> list)
+#ifndef FGI_FINAL_BLOCKS
+#define FGI_FINAL_BLOCKS 1024               // measurement builds: make variant-grid FINAL=<blocks> WPB=<words> INIT=<blocks>
+#endif
+#ifndef FGI_FINAL_WPB
+#define FGI_FINAL_WPB 256
+#endif
+#ifndef FGI_INIT_BLOCKS
+#define FGI_INIT_BLOCKS 512
+#endif
+constexpr uint32_t kFinalBlocks = FGI_FINAL_BLOCKS; // grid of the final collect (invalidated bitmap -> list)
+constexpr uint32_t kFinalWpb = FGI_FINAL_WPB;       // fewest 64-bit bitmap words per final-collect block
+constexpr uint32_t kInitBlocks = FGI_INIT_BLOCKS;   // grid of k_wave_init
 #ifndef FGI_HOT
 #define FGI_HOT 524288                  // measurement builds: make variant-hot HOT=<n> (a multiple of 256)
 #endif

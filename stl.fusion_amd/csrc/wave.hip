@@ -2387,7 +2387,7 @@ ExpandArgs expand_args(fgi_graph* g, int buf) {
 // the invalidated bitmap -> V_inv (ctr->inv) and, with ids, the invalidated list
 hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true) {
     const uint64_t words = ((uint64_t)n_handles + 63) / 64;
-    uint32_t G = (uint32_t)std::min<uint64_t>(kFinalBlocks, std::max<uint64_t>(kStats, (words + 255) / 256));
+    uint32_t G = (uint32_t)std::min<uint64_t>(kFinalBlocks, std::max<uint64_t>(kStats, (words + kFinalWpb - 1) / kFinalWpb));
     const uint64_t wpb = (words + G - 1) / G;
     const auto* inv64 = reinterpret_cast<const unsigned long long*>(g->inv_bm);
     // per-block counts apart from the pull prefixes a collect may still read
@@ -2485,7 +2485,7 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
     FGI_TRY(fold(g));   // visits of a level-launched wave
     if (coop) FGI_TRY(coop_warm(g));
     if (!g->coop_clean)
-        hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
+        hipLaunchKernelGGL(k_wave_init, dim3(kInitBlocks), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
                            (uint32_t*)nullptr, (uint64_t)g->bm_words);
     CoopArgs a{};
     a.roots = roots_dev;
@@ -2669,7 +2669,7 @@ static fgi_status run_wave_fused(fgi_graph* g, uint32_t n_roots, const uint32_t*
     if (g->opt_fused & kFusedMidPush) a.big_push = 0;          // tests: every push level as a k_level launch
     if (g->opt_fused & kFusedTailPush) a.big_push = ~0ull;     // tests: every push level in the fused grid
     const uint64_t words = ((uint64_t)g->n_handles + 63) / 64;
-    a.fin_G = (uint32_t)std::min<uint64_t>(kFinalBlocks, std::max<uint64_t>(kStats, (words + 255) / 256));
+    a.fin_G = (uint32_t)std::min<uint64_t>(kFinalBlocks, std::max<uint64_t>(kStats, (words + kFinalWpb - 1) / kFinalWpb));
     a.fin_wpb = (words + a.fin_G - 1) / a.fin_G;
     a.status = g->bsum + 6ull * kStatBlocks;
     g->vis_stale = false;
@@ -2681,7 +2681,7 @@ static fgi_status run_wave_fused(fgi_graph* g, uint32_t n_roots, const uint32_t*
     const size_t eh = 2 * (size_t)kMidMax;   // the head's / tail's event pair
     if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
     if (!a.do_init)   // the wave state cleared by its own launch: the head's first barrier has no dirty 4 MB
-        hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
+        hipLaunchKernelGGL(k_wave_init, dim3(kInitBlocks), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
                            a.clear_vis ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
     if (timing) FGI_HIP(g, hipEventRecord(ev[eh], s));
     hipLaunchKernelGGL(k_wave_fused<false>, dim3(G), dim3(kBlock), 0, s, a);
@@ -2827,7 +2827,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         const fgi_status r = run_wave_fused(g, n_roots, roots_dev, imm_dev, stats, wp, timing, t0);
         if (r != FGI_ENOTSUP) return r;
     }
-    hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
+    hipLaunchKernelGGL(k_wave_init, dim3(kInitBlocks), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
                        g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
     g->vis_stale = false;
     g->coop_clean = false;
@@ -3199,7 +3199,7 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     const bool coll = pv.world > 1 || g->opt_part_coll;
     if (coll) FGI_HIP(g, hipMemsetAsync(pv.sent_bm, 0, pv.sent_words * 4, s));
     if (coll) FGI_TRY(part_front_reset(g));
-    hipLaunchKernelGGL(k_wave_init, dim3(512), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
+    hipLaunchKernelGGL(k_wave_init, dim3(kInitBlocks), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
                        g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
     g->vis_stale = false;
     g->coop_clean = false;
