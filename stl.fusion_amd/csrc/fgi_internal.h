@@ -133,7 +133,7 @@ constexpr int kDoneStride = 16;         // 128 B apart
 #define FGI_FINAL_WPB 256
 #endif
 #ifndef FGI_INIT_BLOCKS
-#define FGI_INIT_BLOCKS 512
+#define FGI_INIT_BLOCKS 2048
 #endif
 constexpr uint32_t kFinalBlocks = FGI_FINAL_BLOCKS; // grid of the final collect (invalidated bitmap -> list)
 constexpr uint32_t kFinalWpb = FGI_FINAL_WPB;       // fewest 64-bit bitmap words per final-collect block
