@@ -72,3 +72,19 @@ def test_rccl_info_reports_the_bound_library(pkg):
     v, path = pkg.fgi.rccl_info()
     assert v >= 22700 and "rccl" in os.path.basename(path)
     assert os.path.realpath(path).startswith(os.path.realpath("/opt/rocm")), path
+
+
+def test_header_is_plain_c(tmp_path):
+    """include/fgi.h is the drop-in boundary: it compiles as strict C99 (no C++ or HIP types), so a cgo,
+    JNI, N-API or P/Invoke binding can include or mirror it."""
+    import shutil
+    import subprocess
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if cc is None:
+        pytest.skip("no C compiler")
+    src = tmp_path / "h.c"
+    src.write_text('#include "fgi.h"\nint main(void) { fgi_step s; fgi_batch_stats b; (void)s; (void)b; return 0; }\n')
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include")
+    r = subprocess.run([cc, "-std=c99", "-Wall", "-Wextra", "-pedantic", "-Werror", "-I", inc, "-c", str(src), "-o",
+                        str(tmp_path / "h.o")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
