@@ -315,3 +315,85 @@ def live_rows(m):
             continue
         out += [(u, d, t) for d, t in row]
     return out
+
+
+# ---- planned waves (run_part_planned in stl.fusion_amd/csrc/wave.hip) ----------------------------
+# A wave follows a plan (per-level push/pull, learnt from an earlier wave) with fixed-size exchanges:
+# a pull level all-gathers the whole invalidated bitmap; a push level sends each peer a bucket of C
+# words (a count, then at most C - 1 ids) and keeps the ids that did not fit for the next push level;
+# after the plan's levels, push levels are appended while any rank still holds ids to send or has a
+# frontier. One closing all-reduce decides that (the engine's one host synchronisation per round).
+
+def planned_wave(m, roots, plan, C, immediately=None):
+    """Returns (levels run, rounds)."""
+    m.sent[:] = False
+    visited = set()
+    front = []
+    for k, r in enumerate(roots):
+        r = int(r)
+        if m.lo <= r < m.hi and r not in visited:
+            visited.add(r)
+            imm = bool(immediately[k]) if immediately is not None else False
+            if m._visit(r, imm):
+                front.append(r)
+    pending = [[] for _ in range(m.world)]   # ids waiting for a bucket, per owner
+    levels = rounds = 0
+    seq = list(plan)
+    while True:
+        rounds += 1
+        for pull in seq:
+            nxt = []
+            if pull:
+                bm = np.zeros(m.n, bool)
+                # the whole invalidated bitmap: every invalidated owned slot so far, as the engine's
+                # inv_bm (a pull probes parents invalidated at any earlier level)
+                for x in m.inv:
+                    bm[x] = True
+                parts = [torch.zeros(m.n, dtype=torch.bool) for _ in range(m.world)]
+                dist.all_gather(parts, torch.from_numpy(bm))
+                g = np.logical_or.reduce([p.numpy() for p in parts])
+                for d, ps in m.deps.items():
+                    if d in visited:
+                        continue
+                    if any(g[p] for p in ps):
+                        visited.add(d)
+                        if m._visit(d):
+                            nxt.append(d)
+            else:
+                for u in front:
+                    for d, t in m.rows.get(u, ()):
+                        if not m._matches(d, t):
+                            continue
+                        q = m.owner(d)
+                        if q == m.rank:
+                            if d not in visited:
+                                visited.add(d)
+                                if m._visit(d):
+                                    nxt.append(d)
+                        elif not m.sent[d]:
+                            m.sent[d] = True
+                            pending[q].append(d)
+                # fixed-size buckets: a count word, then up to C - 1 ids per peer
+                send = torch.zeros((m.world, C), dtype=torch.int64)
+                for q in range(m.world):
+                    if q == m.rank:
+                        continue
+                    take, pending[q] = pending[q][:C - 1], pending[q][C - 1:]
+                    send[q, 0] = len(take)
+                    if take:
+                        send[q, 1:1 + len(take)] = torch.tensor(take, dtype=torch.int64)
+                recv = torch.zeros((m.world, C), dtype=torch.int64)
+                dist.all_to_all_single(recv, send)
+                for q in range(m.world):
+                    for d in recv[q, 1:1 + int(recv[q, 0])].tolist():
+                        if d not in visited:
+                            visited.add(d)
+                            if m._visit(d):
+                                nxt.append(d)
+            front = nxt
+            levels += 1
+        left = torch.tensor([len(front), sum(len(p) for p in pending)], dtype=torch.int64)
+        dist.all_reduce(left)
+        if int(left[0]) == 0 and int(left[1]) == 0:
+            return levels, rounds
+        seq = [0] * 4   # more push levels while ids wait or a frontier is left

@@ -225,3 +225,57 @@ def test_partitioned_mutation_protocol_matches_oracle(world, direction):
     assert np.array_equal(np.asarray(vers, np.uint64)[:n], ov)
     assert np.array_equal(np.asarray(fl, np.uint32)[:n], of)
     assert rows == o_rows and left == ne, (left, ne, len(rows), len(o_rows))
+
+
+def _plan_worker(rank, world, port, seed, plan, C, q):
+    import torch.distributed as dist
+    import dist_model as DM
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        n, versions, flags, s, d, tags, roots, imm = _case(seed)
+        m = DM.RankModel(rank, world, n, versions, flags, s, d, tags)
+        levels, rounds = DM.planned_wave(m, roots, plan, C, imm)
+        inv, fl = m.gather_results()
+        if rank == 0:
+            q.put((inv, fl.tolist(), levels, rounds))
+        dist.barrier()
+    except Exception:
+        import traceback
+        q.put(("error", rank, traceback.format_exc()))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("plan,C", [((0, 1, 1, 0), 1000), ((0, 0, 0), 3), ((1, 1), 17), ((), 5)])
+def test_planned_wave_protocol_matches_oracle(world, plan, C):
+    """The planned partitioned wave (run_part_planned: the previous wave's directions, full bitmap
+    all-gathers before pull levels, fixed-size all-to-all buckets with carry-over after push levels, push
+    levels appended while ids wait, one closing all-reduce per round) over a gloo group: whatever the
+    plan and however small the buckets, the invalidated set and final flags equal the oracle's."""
+    seed = 3
+    n, versions, flags, s, d, tags, roots, imm = _case(seed)
+    o = O.Oracle(n)
+    o.load_graph(versions, flags, s, d, tags)
+    o.invalidate_slots(roots, imm)
+    o_inv = sorted(int(x) for x in o.inv_log())
+    _, o_flags = o.dump_states()
+    o.close()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_plan_worker, args=(r, world, port, seed, list(plan), C, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=180)
+    assert res[0] != "error", res
+    inv, fl, levels, rounds = res
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert inv == o_inv
+    assert np.array_equal(np.asarray(fl, np.uint32)[:n], o_flags[:n])
+    if C <= 5:
+        assert rounds > 1   # small buckets: ids wait for appended push levels
