@@ -467,7 +467,8 @@ __device__ __forceinline__ void au_reserve(uint64_t i, bool valid, const AuArgs&
     } else {
         pend_pos[i] = pos;
         atomicAdd(&cnt[0], 1ull);
-        if (pos == cap) ovf_rows[atomicAdd(&cnt[1], 1ull)] = c.used;
+        // performed at the coherence point: a batch's last reserve block reads the list (kb_au_reserve)
+        if (pos == cap) __hip_atomic_exchange(&ovf_rows[atomicAdd(&cnt[1], 1ull)], c.used, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
@@ -570,18 +571,49 @@ __device__ __forceinline__ bool batch_aborted(const unsigned long long* ab) {
 __device__ __forceinline__ uint64_t grid_tid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 __device__ __forceinline__ uint64_t grid_threads() { return (uint64_t)gridDim.x * blockDim.x; }
 
-__global__ void kb_bc_classify(const unsigned long long* ab, uint32_t n, const uint32_t* __restrict__ slot,
-                               const unsigned long long* node, uint8_t* cls, uint32_t* roots, unsigned long long* cnt) {
-    if (batch_aborted(ab)) return;
-    const uint64_t i = grid_tid();
-    if (i < n) bc_classify((uint32_t)i, slot, node, cls, roots, cnt);
+// Block-uniform: true in the block that arrives last at this launch's completion counter (two-level,
+// kDoneGroups groups; the last block resets the words). Every block calls it after its own atomics
+// have returned, so the last block sees them all (read at the coherence point: bcoh_read).
+__device__ __forceinline__ unsigned long long bcoh_read(unsigned long long* p) {
+    return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ bool batch_last_block(unsigned long long* done, uint64_t G) {
+    __shared__ bool s_last;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_s_waitcnt(0);
+        const uint32_t grp = blockIdx.x % kDoneGroups;
+        const uint64_t gsize = (G - grp + kDoneGroups - 1) / kDoneGroups;
+        const unsigned long long t = __hip_atomic_fetch_add(done + (1 + grp) * kDoneStride, 1ull, __ATOMIC_RELAXED,
+                                                            __HIP_MEMORY_SCOPE_AGENT);
+        bool last = false;
+        if (t == gsize - 1) {
+            const uint64_t ng = G < (uint64_t)kDoneGroups ? G : (uint64_t)kDoneGroups;
+            last = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    const bool last = s_last;
+    if (last && threadIdx.x <= (uint32_t)kDoneGroups)
+        __hip_atomic_exchange(done + threadIdx.x * kDoneStride, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return last;
 }
 
-// the displaced nodes that survive (cnt[1]) need detached handles: the batch's list has n_take
-__global__ void kb_bc_check(unsigned long long* ab, const unsigned long long* cnt, const unsigned long long* cursor,
-                            uint64_t n_take, uint32_t step) {
-    if (threadIdx.x || blockIdx.x || batch_aborted(ab)) return;
-    if (*cursor + cnt[1] > n_take) *ab = (kAbortDetach << 32) | (step + 1ull);
+__device__ __forceinline__ void batch_abort(unsigned long long* ab, unsigned long long code) {
+    __hip_atomic_exchange(ab, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// classify, then (last block) the check: the displaced nodes that survive (cnt[1]) need detached
+// handles, and the batch's list has n_take (one launch instead of classify + a one-thread check)
+__global__ void kb_bc_classify_check(unsigned long long* ab, uint32_t n, const uint32_t* __restrict__ slot,
+                                     const unsigned long long* node, uint8_t* cls, uint32_t* roots, unsigned long long* cnt,
+                                     unsigned long long* cursor, uint64_t n_take, uint32_t step, unsigned long long* done) {
+    if (batch_aborted(ab)) return;   // uniform over the grid: nothing in this launch sets the word before its end
+    const uint64_t i = grid_tid();
+    if (i < n) bc_classify((uint32_t)i, slot, node, cls, roots, cnt);
+    if (!batch_last_block(done, gridDim.x)) return;
+    if (threadIdx.x == 0 && bcoh_read(cursor) + bcoh_read(cnt + 1) > n_take) batch_abort(ab, (kAbortDetach << 32) | (step + 1ull));
 }
 
 __global__ void kb_bc_install(const unsigned long long* ab, uint32_t n, InstallArgs a) {
@@ -596,25 +628,33 @@ __global__ void kb_au_classify(const unsigned long long* ab, uint32_t n, AuArgs 
     au_classify_block((uint32_t)i, i < n, a);
 }
 
-__global__ void kb_au_reserve(const unsigned long long* ab, AuArgs a) {
-    if (batch_aborted(ab)) return;
+// reserve, then (last block) the overflowing rows' new capacities (cnt[3]) and whether they fit the
+// pool (otherwise the host grows it and finishes the step): one launch instead of reserve + size + check
+__global__ void kb_au_reserve(unsigned long long* ab, AuArgs a, const unsigned long long* top, uint64_t cap, uint32_t step,
+                              unsigned long long* done) {
+    if (batch_aborted(ab)) return;   // uniform over the grid
     const uint64_t nc = a.cnt[0];
     for (uint64_t i0 = grid_tid() - (threadIdx.x & 63); i0 < nc; i0 += grid_threads())   // wave-uniform
         au_reserve(i0 + (threadIdx.x & 63), i0 + (threadIdx.x & 63) < nc, a);
-}
-
-__global__ void kb_au_size(const unsigned long long* ab, AuArgs a) {
-    if (batch_aborted(ab)) return;
-    const uint64_t no = a.cnt[2];
-    for (uint64_t i = grid_tid(); i < no; i += grid_threads())
-        atomicAdd(&a.cnt[3], (unsigned long long)grow_cap(a.row_len[a.ovf_rows[i]]));
-}
-
-// the overflowing rows fit in the pool? (otherwise the host grows it and finishes the step)
-__global__ void kb_au_check(unsigned long long* ab, const unsigned long long* cnt, const unsigned long long* top,
-                            uint64_t cap, uint32_t step) {
-    if (threadIdx.x || blockIdx.x || batch_aborted(ab)) return;
-    if (cnt[2] && *top + cnt[3] > cap) *ab = (kAbortPool << 32) | (step + 1ull);
+    if (!batch_last_block(done, gridDim.x)) return;
+    __shared__ unsigned long long s_need[kBlock / 64];
+    const uint64_t no = bcoh_read(a.cnt + 2);
+    unsigned long long need = 0;
+    for (uint64_t i = threadIdx.x; i < no; i += blockDim.x) {
+        const uint32_t u = __hip_atomic_fetch_add(a.ovf_rows + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        need += grow_cap(__hip_atomic_fetch_add(a.row_len + u, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) need += __shfl_xor(need, d, 64);
+    if ((threadIdx.x & 63) == 0) s_need[threadIdx.x >> 6] = need;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long all = 0;
+        for (uint32_t w = 0; w < blockDim.x / 64; ++w) all += s_need[w];
+        __hip_atomic_exchange(a.cnt + 3, all, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (no && bcoh_read(const_cast<unsigned long long*>(top)) + all > cap)
+            batch_abort(ab, (kAbortPool << 32) | (step + 1ull));
+    }
 }
 
 __global__ void kb_au_relocate(const unsigned long long* ab, AuArgs a, unsigned long long* top) {
@@ -2630,9 +2670,8 @@ static fgi_status batch_launch(fgi_graph* g, uint32_t from, uint32_t n_steps, co
                 break;
             case FGI_STEP_BEGIN_COMPUTE: {
                 FGI_TRY(fold(g));
-                hipLaunchKernelGGL(kb_bc_classify, dim3(nblk(n)), dim3(256), 0, st, abort, n, b.h, node, b.cls, b.roots,
-                                   b.cnt);
-                hipLaunchKernelGGL(kb_bc_check, dim3(1), dim3(64), 0, st, abort, b.cnt, cursor, n_take, k);
+                hipLaunchKernelGGL(kb_bc_classify_check, dim3(nblk(n)), dim3(256), 0, st, abort, n, b.h, node, b.cls, b.roots,
+                                   b.cnt, cursor, n_take, k, g->done);
                 FGI_TRY(wave(n, b.roots, nullptr, b.cnt));   // displacement cascade (ComputedRegistry.cs:91-94)
                 touch(g);
                 note_words(g);
@@ -2655,9 +2694,8 @@ static fgi_status batch_launch(fgi_graph* g, uint32_t from, uint32_t n_steps, co
                 }
                 FGI_HIP(g, hipMemsetAsync(b.hash, 0xFF, b.hcap * sizeof(unsigned long long), st));
                 hipLaunchKernelGGL(kb_au_classify, dim3(nblk(n)), dim3(256), 0, st, abort, n, aa);
-                hipLaunchKernelGGL(kb_au_reserve, dim3(grid), dim3(256), 0, st, abort, aa);
-                hipLaunchKernelGGL(kb_au_size, dim3(grid), dim3(256), 0, st, abort, aa);
-                hipLaunchKernelGGL(kb_au_check, dim3(1), dim3(64), 0, st, abort, b.cnt, g->pool_top_dev, g->pool_cap, k);
+                hipLaunchKernelGGL(kb_au_reserve, dim3(grid), dim3(256), 0, st, abort, aa,
+                                   reinterpret_cast<const unsigned long long*>(g->pool_top_dev), g->pool_cap, k, g->done);
                 hipLaunchKernelGGL(kb_au_relocate, dim3(grid), dim3(256), 0, st, abort, aa, g->pool_top_dev);
                 hipLaunchKernelGGL(kb_au_pending, dim3(grid), dim3(256), 0, st, abort, aa);
                 break;
