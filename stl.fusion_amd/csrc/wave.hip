@@ -2400,16 +2400,21 @@ hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true) {
     return hipGetLastError();
 }
 
+#ifndef FGI_ROOT_BLOCK
+#define FGI_ROOT_BLOCK 256   // measurement builds: make variant-rootblk RB=<threads> (a multiple of 64)
+#endif
 void launch_roots(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev, uint32_t base,
                   uint32_t n_range, int publish) {
-    const uint32_t nb = (n_roots + kBlock - 1) / kBlock;
+    constexpr uint32_t kRootBlock = FGI_ROOT_BLOCK;
+    static_assert(kRootBlock % 64 == 0 && kRootBlock <= kBlock, "root block");
+    const uint32_t nb = (n_roots + kRootBlock - 1) / kRootBlock;
     auto* node = reinterpret_cast<unsigned long long*>(g->node);
     const Out o = out_for(g, 0, &g->ctr->lvl[0]);
     // the immediate roots' launch never publishes: the second launch adds to the same counter
     if (imm_dev)
-        hipLaunchKernelGGL(k_roots<1>, dim3(nb), dim3(kBlock), 0, g->stream, roots_dev, imm_dev, n_roots, base, n_range,
+        hipLaunchKernelGGL(k_roots<1>, dim3(nb), dim3(kRootBlock), 0, g->stream, roots_dev, imm_dev, n_roots, base, n_range,
                            node, g->vis_bm, o, g->ctr, g->done, 0);
-    hipLaunchKernelGGL(k_roots<0>, dim3(nb), dim3(kBlock), 0, g->stream, roots_dev, imm_dev, n_roots, base, n_range, node,
+    hipLaunchKernelGGL(k_roots<0>, dim3(nb), dim3(kRootBlock), 0, g->stream, roots_dev, imm_dev, n_roots, base, n_range, node,
                        g->vis_bm, o, g->ctr, g->done, publish);
 }
 
