@@ -2722,6 +2722,7 @@ static fgi_status run_wave_fused(fgi_graph* g, uint32_t n_roots, const uint32_t*
         }
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
+        if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w1, s));   // the round's end (re-recorded if it goes on)
         FGI_HIP(g, hipStreamSynchronize(s));
         ++syncs;
         const WaveCtr& c = *g->ctr_host;
@@ -2756,10 +2757,6 @@ static fgi_status run_wave_fused(fgi_graph* g, uint32_t n_roots, const uint32_t*
         P = (g->opt_fused & kFusedNoPredict) ? 1 : kMidMax;   // more mid levels than predicted
     }
     const WaveCtr& c = *g->ctr_host;
-    if (timing || stats) {
-        FGI_HIP(g, hipEventRecord(g->ev_w1, s));
-        FGI_HIP(g, hipEventSynchronize(g->ev_w1));
-    }
     g->last_mid = (int)c.n_mid;
     if (imm_dev && n_roots) note_words(g);   // immediate roots changed node words
     g->last_wave_n = c.inv;
@@ -2885,6 +2882,9 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         final_done = true;
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
+        // the wave's end marker rides on the group's synchronisation (re-recorded if the wave goes on):
+        // recording it after the wait would cost the call a further device round trip
+        if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w1, s));
         FGI_HIP(g, hipStreamSynchronize(s));
         ++syncs;
         for (int l = L0; l < L; ++l) {
@@ -2939,11 +2939,8 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         FGI_HIP(g, launch_final(g, g->n_handles, g->want_ids));
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
+        if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w1, s));
         FGI_HIP(g, hipStreamSynchronize(s));
-    }
-    if (timing || stats) {
-        FGI_HIP(g, hipEventRecord(g->ev_w1, s));
-        FGI_HIP(g, hipEventSynchronize(g->ev_w1));
     }
     if (imm_dev && n_roots) note_words(g);   // immediate roots changed node words
     g->last_wave_n = g->ctr_host->inv;
@@ -3098,6 +3095,7 @@ static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveP
         hipLaunchKernelGGL(k_part_tail, dim3(1), dim3(64), 0, s, g->ctr, L0, L, coll ? pv.world : 0u, pv.send_cnt, pb.cur,
                            pb.red, K);
         glob.assign(cnt, 0);
+        FGI_HIP(g, hipEventRecord(g->ev_w1, s));   // the round's end (re-recorded if the wave goes on)
         FGI_TRY(part_allreduce_sum(g, pb.red, glob.data(), cnt));   // the wave's one host synchronisation
         if (rounds == 0) plan_ft.assign(glob.begin() + 2, glob.end());
         ++syncs;
@@ -3134,8 +3132,6 @@ static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveP
         if (rounds > (1u << 20)) return set_err(g, FGI_EDEVICE, "planned partitioned wave: no end in sight");
         plan.assign(16, 0);
     }
-    FGI_HIP(g, hipEventRecord(g->ev_w1, s));
-    FGI_HIP(g, hipEventSynchronize(g->ev_w1));
     // the next wave's plan: Beamer's rules over this wave's global levels (as the host-driven loop
     // decides them), computed alike on every rank from the all-reduced {F, T}
     {
