@@ -138,6 +138,9 @@ constexpr int kDoneStride = 16;         // 128 B apart
 constexpr uint32_t kFinalBlocks = FGI_FINAL_BLOCKS; // grid of the final collect (invalidated bitmap -> list)
 constexpr uint32_t kFinalWpb = FGI_FINAL_WPB;       // fewest 64-bit bitmap words per final-collect block
 constexpr uint32_t kInitBlocks = FGI_INIT_BLOCKS;   // grid of k_wave_init
+#ifndef FGI_SPIN_WAIT
+#define FGI_SPIN_WAIT 1                     // measurement builds: make variant-nospin (stream synchronisation)
+#endif
 #ifndef FGI_HOT
 #define FGI_HOT 524288                  // measurement builds: make variant-hot HOT=<n> (a multiple of 256)
 #endif
@@ -211,7 +214,8 @@ struct WaveCtr {
     unsigned long long mid_kind[16];  // per k_level launch of the round (mid index): 0 nothing, 1 push, 2 pull
     unsigned long long mid_push_edges;  // edges / entries of the push levels run by k_level launches
     unsigned long long mid_push_f;
-    unsigned long long pad2[3];
+    unsigned long long t0;          // device wall clock at k_wave_init (a wave's kernel span without events)
+    unsigned long long pad2[2];
     LevelCtr lvl[kRing];
 };
 constexpr unsigned long long kPhaseDone = 1;
@@ -289,6 +293,11 @@ struct fgi_graph {
     unsigned long long* gbar = nullptr;   // [kGbarWords] grid-barrier counters (k_wave_coop, k_wave_fused)
     unsigned long long* blk_stats = nullptr;   // [kStatBlocks][kStatCols] per-block wave statistics
     fgi::WaveCtr* ctr_host = nullptr;  // pinned
+    // fine-grained host memory the wave's publish kernel writes: the counters, then a sequence word
+    // (ctr_pub[kPubWords]) the host spins on instead of a stream synchronisation (run_wave)
+    unsigned long long* ctr_pub = nullptr;
+    uint64_t pub_seq = 0;
+    int wall_khz = 0;                   // device wall-clock rate (WaveCtr::t0 and the publish time)
     uint32_t* roots_buf = nullptr;     // staging for host roots
     uint8_t* imm_buf = nullptr;
     uint64_t roots_cap = 0;

@@ -33,6 +33,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <vector>
 
@@ -2186,7 +2187,8 @@ __global__ __launch_bounds__(kBlock) void k_wave_init(WaveCtr* ctr, unsigned lon
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t nthr = (uint64_t)gridDim.x * blockDim.x;
     unsigned long long* c = reinterpret_cast<unsigned long long*>(ctr);
-    for (uint64_t i = tid; i < sizeof(WaveCtr) / 8; i += nthr) c[i] = 0ull;
+    // the word's one writer stamps the wave's start (statistics without stream events, run_wave)
+    for (uint64_t i = tid; i < sizeof(WaveCtr) / 8; i += nthr) c[i] = i == offsetof(WaveCtr, t0) / 8 ? wall_clock64() : 0ull;
     for (uint64_t i = tid; i < (uint64_t)kStatBlocks * kStatCols; i += nthr) blk[i] = 0ull;
     uint4* f4 = reinterpret_cast<uint4*>(inv_bm);
     for (uint64_t i = tid; i < bm_words / 4; i += nthr) f4[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -2804,6 +2806,52 @@ static fgi_status run_wave_fused(fgi_graph* g, uint32_t n_roots, const uint32_t*
     return FGI_OK;
 }
 
+// The end of a level group: the counters to the host and the host's wait for them. With
+// FGI_SPIN_WAIT a one-block kernel writes the counters into fine-grained host memory, then (after a
+// system-scope fence) a sequence word the host spins on: the wait ends when that word lands instead of
+// when the runtime observes the stream's completion, and no copy command is issued. The spin polls the
+// stream every 1,024 pauses, so a fault or a lost write still ends the wait. `mark` records the wave's
+// end event before the publish kernel (complete once the word is seen, so its wait costs nothing);
+// the publish kernel also leaves its start on the device wall clock at ctr_pub[kPubWords + 1], which
+// with WaveCtr::t0 times a wave without stream events (each event record costs the stream ~5 us).
+constexpr uint32_t kPubWords = sizeof(WaveCtr) / 8;
+__global__ __launch_bounds__(256) void k_publish_ctr(const unsigned long long* __restrict__ src, unsigned long long* dst,
+                                                     unsigned long long seq) {
+    if (threadIdx.x == 0) dst[kPubWords + 1] = wall_clock64();
+    for (uint32_t i = threadIdx.x; i < kPubWords; i += blockDim.x) dst[i] = src[i];
+    __threadfence_system();
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(dst + kPubWords, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+static fgi_status counters_to_host(fgi_graph* g, hipStream_t s, bool mark) {
+#if FGI_SPIN_WAIT
+    if (mark) FGI_HIP(g, hipEventRecord(g->ev_w1, s));
+    const unsigned long long seq = ++g->pub_seq;
+    hipLaunchKernelGGL(k_publish_ctr, dim3(1), dim3(256), 0, s, reinterpret_cast<const unsigned long long*>(g->ctr),
+                       g->ctr_pub, seq);
+    FGI_HIP(g, hipGetLastError());
+    unsigned long long* word = g->ctr_pub + kPubWords;
+    for (uint64_t k = 1; __atomic_load_n(word, __ATOMIC_ACQUIRE) != seq; ++k) {
+        __builtin_ia32_pause();
+        if ((k & 1023) == 0) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e == hipErrorNotReady) continue;
+            if (e != hipSuccess) FGI_HIP(g, e);
+            if (__atomic_load_n(word, __ATOMIC_ACQUIRE) != seq)
+                return set_err(g, FGI_EDEVICE, "wave counters: the stream completed without publishing them");
+        }
+    }
+    memcpy(g->ctr_host, g->ctr_pub, sizeof(WaveCtr));
+    if (mark) FGI_HIP(g, hipEventSynchronize(g->ev_w1));
+#else
+    FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
+    if (mark) FGI_HIP(g, hipEventRecord(g->ev_w1, s));
+    FGI_HIP(g, hipStreamSynchronize(s));
+#endif
+    return FGI_OK;
+}
+
 fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                     fgi_wave_stats* stats) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -2839,7 +2887,9 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         if (hipGetSymbolAddress(&pp, HIP_SYMBOL(d_probe)) == hipSuccess) (void)hipMemsetAsync(pp, 0, sizeof(d_probe), s);
     }
 #endif
-    if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
+    // the wave's span: stream events with per-level timing, else the device wall clock (spin waits)
+    const bool events = timing || (stats && !FGI_SPIN_WAIT);
+    if (events) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
     if (n_roots) {
         g->v_dirty = true;
         launch_roots(g, n_roots, roots_dev, imm_dev, 0u, g->n_handles, 0);
@@ -2881,11 +2931,9 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         FGI_HIP(g, launch_final(g, g->n_handles, g->want_ids));   // idempotent: repeated if the wave goes on
         final_done = true;
         FGI_HIP(g, hipGetLastError());
-        FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
         // the wave's end marker rides on the group's synchronisation (re-recorded if the wave goes on):
         // recording it after the wait would cost the call a further device round trip
-        if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w1, s));
-        FGI_HIP(g, hipStreamSynchronize(s));
+        FGI_TRY(counters_to_host(g, s, events));
         ++syncs;
         for (int l = L0; l < L; ++l) {
             const LevelCtr& lc = g->ctr_host->lvl[l % kRing];
@@ -2938,9 +2986,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     if (!final_done) {   // no roots
         FGI_HIP(g, launch_final(g, g->n_handles, g->want_ids));
         FGI_HIP(g, hipGetLastError());
-        FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
-        if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w1, s));
-        FGI_HIP(g, hipStreamSynchronize(s));
+        FGI_TRY(counters_to_host(g, s, events));
     }
     if (imm_dev && n_roots) note_words(g);   // immediate roots changed node words
     g->last_wave_n = g->ctr_host->inv;
@@ -2974,7 +3020,13 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         const uint64_t pull_b = pull_level_bytes(c);
         stats->alg_bytes += push_b + pull_b + 4 * v + 5ull * n_roots;
         float wave_ms = 0;
-        hipEventElapsedTime(&wave_ms, g->ev_w0, g->ev_w1);
+        if (events) {
+            hipEventElapsedTime(&wave_ms, g->ev_w0, g->ev_w1);
+        } else {
+            if (!g->wall_khz) FGI_HIP(g, hipDeviceGetAttribute(&g->wall_khz, hipDeviceAttributeWallClockRate, g->device));
+            const uint64_t t1 = g->ctr_pub[kPubWords + 1];
+            wave_ms = t1 > c.t0 && g->wall_khz > 0 ? (float)((double)(t1 - c.t0) / g->wall_khz) : 0.f;
+        }
         stats->kernel_ms += wave_ms;
         stats->expand_ms += expand_ms;
         stats->pull_ms += pull_ms;
