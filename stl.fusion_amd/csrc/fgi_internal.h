@@ -298,6 +298,8 @@ struct fgi_graph {
     unsigned long long* ctr_pub = nullptr;
     uint64_t pub_seq = 0;
     int wall_khz = 0;                   // device wall-clock rate (WaveCtr::t0 and the publish time)
+    uint64_t last_pub_t = 0;            // the last publish_wait's device wall-clock stamp
+    unsigned long long* red_pub = nullptr;   // fine-grained host words of the partition's all-reduce results
     uint32_t* roots_buf = nullptr;     // staging for host roots
     uint8_t* imm_buf = nullptr;
     uint64_t roots_cap = 0;
@@ -527,6 +529,11 @@ bool part_view(fgi_graph* g, PartView* v);
 // Returns the number of target ids received (concatenated at recv_buf) and sent.
 fgi_status part_exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent, uint64_t* glob);
 // Sum of count (1..kPartRedMax) device u64 over all ranks, returned on the host.
+// src[0, words) of device memory into the fine-grained host buffer dst (words + 2 long), the host
+// spinning on the sequence word dst[words]; dst[words + 1] = the publish's device wall-clock stamp
+// (wave.hip). wall_ms: milliseconds between two such stamps (WaveCtr::t0 is one).
+fgi_status publish_wait(fgi_graph* g, hipStream_t s, const unsigned long long* src, uint32_t words, unsigned long long* dst);
+float wall_ms(fgi_graph* g, uint64_t t0, uint64_t t1);
 fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out,
                               uint32_t count = 1);
 // all-gather every rank's local invalidated-bitmap words into front_global (part.hip)

@@ -1866,9 +1866,11 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
     hipMemset(g->uin_more, 0, g->bm_words * 4);
     if (hipHostMalloc(reinterpret_cast<void**>(&g->ctr_host), sizeof(WaveCtr)) != hipSuccess ||
         hipHostMalloc(reinterpret_cast<void**>(&g->misc_host), 16 * sizeof(unsigned long long)) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&g->ctr_pub), sizeof(WaveCtr) + 128, hipHostMallocCoherent) != hipSuccess)
+        hipHostMalloc(reinterpret_cast<void**>(&g->ctr_pub), sizeof(WaveCtr) + 128, hipHostMallocCoherent) != hipSuccess ||
+        hipHostMalloc(reinterpret_cast<void**>(&g->red_pub), (kPartRedMax + 16) * 8, hipHostMallocCoherent) != hipSuccess)
         return fail(FGI_ENOMEM);
     memset(g->ctr_pub, 0, sizeof(WaveCtr) + 128);
+    memset(g->red_pub, 0, (kPartRedMax + 16) * 8);
     hipMemset(g->node, 0, H * sizeof(uint64_t));
     hipMemset(g->row_off, 0, H * sizeof(uint64_t));
     hipMemset(g->row_len, 0, H * sizeof(uint32_t));
@@ -1944,6 +1946,7 @@ fgi_status fgi_destroy(fgi_graph* g) {
     if (g->scratch) hipFree(g->scratch);
     if (g->ctr_host) hipHostFree(g->ctr_host);
     if (g->ctr_pub) hipHostFree(g->ctr_pub);
+    if (g->red_pub) hipHostFree(g->red_pub);
     if (g->misc_host) hipHostFree(g->misc_host);
     for (hipEvent_t e : g->ev) hipEventDestroy(e);
     for (hipEvent_t e : g->batch_ev) hipEventDestroy(e);

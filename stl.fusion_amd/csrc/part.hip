@@ -250,14 +250,20 @@ struct RcclComm final : PartComm {
         const bool big = count > 4;
         unsigned long long* dst = big ? p->red : p->scalar;
         unsigned long long* host = big ? p->red_host : p->scalar_host;
+        const unsigned long long* src = dev_val;   // one rank: the sum is the value
         if (p->v.world > 1 || g->opt_part_coll) {
             FGI_NCCL(g, rccl().AllReduce(dev_val, dst, count, ncclUint64, ncclSum, p->comm, s));
-            FGI_HIP(g, hipMemcpyAsync(host, dst, 8 * count, hipMemcpyDeviceToHost, s));
-        } else {   // one rank: the sum is the value
-            FGI_HIP(g, hipMemcpyAsync(host, dev_val, 8 * count, hipMemcpyDeviceToHost, s));
+            src = dst;
         }
+#if FGI_SPIN_WAIT
+        (void)host;
+        FGI_TRY(publish_wait(g, s, src, count, g->red_pub));   // the host spins instead of a stream sync
+        for (uint32_t i = 0; i < count; ++i) out[i] = g->red_pub[i];
+#else
+        FGI_HIP(g, hipMemcpyAsync(host, src, 8 * count, hipMemcpyDeviceToHost, s));
         FGI_HIP(g, hipStreamSynchronize(s));
         for (uint32_t i = 0; i < count; ++i) out[i] = host[i];
+#endif
         return FGI_OK;
     }
     fgi_status allgather_front_async(fgi_graph* g) override { return allgather_front(g); }   // stream-ordered
@@ -406,9 +412,15 @@ struct LocalComm final : PartComm {
 
     fgi_status allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out, uint32_t count) override {
         PartState* p = ps(g);
+#if FGI_SPIN_WAIT
+        (void)p;
+        FGI_TRY(publish_wait(g, g->stream, dev_val, count, g->red_pub));
+        const unsigned long long* host = g->red_pub;
+#else
         unsigned long long* host = count > 4 ? p->red_host : p->scalar_host;
         FGI_HIP(g, hipMemcpyAsync(host, dev_val, 8 * count, hipMemcpyDeviceToHost, g->stream));
         FGI_HIP(g, hipStreamSynchronize(g->stream));
+#endif
         {
             std::lock_guard<std::mutex> lk(grp->mu);
             for (uint32_t i = 0; i < count; ++i) grp->vals[(size_t)rank * kPartRedMax + i] = host[i];

@@ -2814,24 +2814,26 @@ static fgi_status run_wave_fused(fgi_graph* g, uint32_t n_roots, const uint32_t*
 // end event before the publish kernel (complete once the word is seen, so its wait costs nothing);
 // the publish kernel also leaves its start on the device wall clock at ctr_pub[kPubWords + 1], which
 // with WaveCtr::t0 times a wave without stream events (each event record costs the stream ~5 us).
-constexpr uint32_t kPubWords = sizeof(WaveCtr) / 8;
-__global__ __launch_bounds__(256) void k_publish_ctr(const unsigned long long* __restrict__ src, unsigned long long* dst,
-                                                     unsigned long long seq) {
-    if (threadIdx.x == 0) dst[kPubWords + 1] = wall_clock64();
-    for (uint32_t i = threadIdx.x; i < kPubWords; i += blockDim.x) dst[i] = src[i];
+[[maybe_unused]] constexpr uint32_t kPubWords = sizeof(WaveCtr) / 8;
+namespace {
+__global__ __launch_bounds__(256) void k_publish(const unsigned long long* __restrict__ src, uint32_t words,
+                                                 unsigned long long* dst, unsigned long long seq) {
+    if (threadIdx.x == 0) dst[words + 1] = wall_clock64();
+    for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) dst[i] = src[i];
     __threadfence_system();
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(dst + kPubWords, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) __hip_atomic_store(dst + words, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-static fgi_status counters_to_host(fgi_graph* g, hipStream_t s, bool mark) {
-#if FGI_SPIN_WAIT
-    if (mark) FGI_HIP(g, hipEventRecord(g->ev_w1, s));
+}  // namespace
+
+// src[0, words) into the fine-grained host buffer dst (words + 2 long), waiting for the sequence word
+// dst[words]; dst[words + 1] is the publish kernel's start on the device wall clock
+fgi_status publish_wait(fgi_graph* g, hipStream_t s, const unsigned long long* src, uint32_t words, unsigned long long* dst) {
     const unsigned long long seq = ++g->pub_seq;
-    hipLaunchKernelGGL(k_publish_ctr, dim3(1), dim3(256), 0, s, reinterpret_cast<const unsigned long long*>(g->ctr),
-                       g->ctr_pub, seq);
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, src, words, dst, seq);
     FGI_HIP(g, hipGetLastError());
-    unsigned long long* word = g->ctr_pub + kPubWords;
+    unsigned long long* word = dst + words;
     for (uint64_t k = 1; __atomic_load_n(word, __ATOMIC_ACQUIRE) != seq; ++k) {
         __builtin_ia32_pause();
         if ((k & 1023) == 0) {
@@ -2839,9 +2841,26 @@ static fgi_status counters_to_host(fgi_graph* g, hipStream_t s, bool mark) {
             if (e == hipErrorNotReady) continue;
             if (e != hipSuccess) FGI_HIP(g, e);
             if (__atomic_load_n(word, __ATOMIC_ACQUIRE) != seq)
-                return set_err(g, FGI_EDEVICE, "wave counters: the stream completed without publishing them");
+                return set_err(g, FGI_EDEVICE, "publish: the stream completed without the sequence word");
         }
     }
+    g->last_pub_t = dst[words + 1];
+    return FGI_OK;
+}
+
+// the device wall clock in ms between two stamps (0 if unknown)
+float wall_ms(fgi_graph* g, uint64_t t0, uint64_t t1) {
+    if (!g->wall_khz && hipDeviceGetAttribute(&g->wall_khz, hipDeviceAttributeWallClockRate, g->device) != hipSuccess)
+        g->wall_khz = -1;
+    return t1 > t0 && g->wall_khz > 0 ? (float)((double)(t1 - t0) / g->wall_khz) : 0.f;
+}
+
+namespace {
+
+static fgi_status counters_to_host(fgi_graph* g, hipStream_t s, bool mark) {
+#if FGI_SPIN_WAIT
+    if (mark) FGI_HIP(g, hipEventRecord(g->ev_w1, s));
+    FGI_TRY(publish_wait(g, s, reinterpret_cast<const unsigned long long*>(g->ctr), kPubWords, g->ctr_pub));
     memcpy(g->ctr_host, g->ctr_pub, sizeof(WaveCtr));
     if (mark) FGI_HIP(g, hipEventSynchronize(g->ev_w1));
 #else
@@ -2851,6 +2870,8 @@ static fgi_status counters_to_host(fgi_graph* g, hipStream_t s, bool mark) {
 #endif
     return FGI_OK;
 }
+
+}  // namespace
 
 fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                     fgi_wave_stats* stats) {
@@ -3023,9 +3044,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         if (events) {
             hipEventElapsedTime(&wave_ms, g->ev_w0, g->ev_w1);
         } else {
-            if (!g->wall_khz) FGI_HIP(g, hipDeviceGetAttribute(&g->wall_khz, hipDeviceAttributeWallClockRate, g->device));
-            const uint64_t t1 = g->ctr_pub[kPubWords + 1];
-            wave_ms = t1 > c.t0 && g->wall_khz > 0 ? (float)((double)(t1 - c.t0) / g->wall_khz) : 0.f;
+            wave_ms = wall_ms(g, c.t0, g->last_pub_t);
         }
         stats->kernel_ms += wave_ms;
         stats->expand_ms += expand_ms;
@@ -3077,6 +3096,10 @@ uint64_t part_plan_key(const fgi_graph* g) {
 // frontier, the ids still waiting and every level's {F, T}. If that finds work left, push levels
 // follow, planned the same way, until none is left. The direction of a level is a cost choice:
 // results do not depend on the plan.
+// a partitioned wave times itself with stream events only when per-level timing is on (or without the
+// spin wait); otherwise by the device wall clock between WaveCtr::t0 and the wave's last publish
+static inline bool part_events(const fgi_graph* g) { return g->opt_level_timing != 0 || !FGI_SPIN_WAIT; }
+
 static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveParams& wp, const PartBuckets& pb,
                                    uint32_t n_roots, fgi_wave_stats* stats, std::chrono::steady_clock::time_point t0) {
     hipStream_t s = g->stream;
@@ -3147,8 +3170,9 @@ static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveP
         hipLaunchKernelGGL(k_part_tail, dim3(1), dim3(64), 0, s, g->ctr, L0, L, coll ? pv.world : 0u, pv.send_cnt, pb.cur,
                            pb.red, K);
         glob.assign(cnt, 0);
-        FGI_HIP(g, hipEventRecord(g->ev_w1, s));   // the round's end (re-recorded if the wave goes on)
+        if (part_events(g)) FGI_HIP(g, hipEventRecord(g->ev_w1, s));   // the round's end (re-recorded if the wave goes on)
         FGI_TRY(part_allreduce_sum(g, pb.red, glob.data(), cnt));   // the wave's one host synchronisation
+        if (timing) FGI_HIP(g, hipEventSynchronize(g->ev_w1));       // complete already: the level events too
         if (rounds == 0) plan_ft.assign(glob.begin() + 2, glob.end());
         ++syncs;
         ++rounds;
@@ -3227,7 +3251,8 @@ static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveP
         stats->pull_bytes += pull_b;
         stats->pull_launches += pull_launches;
         float wave_ms = 0;
-        hipEventElapsedTime(&wave_ms, g->ev_w0, g->ev_w1);
+        if (part_events(g)) hipEventElapsedTime(&wave_ms, g->ev_w0, g->ev_w1);
+        else wave_ms = wall_ms(g, c.t0, g->last_pub_t);
         stats->kernel_ms += wave_ms;
         stats->expand_ms += expand_ms;
         stats->expand_launches += expand_launches;
@@ -3261,7 +3286,9 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
         FGI_HIP(g, hipEventCreateWithFlags(&e, event_flags()));
         g->ev.push_back(e);
     }
-    FGI_HIP(g, hipEventRecord(g->ev_w0, s));
+    // the wave's span: stream events with per-level timing, else the device wall clock (spin waits:
+    // WaveCtr::t0 from k_wave_init, the end from the last publish)
+    if (part_events(g)) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
     g->v_dirty = true;
     if (n_roots) launch_roots(g, n_roots, roots_dev, imm_dev, pv.base, pv.n_local, 1);
     if (imm_dev && n_roots) note_words(g);
@@ -3401,9 +3428,7 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     }
     FGI_HIP(g, launch_final(g, pv.n_local));
     FGI_HIP(g, hipGetLastError());
-    FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
-    FGI_HIP(g, hipEventRecord(g->ev_w1, s));
-    FGI_HIP(g, hipStreamSynchronize(s));
+    FGI_TRY(counters_to_host(g, s, part_events(g)));
     g->last_wave_n = g->ctr_host->inv;
     g->ids_valid = true;
     if (stats) {
@@ -3426,7 +3451,8 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
         stats->pull_bytes += pull_b;
         stats->pull_launches += pull_launches;
         float wave_ms = 0;
-        hipEventElapsedTime(&wave_ms, g->ev_w0, g->ev_w1);
+        if (part_events(g)) hipEventElapsedTime(&wave_ms, g->ev_w0, g->ev_w1);
+        else wave_ms = wall_ms(g, c.t0, g->last_pub_t);
         stats->kernel_ms += wave_ms;
         stats->expand_ms += expand_ms;
         stats->expand_launches += expand_launches;
