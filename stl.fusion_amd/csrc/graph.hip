@@ -2943,7 +2943,14 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
         if (spec) FGI_HIP(g, hipMemcpyAsync(H + ids_off, g->bout, spec * 4, hipMemcpyDeviceToHost, st));
         FGI_HIP(g, hipEventRecord(b1, st));
         if (times) t_enq = clk::now();
+#if FGI_SPIN_WAIT
+        // the host spins on a published sequence word behind the copies (wave.hip publish_wait) instead
+        // of a stream synchronisation; b1 is complete by then, so its wait returns at once
+        FGI_TRY(publish_wait(g, st, g->pool_top_dev, 0, g->red_pub));
+        FGI_HIP(g, hipEventSynchronize(b1));
+#else
         FGI_HIP(g, hipStreamSynchronize(st));
+#endif
         if (times) t_wait = clk::now();
         ++syncs;
         g->pool_top = scr_h[ptop_word];
