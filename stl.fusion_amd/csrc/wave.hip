@@ -2848,6 +2848,14 @@ fgi_status publish_wait(fgi_graph* g, hipStream_t s, const unsigned long long* s
     return FGI_OK;
 }
 
+// src[0, words) into dst (fine-grained host memory) without waiting: a later publish_wait on the same
+// stream covers it (its sequence word lands after this kernel's system-scope fence)
+static fgi_status publish_async(fgi_graph* g, hipStream_t s, const unsigned long long* src, uint32_t words, unsigned long long* dst) {
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, src, words, dst, 0ull);
+    FGI_HIP(g, hipGetLastError());
+    return FGI_OK;
+}
+
 // the device wall clock in ms between two stamps (0 if unknown)
 float wall_ms(fgi_graph* g, uint64_t t0, uint64_t t1) {
     if (!g->wall_khz && hipDeviceGetAttribute(&g->wall_khz, hipDeviceAttributeWallClockRate, g->device) != hipSuccess)
@@ -3163,7 +3171,12 @@ static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveP
         }
         // the final collect may be repeated if the wave goes on (it only reads the invalidated bitmap)
         FGI_HIP(g, launch_final(g, pv.n_local));
+#if FGI_SPIN_WAIT
+        // the counters ride to fine-grained host memory ahead of the all-reduce's published result
+        FGI_TRY(publish_async(g, s, reinterpret_cast<const unsigned long long*>(g->ctr), kPubWords, g->ctr_pub));
+#else
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
+#endif
         // the first round's levels decide the next wave's plan: their {F, T} ride on the all-reduce
         const int K = rounds == 0 ? L - L0 : 0;
         const uint32_t cnt = 2 + 2 * (uint32_t)K;
@@ -3172,6 +3185,9 @@ static fgi_status run_part_planned(fgi_graph* g, const PartView& pv, const WaveP
         glob.assign(cnt, 0);
         if (part_events(g)) FGI_HIP(g, hipEventRecord(g->ev_w1, s));   // the round's end (re-recorded if the wave goes on)
         FGI_TRY(part_allreduce_sum(g, pb.red, glob.data(), cnt));   // the wave's one host synchronisation
+#if FGI_SPIN_WAIT
+        memcpy(g->ctr_host, g->ctr_pub, sizeof(WaveCtr));
+#endif
         if (timing) FGI_HIP(g, hipEventSynchronize(g->ev_w1));       // complete already: the level events too
         if (rounds == 0) plan_ft.assign(glob.begin() + 2, glob.end());
         ++syncs;
