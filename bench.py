@@ -154,6 +154,27 @@ def dump_maps():
             dst.write(src.read())
 
 
+def select_workloads(world: int, config: str, partition: bool) -> dict:
+    """Which workloads a run measures (pinned by tests/test_bench_select.py).
+
+    N = 1: the headline is `config` (default rmat24 = BASELINE.json configs[1], the configuration the
+    metric is quoted on and which fits one GPU); with the default config the line also carries a
+    `configs2_single_gpu` sub-record — configs[2]'s graph on the same GPU, the base of the 2/4/8-GPU
+    curve. N > 1: BASELINE.json configs[2] exactly (R-MAT 27, edge factor 8, seed 0x5EED0027, 4,096
+    roots) over the N ranks — strong scaling, the total work fixed — and, secondary, the weak-scaling
+    point (configs[1]'s generator at scale 24 + log2 N, 16.8 M slots per GPU)."""
+    out = {"headline": config, "scaling": "weak", "secondary": []}
+    partitioned = world > 1 or partition
+    if world > 1 and config in ("rmat24", "rmat27"):
+        out["headline"] = "rmat27"
+        out["scaling"] = "strong"
+        out["secondary"] = [("weak_scaling", "rmat24", 24 + (world - 1).bit_length())]
+    elif world == 1 and config == "rmat24" and not partitioned:
+        out["secondary"] = [("configs2_single_gpu", "rmat27", None)]
+    out["partitioned"] = partitioned
+    return out
+
+
 def main():
     # Libraries (RCCL prints a banner on communicator init) must not write to stdout: the driver
     # reads exactly one JSON line from it. Route fd 1 to stderr and keep a handle on the real one.
@@ -171,7 +192,10 @@ def main():
     ap.add_argument("--partition", action="store_true",
                     help="use the partitioned RCCL engine even at N=1 (it is always used for N>1)")
     ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU waves after one warm-up (median reported)")
-    ap.add_argument("--cpu-single", action="store_true", help="also time the CPU oracle single-threaded")
+    ap.add_argument("--no-cpu-single", action="store_true",
+                    help="skip the single-threaded CPU wave (one wave at T = 1 on the identical graph, ~1 min)")
+    ap.add_argument("--cpu-c2-scale", type=int, default=25,
+                    help="R-MAT scale of the labelled configs[2] CPU sample (configs[2]'s generator; 0 skips it)")
     args = ap.parse_args()
 
     import torch
@@ -180,7 +204,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
+    gpu = local_rank % max(1, n_gpus_visible())
+    torch.cuda.set_device(gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -191,103 +216,165 @@ def main():
         # (FGI_BENCH_TORCH_BACKEND=nccl selects torch's RCCL for it instead).
         backend = os.environ.get("FGI_BENCH_TORCH_BACKEND", "gloo")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
         else:
             dist.init_process_group(backend)
-    tdev = "cpu" if (dist is not None and dist.get_backend() != "nccl") else f"cuda:{local_rank}"
+    tdev = "cpu" if (dist is not None and dist.get_backend() != "nccl") else f"cuda:{gpu}"
 
     pkg = _pkg.load()
     from stl_fusion_amd import workloads as W
-    partitioned = world > 1 or args.partition
-    cfg = dict(W.CONFIGS[args.config])
-    if partitioned:
-        # weak scaling: R-MAT scale 24 + log2(N) keeps configs[1]'s 16M slots per GPU (N = 8 is
-        # scale 27, the node count of configs[2]); --config rmat27 runs configs[2] exactly.
-        if cfg["kind"] != "rmat":
-            raise SystemExit("the partitioned engine runs R-MAT workloads")
-        if args.config == "rmat24":
-            cfg["scale"] = 24 + (world - 1).bit_length()
-    n = W.n_slots(cfg)
-    t0 = time.time()
-    if partitioned:
-        block = -(-n // world)
-        g = pkg.Graph(block, device=local_rank, rank=rank, world=world)
-        uid = [pkg.fgi.part_unique_id() if rank == 0 else None]
-        if dist:
-            dist.broadcast_object_list(uid, src=0)
-        g.part_init(n, uid[0])
-        g.part_synth_rmat(cfg["scale"], cfg["edge_factor"], cfg["seed"], cfg.get("stale_pct", 0),
-                          cfg.get("stale_seed", 0))
-        n_local = min(block, n - rank * block)
-        deg_local, _ = g.degrees()
-        deg = torch.zeros(block * world, dtype=torch.int32, device=tdev)
-        mine = torch.zeros(block, dtype=torch.int32, device=tdev)
-        mine[:n_local] = torch.from_numpy(deg_local[:n_local].astype(np.int32)).to(mine.device)
-        if dist and tdev == "cpu":
-            parts = [torch.zeros(block, dtype=torch.int32) for _ in range(world)]
-            dist.all_gather(parts, mine)
-            deg = torch.cat(parts)
-        elif dist:
-            dist.all_gather_into_tensor(deg, mine)
-        else:
-            deg = mine
-        deg_all = deg.cpu().numpy()[:n]
-        roots = W.pick_roots(cfg["roots"], n, cfg["roots_seed"], deg_all)
-        n_edges = int(deg_all.astype(np.int64).sum())
-    else:
-        g = pkg.Graph(n, device=local_rank)
-        W.build(g, cfg)
-        roots = W.roots_for(g, cfg)
-        _, n_edges = g.degrees()
-    build_s = time.time() - t0
-    for k, v in (("FGI_PULL_ALPHA", "OPT_PULL_ALPHA"), ("FGI_PULL_BETA", "OPT_PULL_BETA"), ("FGI_PULL_TPB", "OPT_PULL_TPB"),
-                 ("FGI_PART_PLAN", "OPT_PART_PLAN"), ("FGI_PROBE_SUMMARY", "OPT_PROBE_SUMMARY"),
-                 ("FGI_HOT_HEADS", "OPT_HOT_HEADS")):
-        if os.environ.get(k):   # measurement knobs (results never depend on them)
-            g.set_option(getattr(pkg.fgi, v), int(os.environ[k]))
-    d_roots = torch.from_numpy(roots.astype(np.int32)).to(f"cuda:{local_rank}")
-    g.snapshot()
-    log(f"[rank {rank}] built {args.config} (scale {cfg.get('scale')}): {n} slots, {n_edges} edges, "
-        f"{len(roots)} roots in {build_s:.1f}s, partitioned={partitioned}")
+    sel = select_workloads(world, args.config, args.partition)
+    partitioned = sel["partitioned"]
+    # one process per GPU; ranks beyond the node's GPUs (a rehearsal of N ranks on a smaller box) share
+    # device local_rank % count, and then the engine's collectives go through the host (torch's gloo
+    # group, fgi_part_init_host): RCCL refuses two ranks on one GPU
+    comm = os.environ.get("FGI_PART_COMM", "")
+    if partitioned and world > 1 and not comm:
+        comm = "host" if world > max(1, n_gpus_visible()) else "rccl"
+    knobs = (("FGI_PULL_ALPHA", "OPT_PULL_ALPHA"), ("FGI_PULL_BETA", "OPT_PULL_BETA"), ("FGI_PULL_TPB", "OPT_PULL_TPB"),
+             ("FGI_PART_PLAN", "OPT_PART_PLAN"), ("FGI_PROBE_SUMMARY", "OPT_PROBE_SUMMARY"),
+             ("FGI_HOT_HEADS", "OPT_HOT_HEADS"))
 
-    def step(stats):
-        g.restore()
+    def build(name, scale=None):
+        """The workload's graph (single device, or this rank's partition) and its root batch."""
+        cfg = dict(W.CONFIGS[name])
+        if scale:
+            cfg["scale"] = scale
+        n = W.n_slots(cfg)
+        t0 = time.time()
         if partitioned:
-            return g.part_invalidate(len(roots), d_roots.data_ptr(), 0, stats)
-        return g.invalidate_dev(len(roots), d_roots.data_ptr(), 0, stats)
+            if cfg["kind"] != "rmat":
+                raise SystemExit("the partitioned engine runs R-MAT workloads")
+            block = -(-n // world)
+            g = pkg.Graph(block, device=gpu, rank=rank, world=world)
+            if comm == "host":
+                g.part_init_host(n)
+            else:
+                uid = [pkg.fgi.part_unique_id() if rank == 0 else None]
+                if dist:
+                    dist.broadcast_object_list(uid, src=0)
+                g.part_init(n, uid[0])
+            g.part_synth_rmat(cfg["scale"], cfg["edge_factor"], cfg["seed"], cfg.get("stale_pct", 0),
+                              cfg.get("stale_seed", 0))
+            n_local = min(block, n - rank * block)
+            deg_local, _ = g.degrees()
+            mine = torch.zeros(block, dtype=torch.int32, device=tdev)
+            mine[:n_local] = torch.from_numpy(deg_local[:n_local].astype(np.int32)).to(mine.device)
+            if dist and tdev == "cpu":
+                parts = [torch.zeros(block, dtype=torch.int32) for _ in range(world)]
+                dist.all_gather(parts, mine)
+                deg = torch.cat(parts)
+            elif dist:
+                deg = torch.zeros(block * world, dtype=torch.int32, device=tdev)
+                dist.all_gather_into_tensor(deg, mine)
+            else:
+                deg = mine
+            deg_all = deg.cpu().numpy()[:n]
+            roots = W.pick_roots(cfg["roots"], n, cfg["roots_seed"], deg_all)
+            n_edges = int(deg_all.astype(np.int64).sum())
+        else:
+            g = pkg.Graph(n, device=gpu)
+            W.build(g, cfg)
+            roots = W.roots_for(g, cfg)
+            _, n_edges = g.degrees()
+        for k, v in knobs:
+            if os.environ.get(k):   # measurement knobs (results never depend on them)
+                g.set_option(getattr(pkg.fgi, v), int(os.environ[k]))
+        g.snapshot()
+        build_s = time.time() - t0
+        log(f"[rank {rank}] built {name} (scale {cfg.get('scale')}): {n} slots, {n_edges} edges, "
+            f"{len(roots)} roots in {build_s:.1f}s, partitioned={partitioned}, comm={comm or 'none'}")
+        return g, cfg, n, roots, n_edges, build_s
 
-    # the first wave may build the pull dependency-list cache (a per-topology index, like the
-    # rows themselves); it is timed separately and reported, never inside the timed steps
-    t_first = time.perf_counter()
-    step(pkg.WaveStats())
-    torch.cuda.synchronize()
-    first_wave_s = time.perf_counter() - t_first
+    def measure(g, roots):
+        """W untimed warm-up steps, then K timed steps between barriers (max over ranks), then the
+        same K steps again with per-level HIP events (the roofline figures)."""
+        d_roots = torch.from_numpy(roots.astype(np.int32)).to(f"cuda:{gpu}")
 
-    for _ in range(args.warmup):
+        def step(stats):
+            g.restore()
+            if partitioned:
+                return g.part_invalidate(len(roots), d_roots.data_ptr(), 0, stats)
+            return g.invalidate_dev(len(roots), d_roots.data_ptr(), 0, stats)
+
+        # the first wave may build the pull dependency-list cache (a per-topology index, like the
+        # rows themselves); it is timed separately and reported, never inside the timed steps
+        t_first = time.perf_counter()
         step(pkg.WaveStats())
+        torch.cuda.synchronize()
+        first_wave_s = time.perf_counter() - t_first
+        for _ in range(args.warmup):
+            step(pkg.WaveStats())
+        # headline: K steps with no per-level HIP events in the stream; the roofline figures come from
+        # a second, instrumented pass of the same steps, which times every k_level launch on the
+        # engine's stream
+        st = pkg.WaveStats()
+        g.set_option(pkg.fgi.OPT_LEVEL_TIMING, 0)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_start = time.perf_counter()
+        for _ in range(args.steps):
+            step(st)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        elapsed = time.perf_counter() - t_start
+        g.set_option(pkg.fgi.OPT_LEVEL_TIMING, 1)
+        st_k = pkg.WaveStats()
+        t_k = time.perf_counter()
+        for _ in range(args.steps):
+            step(st_k)
+        torch.cuda.synchronize()
+        instrumented_ms = (time.perf_counter() - t_k) / args.steps * 1e3
+        v_inv, e_trav, e_match = st.v_inv, st.e_trav, st.e_match
+        if dist:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            c = torch.tensor([v_inv, e_trav, e_match], dtype=torch.float64, device=tdev)
+            dist.all_reduce(c, op=dist.ReduceOp.SUM)
+            v_inv, e_trav, e_match = int(c[0].item()), int(c[1].item()), int(c[2].item())
+        return dict(st=st, st_k=st_k, elapsed=elapsed, first_wave_s=first_wave_s, instrumented_ms=instrumented_ms,
+                    v_inv=v_inv, e_trav=e_trav, e_match=e_match)
 
-    # headline: K steps with no per-level HIP events in the stream (only the wave-boundary pair the
-    # statistics need); the roofline figures come from a second, instrumented pass of the same
-    # steps, which times every k_level launch on the engine's stream
-    st = pkg.WaveStats()
-    g.set_option(pkg.fgi.OPT_LEVEL_TIMING, 0)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        step(st)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    g.set_option(pkg.fgi.OPT_LEVEL_TIMING, 1)
-    st_k = pkg.WaveStats()
-    t_k = time.perf_counter()
-    for _ in range(args.steps):
-        step(st_k)
-    torch.cuda.synchronize()
-    instrumented_ms = (time.perf_counter() - t_k) / args.steps * 1e3
+    def brief(m, cfg, n, roots, n_edges, build_s):
+        """A secondary workload's figures (the same measurement as the headline's)."""
+        st, st_k, K = m["st"], m["st_k"], args.steps
+        return {"workload": workload_name(cfg), "nodes": n, "edges": int(n_edges), "roots": int(len(roots)),
+                "scale": cfg.get("scale"), "edge_factor": cfg.get("edge_factor"),
+                "value": m["v_inv"] / m["elapsed"], "unit": "invalidated nodes/s",
+                "ms_per_step": m["elapsed"] / K * 1e3, "gteps": m["e_trav"] / m["elapsed"] / 1e9,
+                "v_inv_per_step": m["v_inv"] // K, "e_trav_per_step": m["e_trav"] // K,
+                "levels_per_step": st.levels / K, "pull_levels_per_step": st.pull_levels / K,
+                "host_syncs_per_step": st.host_syncs / K, "wave_kernel_ms": st.kernel_ms / K,
+                "pull_ms_per_step": st_k.pull_ms / K, "push_ms_per_step": st_k.expand_ms / K,
+                "first_wave_s": m["first_wave_s"], "build_s": build_s,
+                "parallelism": parallelism(), "n_gpus": world}
+
+    def parallelism():
+        if not partitioned:
+            return "single"
+        how = "host (gloo) collectives" if comm == "host" else "RCCL all-gather counts + all-to-all frontier"
+        return f"vertex-partition x{world} ({how})"
+
+    def workload_name(cfg):
+        names = {("rmat", 24, 16): "R-MAT scale 24 (16,777,216 nodes, 268,435,456 generated edges, dedup), "
+                                   "4,096-root batched invalidation (BASELINE.json configs[1])",
+                 ("rmat", 27, 8): "R-MAT scale 27, edge factor 8 (134,217,728 nodes, 1,073,741,824 generated edges, "
+                                  "dedup), 4,096 roots (BASELINE.json configs[2])",
+                 ("layered", None, None): "1.05M-node compute-method graph, fan-out 8, depth 6, 1k roots (configs[0])"}
+        key = (cfg["kind"], cfg.get("scale"), cfg.get("edge_factor"))
+        if cfg.get("stale_pct"):
+            return "configs[1] graph with 50% stale edges (configs[3])"
+        return names.get(key, names.get((cfg["kind"], None, None)) if cfg["kind"] == "layered" else
+                         f"R-MAT scale {cfg.get('scale')}, edge factor {cfg.get('edge_factor')} "
+                         f"({'weak-scaling point: configs[1] generator, 16.8M slots per GPU' if partitioned else 'size sweep'})")
+
+    g, cfg, n, roots, n_edges, build_s = build(sel["headline"])
+    m = measure(g, roots)
+    st, st_k = m["st"], m["st_k"]
+    elapsed = m["elapsed"]
 
     # end-to-end leg (SURVEY.md §8(d)'s t: root H2D -> wave -> V_inv D2H complete): fgi_invalidate
     # with the roots in host memory and the invalidated ids copied into a pinned host buffer
@@ -345,14 +432,21 @@ def main():
     if e2e is None and not partitioned:
         g.restore()
         ids_host = np.asarray(g.invalidate(roots), np.uint32)
-    v_inv, e_trav, e_match_all = st.v_inv, st.e_trav, st.e_match
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=tdev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        c = torch.tensor([v_inv, e_trav, e_match_all], dtype=torch.float64, device=tdev)
-        dist.all_reduce(c, op=dist.ReduceOp.SUM)
-        v_inv, e_trav, e_match_all = int(c[0].item()), int(c[1].item()), int(c[2].item())
+    v_inv, e_trav, e_match_all = m["v_inv"], m["e_trav"], m["e_match"]
+    try:
+        rv, rpath = pkg.fgi.rccl_info()
+        # libfgi resolves RCCL from /opt/rocm's librccl.so.1 at run time (RTLD_LOCAL, part.hip rccl()),
+        # so torch's bundled librccl, loaded first in this process, does not take its place
+        linked = "/opt/rocm"
+        differs = not os.path.realpath(rpath).startswith(os.path.realpath(linked))
+        rccl = {"version": rv, "path": rpath, "linked": linked + "/lib/librccl.so.1",
+                "differs_from_linked": differs, "torch_loaded_first": True}
+        log(f"[rank {rank}] libfgi RCCL: ncclGetVersion {rv} from {rpath}")
+        if differs:
+            log(f"[rank {rank}] WARNING: libfgi is bound to {rpath}, not {linked}/lib/librccl.so.1")
+    except Exception as e:  # informational only
+        rccl = {"error": repr(e)}
+    g.close()
 
     value = v_inv / elapsed
     gteps = e_trav / elapsed / 1e9
@@ -374,25 +468,22 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.config in ("rmat24", "rmat27") else "weak",
+        "scaling_note": ("N > 1 runs BASELINE.json configs[2] (R-MAT 27, edge factor 8) over the N GPUs: total work "
+                         "fixed. At N = 1 the headline is configs[1] (the metric's one-GPU configuration) and the "
+                         "curve's base is the `configs2_single_gpu` sub-record (configs[2]'s graph on this GPU)"),
         "vs_baseline": None,
         "dtype": "u64",
         "data": "synthetic",
         "config": {
-            "workload": {"rmat24": "R-MAT scale 24 (16,777,216 nodes, 268,435,456 generated edges, dedup), "
-                                   "4,096-root batched invalidation (BASELINE.json configs[1])",
-                         "layered_1m": "1.05M-node compute-method graph, fan-out 8, depth 6, 1k roots (configs[0])",
-                         "rmat27": "R-MAT scale 27, edge factor 8 (configs[2])",
-                         "rmat24_churn": "configs[1] graph with 50% stale edges (configs[3])"}.get(
-                args.config, f"R-MAT scale {cfg.get('scale')}, edge factor {cfg.get('edge_factor')} (size sweep)"),
+            "workload": workload_name(cfg),
             "nodes": n, "edges": int(n_edges), "roots": int(len(roots)),
-            "parallelism": (f"vertex-partition x{world} (RCCL all-gather counts + send/recv frontier)"
-                            if partitioned else "single"),
+            "parallelism": parallelism(),
             "scale": cfg.get("scale"), "edge_factor": cfg.get("edge_factor"),
         },
         "gteps": gteps,
-        "v_inv_per_step": st.v_inv // args.steps,
-        "e_trav_per_step": st.e_trav // args.steps,
+        "v_inv_per_step": v_inv // args.steps,
+        "e_trav_per_step": e_trav // args.steps,
         "e_trav_semantics": ("sum of |_usedBy| over the invalidated nodes at wave start; rows keep RemoveUsedBy'd "
                              "entries until the next prune, so later waves of a mutated graph count them. Here every "
                              "timed wave runs on the freshly built graph (restore only), which has none"),
@@ -402,7 +493,7 @@ def main():
         "wave_alg_gbs": wave_gbs,
         "pull_levels_per_step": st.pull_levels / args.steps,
         "remote_msgs_per_step": st.remote_msgs / args.steps,
-        "first_wave_s": first_wave_s,
+        "first_wave_s": m["first_wave_s"],
         "build_s": build_s,
         "roofline": {
             "bound": "hbm",
@@ -416,23 +507,15 @@ def main():
             "launches_per_step": k_launches / args.steps,
             "avg_launch_ms": k_ms / max(1, k_launches),
             "alg_bytes_per_launch": k_bytes / max(1, k_launches),
-            "timing_pass_ms_per_step": instrumented_ms,
+            "timing_pass_ms_per_step": m["instrumented_ms"],
             "push_levels": {"ms_per_step": st_k.expand_ms / args.steps,
                             "launches_per_step": st_k.expand_launches / args.steps,
-                            "gbs": (st_k.expand_bytes / (st_k.expand_ms * 1e-3) / 1e9) if st_k.expand_ms > 0 else 0.0,
-                            "note": "push levels run as their own k_level launches (more edges than one round "
-                                    "of the fused grid)"},
-            "fused": {"ms_per_step": st_k.fused_ms / args.steps,
-                      "launches_per_step": st_k.fused_launches / args.steps,
-                      "push_bytes_per_step": st_k.fused_push_bytes / args.steps,
-                      "gbs": (st_k.fused_push_bytes / (st_k.fused_ms * 1e-3) / 1e9) if st_k.fused_ms > 0 else 0.0,
-                      "note": "k_wave_fused head + tail: wave init, roots, every push level of at most one "
-                              "round of the grid, the collect after the pull levels and the final count; gbs "
-                              "counts only the push levels' bytes over the whole time of both launches"},
+                            "gbs": (st_k.expand_bytes / (st_k.expand_ms * 1e-3) / 1e9) if st_k.expand_ms > 0 else 0.0},
             "pull_levels": {"ms_per_step": st_k.pull_ms / args.steps,
                             "launches_per_step": st_k.pull_launches / args.steps,
                             "gbs": (st_k.pull_bytes / (st_k.pull_ms * 1e-3) / 1e9) if st_k.pull_ms > 0 else 0.0},
         },
+        "rccl": rccl,
     }
     # SURVEY.md §8(d)'s layout-A formula B = 28 V_exp + 24 E_trav + 4 E_match + 4 R counts every
     # edge of every expanded node, as a push-only traversal would read them. Pull levels read
@@ -450,64 +533,96 @@ def main():
     if e2e:
         result["e2e_ms_per_step"] = e2e["ms_per_step"]
         result["e2e"] = e2e
-    try:
-        rv, rpath = pkg.fgi.rccl_info()
-        # libfgi resolves RCCL from /opt/rocm's librccl.so.1 at run time (RTLD_LOCAL, part.hip rccl()),
-        # so torch's bundled librccl, loaded first in this process, does not take its place
-        linked = "/opt/rocm"
-        differs = not os.path.realpath(rpath).startswith(os.path.realpath(linked))
-        result["rccl"] = {"version": rv, "path": rpath, "linked": linked + "/lib/librccl.so.1",
-                          "differs_from_linked": differs, "torch_loaded_first": True}
-        log(f"[rank {rank}] libfgi RCCL: ncclGetVersion {rv} from {rpath}")
-        if differs:
-            log(f"[rank {rank}] WARNING: libfgi is bound to {rpath}, not {linked}/lib/librccl.so.1")
-    except Exception as e:  # informational only
-        result["rccl"] = {"error": repr(e)}
+
+    # secondary workloads: configs[2] on this one GPU (N = 1), the weak-scaling point (N > 1)
+    for key, name, scale in sel["secondary"]:
+        g2, cfg2, n2, roots2, e2, b2 = build(name, scale)
+        m2 = measure(g2, roots2)
+        g2.close()
+        result[key] = brief(m2, cfg2, n2, roots2, e2, b2)
+        log(f"[rank {rank}] {key}: {result[key]['ms_per_step']:.4f} ms/step, {result[key]['value'] / 1e9:.2f} G nodes/s")
+
     if rank == 0 and world == 1 and not args.no_cpu and cfg["kind"] == "rmat":
-        info = host_cpu_info()
-        threads = info["nproc"]
-        cscale = args.cpu_scale or cfg["scale"]
-        try:
-            cpu, cbuild, cm, cr, same_roots, same_set = cpu_baseline(threads, cfg, cscale, roots, ids_host,
-                                                                      args.cpu_runs, args.cpu_single)
-            best = cpu[threads]
-            same = cscale == cfg["scale"]
-            result["cpu_baseline"] = {
-                "value": best["v_inv"] / best["s"],
-                "unit": "invalidated nodes/s",
-                "cores": threads,
-                "kind": "port",
-                "sample": (f"oracle (C++ restatement of the Computed.Invalidate cascade: per-node mutex, HashSetSlim3 "
-                           f"usedBy, hash registry, RemoveUsedBy) on "
-                           + (f"the identical {args.config} graph and {cr}-root batch (BASELINE.json configs[1]: R-MAT "
-                              f"scale {cscale}, {cm} edges; roots equal to the GPU's: {same_roots})" if same else
-                              f"a labelled sample: R-MAT scale {cscale} ({cm} edges), {cr} roots")
-                           + f", parallel over roots at T = nproc = {threads}; median of {len(best['runs'])} timed "
-                             f"waves after a warm-up, each from a restored pristine copy; "
-                             f"{best['v_inv']} nodes / {best['e_trav']} edges per wave"),
-                "gteps": best["e_trav"] / best["s"] / 1e9,
-                "wave_s": best["s"],
-                "wave_s_runs": best["runs"],
-                "single_thread_value": (cpu[1]["v_inv"] / cpu[1]["s"]) if 1 in cpu else None,
-                "single_thread_wave_s": cpu[1]["s"] if 1 in cpu else None,
-                "same_result_as_gpu": bool(same and same_set and best["v_inv"] == st.v_inv // args.steps
-                                           and best["e_trav"] == st.e_trav // args.steps),
-                "same_set_as_gpu": same_set,
-                "host": info,
-                "build_s": cbuild,
-                "peak_rss_gb": peak_rss_gb(),
-            }
-            if same:
-                result["cpu_baseline"]["gpu_speedup"] = value / result["cpu_baseline"]["value"]
-            log(f"cpu baseline: {cpu} (build {cbuild:.1f}s, host {info})")
-        except Exception as e:  # the CPU leg must not hide the GPU number
-            result["cpu_baseline"] = {"value": None, "error": repr(e)}
+        result["cpu_baseline"] = cpu_legs(args, cfg, roots, ids_host, st, value, result.get("configs2_single_gpu"))
     if rank == 0:
         json_out.write(json.dumps(result) + "\n")
         json_out.flush()
-    g.close()
     if dist:
         dist.destroy_process_group()
+
+
+def cpu_legs(args, cfg, roots, ids_host, st, value, c2):
+    """The cpu_baseline object: the oracle on the identical configs[1] graph and roots at T = nproc
+    (median of --cpu-runs after a warm-up) and at T = 1 (one wave: the closure of 4,096 roots is the
+    giant component's, so fewer roots would not shorten it), and a labelled sample of configs[2]'s
+    generator at --cpu-c2-scale beside the GPU's configs[2] figure."""
+    info = host_cpu_info()
+    threads = info["nproc"]
+    cscale = args.cpu_scale or cfg["scale"]
+    try:
+        cpu, cbuild, cm, cr, same_roots, same_set = cpu_baseline(threads, cfg, cscale, roots, ids_host,
+                                                                  args.cpu_runs, not args.no_cpu_single)
+    except Exception as e:  # the CPU leg must not hide the GPU number
+        return {"value": None, "error": repr(e)}
+    best = cpu[threads]
+    same = cscale == cfg["scale"]
+    rec = {
+        "value": best["v_inv"] / best["s"],
+        "unit": "invalidated nodes/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"oracle (C++ restatement of the Computed.Invalidate cascade: per-node mutex, HashSetSlim3 "
+                   f"usedBy, hash registry, RemoveUsedBy) on "
+                   + (f"the identical {cfg['scale']}-scale graph and {cr}-root batch (BASELINE.json configs[1]: R-MAT "
+                      f"scale {cscale}, {cm} edges; roots equal to the GPU's: {same_roots})" if same else
+                      f"a labelled sample: R-MAT scale {cscale} ({cm} edges), {cr} roots")
+                   + f", parallel over roots at T = nproc = {threads}; median of {len(best['runs'])} timed "
+                     f"waves after a warm-up, each from a restored pristine copy; "
+                     f"{best['v_inv']} nodes / {best['e_trav']} edges per wave"),
+        "gteps": best["e_trav"] / best["s"] / 1e9,
+        "wave_s": best["s"],
+        "wave_s_runs": best["runs"],
+        "single_thread_value": (cpu[1]["v_inv"] / cpu[1]["s"]) if 1 in cpu else None,
+        "single_thread_wave_s": cpu[1]["s"] if 1 in cpu else None,
+        "single_thread_sample": ("one wave at T = 1 on the same graph and roots, after the T = nproc waves"
+                                 if 1 in cpu else None),
+        "same_result_as_gpu": bool(same and same_set and best["v_inv"] == st.v_inv // args.steps
+                                   and best["e_trav"] == st.e_trav // args.steps),
+        "same_set_as_gpu": same_set,
+        "host": info,
+        "build_s": cbuild,
+        "peak_rss_gb": peak_rss_gb(),
+    }
+    if same:
+        rec["gpu_speedup"] = value / rec["value"]
+        if 1 in cpu:
+            rec["gpu_speedup_vs_single_thread"] = value / rec["single_thread_value"]
+    log(f"cpu baseline: {cpu} (build {cbuild:.1f}s, host {info})")
+    if c2 is not None and args.cpu_c2_scale:
+        from stl_fusion_amd import workloads as W
+        cfg2 = W.CONFIGS["rmat27"]
+        try:
+            cpu2, b2, m2, r2, _, _ = cpu_baseline(threads, cfg2, args.cpu_c2_scale, None, None, runs=2)
+            v2 = cpu2[threads]["v_inv"] / cpu2[threads]["s"]
+            rec["configs2_sample"] = {
+                "value": v2, "unit": "invalidated nodes/s", "cores": threads,
+                "sample": (f"labelled sample of configs[2]: its generator (edge factor 8, seed 0x5EED0027) at R-MAT "
+                           f"scale {args.cpu_c2_scale} ({m2} edges, {r2} roots) instead of 27, T = {threads}, median of "
+                           f"2 timed waves after a warm-up"),
+                "v_inv_per_wave": cpu2[threads]["v_inv"], "wave_s": cpu2[threads]["s"], "build_s": b2,
+                "gpu_configs2_value": c2["value"],
+                "gpu_speedup": c2["value"] / v2,
+                "note": "GPU: configs[2] itself (R-MAT 27) on one MI355X (configs2_single_gpu); CPU: the scale stated"}
+            log(f"cpu configs[2] sample: {cpu2} (build {b2:.1f}s)")
+        except Exception as e:
+            rec["configs2_sample"] = {"value": None, "error": repr(e)}
+    return rec
+
+
+def n_gpus_visible() -> int:
+    """GPUs this process can use (torch.cuda.device_count does not initialise the device)."""
+    import torch
+    return torch.cuda.device_count()
 
 
 if __name__ == "__main__":

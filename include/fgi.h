@@ -391,6 +391,14 @@ fgi_status fgi_part_unique_id(uint8_t* id128);
 /* Join the partitioned engine: this graph owns slots [rank*ceil(N/world), ...) of a global
  * N = n_global slots; cfg->rank/world must be set. */
 fgi_status fgi_part_init(fgi_graph* g, uint32_t n_global, const uint8_t* id128);
+/* Join the partitioned engine with the host's own transport instead of RCCL: every collective of the
+ * partition (the waves' exchanges, the mutations' all-reduces, the prune's all-gather) reduces to
+ * fn(ctx, send, bytes, recv) — an all-gather of `bytes` from every rank into recv (world * bytes,
+ * rank-major; 0 = success), e.g. torch.distributed over gloo. The ranks may then share a GPU (RCCL
+ * refuses two ranks on one device): the multi-process path runs on any box. Every collective
+ * synchronises the rank's stream (correct, not fast). Same results as fgi_part_init's. */
+typedef int (*fgi_allgather_fn)(void* ctx, const void* send, uint64_t bytes, void* recv);
+fgi_status fgi_part_init_host(fgi_graph* g, uint32_t n_global, fgi_allgather_fn fn, void* ctx);
 /* Partitioned R-MAT: every rank walks the global edge sequence by index (edge i is a pure function of
  * i) and keeps only its share — the rows of its slots and the dependency entries of its slots —
  * without materialising the global edge list. */

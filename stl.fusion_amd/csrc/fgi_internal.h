@@ -242,6 +242,46 @@ inline int fused_default() {
     return (e && e[0] == '1') ? kFusedOn : 0;
 }
 
+// ---- cross-block hand-off shared by the kernels' last-block epilogues (wave.hip, graph.hip) ---------
+// Block-uniform: true in the block that arrives last at this launch's completion counter, over the
+// blocks [0, G) taking part. The counter is two-level (one word serialises near 88 atomics/us,
+// MI355X_MICROARCH.md "dequeue"): block b counts into group b % kDoneGroups, the last block of a group
+// into the top word; the last block resets every word for the next launch. Agent-scope atomic RMWs are
+// performed at the coherence point shared by the XCDs, so what the last block must see has to be
+// performed before its block arrives:
+//   kDrainAll = false: the block's hand-off values are written by thread 0 (or by atomics whose result
+//     a thread waited for); wave 0 drains its own memory counter before the arrival (the traversal
+//     kernels: one wave's wait, not every wave's, sits on their critical path);
+//   kDrainAll = true: any wave may have issued returnless atomics the last block reads (a batch's
+//     classify counts, the overflow-row list): every wave drains its vector-memory counter (returnless
+//     atomics included, gfx9 counts them in vmcnt) before the block's barrier, and the arrivals are
+//     acquire-release at agent scope.
+template <bool kDrainAll>
+__device__ inline bool last_block_arrive(unsigned long long* done, uint64_t G) {
+    __shared__ bool s_last;
+    if (kDrainAll) __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_s_waitcnt(0);
+        constexpr int kOrd = kDrainAll ? __ATOMIC_ACQ_REL : __ATOMIC_RELAXED;
+        const uint32_t grp = blockIdx.x % kDoneGroups;
+        const uint64_t gsize = (G - grp + kDoneGroups - 1) / kDoneGroups;
+        const unsigned long long t =
+            __hip_atomic_fetch_add(done + (1 + grp) * kDoneStride, 1ull, kOrd, __HIP_MEMORY_SCOPE_AGENT);
+        bool last = false;
+        if (t == gsize - 1) {
+            const uint64_t ng = G < (uint64_t)kDoneGroups ? G : (uint64_t)kDoneGroups;
+            last = __hip_atomic_fetch_add(done, 1ull, kOrd, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+        }
+        s_last = last;
+    }
+    __syncthreads();
+    const bool last = s_last;
+    if (last && threadIdx.x <= (uint32_t)kDoneGroups)
+        __hip_atomic_exchange(done + threadIdx.x * kDoneStride, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return last;
+}
+
 // ---- host-side graph object -------------------------------------------------------------------
 struct DevBuf {
     void* p = nullptr;

@@ -571,33 +571,15 @@ __device__ __forceinline__ bool batch_aborted(const unsigned long long* ab) {
 __device__ __forceinline__ uint64_t grid_tid() { return (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; }
 __device__ __forceinline__ uint64_t grid_threads() { return (uint64_t)gridDim.x * blockDim.x; }
 
-// Block-uniform: true in the block that arrives last at this launch's completion counter (two-level,
-// kDoneGroups groups; the last block resets the words). Every block calls it after its own atomics
-// have returned, so the last block sees them all (read at the coherence point: bcoh_read).
+// Block-uniform: true in the block that arrives last at this launch's completion counter
+// (fgi_internal.h). Any wave of a batch kernel may have issued the returnless atomics the last block
+// reads (classify counts, the overflow-row list), so every wave drains before the block arrives; the
+// last block reads them at the coherence point (bcoh_read).
 __device__ __forceinline__ unsigned long long bcoh_read(unsigned long long* p) {
     return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ bool batch_last_block(unsigned long long* done, uint64_t G) {
-    __shared__ bool s_last;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_s_waitcnt(0);
-        const uint32_t grp = blockIdx.x % kDoneGroups;
-        const uint64_t gsize = (G - grp + kDoneGroups - 1) / kDoneGroups;
-        const unsigned long long t = __hip_atomic_fetch_add(done + (1 + grp) * kDoneStride, 1ull, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT);
-        bool last = false;
-        if (t == gsize - 1) {
-            const uint64_t ng = G < (uint64_t)kDoneGroups ? G : (uint64_t)kDoneGroups;
-            last = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
-        }
-        s_last = last;
-    }
-    __syncthreads();
-    const bool last = s_last;
-    if (last && threadIdx.x <= (uint32_t)kDoneGroups)
-        __hip_atomic_exchange(done + threadIdx.x * kDoneStride, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return last;
+__device__ __forceinline__ bool batch_last_block(unsigned long long* done, uint64_t G) {
+    return last_block_arrive<true>(done, G);
 }
 
 __device__ __forceinline__ void batch_abort(unsigned long long* ab, unsigned long long code) {

@@ -345,6 +345,153 @@ struct RcclComm final : PartComm {
     }
 };
 
+// ---- host collectives (one process per rank, the host's own transport) -------------------------------
+// Every collective reduces to one primitive the caller supplies (fgi_part_init_host): an all-gather of
+// equal-size host buffers, e.g. torch.distributed over gloo. The ranks then need not sit on distinct
+// GPUs (RCCL refuses two ranks on one device), so the planned and host-driven waves, the mutations and
+// the prune of run_part_wave execute across real process boundaries on any box. Each collective
+// synchronises the rank's stream, moves its part through host memory and copies the result back:
+// correct, not fast (the async variants are synchronous here).
+struct HostComm final : PartComm {
+    fgi_allgather_fn fn;
+    void* ctx;
+    std::vector<uint8_t> sbuf, rbuf;
+    HostComm(fgi_allgather_fn f, void* c) : fn(f), ctx(c) {}
+
+    // all-gather `bytes` from sbuf into rbuf (world * bytes)
+    fgi_status gather(fgi_graph* g, uint64_t bytes) {
+        const uint32_t W = ps(g)->v.world;
+        rbuf.resize((size_t)W * bytes + 1);
+        if (sbuf.size() < bytes) sbuf.resize(bytes);
+        const int rc = fn(ctx, sbuf.data(), bytes, rbuf.data());
+        return rc == 0 ? FGI_OK : set_err(g, FGI_EDEVICE, "host all-gather failed (%d)", rc);
+    }
+    // device -> sbuf (synchronises the stream: the device words are final)
+    fgi_status stage(fgi_graph* g, const void* dev, uint64_t bytes, uint64_t at = 0) {
+        if (sbuf.size() < at + bytes) sbuf.resize(at + bytes);
+        if (bytes) FGI_HIP(g, hipMemcpyAsync(sbuf.data() + at, dev, bytes, hipMemcpyDeviceToHost, g->stream));
+        FGI_HIP(g, hipStreamSynchronize(g->stream));
+        return FGI_OK;
+    }
+    fgi_status upload(fgi_graph* g, void* dev, const void* host, uint64_t bytes) {
+        if (bytes) FGI_HIP(g, hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, g->stream));
+        FGI_HIP(g, hipStreamSynchronize(g->stream));   // the host buffer is reused by the next collective
+        return FGI_OK;
+    }
+    const uint64_t* u64(uint32_t q, uint64_t words) const { return reinterpret_cast<const uint64_t*>(rbuf.data()) + q * words; }
+
+    fgi_status allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, uint64_t* out, uint32_t count) override {
+        FGI_TRY(stage(g, dev_val, 8ull * count));
+        FGI_TRY(gather(g, 8ull * count));
+        for (uint32_t i = 0; i < count; ++i) {
+            uint64_t t = 0;
+            for (uint32_t q = 0; q < ps(g)->v.world; ++q) t += u64(q, count)[i];
+            out[i] = t;
+        }
+        return FGI_OK;
+    }
+    fgi_status exchange(fgi_graph* g, uint64_t* n_recv, uint64_t* n_sent, uint64_t* glob) override {
+        PartState* p = ps(g);
+        const uint32_t W = p->v.world, R = p->v.rank, S = W + 2;
+        FGI_TRY(stage(g, p->v.send_cnt, 8ull * S));
+        FGI_TRY(gather(g, 8ull * S));
+        std::vector<uint64_t> c(reinterpret_cast<const uint64_t*>(rbuf.data()),
+                                reinterpret_cast<const uint64_t*>(rbuf.data()) + (size_t)W * S);
+        sum_counts(c.data(), W, glob);
+        uint64_t mx = 0;   // the payload moves as one all-gather of [W][mx] ids per rank
+        for (uint32_t q = 0; q < W; ++q)
+            for (uint32_t r = 0; r < W; ++r)
+                if (r != q) mx = std::max<uint64_t>(mx, c[(size_t)q * S + r]);
+        uint64_t sent = 0, recv = 0;
+        if (mx) {
+            sbuf.assign((size_t)W * mx * 4, 0);
+            for (uint32_t q = 0; q < W; ++q) {
+                const uint64_t to_q = q == R ? 0 : c[(size_t)R * S + q];
+                if (to_q)
+                    FGI_HIP(g, hipMemcpyAsync(sbuf.data() + (size_t)q * mx * 4, p->v.send_buf + (uint64_t)q * p->v.block,
+                                              to_q * 4, hipMemcpyDeviceToHost, g->stream));
+                sent += to_q;
+            }
+            FGI_HIP(g, hipStreamSynchronize(g->stream));
+            FGI_TRY(gather(g, (uint64_t)W * mx * 4));
+            std::vector<uint32_t> in;
+            for (uint32_t q = 0; q < W; ++q) {
+                if (q == R) continue;
+                const uint64_t from_q = c[(size_t)q * S + R];
+                const uint32_t* src = reinterpret_cast<const uint32_t*>(rbuf.data() + ((size_t)q * W + R) * mx * 4);
+                in.insert(in.end(), src, src + from_q);
+            }
+            recv = in.size();
+            FGI_TRY(upload(g, p->v.recv_buf, in.data(), recv * 4));
+        }
+        *n_recv = recv;
+        *n_sent = sent;
+        return FGI_OK;
+    }
+    fgi_status allgather_front(fgi_graph* g) override {
+        PartState* p = ps(g);
+        const uint64_t bytes = (uint64_t)(p->v.block / 32) * 4;
+        FGI_TRY(stage(g, g->inv_bm, bytes));
+        FGI_TRY(gather(g, bytes));
+        return upload(g, p->v.front_global, rbuf.data(), (uint64_t)p->v.world * bytes);
+    }
+    fgi_status allgather_count(fgi_graph* g, uint64_t mine, uint64_t* all) override {
+        sbuf.resize(std::max<size_t>(sbuf.size(), 8));
+        std::memcpy(sbuf.data(), &mine, 8);
+        FGI_TRY(gather(g, 8));
+        for (uint32_t q = 0; q < ps(g)->v.world; ++q) all[q] = u64(q, 1)[0];
+        return FGI_OK;
+    }
+    fgi_status exchange_delta(fgi_graph* g, const uint64_t* cnt, uint64_t* n_recv) override {
+        PartState* p = ps(g);
+        const uint32_t W = p->v.world, R = p->v.rank;
+        uint64_t mx = 0;
+        for (uint32_t q = 0; q < W; ++q) mx = std::max<uint64_t>(mx, cnt[q]);
+        uint64_t recv = 0;
+        if (mx) {
+            sbuf.assign(mx * 8, 0);
+            FGI_TRY(stage(g, p->dbuf, cnt[R] * 8));
+            FGI_TRY(gather(g, mx * 8));
+            std::vector<uint64_t> in;
+            for (uint32_t q = 0; q < W; ++q)
+                if (q != R) in.insert(in.end(), u64(q, mx), u64(q, mx) + cnt[q]);
+            recv = in.size();
+            FGI_TRY(upload(g, p->rbuf, in.data(), recv * 8));
+        }
+        *n_recv = recv;
+        return FGI_OK;
+    }
+    fgi_status allgather_front_async(fgi_graph* g) override { return allgather_front(g); }
+    fgi_status alltoall_async(fgi_graph* g) override {
+        PartState* p = ps(g);
+        const uint32_t W = p->v.world, R = p->v.rank;
+        const uint64_t C = p->a2a_C;
+        FGI_TRY(stage(g, p->a2a_send, (uint64_t)W * C * 4));
+        FGI_TRY(gather(g, (uint64_t)W * C * 4));
+        std::vector<uint32_t> in((size_t)W * C);
+        for (uint32_t q = 0; q < W; ++q)
+            std::memcpy(in.data() + (size_t)q * C, rbuf.data() + ((size_t)q * W + R) * C * 4, C * 4);
+        return upload(g, p->a2a_recv, in.data(), (uint64_t)W * C * 4);
+    }
+    fgi_status allreduce_u32(fgi_graph* g, uint32_t* dev, uint64_t n) override {
+        const uint32_t W = ps(g)->v.world;
+        FGI_TRY(stage(g, dev, n * 4));
+        FGI_TRY(gather(g, n * 4));
+        std::vector<uint32_t> sum(n, 0);
+        for (uint32_t q = 0; q < W; ++q) {
+            const uint32_t* v = reinterpret_cast<const uint32_t*>(rbuf.data() + (size_t)q * n * 4);
+            for (uint64_t i = 0; i < n; ++i) sum[i] += v[i];
+        }
+        return upload(g, dev, sum.data(), n * 4);
+    }
+    fgi_status allgather_cur_async(fgi_graph* g) override {
+        PartState* p = ps(g);
+        FGI_TRY(stage(g, p->cur_local, p->cur_w64 * 8));
+        FGI_TRY(gather(g, p->cur_w64 * 8));
+        return upload(g, p->cur_all, rbuf.data(), (uint64_t)p->v.world * p->cur_w64 * 8);
+    }
+};
+
 // ---- in-process group (P graphs, one host thread per rank) ---------------------------------------
 // The ranks meet at a generation barrier; a rank that fails marks the group failed and releases
 // the others, whose collectives then return FGI_EDEVICE instead of waiting forever.
@@ -1075,6 +1222,14 @@ fgi_status fgi_part_init(fgi_graph* g, uint32_t n_global, const uint8_t* id128) 
         return set_err(g, FGI_EDEVICE, "ncclCommInitRank: %s", rccl().GetErrorString(r));
     }
     p->ops.reset(new RcclComm());
+    return FGI_OK;
+}
+
+fgi_status fgi_part_init_host(fgi_graph* g, uint32_t n_global, fgi_allgather_fn fn, void* ctx) {
+    if (!g || !fn) return FGI_EINVAL;
+    if (g->part) return set_err(g, FGI_ESTATE, "partition already initialised");
+    FGI_TRY(part_alloc(g, n_global));
+    ps(g)->ops.reset(new HostComm(fn, ctx));
     return FGI_OK;
 }
 

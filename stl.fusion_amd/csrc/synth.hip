@@ -2,6 +2,10 @@
 // Same definitions as the CPU oracle's oracle/synth.cpp (checked equal in tests), written for the
 // device so a 256M-edge graph is generated and turned into rows in HBM in well under a second.
 #include <hip/hip_runtime.h>
+#include <stdio.h>
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include "fgi_internal.h"
 
@@ -42,7 +46,89 @@ __global__ void k_gen_rmat(uint64_t m, uint32_t scale, uint64_t seed, uint64_t* 
     }
 }
 
+// ---- measurement experiment: R-MAT keys relabelled by degree (FGI_EXP_RELABEL) -------------------
+__global__ void kx_deg(uint64_t m, const uint64_t* __restrict__ keys, uint32_t which, uint32_t* cnt) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = keys[i];
+        if (which != 1) atomicAdd(cnt + (uint32_t)(k >> 32), 1u);
+        if (which != 2) atomicAdd(cnt + (uint32_t)k, 1u);
+    }
+}
+__global__ void kx_sortkey(uint32_t n, const uint32_t* __restrict__ cnt, uint64_t* key) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u < n) key[u] = ((uint64_t)cnt[u] << 32) | (uint32_t)~u;
+}
+// hot[u] = rank + 1 for the K heaviest, 0 otherwise
+__global__ void kx_hot(uint32_t n, uint32_t K, const uint64_t* __restrict__ sorted, uint32_t* hot) {
+    const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < K && r < n) hot[~(uint32_t)sorted[r]] = r + 1;
+}
+__global__ void kx_cold(uint32_t n, const uint32_t* __restrict__ hot, uint32_t* cold) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u < n) cold[u] = hot[u] ? 0u : 1u;
+}
+__global__ void kx_perm(uint32_t n, uint32_t K, const uint32_t* __restrict__ hot, const uint32_t* __restrict__ cold_pos,
+                        uint32_t slot_order, uint32_t* perm) {
+    const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+    // slot_order: the hot labels keep the slots' order among themselves (hot position = u - cold before u)
+    if (u < n) perm[u] = hot[u] ? (slot_order ? u - cold_pos[u] : hot[u] - 1) : K + cold_pos[u];
+}
+__global__ void kx_apply(uint64_t m, const uint32_t* __restrict__ perm, uint64_t* keys) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = keys[i];
+        keys[i] = ((uint64_t)perm[(uint32_t)(k >> 32)] << 32) | perm[(uint32_t)k];
+    }
+}
+
 }  // namespace
+
+// FGI_EXP_RELABEL=K (measurement only): the K heaviest slots (FGI_EXP_RELABEL_W: 0 total degree, 1 as
+// dependant, 2 as used) take labels 0..K-1 by weight, the others keep their order after them; K < 0:
+// every slot by weight. The graph is isomorphic to the unrelabelled one.
+static fgi_status exp_relabel(fgi_graph* g, uint32_t n, uint64_t* keys, uint64_t m) {
+    const char* e = getenv("FGI_EXP_RELABEL");
+    if (!e || !*e) return FGI_OK;
+    long long K = atoll(e);
+    if (K == 0) return FGI_OK;
+    if (K < 0 || K > n) K = n;
+    const char* w = getenv("FGI_EXP_RELABEL_W");
+    const uint32_t which = w ? (uint32_t)atoi(w) : 0u;
+    const char* o = getenv("FGI_EXP_RELABEL_ORDER");
+    const uint32_t slot_order = o ? (uint32_t)atoi(o) : 0u;
+    hipStream_t s = g->stream;
+    uint32_t *cnt, *hot, *cold, *pos, *perm;
+    uint64_t *k0, *k1;
+    FGI_HIP(g, hipMalloc(&cnt, (size_t)n * 4));
+    FGI_HIP(g, hipMalloc(&hot, (size_t)n * 4));
+    FGI_HIP(g, hipMalloc(&cold, (size_t)n * 4));
+    FGI_HIP(g, hipMalloc(&pos, (size_t)n * 4));
+    FGI_HIP(g, hipMalloc(&perm, (size_t)n * 4));
+    FGI_HIP(g, hipMalloc(&k0, (size_t)n * 8));
+    FGI_HIP(g, hipMalloc(&k1, (size_t)n * 8));
+    FGI_HIP(g, hipMemsetAsync(cnt, 0, (size_t)n * 4, s));
+    FGI_HIP(g, hipMemsetAsync(hot, 0, (size_t)n * 4, s));
+    hipLaunchKernelGGL(kx_deg, dim3(8192), dim3(256), 0, s, m, keys, which, cnt);
+    hipLaunchKernelGGL(kx_sortkey, dim3((n + 255) / 256), dim3(256), 0, s, n, cnt, k0);
+    size_t tb = 0;
+    FGI_HIP(g, rocprim::radix_sort_keys_desc(nullptr, tb, k0, k1, (size_t)n, 0, 64, s));
+    void* tmp;
+    FGI_HIP(g, hipMalloc(&tmp, tb));
+    FGI_HIP(g, rocprim::radix_sort_keys_desc(tmp, tb, k0, k1, (size_t)n, 0, 64, s));
+    hipLaunchKernelGGL(kx_hot, dim3((uint32_t)((K + 255) / 256)), dim3(256), 0, s, n, (uint32_t)K, k1, hot);
+    hipLaunchKernelGGL(kx_cold, dim3((n + 255) / 256), dim3(256), 0, s, n, hot, cold);
+    size_t sb = 0;
+    FGI_HIP(g, rocprim::exclusive_scan(nullptr, sb, cold, pos, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
+    void* stmp;
+    FGI_HIP(g, hipMalloc(&stmp, sb));
+    FGI_HIP(g, rocprim::exclusive_scan(stmp, sb, cold, pos, 0u, (size_t)n, rocprim::plus<uint32_t>(), s));
+    hipLaunchKernelGGL(kx_perm, dim3((n + 255) / 256), dim3(256), 0, s, n, (uint32_t)K, hot, pos, slot_order, perm);
+    hipLaunchKernelGGL(kx_apply, dim3(8192), dim3(256), 0, s, m, perm, keys);
+    FGI_HIP(g, hipStreamSynchronize(s));
+    for (void* p : {(void*)cnt, (void*)hot, (void*)cold, (void*)pos, (void*)perm, (void*)k0, (void*)k1, tmp, stmp})
+        hipFree(p);
+    fprintf(stderr, "[fgi] FGI_EXP_RELABEL: %lld heaviest of %u slots (weight %u) relabelled first (slot order %u)\n", K, n, which, slot_order);
+    return FGI_OK;
+}
 
 fgi_status synth_rmat_keys(fgi_graph* g, uint32_t scale, uint32_t edge_factor, uint64_t seed, uint64_t** keys,
                            uint64_t* m) {
@@ -97,6 +183,7 @@ fgi_status fgi_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_factor, ui
     uint64_t* keys = nullptr;
     uint64_t m = 0;
     FGI_TRY(synth_rmat_keys(g, scale, edge_factor, seed, &keys, &m));
+    FGI_TRY(exp_relabel(g, 1u << scale, keys, m));
     fgi_status st = build_rows_from_keys(g, m, keys, nullptr, seed, stale_pct, stale_seed);
     hipFree(keys);
     return st;

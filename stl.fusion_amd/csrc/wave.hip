@@ -218,32 +218,9 @@ __device__ __forceinline__ unsigned long long coh_read(unsigned long long* p) {
     return __hip_atomic_fetch_add(p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Block-uniform: true in the block that arrives last at this launch's completion counter, over the
-// blocks [0, G) taking part (G = the grid unless the level leaves blocks idle). The counter is
-// two-level (one word serialises near 88 atomics/us, MI355X_MICROARCH.md "dequeue"): block b counts
-// into group b % kDoneGroups, the last block of a group into the top word; the last block resets
-// every word for the next launch.
-__device__ bool last_block(unsigned long long* done, uint64_t G) {
-    __shared__ bool s_last;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_s_waitcnt(0);
-        const uint32_t grp = blockIdx.x % kDoneGroups;
-        const uint64_t gsize = (G - grp + kDoneGroups - 1) / kDoneGroups;
-        const unsigned long long t = __hip_atomic_fetch_add(done + (1 + grp) * kDoneStride, 1ull, __ATOMIC_RELAXED,
-                                                            __HIP_MEMORY_SCOPE_AGENT);
-        bool last = false;
-        if (t == gsize - 1) {
-            const uint64_t ng = G < (uint64_t)kDoneGroups ? G : (uint64_t)kDoneGroups;
-            last = __hip_atomic_fetch_add(done, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
-        }
-        s_last = last;
-    }
-    __syncthreads();
-    const bool last = s_last;
-    if (last && threadIdx.x <= (uint32_t)kDoneGroups) coh_xchg(done + threadIdx.x * kDoneStride, 0ull);
-    return last;
-}
+// the traversal kernels' completion counter (fgi_internal.h): their hand-off values are written by
+// thread 0 (coh_xchg) or by atomics whose result was waited for
+__device__ __forceinline__ bool last_block(unsigned long long* done, uint64_t G) { return last_block_arrive<false>(done, G); }
 
 // Called by the last block: exclusive prefixes over blocks of three columns, packed per block in
 // src[k] (bits 48-63, 32-47, 0-31: pack3), into dst[q * G + k], column totals into tot[q]. In rounds

@@ -150,12 +150,15 @@ SIGNATURES = {
     "fgi_part_invalidate_all": [_G, _u32p, C.c_uint64, _u64p, C.POINTER(WaveStats)],
     "fgi_part_run_batch": [_G, C.c_uint32, C.POINTER(Step), _u32p, C.c_uint64, _u64p, C.POINTER(BatchStats)],
     "fgi_part_prune": [_G, C.POINTER(PruneStats)],
+    "fgi_part_init_host": [_G, C.c_uint32, C.c_void_p, C.c_void_p],
     "fgi_part_local_run_batch": [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32, C.POINTER(Step), _u32p, C.c_uint64,
                                  _u64p, C.POINTER(BatchStats)],
     "fgi_part_local_prune": [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(PruneStats)],
 }
 
 _lib = None
+# fgi_allgather_fn: int (*)(void* ctx, const void* send, uint64_t bytes, void* recv)
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p)
 
 
 def load_library(path: str = LIB_PATH) -> C.CDLL:
@@ -492,6 +495,33 @@ class Graph:
     def part_init(self, n_global: int, unique_id: bytes):
         buf = (C.c_uint8 * 128).from_buffer_copy(unique_id)
         self._check(self.lib.fgi_part_init(self.h, n_global, buf), "part_init")
+
+    def part_init_host(self, n_global: int, group=None):
+        """Join the partition with host collectives (fgi_part_init_host): every collective is an
+        all-gather of host bytes through torch.distributed (`group`: a process group, default the
+        world; gloo works, so the ranks may share one GPU)."""
+        import torch
+        import torch.distributed as dist
+
+        world = dist.get_world_size(group)
+
+        def allgather(_ctx, send, nbytes, recv):
+            try:
+                src = torch.frombuffer((C.c_uint8 * nbytes).from_address(send), dtype=torch.uint8).clone() \
+                    if nbytes else torch.zeros(0, dtype=torch.uint8)
+                out = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
+                dist.all_gather(out, src, group=group)
+                if nbytes:
+                    C.memmove(recv, torch.cat(out).numpy().ctypes.data, nbytes * world)
+                return 0
+            except Exception as e:  # reported as FGI_EDEVICE by the engine
+                import sys
+                print(f"fgi host all-gather failed: {e!r}", file=sys.stderr)
+                return 1
+
+        self._allgather_cb = ALLGATHER_FN(allgather)   # kept alive with the graph
+        self._check(self.lib.fgi_part_init_host(self.h, n_global, C.cast(self._allgather_cb, C.c_void_p), None),
+                    "part_init_host")
 
     def part_synth_rmat(self, scale, edge_factor, seed, stale_pct=0, stale_seed=0):
         self._check(self.lib.fgi_part_synth_rmat(self.h, scale, edge_factor, seed, stale_pct, stale_seed),

@@ -1,0 +1,43 @@
+"""bench.py's workload selection: N = 1 measures BASELINE.json
+configs[1] with configs[2]'s graph on the same GPU as a sub-record (the base of the scaling curve);
+N > 1 measures configs[2] exactly as strong scaling, with the weak-scaling point as a secondary record."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import _pkg  # noqa: E402
+import bench  # noqa: E402
+
+_pkg.load()
+from stl_fusion_amd import workloads as W  # noqa: E402
+
+
+def test_single_gpu_headline_is_configs1_with_configs2_subrecord():
+    sel = bench.select_workloads(1, "rmat24", False)
+    assert sel["headline"] == "rmat24" and not sel["partitioned"]
+    assert sel["secondary"] == [("configs2_single_gpu", "rmat27", None)]
+    cfg = W.CONFIGS["rmat24"]
+    assert (cfg["scale"], cfg["edge_factor"], cfg["seed"], cfg["roots"]) == (24, 16, 0x5EED0024, 4096)
+
+
+def test_multi_gpu_runs_configs2_exactly_as_strong_scaling():
+    for n in (2, 4, 8):
+        sel = bench.select_workloads(n, "rmat24", False)
+        assert sel["headline"] == "rmat27" and sel["partitioned"] and sel["scaling"] == "strong"
+        cfg = W.CONFIGS[sel["headline"]]
+        # BASELINE.json configs[2]: R-MAT scale 27, edge factor 8, seed 0x5EED0027, 4,096 roots
+        assert (cfg["scale"], cfg["edge_factor"], cfg["seed"], cfg["roots"], cfg["roots_seed"]) == \
+            (27, 8, 0x5EED0027, 4096, 0x5EED1027)
+        # the weak-scaling point stays as a secondary record: 16.8M slots per GPU
+        (key, name, scale), = sel["secondary"]
+        assert key == "weak_scaling" and name == "rmat24" and (1 << scale) == n * (1 << 24)
+
+
+def test_explicit_configs_are_kept():
+    assert bench.select_workloads(1, "rmat27", False)["headline"] == "rmat27"
+    assert bench.select_workloads(1, "rmat27", False)["secondary"] == []
+    sel = bench.select_workloads(1, "rmat24", True)   # --partition at N = 1: the partitioned engine
+    assert sel["partitioned"] and sel["headline"] == "rmat24" and sel["secondary"] == []
+    assert bench.select_workloads(1, "layered_1m", False)["secondary"] == []
