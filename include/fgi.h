@@ -81,6 +81,13 @@ typedef struct fgi_config {
     /* multi-GPU 1-D vertex partition (fgi_part_*); 0/1 for a single device */
     int32_t rank;
     int32_t world;
+    /* Internal labels: 0 auto — a single-device graph of at least 2^25 slots (an
+     * invalidated bitmap larger than one XCD's L2) relabels its heaviest slots into a prefix of the
+     * engine's handle space at its first bulk edge load; 1 always (tests); -1 never. Invisible at the
+     * boundary: every entry point takes and returns slots and handles as before. Callers built against
+     * the previous layout of this struct (struct_size without this field) get 0. */
+    int32_t labels;
+    int32_t reserved;
 } fgi_config;
 
 typedef struct fgi_wave_stats {
@@ -302,7 +309,10 @@ fgi_status fgi_release(fgi_graph* g, uint32_t n, const uint32_t* handle);
  * fgi_restore is stream-ordered: it may return before the device copies finish; every later call
  * on the graph runs after them. On a poisoned graph (a failed fgi_run_batch, FGI_EDEVICE) fgi_restore
  * copies back every saved table, clears the wave bitmaps and the detached-handle list to the
- * snapshot's, and makes the graph usable again. */
+ * snapshot's, and makes the graph usable again. fgi_restore refuses (FGI_ESTATE) once the edge pool
+ * was rebuilt or rows were compacted since the snapshot (a bulk load, fgi_prune / fgi_prune_range that
+ * moved entries, a defragmentation): a poisoned graph then stays poisoned, and fgi_destroy is all that
+ * is left for it — take a new snapshot after such a call. */
 fgi_status fgi_snapshot(fgi_graph* g);
 fgi_status fgi_restore(fgi_graph* g);
 /* Device-side synthetic workloads. All nodes Consistent with
@@ -341,14 +351,6 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *                            it from the graph (65,536-262,144); n > 0 caps it at n rounded up to 256,
  *                            so the other heads are probed in the invalidated bitmap itself (tests pin
  *                            that path on small graphs; results never depend on it)
- *   FGI_OPT_FUSED       [0]  1: waves whose directions are settled (pull lists ready, or push only)
- *                            run their roots and small push levels inside two persistent launches and
- *                            only the pull levels (and push levels over one round of the fused grid)
- *                            as separate launches, with one host synchronisation (DESIGN.md §3;
- *                            measured slower than the default level groups on MI355X). Tests add 2
- *                            (no prediction of the launches: extra rounds), 4 (every push level as its
- *                            own launch) or 8 (every push level in the fused grid); the environment's
- *                            FGI_FUSED=1 makes 1 the default
  *   FGI_OPT_PART_PLAN   [1]  partitions: a wave follows the previous wave's directions (when every
  *                            rank can) and queues all its levels' collectives at fixed sizes, with one
  *                            host synchronisation at its end (two with remote ranks: the start's
@@ -357,12 +359,6 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *   FGI_OPT_PART_BUCKET [0]  partitions, planned waves: words per peer of a push level's bucket (a
  *                            count, then ids; 0 = the allocated 65,536); smaller buckets only delay
  *                            ids to later push levels (tests pin that path; results never change)
- *   FGI_OPT_PROBE_SUMMARY [-1] before a pull level while few invalidated-bitmap words can be nonzero
- *                            (the invalidated count so far, by the levels' frontiers, under 1/8 of the
- *                            words), build a one-bit-per-64-bit-word summary and answer cold head /
- *                            tail probes of zero words from it, on graphs whose bitmap has at least
- *                            this many 64-bit words; 0 on any graph (tests), -1 never (the default:
- *                            measured slower on configs[2]; results never change)
  *   FGI_OPT_FAULT_INJECT [0] tests only: value (k << 16) | b, b > 0: in the (k+1)-th streaming
  *                            cascade launched from now (fgi_run_batch), block b - 1 leaves at its first
  *                            grid barrier without arriving, and that cascade's barrier times out after
@@ -379,10 +375,9 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
 #define FGI_OPT_FRONT_EXCHANGE 9
 #define FGI_OPT_HOT_HEADS 10
 #define FGI_OPT_FAULT_INJECT 11
-#define FGI_OPT_FUSED 12
 #define FGI_OPT_PART_PLAN 13
 #define FGI_OPT_PART_BUCKET 14
-#define FGI_OPT_PROBE_SUMMARY 15
+/* 12 and 15: the measurement variants' options (include/fgi_variants.h); FGI_ENOTSUP here */
 fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value);
 
 /* ---- multi-GPU (1-D vertex-range partition, RCCL all-to-all frontier exchange) --------------- */

@@ -1,0 +1,27 @@
+#!/bin/bash
+# Round 5: hub-first labels (labels.hip) and the wave tail (k_wave_tail) on the GPU: new tests, the
+# whole suite, the whole suite with labels forced on every graph (FGI_LABELS=1), then A/B benches:
+# configs[2] labels on / off, configs[1] tail on / off (one box).
+set -u
+out=gpurun_out/r11a; mkdir -p $out
+T="timeout -k 10"
+$T 300 python -u -m pytest tests/test_gpu_labels.py -x -v --timeout 120 --timeout-method thread > $out/labels_tests.log 2>&1 || { echo "labels tests rc=$?"; tail -30 $out/labels_tests.log; exit 1; }
+tail -2 $out/labels_tests.log
+$T 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $out/gpu_tests.log 2>&1 || { echo "gpu tests rc=$?"; tail -30 $out/gpu_tests.log; exit 1; }
+tail -2 $out/gpu_tests.log
+FGI_LABELS=1 $T 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $out/gpu_tests_labels.log 2>&1 || { echo "forced-label gpu tests rc=$?"; tail -30 $out/gpu_tests_labels.log; exit 1; }
+tail -2 $out/gpu_tests_labels.log
+bench() {  # tag config setting
+  local tag=$1 cfg=$2 setting=$3
+  envs=(); [ "$setting" != "-" ] && read -r -a envs <<< "$setting"
+  env "${envs[@]}" $T 240 python bench.py --no-cpu --no-e2e --steps 30 --warmup 5 --config $cfg > $out/$tag.json 2> $out/$tag.err || { echo "bench rc=$?"; tail -5 $out/$tag.err; exit 1; }
+  python -c "
+import json; d = json.load(open('$out/$tag.json')); r = d['roofline']
+print('$cfg', '$setting', round(d['ms_per_step'], 4), 'pull', round(r['pull_levels']['ms_per_step'], 4), 'push', round(r['push_levels']['ms_per_step'], 4), 'tail', round(r.get('fused', {}).get('ms_per_step', 0), 4), 'kern', round(d['wave_kernel_ms'], 4), 'vinv', d['v_inv_per_step'], 'lv', d['levels_per_step'], 'syncs', d['host_syncs_per_step'], 'first', round(d['first_wave_s'], 3), 'build', round(d['build_s'], 2), flush=True)"
+}
+for r in 1 2; do
+  bench c2_on_$r rmat27 "-"
+  bench c2_off_$r rmat27 "FGI_LABELS=-1"
+  bench c1_tail_$r rmat24 "-"
+  bench c1_notail_$r rmat24 "FGI_TAIL=0"
+done

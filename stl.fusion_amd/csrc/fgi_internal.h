@@ -22,6 +22,14 @@
 #include <vector>
 
 #include "../../include/fgi.h"
+#include "../../include/fgi_variants.h"
+
+// Measurement variants (make variant-all -> libfgi_variants.so): the fused waves, the probe summary and
+// the cooperative launch of streaming cascades, each measured slower than the shipping paths on MI355X
+// (DESIGN.md §3, §7b). The shipping library leaves them out: their options return FGI_ENOTSUP.
+#ifndef FGI_VARIANTS
+#define FGI_VARIANTS 0
+#endif
 
 namespace fgi {
 
@@ -238,8 +246,12 @@ constexpr int kFusedOn = 1, kFusedNoPredict = 2, kFusedMidPush = 4, kFusedTailPu
 // §3: a grid barrier's cache maintenance costs what a launch does, and the fused grid runs the push
 // levels' dependent round trips with fewer blocks). FGI_FUSED=1 in the environment turns them on.
 inline int fused_default() {
+#if FGI_VARIANTS
     const char* e = getenv("FGI_FUSED");
     return (e && e[0] == '1') ? kFusedOn : 0;
+#else
+    return 0;
+#endif
 }
 
 // ---- cross-block hand-off shared by the kernels' last-block epilogues (wave.hip, graph.hip) ---------
@@ -294,7 +306,23 @@ struct fgi_graph {
     int device = 0;
     int n_cu = 256;                    // compute units of the device (queried once at create)
     hipStream_t stream = nullptr;
+    // Internal handle space (labels). n_slots / n_handles count the engine's labels:
+    // K hot labels [0, K) for the heaviest slots, then label K + x for every other slot or detached
+    // handle x (the labels K + x of hot slots stay empty). ext_slots / ext_handles are the boundary's
+    // counts (fgi_config.n_slots, + n_detached). K = 0 (labels are the handles) unless the graph uses
+    // hub-first labels.
     uint32_t n_slots = 0, n_detached = 0, n_handles = 0;
+    uint32_t ext_slots = 0, ext_handles = 0;
+    uint32_t lbl_K = 0;                // label capacity of the hot prefix (a multiple of kFoldTile)
+    uint32_t lbl_hot = 0;              // hot labels in use (<= lbl_K), set at the first bulk edge load
+    int opt_labels = 0;                // fgi_config.labels: 0 auto, 1 always, -1 never
+    bool lbl_done = false;             // the hot set has been chosen (first bulk edge load)
+    uint32_t* s2l = nullptr;           // [ext_slots] hot label of a slot, FGI_NONE if cold
+    uint32_t* l2s = nullptr;           // [lbl_K] slot of a hot label
+    uint32_t* fold_start = nullptr;    // [lbl_ncls][fold_tiles + 1] first hot label of class c at slots >= t * kFoldTile
+    uint32_t lbl_ncls = 0, fold_tiles = 0;
+    unsigned long long* xbm = nullptr; // [ext words] the wave's invalidated set over the boundary's handles
+    unsigned long long* fold_status = nullptr;   // [fold tiles, >= kStats] per-tile counts of the final collect
     int rank = 0, world = 1;
 
     // node table
@@ -347,6 +375,7 @@ struct fgi_graph {
     bool want_ids = true;              // run_wave writes the invalidated list (false: bitmap and count only)
     bool ids_valid = false;            // inv holds the last wave's list (else ensure_ids rebuilds it)
     int last_levels = 4;               // non-empty levels of the last wave (sizes the first level group)
+    int last_head = 4;                 // levels up to the last one the tail cannot run (pull, or large push)
     int last_mid = 3;                  // k_level launches the last fused wave needed (its mid pairs)
     int fused_per_cu = 0;              // resident k_wave_fused blocks per CU (0: not queried yet)
     bool coop_warm = false;            // a cooperative launch has run (coop_warm)
@@ -487,14 +516,50 @@ struct fgi_graph {
 
 // ---- internal entry points shared between translation units ----------------------------------
 namespace fgi {
+// ---- hub-first labels (labels.hip) ----
+constexpr uint32_t kFoldTile = 16384;            // slots per fold tile (256 bitmap words)
+constexpr uint32_t kFoldWords = kFoldTile / 64;
+constexpr uint32_t kLabelAutoSlots = 1u << 25;   // auto: graphs whose bitmap outgrows one XCD's L2 (4 MB)
+constexpr uint32_t kClassPerOctave = 8;          // weight classes per octave of (dependencies + 1)
+constexpr uint32_t kLabelClasses = 33 * kClassPerOctave;
+constexpr uint32_t kMaxHotClasses = 256;        // hot classes (one per thread of a fold block)
+// hot-prefix capacity of a graph of n boundary slots (0: the graph keeps labels = handles)
+uint32_t labels_capacity(uint32_t n_slots, int opt);
+// boundary handle x -> label (x < ext_handles) and back, on the device (in place; no-ops with K = 0)
+fgi_status labels_map_in(fgi_graph* g, uint32_t* dev, uint64_t n);
+fgi_status labels_map_out(fgi_graph* g, uint32_t* dev, uint64_t n);
+// both halves of edge keys (used << 32 | dependant), boundary -> labels / labels -> boundary
+fgi_status labels_map_keys(fgi_graph* g, uint64_t* keys, uint64_t m);
+fgi_status labels_unmap_keys(fgi_graph* g, uint64_t* keys, uint64_t m);
+// first bulk edge load (keys in boundary handles): choose the hot set from the keys' dependants and
+// move the node words already registered to their labels. No-op unless the graph wants labels and has
+// not chosen them yet.
+fgi_status labels_choose(fgi_graph* g, const uint64_t* keys, uint64_t m);
+// the words of a fold tile's slots: per hot class, the hot labels of the tile's slots, or none
+struct FoldArgs {
+    const uint32_t* l2s;           // null: no hot labels (the bitmap of handles is the labels' own)
+    const uint32_t* fold_start;
+    uint32_t ncls, tiles;          // fold_start is [ncls][tiles + 1]
+    uint32_t K;                    // cold label of handle x: K + x
+    unsigned long long* xbm;       // out: the invalidated set over boundary handles
+};
+// active (xbm set) iff the graph has a hot-label prefix (K > 0): the boundary's bitmap is then the
+// labels' one shifted by K, ORed with the hot labels' bits at their slots
+inline FoldArgs fold_args(const fgi_graph* g) {
+    return FoldArgs{g->lbl_hot ? g->l2s : nullptr, g->fold_start, g->lbl_hot ? g->lbl_ncls : 0u, g->fold_tiles, g->lbl_K,
+                    g->lbl_K ? g->xbm : nullptr};
+}
+
 fgi_status set_err(fgi_graph* g, fgi_status st, const char* fmt, ...);
 fgi_status hip_check(fgi_graph* g, hipError_t e, const char* what);
 fgi_status ensure_scratch(fgi_graph* g, size_t bytes);
 fgi_status ensure_pool(fgi_graph* g, uint64_t entries);
 fgi_status ensure_cstart(fgi_graph* g, uint64_t total_edges);
 // Run one cascade wave from `n_roots` device-resident roots. Fills stats (nullable).
+// ext_roots: the roots are boundary handles (the entry points' own arrays), mapped to labels by the
+// roots kernel; internal callers pass labels.
 fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
-                    fgi_wave_stats* stats);
+                    fgi_wave_stats* stats, bool ext_roots = false);
 // The last single-device wave's invalidated list in g->inv (rebuilt from the invalidated bitmap if
 // the wave ran in bitmap mode).
 fgi_status ensure_ids(fgi_graph* g);

@@ -15,6 +15,7 @@
 #include <rocprim/device/device_scan.hpp>
 
 #include <algorithm>
+#include <cstddef>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
@@ -233,6 +234,17 @@ __global__ void k_gather_words(uint32_t n, const uint32_t* __restrict__ h, const
                                unsigned long long* out) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) out[i] = node[h[i]];
+}
+
+__global__ void k_degree_of(uint32_t n, const uint32_t* __restrict__ h, const unsigned long long* __restrict__ node,
+                            const uint32_t* __restrict__ row_len, uint32_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = word_is_current(node[h[i]]) ? row_len[h[i]] : 0u;
+}
+
+__global__ void k_iota(uint32_t n, uint32_t* out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = i;
 }
 
 // ---- begin_compute ---------------------------------------------------------------------------
@@ -740,6 +752,9 @@ enum : int { kPrOld, kPrNew, kPrChunks, kPrDropped, kPrLive, kPrN };
 
 struct PruneArgs {
     uint32_t lo, hi, n_slots;
+    // [lo, hi) are boundary handles: row of handle x = its label (hot: s2l[x], else K + x)
+    const uint32_t* s2l;
+    uint32_t ext_slots, K;
     const unsigned long long* node;
     const uint64_t* row_off;
     uint32_t* row_len;
@@ -786,7 +801,12 @@ __device__ void prune_short_rows(const PruneArgs& a, uint32_t* s_lh, uint32_t* s
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const uint64_t n_rows = a.hi - a.lo;
     for (uint64_t r0 = (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * 64; r0 < n_rows; r0 += nw * 64) {
-        const uint64_t h = a.lo + r0 + lane;
+        const uint64_t x = a.lo + r0 + lane;
+        uint64_t h = x + a.K;
+        if (a.s2l && x < a.ext_slots && r0 + lane < n_rows) {
+            const uint32_t l = a.s2l[x];
+            if (l != FGI_NONE) h = l;
+        }
         uint32_t len = 0, eff = 0;
         uint64_t off = 0;
         int mode = 2;
@@ -1640,6 +1660,10 @@ fgi_status load_rows(fgi_graph* g, uint64_t m, const uint64_t* host_keys, const 
     FGI_TRY(gather_live(g, tk, tt, &keys, &tags, m, &m0));
     FGI_TRY(h2d(g, keys + m0, host_keys, m));
     FGI_TRY(h2d(g, tags + m0, host_tags, m));
+    if (!g->part) {   // boundary handles -> labels (the first bulk load chooses the hot labels)
+        if (m0 == 0) FGI_TRY(labels_choose(g, keys, m));
+        FGI_TRY(labels_map_keys(g, keys + m0, m));
+    }
     return build_rows_from_keys(g, m0 + m, keys, tags, 0, 0, 0, src_base, dst_base);
 }
 
@@ -1788,6 +1812,24 @@ using namespace fgi;
 static fgi_status single_only(fgi_graph* g, const char* what);
 // A graph a failed batch poisoned (fgi_run_batch, FGI_EDEVICE) takes no call but fgi_restore,
 // fgi_destroy, fgi_last_error and fgi_set_option.
+// a boundary handle's label, on the host (one lookup for a hot slot)
+static fgi_status label_of(fgi_graph* g, uint32_t x, uint32_t* out) {
+    if (!g->lbl_K) {
+        *out = x;
+        return FGI_OK;
+    }
+    if (g->lbl_hot && x < g->ext_slots) {
+        uint32_t l = FGI_NONE;
+        FGI_TRY(d2h(g, &l, g->s2l + x, 1));
+        if (l != FGI_NONE) {
+            *out = l;
+            return FGI_OK;
+        }
+    }
+    *out = x + g->lbl_K;
+    return FGI_OK;
+}
+
 static fgi_status usable(fgi_graph* g) {
     return g->failed ? set_err(g, FGI_ESTATE, "a streaming batch failed on the device (%s); fgi_restore or fgi_destroy",
                                "grid barrier timeout")
@@ -1805,14 +1847,21 @@ fgi_status fgi_version(uint32_t* major, uint32_t* minor) {
 const char* fgi_last_error(const fgi_graph* g) { return g ? g->err.c_str() : "null graph"; }
 
 fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
-    if (!cfg || !out || cfg->struct_size < sizeof(fgi_config) || cfg->n_slots == 0) return FGI_EINVAL;
-    if ((uint64_t)cfg->n_slots + cfg->n_detached >= 0xFFFFFFF0ull) return FGI_EINVAL;
+    // callers built against the fgi_config before `labels` pass the shorter struct (labels: auto)
+    if (!cfg || !out || cfg->struct_size < offsetof(fgi_config, labels) || cfg->n_slots == 0) return FGI_EINVAL;
+    const int labels = cfg->struct_size >= offsetof(fgi_config, labels) + sizeof(int32_t) ? cfg->labels : 0;
+    const uint32_t K = cfg->world > 1 ? 0u : labels_capacity(cfg->n_slots, labels);
+    if ((uint64_t)K + cfg->n_slots + cfg->n_detached >= 0xFFFFFFF0ull) return FGI_EINVAL;
     *out = nullptr;
     fgi_graph* g = new fgi_graph();
     g->device = cfg->device;
-    g->n_slots = cfg->n_slots;
+    g->opt_labels = labels;
+    g->lbl_K = K;
+    g->ext_slots = cfg->n_slots;
+    g->ext_handles = cfg->n_slots + cfg->n_detached;
+    g->n_slots = K + cfg->n_slots;
     g->n_detached = cfg->n_detached;
-    g->n_handles = cfg->n_slots + cfg->n_detached;
+    g->n_handles = g->n_slots + cfg->n_detached;
     g->rank = cfg->rank;
     g->world = cfg->world > 0 ? cfg->world : 1;
     auto fail = [&](fgi_status st) {
@@ -1836,6 +1885,9 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
         return fail(FGI_ENOMEM);
     g->bm_words = (H + 63) / 64 * 2 + 2;
     // the invalidated bitmap carries the hot heads' snapshot past its end (build_candidates)
+    if (K && (dmalloc(g, &g->xbm, ((uint64_t)g->ext_handles + 63) / 64 + 2) ||
+              dmalloc(g, &g->fold_status, ((uint64_t)g->ext_handles + kFoldTile - 1) / kFoldTile + kStatCols + 1)))
+        return fail(FGI_ENOMEM);
     if (dmalloc(g, &g->vis_bm, g->bm_words) || dmalloc(g, &g->inv_bm, g->bm_words + kHot / 32) ||
         dmalloc(g, &g->cls_bm, g->bm_words) || dmalloc(g, &g->uin_more, g->bm_words) ||
         dmalloc(g, &g->sum_bm, ((uint64_t)H + 4095) / 4096 * 2 + 2))
@@ -1925,6 +1977,11 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->snap_row_cap);
     dfree(g->snap_used);
     dfree(g->snap_home);
+    dfree(g->s2l);
+    dfree(g->l2s);
+    dfree(g->fold_start);
+    dfree(g->xbm);
+    dfree(g->fold_status);
     if (g->scratch) hipFree(g->scratch);
     if (g->ctr_host) hipHostFree(g->ctr_host);
     if (g->ctr_pub) hipHostFree(g->ctr_pub);
@@ -1953,7 +2010,7 @@ fgi_status fgi_register_nodes(fgi_graph* g, uint32_t n, const uint32_t* slot, co
     if (!g || (n && (!slot || !version))) return FGI_EINVAL;
     FGI_TRY(single_only(g, "fgi_register_nodes"));
     for (uint32_t i = 0; i < n; ++i) {
-        if (slot[i] >= g->n_slots) return set_err(g, FGI_EINVAL, "slot %u out of range", slot[i]);
+        if (slot[i] >= g->ext_slots) return set_err(g, FGI_EINVAL, "slot %u out of range", slot[i]);
         if (version[i] > kVMask) return set_err(g, FGI_EINVAL, "version of slot %u exceeds 2^56-1", slot[i]);
         if (state_flags && (state_flags[i] & 3u) == 3u) return set_err(g, FGI_EINVAL, "bad state for slot %u", slot[i]);
     }
@@ -1966,6 +2023,7 @@ fgi_status fgi_register_nodes(fgi_graph* g, uint32_t n, const uint32_t* slot, co
     FGI_TRY(tmalloc(g, tv, &dv, n));
     if (state_flags) FGI_TRY(tmalloc(g, tf, &df, n));
     FGI_TRY(h2d(g, ds, slot, n));
+    FGI_TRY(labels_map_in(g, ds, n));
     FGI_TRY(h2d(g, dv, version, n));
     if (state_flags) FGI_TRY(h2d(g, df, state_flags, n));
     FGI_TRY(fold(g));
@@ -1986,7 +2044,7 @@ fgi_status fgi_load_edges(fgi_graph* g, uint64_t m, const uint32_t* used, const 
     if (!g || (m && (!used || !dependant_slot || !tag))) return FGI_EINVAL;
     FGI_TRY(single_only(g, "fgi_load_edges"));
     for (uint64_t e = 0; e < m; ++e) {
-        if (used[e] >= g->n_handles || dependant_slot[e] >= g->n_slots)
+        if (used[e] >= g->ext_handles || dependant_slot[e] >= g->ext_slots)
             return set_err(g, FGI_EINVAL, "edge %llu out of range", (unsigned long long)e);
         if (tag[e] == 0) return set_err(g, FGI_EINVAL, "edge %llu has tag 0 (LTags are positive)", (unsigned long long)e);
     }
@@ -2000,7 +2058,7 @@ fgi_status fgi_get_state(fgi_graph* g, uint32_t n, const uint32_t* handle, uint6
     if (!g || (n && !handle)) return FGI_EINVAL;
     FGI_TRY(usable(g));
     for (uint32_t i = 0; i < n; ++i)
-        if (handle[i] >= g->n_handles) return set_err(g, FGI_EINVAL, "handle %u out of range", handle[i]);
+        if (handle[i] >= g->ext_handles) return set_err(g, FGI_EINVAL, "handle %u out of range", handle[i]);
     if (n == 0) return FGI_OK;
     hipSetDevice(g->device);
     FGI_TRY(fold(g));
@@ -2010,6 +2068,7 @@ fgi_status fgi_get_state(fgi_graph* g, uint32_t n, const uint32_t* handle, uint6
     FGI_TRY(tmalloc(g, th, &dh, n));
     FGI_TRY(tmalloc(g, tw, &dw, n));
     FGI_TRY(h2d(g, dh, handle, n));
+    FGI_TRY(labels_map_in(g, dh, n));
     hipLaunchKernelGGL(k_gather_words, dim3(nblk(n)), dim3(256), 0, g->stream, n, dh,
                        reinterpret_cast<const unsigned long long*>(g->node), dw);
     std::vector<unsigned long long> w(n);
@@ -2026,9 +2085,23 @@ fgi_status fgi_dump_states(fgi_graph* g, uint64_t* version, uint32_t* state_flag
     FGI_TRY(usable(g));
     hipSetDevice(g->device);
     FGI_TRY(fold(g));
-    std::vector<uint64_t> w(g->n_handles);
-    FGI_TRY(d2h(g, w.data(), g->node, g->n_handles));
-    for (uint32_t h = 0; h < g->n_handles; ++h) {
+    const uint32_t H = g->ext_handles;
+    std::vector<uint64_t> w(H);
+    if (g->lbl_K) {   // the words of boundary handles 0 .. H-1 at their labels
+        Tmp th, tw;
+        uint32_t* dh;
+        unsigned long long* dw;
+        FGI_TRY(tmalloc(g, th, &dh, H));
+        FGI_TRY(tmalloc(g, tw, &dw, H));
+        hipLaunchKernelGGL(k_iota, dim3(nblk(H)), dim3(256), 0, g->stream, H, dh);
+        FGI_TRY(labels_map_in(g, dh, H));
+        hipLaunchKernelGGL(k_gather_words, dim3(nblk(H)), dim3(256), 0, g->stream, H, dh,
+                           reinterpret_cast<const unsigned long long*>(g->node), dw);
+        FGI_TRY(d2h(g, reinterpret_cast<unsigned long long*>(w.data()), dw, H));
+    } else {
+        FGI_TRY(d2h(g, w.data(), g->node, H));
+    }
+    for (uint32_t h = 0; h < H; ++h) {
         if (version) version[h] = w[h] & kVMask;
         if (state_flags) state_flags[h] = word_to_flags(w[h]);
     }
@@ -2063,10 +2136,11 @@ __global__ void k_used_by_live(uint32_t len, const uint32_t* __restrict__ col, c
 }
 
 fgi_status fgi_get_used_by(fgi_graph* g, uint32_t handle, uint32_t* dep, uint64_t* tag, uint64_t cap, uint64_t* out_n) {
-    if (!g || handle >= g->n_handles) return FGI_EINVAL;
+    if (!g || handle >= g->ext_handles) return FGI_EINVAL;
     FGI_TRY(usable(g));
     hipSetDevice(g->device);
     FGI_TRY(fold(g));
+    FGI_TRY(label_of(g, handle, &handle));
     uint64_t w = 0, off = 0;
     uint32_t len = 0;
     FGI_TRY(d2h(g, &w, g->node + handle, 1));
@@ -2084,7 +2158,16 @@ fgi_status fgi_get_used_by(fgi_graph* g, uint32_t handle, uint32_t* dep, uint64_
                            g->pool_tag + off, reinterpret_cast<const unsigned long long*>(g->node), g->n_slots,
                            g->n_detached, g->home, dkeep);
         FGI_HIP(g, hipGetLastError());
-        FGI_TRY(d2h(g, d.data(), g->pool_col + off, len));
+        if (g->lbl_K) {   // the entries' dependants as boundary slots
+            Tmp tc;
+            uint32_t* dc;
+            FGI_TRY(tmalloc(g, tc, &dc, len));
+            FGI_HIP(g, hipMemcpyAsync(dc, g->pool_col + off, (size_t)len * 4, hipMemcpyDeviceToDevice, g->stream));
+            FGI_TRY(labels_map_out(g, dc, len));
+            FGI_TRY(d2h(g, d.data(), dc, len));
+        } else {
+            FGI_TRY(d2h(g, d.data(), g->pool_col + off, len));
+        }
         FGI_TRY(d2h(g, t.data(), g->pool_tag + off, len));
         FGI_TRY(d2h(g, keep.data(), dkeep, len));
     }
@@ -2102,10 +2185,11 @@ fgi_status fgi_get_used_by(fgi_graph* g, uint32_t handle, uint32_t* dep, uint64_
 }
 
 fgi_status fgi_get_used_count(fgi_graph* g, uint32_t handle, uint32_t* out) {
-    if (!g || !out || handle >= g->n_handles) return FGI_EINVAL;
+    if (!g || !out || handle >= g->ext_handles) return FGI_EINVAL;
     FGI_TRY(usable(g));
     hipSetDevice(g->device);
     FGI_TRY(fold(g));
+    FGI_TRY(label_of(g, handle, &handle));
     uint64_t w = 0;
     uint32_t c = 0;
     FGI_TRY(d2h(g, &w, g->node + handle, 1));
@@ -2119,16 +2203,24 @@ fgi_status fgi_get_degrees(fgi_graph* g, uint32_t* degree, uint64_t* total) {
     FGI_TRY(usable(g));
     hipSetDevice(g->device);
     FGI_TRY(fold(g));
-    const uint32_t H = g->n_handles;
-    std::vector<uint64_t> w(H);
-    std::vector<uint32_t> len(H);
-    FGI_TRY(d2h(g, w.data(), g->node, H));
-    FGI_TRY(d2h(g, len.data(), g->row_len, H));
+    const uint32_t H = g->ext_handles;
+    std::vector<uint32_t> deg(H);
+    {   // |_usedBy| of boundary handles 0 .. H-1 (at their labels)
+        Tmp th, td;
+        uint32_t *dh, *dd;
+        FGI_TRY(tmalloc(g, th, &dh, H));
+        FGI_TRY(tmalloc(g, td, &dd, H));
+        hipLaunchKernelGGL(k_iota, dim3(nblk(H)), dim3(256), 0, g->stream, H, dh);
+        FGI_TRY(labels_map_in(g, dh, H));
+        hipLaunchKernelGGL(k_degree_of, dim3(nblk(H)), dim3(256), 0, g->stream, H, dh,
+                           reinterpret_cast<const unsigned long long*>(g->node), g->row_len, dd);
+        FGI_HIP(g, hipGetLastError());
+        FGI_TRY(d2h(g, deg.data(), dd, H));
+    }
     uint64_t t = 0;
     for (uint32_t h = 0; h < H; ++h) {
-        const uint32_t d = word_is_current(w[h]) ? len[h] : 0;
-        if (degree) degree[h] = d;
-        t += d;
+        if (degree) degree[h] = deg[h];
+        t += deg[h];
     }
     if (total) *total = t;
     return FGI_OK;
@@ -2144,6 +2236,20 @@ fgi_status fgi_export_edges(fgi_graph* g, uint32_t* used, uint32_t* dep, uint64_
     FGI_TRY(gather_live(g, tk, tt, &keys, &tags, 0, &m));
     if (out_n) *out_n = m;
     if (m > cap) return FGI_ECAPACITY;
+    Tmp tk2, tt2, ts;
+    if (g->lbl_K && m) {   // as boundary handles, in (used, dependant) order again
+        FGI_TRY(labels_unmap_keys(g, keys, m));
+        uint64_t *k2, *t2;
+        FGI_TRY(tmalloc(g, tk2, &k2, m));
+        FGI_TRY(tmalloc(g, tt2, &t2, m));
+        size_t tb = 0;
+        FGI_HIP(g, rocprim::radix_sort_pairs(nullptr, tb, keys, k2, tags, t2, (size_t)m, 0, 64, g->stream));
+        char* st;
+        FGI_TRY(tmalloc(g, ts, &st, tb));
+        FGI_HIP(g, rocprim::radix_sort_pairs(st, tb, keys, k2, tags, t2, (size_t)m, 0, 64, g->stream));
+        keys = k2;
+        tags = t2;
+    }
     std::vector<uint64_t> hk(m);
     FGI_TRY(d2h(g, hk.data(), keys, m));
     if (tag) FGI_TRY(d2h(g, tag, tags, m));
@@ -2290,10 +2396,14 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
     case FGI_OPT_PART_BUCKET: return part_set_bucket(g, value);
     case FGI_OPT_PROBE_SUMMARY:
         if (value < -1 || value > (int64_t)FGI_NONE) return set_err(g, FGI_EINVAL, "probe summary: -1 or a word count");
+        if (!FGI_VARIANTS && value != -1)
+            return set_err(g, FGI_ENOTSUP, "the probe summary is in the variant build only (make variant-all)");
         g->opt_sum_min = value;
         return FGI_OK;
     case FGI_OPT_FUSED:
         if (value < 0 || value > 15) return set_err(g, FGI_EINVAL, "fused-wave bits must be 0..15");
+        if (!FGI_VARIANTS && value != 0)
+            return set_err(g, FGI_ENOTSUP, "fused waves are in the variant build only (make variant-all)");
         g->opt_fused = (int)value;
         return FGI_OK;
     case FGI_OPT_FAULT_INJECT:
@@ -2341,7 +2451,7 @@ fgi_status fgi_invalidate(fgi_graph* g, uint32_t n_roots, const uint32_t* roots,
     FGI_TRY(stage_roots(g, n_roots));
     FGI_TRY(h2d(g, g->roots_buf, roots, n_roots));
     if (immediately) FGI_TRY(h2d(g, g->imm_buf, immediately, n_roots));
-    FGI_TRY(run_wave(g, n_roots, g->roots_buf, immediately ? g->imm_buf : nullptr, stats));
+    FGI_TRY(run_wave(g, n_roots, g->roots_buf, immediately ? g->imm_buf : nullptr, stats, true));
     return copy_ids(g, out_ids, cap, out_n);
 }
 
@@ -2350,7 +2460,7 @@ fgi_status fgi_invalidate_dev(fgi_graph* g, uint32_t n_roots, const uint32_t* ro
     if (!g || (n_roots && !roots_dev)) return FGI_EINVAL;
     FGI_TRY(single_only(g, "fgi_invalidate_dev"));
     hipSetDevice(g->device);
-    FGI_TRY(run_wave(g, n_roots, roots_dev, imm_dev, stats));
+    FGI_TRY(run_wave(g, n_roots, roots_dev, imm_dev, stats, true));
     if (out_n) *out_n = g->last_wave_n;
     if (out_ids_dev && g->last_wave_n) {
         FGI_TRY(ensure_ids(g));
@@ -2365,7 +2475,7 @@ fgi_status fgi_invalidate_bits(fgi_graph* g, uint32_t n_roots, const uint32_t* r
     if (!g || (n_roots && !roots)) return FGI_EINVAL;
     FGI_TRY(single_only(g, "fgi_invalidate_bits"));
     hipSetDevice(g->device);
-    const uint64_t need = ((uint64_t)g->n_handles + 63) / 64;
+    const uint64_t need = ((uint64_t)g->ext_handles + 63) / 64;
     if (out_bits && words < need)
         return set_err(g, FGI_ECAPACITY, "bitmap of %llu words needs %llu", (unsigned long long)words,
                        (unsigned long long)need);
@@ -2373,13 +2483,15 @@ fgi_status fgi_invalidate_bits(fgi_graph* g, uint32_t n_roots, const uint32_t* r
     FGI_TRY(h2d(g, g->roots_buf, roots, n_roots));
     if (immediately) FGI_TRY(h2d(g, g->imm_buf, immediately, n_roots));
     g->want_ids = false;   // the final collect only counts; the list is made on demand (ensure_ids)
-    const fgi_status st = run_wave(g, n_roots, g->roots_buf, immediately ? g->imm_buf : nullptr, stats);
+    const fgi_status st = run_wave(g, n_roots, g->roots_buf, immediately ? g->imm_buf : nullptr, stats, true);
     g->want_ids = true;
     FGI_TRY(st);
     if (out_n) *out_n = g->last_wave_n;
     if (!out_bits) return FGI_OK;
-    // the wave's invalidated bitmap (bit h of 32-bit word h / 32 = bit h of 64-bit word h / 64)
-    return d2h(g, out_bits, reinterpret_cast<const uint64_t*>(g->inv_bm), need);
+    // the wave's invalidated bitmap over boundary handles (bit h of 32-bit word h / 32 = bit h of 64-bit
+    // word h / 64): the labels' own, or, with hot labels, the one the final collect folded (xbm)
+    return d2h(g, out_bits, g->xbm ? reinterpret_cast<const uint64_t*>(g->xbm) : reinterpret_cast<const uint64_t*>(g->inv_bm),
+               need);
 }
 
 fgi_status fgi_alloc_pinned(uint64_t bytes, void** out) {
@@ -2433,13 +2545,13 @@ fgi_status fgi_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, con
     {
         // O(n) validation over a reusable slot bitmap (cleared again bit by bit)
         std::vector<uint64_t>& seen = g->seen_bits;
-        if (seen.size() < ((size_t)g->n_slots + 63) / 64) seen.assign(((size_t)g->n_slots + 63) / 64, 0);
+        if (seen.size() < ((size_t)g->ext_slots + 63) / 64) seen.assign(((size_t)g->ext_slots + 63) / 64, 0);
         uint32_t bad = FGI_NONE;
         const char* why = nullptr;
         uint32_t i = 0;
         for (; i < n; ++i) {
             const uint32_t x = slot[i];
-            if (x >= g->n_slots) { why = "slot out of range"; bad = x; break; }
+            if (x >= g->ext_slots) { why = "slot out of range"; bad = x; break; }
             if (version[i] == 0 || version[i] > kVMask) { why = "bad version"; bad = i; break; }
             const uint64_t m = 1ull << (x & 63);
             if (seen[x >> 6] & m) { why = "slot repeated in one batch"; bad = x; break; }
@@ -2465,6 +2577,7 @@ fgi_status fgi_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, con
         FGI_TRY(h2d(g, dd, has_delay, n));
     }
     FGI_TRY(h2d(g, ds, slot, n));
+    FGI_TRY(labels_map_in(g, ds, n));
     FGI_TRY(h2d(g, dv, version, n));
     FGI_TRY(fold(g));
     FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, 4 * sizeof(unsigned long long), st));
@@ -2490,6 +2603,7 @@ fgi_status fgi_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, con
                          g->used_cnt, g->home, dout};
     hipLaunchKernelGGL(k_bc_install, dim3(nblk(n)), dim3(256), 0, st, n, ia);
     FGI_HIP(g, hipGetLastError());
+    FGI_TRY(labels_map_out(g, dout, n));   // detached handles as the boundary numbers them
     std::vector<uint32_t> od(n);
     FGI_TRY(d2h(g, od.data(), dout, n));
     g->free_detached.resize(g->free_detached.size() - take.size());
@@ -2500,7 +2614,7 @@ fgi_status fgi_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot, con
 fgi_status fgi_add_used(fgi_graph* g, uint32_t n, const uint32_t* dependant, const uint32_t* used, uint32_t* out_result) {
     if (!g || (n && (!dependant || !used))) return FGI_EINVAL;
     for (uint32_t i = 0; i < n; ++i)
-        if (dependant[i] >= g->n_handles || used[i] >= g->n_handles)
+        if (dependant[i] >= g->ext_handles || used[i] >= g->ext_handles)
             return set_err(g, FGI_EINVAL, "handle out of range at %u", i);
     if (n == 0) return FGI_OK;
     FGI_TRY(single_only(g, "fgi_add_used"));
@@ -2521,6 +2635,8 @@ fgi_status fgi_add_used(fgi_graph* g, uint32_t n, const uint32_t* dependant, con
     FGI_TRY(tmalloc(g, tovf, &dovf, n));
     FGI_TRY(h2d(g, ddep, dependant, n));
     FGI_TRY(h2d(g, duse, used, n));
+    FGI_TRY(labels_map_in(g, ddep, n));
+    FGI_TRY(labels_map_in(g, duse, n));
     FGI_TRY(fold(g));
     note_words(g);   // may set InvalidateOnSetOutput (Computed.cs:376-378)
     FGI_HIP(g, hipMemsetAsync(dhash, 0xFF, hcap * sizeof(unsigned long long), st));
@@ -2573,6 +2689,7 @@ fgi_status fgi_set_output(fgi_graph* g, uint32_t n, const uint32_t* handle, uint
     FGI_TRY(tmalloc(g, ts, &dset, n));
     FGI_TRY(tmalloc(g, tr, &droots, n));
     FGI_TRY(h2d(g, dh, handle, n));
+    FGI_TRY(labels_map_in(g, dh, n));
     FGI_TRY(fold(g));
     note_words(g);
     FGI_HIP(g, hipMemsetAsync(g->misc_dev, 0, sizeof(unsigned long long), st));
@@ -2821,21 +2938,21 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
                 vbad |= (uint64_t)(v - 1 >= kVMask);   // version 0 or > kVMask
             }
             std::vector<uint8_t>& seen = g->seen_slots;
-            if (seen.size() < g->n_slots) seen.assign(g->n_slots, 0);
+            if (seen.size() < g->ext_slots) seen.assign(g->ext_slots, 0);
             uint32_t dup = 0;
-            if (hmax < g->n_slots && !vbad) {
+            if (hmax < g->ext_slots && !vbad) {
                 for (uint32_t i = 0; i < n; ++i) {
                     dup |= seen[hh[i]];
                     seen[hh[i]] = 1;
                 }
                 for (uint32_t i = 0; i < n; ++i) seen[hh[i]] = 0;
             }
-            if (hmax >= g->n_slots || vbad || dup) {
+            if (hmax >= g->ext_slots || vbad || dup) {
                 const char* why = "bad step";
                 uint32_t i = 0, bad = 0;
                 for (; i < n; ++i) {
                     const uint32_t x = sp.handles[i];
-                    if (x >= g->n_slots) { why = "slot out of range"; bad = x; break; }
+                    if (x >= g->ext_slots) { why = "slot out of range"; bad = x; break; }
                     if (sp.version[i] == 0 || sp.version[i] > kVMask) { why = "bad version"; bad = i; break; }
                     if (seen[x]) { why = "slot repeated in one step"; bad = x; break; }
                     seen[x] = 1;
@@ -2853,9 +2970,9 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
                 hu[i] = u;
                 hmax = std::max(hmax, std::max(d, u));
             }
-            if (n && hmax >= g->n_handles)
+            if (n && hmax >= g->ext_handles)
                 for (uint32_t i = 0; i < n; ++i)
-                    if (sp.handles[i] >= g->n_handles || sp.used[i] >= g->n_handles)
+                    if (sp.handles[i] >= g->ext_handles || sp.used[i] >= g->ext_handles)
                         return set_err(g, FGI_EINVAL, "step %u: handle out of range at %u", k, i);
             bs[k].used = reinterpret_cast<const uint32_t*>(D + in_off[4 * k + 1]);
         } else {
@@ -2879,6 +2996,11 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
     clk::time_point t_enq = t_pack, t_wait = t_pack;
     FGI_HIP(g, hipEventRecord(b0, st));
     FGI_HIP(g, hipMemcpyAsync(D, H, in_bytes + scr_words * 8, hipMemcpyHostToDevice, st));   // one upload
+    for (uint32_t k = 0; k < n_steps && g->lbl_K; ++k) {   // the steps' handles as labels
+        const fgi_step& sp = steps[k];
+        FGI_TRY(labels_map_in(g, reinterpret_cast<uint32_t*>(D + in_off[4 * k]), sp.n));
+        if (sp.kind == FGI_STEP_ADD_USED) FGI_TRY(labels_map_in(g, reinterpret_cast<uint32_t*>(D + in_off[4 * k + 1]), sp.n));
+    }
     // per-step device temporaries
     for (uint32_t k = 0; k < n_steps; ++k) {
         const fgi_step& sp = steps[k];
@@ -2975,6 +3097,11 @@ fgi_status fgi_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* steps, 
         const char* src = H + res_off + bs[k].out_off;
         if (sp.kind == FGI_STEP_SET_OUTPUT) std::memcpy(sp.out, src, sp.n);
         else if (sp.kind == FGI_STEP_BEGIN_COMPUTE || sp.kind == FGI_STEP_ADD_USED) std::memcpy(sp.out, src, sp.n * 4);
+        if (sp.kind == FGI_STEP_BEGIN_COMPUTE && g->lbl_K) {   // detached handles: label K + handle
+            uint32_t* o = static_cast<uint32_t*>(sp.out);
+            for (uint32_t i = 0; i < sp.n; ++i)
+                if (o[i] != FGI_NONE) o[i] -= g->lbl_K;
+        }
     }
     g->stale_est += scr_h[3 + 3] + scr_h[3 + 4];   // the cascades' E_trav + E_match (fgi_prune_step)
 #if FGI_PROBE
@@ -3046,6 +3173,9 @@ static fgi_status prune_range_launch(fgi_graph* g, uint32_t lo, uint32_t hi, Tmp
     a.lo = lo;
     a.hi = hi;
     a.n_slots = g->n_slots;
+    a.s2l = g->lbl_hot ? g->s2l : nullptr;
+    a.ext_slots = g->ext_slots;
+    a.K = g->lbl_K;
     a.node = reinterpret_cast<const unsigned long long*>(g->node);
     a.row_off = g->row_off;
     a.row_len = g->row_len;
@@ -3158,7 +3288,7 @@ static fgi_status prune_rows(fgi_graph* g, uint32_t lo, uint32_t hi, bool allow_
     if (c[kPrNew] != c[kPrOld] || c[kPrDropped] != 0) g->pool_epoch++;
     const uint64_t pool_before = g->pool_top;
     // the full pass knows every row's length: defragment when holes are most of the pool
-    if (allow_defrag && lo == 0 && hi == g->n_handles && g->opt_defrag_pct > 0 &&
+    if (allow_defrag && lo == 0 && hi == g->ext_handles && g->opt_defrag_pct > 0 &&
         (g->pool_top - std::min<uint64_t>(g->pool_top, c[kPrLive])) * 100 > (uint64_t)g->opt_defrag_pct * g->pool_top)
         FGI_TRY(defragment(g));
     if (stats) {
@@ -3181,15 +3311,15 @@ fgi_status fgi_prune(fgi_graph* g, fgi_prune_stats* stats) {
     if (!g) return FGI_EINVAL;
     FGI_TRY(usable(g));
     if (stats) *stats = fgi_prune_stats{};
-    return prune_rows(g, 0, g->n_handles, true, stats);
+    return prune_rows(g, 0, g->ext_handles, true, stats);
 }
 
 fgi_status fgi_prune_range(fgi_graph* g, uint32_t first, uint32_t count, fgi_prune_stats* stats) {
     if (!g) return FGI_EINVAL;
     FGI_TRY(usable(g));
     if (stats) *stats = fgi_prune_stats{};
-    if (first > g->n_handles) return set_err(g, FGI_EINVAL, "first handle %u out of range", first);
-    const uint32_t hi = (uint32_t)std::min<uint64_t>((uint64_t)first + count, g->n_handles);
+    if (first > g->ext_handles) return set_err(g, FGI_EINVAL, "first handle %u out of range", first);
+    const uint32_t hi = (uint32_t)std::min<uint64_t>((uint64_t)first + count, g->ext_handles);
     return prune_rows(g, first, hi, false, stats);
 }
 
@@ -3201,12 +3331,12 @@ fgi_status fgi_prune_step(fgi_graph* g, uint32_t batch, uint32_t stale_pct, fgi_
     // here a batch runs only while the estimated stale entries exceed stale_pct of the pool
     if ((uint64_t)g->stale_est * 100 < (uint64_t)stale_pct * std::max<uint64_t>(g->pool_top, 1)) return FGI_OK;
     const uint32_t lo = g->prune_cursor;
-    const uint32_t hi = (uint32_t)std::min<uint64_t>((uint64_t)lo + batch, g->n_handles);
+    const uint32_t hi = (uint32_t)std::min<uint64_t>((uint64_t)lo + batch, g->ext_handles);
     const uint64_t est = g->stale_est;
     FGI_TRY(prune_rows(g, lo, hi, false, stats));
-    g->prune_cursor = hi >= g->n_handles ? 0 : hi;
+    g->prune_cursor = hi >= g->ext_handles ? 0 : hi;
     // the estimate shrinks by the share of the handles this batch covered
-    g->stale_est = hi >= g->n_handles ? 0 : est - est * (uint64_t)(hi - lo) / std::max<uint32_t>(g->n_handles, 1);
+    g->stale_est = hi >= g->ext_handles ? 0 : est - est * (uint64_t)(hi - lo) / std::max<uint32_t>(g->ext_handles, 1);
     if (stats) stats->stale_estimate = est;
     return FGI_OK;
 }
@@ -3218,8 +3348,9 @@ fgi_status fgi_release(fgi_graph* g, uint32_t n, const uint32_t* handle) {
     FGI_TRY(fold(g));
     if (n) note_words(g);
     for (uint32_t i = 0; i < n; ++i) {
-        const uint32_t h = handle[i];
-        if (h < g->n_slots || h >= g->n_handles) return set_err(g, FGI_EINVAL, "handle %u is not detached", h);
+        if (handle[i] < g->ext_slots || handle[i] >= g->ext_handles)
+            return set_err(g, FGI_EINVAL, "handle %u is not detached", handle[i]);
+        const uint32_t h = handle[i] + g->lbl_K;   // a detached handle's label
         if (std::find(g->free_detached.begin(), g->free_detached.end(), h) != g->free_detached.end())
             return set_err(g, FGI_EINVAL, "handle %u released twice", h);
         const uint64_t zero = 0;

@@ -1235,6 +1235,14 @@ fgi_status fgi_part_init_host(fgi_graph* g, uint32_t n_global, fgi_allgather_fn 
 
 static fgi_status part_alloc(fgi_graph* g, uint32_t n_global) {
     if (!g || g->world < 1 || g->rank < 0 || g->rank >= g->world) return FGI_EINVAL;
+    if (g->lbl_K) {   // a partition numbers its slots by rank ranges: no hub-first labels (a fresh graph drops them)
+        if (g->lbl_done || g->pool_top) return set_err(g, FGI_ESTATE, "a graph with loaded edges cannot join a partition");
+        g->lbl_K = 0;
+        g->n_slots = g->ext_slots;
+        g->n_handles = g->ext_handles;
+        g->free_detached.clear();
+        for (uint32_t i = g->n_detached; i > 0; --i) g->free_detached.push_back(g->n_slots + i - 1);
+    }
     if ((uint32_t)g->world > 8) return set_err(g, FGI_ENOTSUP, "at most 8 partitions (one node)");
     if (g->part) return set_err(g, FGI_ESTATE, "partition already initialised");
     const uint32_t W = (uint32_t)g->world;

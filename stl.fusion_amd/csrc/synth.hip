@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 
+#include <algorithm>
+
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 
@@ -12,9 +14,20 @@
 namespace fgi {
 namespace {
 
-__global__ void k_versions(uint32_t n, uint64_t seed, unsigned long long* node) {
+// slot s's node at label K + s (labels.hip moves the hot ones when it chooses them)
+__global__ void k_versions(uint32_t n, uint64_t seed, uint32_t K, unsigned long long* node) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s < n) node[s] = synth_version(seed, s) | kW_Consistent;
+    if (s < n) node[K + s] = synth_version(seed, s) | kW_Consistent;
+}
+
+// the generated edges' tags, from boundary slots (before the keys become labels)
+__global__ void k_synth_tags(uint64_t m, const uint64_t* __restrict__ keys, uint64_t seed, uint32_t stale_pct,
+                             uint64_t stale_seed, uint64_t* tags) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = keys[i];
+        const uint32_t src = (uint32_t)(k >> 32), dst = (uint32_t)k;
+        tags[i] = synth_version(seed, dst) + (synth_stale(stale_pct, stale_seed, src, dst) ? 1ull : 0ull);
+    }
 }
 
 __global__ void k_gen_layered(uint32_t levels, uint32_t width, uint32_t fanout, uint64_t seed, uint64_t* keys) {
@@ -54,9 +67,19 @@ __global__ void kx_deg(uint64_t m, const uint64_t* __restrict__ keys, uint32_t w
         if (which != 2) atomicAdd(cnt + (uint32_t)k, 1u);
     }
 }
-__global__ void kx_sortkey(uint32_t n, const uint32_t* __restrict__ cnt, uint64_t* key) {
+// weight classes: `per` classes per octave of (w + 1)
+__device__ __forceinline__ uint32_t kx_class(uint32_t w, uint32_t per) {
+    const uint32_t x = w + 1u;
+    const uint32_t l = 31u - (uint32_t)__builtin_clz(x);
+    const uint32_t frac = l ? ((x << (31u - l)) >> 28) & 7u : 0u;   // the 3 bits after the leading one
+    return l * per + (per == 4 ? frac >> 1 : per == 2 ? frac >> 2 : per == 8 ? frac : 0u);
+}
+// order 3 / 4 / 5: (weight class, slot) with 4 / 1 / 8 classes per octave, else (weight, slot)
+__global__ void kx_sortkey(uint32_t n, const uint32_t* __restrict__ cnt, uint32_t order, uint64_t* key) {
     const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-    if (u < n) key[u] = ((uint64_t)cnt[u] << 32) | (uint32_t)~u;
+    if (u >= n) return;
+    const uint32_t w = order == 3 ? kx_class(cnt[u], 4) : order == 4 ? kx_class(cnt[u], 1) : order == 5 ? kx_class(cnt[u], 8) : cnt[u];
+    key[u] = ((uint64_t)w << 32) | (uint32_t)~u;
 }
 // hot[u] = rank + 1 for the K heaviest, 0 otherwise
 __global__ void kx_hot(uint32_t n, uint32_t K, const uint64_t* __restrict__ sorted, uint32_t* hot) {
@@ -67,11 +90,21 @@ __global__ void kx_cold(uint32_t n, const uint32_t* __restrict__ hot, uint32_t* 
     const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
     if (u < n) cold[u] = hot[u] ? 0u : 1u;
 }
+// swizzle of a weight rank inside superblocks of 32,768 labels (32 lines x 32 words x 32 bits of a
+// bitmap): consecutive ranks fall in different 128-byte lines, then different words, so the heaviest
+// slots do not share a bitmap word or line (push levels' atomics), while the superblock stays compact
+__device__ __forceinline__ uint32_t kx_swz(uint32_t r) {
+    const uint32_t i = r & 32767u;
+    return (r & ~32767u) | ((i & 31u) << 10) | (((i >> 5) & 31u) << 5) | (i >> 10);
+}
 __global__ void kx_perm(uint32_t n, uint32_t K, const uint32_t* __restrict__ hot, const uint32_t* __restrict__ cold_pos,
                         uint32_t slot_order, uint32_t* perm) {
     const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-    // slot_order: the hot labels keep the slots' order among themselves (hot position = u - cold before u)
-    if (u < n) perm[u] = hot[u] ? (slot_order ? u - cold_pos[u] : hot[u] - 1) : K + cold_pos[u];
+    // slot_order: the hot labels keep the slots' order among themselves (hot position = u - cold before u);
+    // 2: weight order, swizzled within superblocks (K a multiple of 32,768)
+    if (u < n)
+        perm[u] = hot[u] ? (slot_order == 1 ? u - cold_pos[u] : slot_order == 2 ? kx_swz(hot[u] - 1) : hot[u] - 1)
+                         : K + cold_pos[u];
 }
 __global__ void kx_apply(uint64_t m, const uint32_t* __restrict__ perm, uint64_t* keys) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -108,7 +141,7 @@ static fgi_status exp_relabel(fgi_graph* g, uint32_t n, uint64_t* keys, uint64_t
     FGI_HIP(g, hipMemsetAsync(cnt, 0, (size_t)n * 4, s));
     FGI_HIP(g, hipMemsetAsync(hot, 0, (size_t)n * 4, s));
     hipLaunchKernelGGL(kx_deg, dim3(8192), dim3(256), 0, s, m, keys, which, cnt);
-    hipLaunchKernelGGL(kx_sortkey, dim3((n + 255) / 256), dim3(256), 0, s, n, cnt, k0);
+    hipLaunchKernelGGL(kx_sortkey, dim3((n + 255) / 256), dim3(256), 0, s, n, cnt, slot_order, k0);
     size_t tb = 0;
     FGI_HIP(g, rocprim::radix_sort_keys_desc(nullptr, tb, k0, k1, (size_t)n, 0, 64, s));
     void* tmp;
@@ -139,13 +172,28 @@ fgi_status synth_rmat_keys(fgi_graph* g, uint32_t scale, uint32_t edge_factor, u
     return FGI_OK;
 }
 
+// rows from generated keys (boundary slots): with hub-first labels the tags are computed from the
+// slots first, then the first load chooses the labels and the keys become labels
+static fgi_status synth_rows(fgi_graph* g, uint64_t m, uint64_t* keys, uint64_t seed, uint32_t stale_pct, uint64_t stale_seed) {
+    if (!g->lbl_K) return build_rows_from_keys(g, m, keys, nullptr, seed, stale_pct, stale_seed);
+    uint64_t* tags = nullptr;
+    FGI_HIP(g, hipMalloc(reinterpret_cast<void**>(&tags), std::max<uint64_t>(m, 1) * sizeof(uint64_t)));
+    hipLaunchKernelGGL(k_synth_tags, dim3(8192), dim3(256), 0, g->stream, m, keys, seed, stale_pct, stale_seed, tags);
+    fgi_status st = hipGetLastError() == hipSuccess ? FGI_OK : FGI_EDEVICE;
+    if (st == FGI_OK) st = labels_choose(g, keys, m);
+    if (st == FGI_OK) st = labels_map_keys(g, keys, m);
+    if (st == FGI_OK) st = build_rows_from_keys(g, m, keys, tags, seed, stale_pct, stale_seed);
+    hipFree(tags);
+    return st;
+}
+
 fgi_status synth_versions(fgi_graph* g, uint32_t n, uint64_t seed) {
     FGI_HIP(g, hipMemsetAsync(g->node, 0, (size_t)g->n_handles * 8, g->stream));
     FGI_HIP(g, hipMemsetAsync(g->vis_bm, 0, g->bm_words * 4, g->stream));   // a new node table
     g->v_dirty = false;
     g->vis_stale = false;
     note_words(g);
-    hipLaunchKernelGGL(k_versions, dim3((n + 255) / 256), dim3(256), 0, g->stream, n, seed,
+    hipLaunchKernelGGL(k_versions, dim3((n + 255) / 256), dim3(256), 0, g->stream, n, seed, g->lbl_K,
                        reinterpret_cast<unsigned long long*>(g->node));
     FGI_HIP(g, hipGetLastError());
     return FGI_OK;
@@ -160,7 +208,7 @@ extern "C" {
 fgi_status fgi_synth_layered(fgi_graph* g, uint32_t levels, uint32_t width, uint32_t fanout, uint64_t seed) {
     if (!g || levels < 2 || width == 0 || fanout == 0 || fanout > 64 || fanout > width) return FGI_EINVAL;
     const uint64_t n = (uint64_t)levels * width;
-    if (n > g->n_slots) return set_err(g, FGI_EINVAL, "graph needs %llu slots", (unsigned long long)n);
+    if (n > g->ext_slots) return set_err(g, FGI_EINVAL, "graph needs %llu slots", (unsigned long long)n);
     hipSetDevice(g->device);
     FGI_TRY(synth_versions(g, (uint32_t)n, seed));
     const uint64_t m = (uint64_t)(levels - 1) * width * fanout;
@@ -169,7 +217,7 @@ fgi_status fgi_synth_layered(fgi_graph* g, uint32_t levels, uint32_t width, uint
     const uint64_t threads = (uint64_t)(levels - 1) * width;
     hipLaunchKernelGGL(k_gen_layered, dim3((uint32_t)((threads + 255) / 256)), dim3(256), 0, g->stream, levels, width,
                        fanout, seed, keys);
-    fgi_status st = hipGetLastError() == hipSuccess ? build_rows_from_keys(g, m, keys, nullptr, seed, 0, 0) : FGI_EDEVICE;
+    fgi_status st = hipGetLastError() == hipSuccess ? synth_rows(g, m, keys, seed, 0, 0) : FGI_EDEVICE;
     hipFree(keys);
     return st;
 }
@@ -177,14 +225,14 @@ fgi_status fgi_synth_layered(fgi_graph* g, uint32_t levels, uint32_t width, uint
 fgi_status fgi_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_factor, uint64_t seed, uint32_t stale_pct,
                           uint64_t stale_seed) {
     if (!g || scale == 0 || scale > 31 || edge_factor == 0 || stale_pct > 100) return FGI_EINVAL;
-    if ((1ull << scale) > g->n_slots) return set_err(g, FGI_EINVAL, "graph needs 2^%u slots", scale);
+    if ((1ull << scale) > g->ext_slots) return set_err(g, FGI_EINVAL, "graph needs 2^%u slots", scale);
     hipSetDevice(g->device);
     FGI_TRY(synth_versions(g, 1u << scale, seed));
     uint64_t* keys = nullptr;
     uint64_t m = 0;
     FGI_TRY(synth_rmat_keys(g, scale, edge_factor, seed, &keys, &m));
-    FGI_TRY(exp_relabel(g, 1u << scale, keys, m));
-    fgi_status st = build_rows_from_keys(g, m, keys, nullptr, seed, stale_pct, stale_seed);
+    if (!g->lbl_K) FGI_TRY(exp_relabel(g, 1u << scale, keys, m));
+    fgi_status st = synth_rows(g, m, keys, seed, stale_pct, stale_seed);
     hipFree(keys);
     return st;
 }

@@ -30,6 +30,8 @@
 #include <hip/hip_cooperative_groups.h>
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
@@ -575,13 +577,29 @@ __device__ __forceinline__ void msg_flush(MsgEmit<true>& me, uint32_t at, const 
 // which visits the other roots through the visit bitmap.
 // One root per lane (i < n), every lane of the wave calls it: the visit, the frontier entry, the
 // root counters.
+// Roots given as boundary handles (fgi_invalidate*, labels active): handle x is label s2l[x] if hot,
+// else K + x; anything past ext_handles is no handle (ignored like any out-of-range root)
+struct RootMap {
+    const uint32_t* s2l;
+    uint32_t ext_slots, ext_handles, K;
+    int on;
+};
+__device__ __forceinline__ uint32_t root_label(const RootMap& m, uint32_t x) {
+    if (x >= m.ext_handles) return FGI_NONE;
+    if (m.s2l && x < m.ext_slots) {
+        const uint32_t l = m.s2l[x];
+        if (l != FGI_NONE) return l;
+    }
+    return x + m.K;
+}
+
 template <int IMM>
 __device__ __forceinline__ void root_step(uint32_t i, const uint32_t* __restrict__ roots, const uint8_t* __restrict__ imm,
                                           uint32_t n, uint32_t base, uint32_t n_range, unsigned long long* node,
-                                          uint32_t* vis, const Out& o, WaveCtr* ctr) {
+                                          uint32_t* vis, const Out& o, WaveCtr* ctr, const RootMap& rm = RootMap{}) {
     uint32_t win = 0, flagged = 0, h = 0;
     if (i < n) {
-        h = roots[i] - base;
+        h = rm.on ? root_label(rm, roots[i]) : roots[i] - base;
         const bool is_imm = imm ? imm[i] != 0 : false;
         if (h < n_range && is_imm == (IMM != 0)) {
             unsigned long long w = node[h];
@@ -621,8 +639,8 @@ template <int IMM>
 __global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ roots, const uint8_t* __restrict__ imm,
                                                   uint32_t n, uint32_t base, uint32_t n_range, unsigned long long* node,
                                                   uint32_t* vis, Out o, WaveCtr* ctr, unsigned long long* done,
-                                                  int publish) {
-    root_step<IMM>(blockIdx.x * blockDim.x + threadIdx.x, roots, imm, n, base, n_range, node, vis, o, ctr);
+                                                  int publish, RootMap rm) {
+    root_step<IMM>(blockIdx.x * blockDim.x + threadIdx.x, roots, imm, n, base, n_range, node, vis, o, ctr, rm);
     if (publish) publish_ft(o.ln, done, gridDim.x);
 }
 
@@ -779,7 +797,7 @@ __device__ __forceinline__ int mid_level(const WaveCtr* ctr, int L) {
 // their collect run in the fused tail kernel.
 __global__ __launch_bounds__(kCollectThreads) void k_collect(int L, WaveCtr* ctr, WaveParams wp, CollectArgs c,
                                                              CollectArgs c1, uint64_t big_push) {
-    const bool fused = L < 0;
+    const bool fused = FGI_VARIANTS && L < 0;
     L = mid_level(ctr, L);
     if (L < 0) return;
     if (fused && (L & 1)) c = c1;   // a fused wave's level is known on the device only: odd levels, buffer 1
@@ -789,7 +807,7 @@ __global__ __launch_bounds__(kCollectThreads) void k_collect(int L, WaveCtr* ctr
     if (lvl_F(lc) == 0 && !wp.multi) return;
     if (level_pulls(ctr, L, wp)) {
         collect_hot(c, (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, (uint64_t)gridDim.x * blockDim.x);
-        if (c.sum_bm)
+        if (FGI_VARIANTS && c.sum_bm)
             collect_sum(c, ctr, L, (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6),
                         (uint64_t)gridDim.x * (blockDim.x >> 6));
         return;
@@ -1450,7 +1468,7 @@ __global__ __launch_bounds__(kBlock, kLevelOcc) void k_level(int Larg, WaveParam
     __shared__ unsigned long long s_red[kBlock / 64];
     static_assert(sizeof(PullLds) <= (kLevelLds - kChunk - 4) * 4 && kTailCap <= kChunk, "pull LDS");
     static_assert(kPushLds % 2 == 0 && (kPushLds + sizeof(MsgEmit<true>) / 4) <= kLevelLds, "push LDS");
-    const bool fused = !PART && Larg < 0;
+    const bool fused = FGI_VARIANTS && !PART && Larg < 0;
     const int L = mid_level(ctr, Larg);
     if (L < 0) return;
     if (fused && (L & 1)) {
@@ -1485,7 +1503,7 @@ __global__ __launch_bounds__(kBlock, kLevelOcc) void k_level(int Larg, WaveParam
     // multi-GPU pull levels run on every rank (parents may be remote); otherwise no frontier, no work
     if (pull) {
         unsigned long long bs[3] = {0, 0, 0};
-        const bool sum = p.sum != nullptr && lc.sum != 0;
+        const bool sum = FGI_VARIANTS && p.sum != nullptr && lc.sum != 0;
         pull_level(L, p, wp, npull, sum, node, vis, s_rel, *reinterpret_cast<PullLds*>(s_base), blk, s_st, bs);
         PROBE(L, 4);
         pull_epilogue(L, p, o.ln, done, bs, s_red, fused ? &ctr->cur : nullptr);
@@ -1595,10 +1613,94 @@ __global__ void k_part_tail(const WaveCtr* ctr, int L0, int L, uint32_t W, const
 // handles per lane, staged in LDS and stored coalesced.
 // total = 1 (bitmap mode, no k_final_write follows): the last block also sums the counts into
 // ctr->inv (V_inv).
+// Hub-first labels (labels.hip): the bitmap over boundary handles of fold tile t
+// (handles [t * kFoldTile, + kFoldTile), kFoldWords 64-bit words) is the labels' bitmap shifted by K
+// (K + x is the label of every handle x that has no hot label; K is a multiple of kFoldTile), ORed with
+// the tile's hot labels' bits at their slots: per hot class j, the labels [fold_start[j][t],
+// fold_start[j][t + 1]), which keep slot order. Written to f.xbm; returns the tile's set bits (every
+// thread). Block-uniform call; s_w: kFoldWords words, s_a / s_o: kMaxHotClasses + 1 words of LDS.
+__device__ unsigned long long fold_tile(const FoldArgs& f, const unsigned long long* __restrict__ inv64, uint64_t ext_words,
+                                        uint32_t t, unsigned long long* s_w, uint32_t* s_a, uint32_t* s_o,
+                                        unsigned long long* s_red) {
+    const uint64_t w0 = (uint64_t)t * kFoldWords;
+    const uint32_t nw = (uint32_t)std::min<uint64_t>(kFoldWords, ext_words > w0 ? ext_words - w0 : 0);
+    const uint64_t kw = f.K / 64;
+    for (uint32_t i = threadIdx.x; i < kFoldWords; i += blockDim.x) s_w[i] = i < nw ? inv64[kw + w0 + i] : 0ull;
+    if (f.l2s && f.ncls) {
+        // this tile's run of each hot class: offsets by one block scan over the classes
+        uint32_t len = 0, a = 0;
+        if (threadIdx.x < f.ncls) {
+            const uint32_t* fs = f.fold_start + (uint64_t)threadIdx.x * (f.tiles + 1) + t;
+            a = fs[0];
+            len = fs[1] - a;
+        }
+        uint32_t tot;
+        const uint32_t ex = wave_excl_scan(len, tot);
+        const uint32_t wid = threadIdx.x >> 6;
+        __shared__ uint32_t s_wt[kBlock / 64];
+        if (lane_id() == 0) s_wt[wid] = tot;
+        __syncthreads();
+        uint32_t before = 0, total = 0;
+        for (uint32_t k = 0; k < blockDim.x / 64; ++k) {
+            before += k < wid ? s_wt[k] : 0u;
+            total += s_wt[k];
+        }
+        if (threadIdx.x < f.ncls) {
+            s_a[threadIdx.x] = a;
+            s_o[threadIdx.x] = before + ex;
+        }
+        if (threadIdx.x == 0) s_o[f.ncls] = total;
+        __syncthreads();
+        // one hot label per lane, four in flight per thread: its class by a binary search over the
+        // offsets, its bit, then (set bits only) its slot
+        constexpr int kPer = 4;
+        for (uint32_t k0 = 0; k0 < total; k0 += kPer * blockDim.x) {   // block-uniform
+            uint32_t lab[kPer];
+            bool hit[kPer];
+#pragma unroll
+            for (int q = 0; q < kPer; ++q) {
+                const uint32_t k = k0 + q * blockDim.x + threadIdx.x;
+                lab[q] = FGI_NONE;
+                if (k < total) {
+                    uint32_t lo = 0, hi = f.ncls;   // the last class j with s_o[j] <= k
+                    while (hi - lo > 1) {
+                        const uint32_t mid = (lo + hi) >> 1;
+                        if (s_o[mid] <= k) lo = mid;
+                        else hi = mid;
+                    }
+                    lab[q] = s_a[lo] + (k - s_o[lo]);
+                }
+            }
+#pragma unroll
+            for (int q = 0; q < kPer; ++q) hit[q] = lab[q] != FGI_NONE && ((inv64[lab[q] >> 6] >> (lab[q] & 63)) & 1ull);
+#pragma unroll
+            for (int q = 0; q < kPer; ++q)
+                if (hit[q]) {
+                    const uint32_t x = f.l2s[lab[q]] - (uint32_t)(w0 * 64);
+                    if (x < kFoldTile) atomicOr(&s_w[x >> 6], 1ull << (x & 63));   // always: the run is this tile's
+                }
+        }
+    }
+    __syncthreads();
+    unsigned long long c = 0;
+    for (uint32_t i = threadIdx.x; i < nw; i += blockDim.x) {
+        const unsigned long long v = s_w[i];
+        c += (unsigned long long)__popcll(v);
+        f.xbm[w0 + i] = v;
+    }
+    c = block_sum(c, s_red);
+    __syncthreads();   // s_w, s_a, s_o are reused by the block's next tile
+    return c;
+}
+
+// The final count: tickets 0..kStats-1 fold the per-block statistics into the wave counters; every
+// block counts the set bits of its 64-bit words [t * wpb, (t + 1) * wpb) into status[t]. With hot labels
+// (f.xbm), block t is fold tile t instead: it writes the tile's bitmap over boundary handles into xbm
+// and counts that.
 __global__ __launch_bounds__(kBlock) void k_final_count(const unsigned long long* __restrict__ inv64, uint64_t words,
                                                         uint64_t wpb, unsigned long long* status, WaveCtr* ctr,
                                                         const unsigned long long* __restrict__ blk, int total,
-                                                        unsigned long long* done) {
+                                                        unsigned long long* done, FoldArgs f) {
     __shared__ unsigned long long s_red[kBlock / 64];
     const uint32_t t = blockIdx.x;
     if (t < (uint32_t)kStats) {
@@ -1612,10 +1714,16 @@ __global__ __launch_bounds__(kBlock) void k_final_count(const unsigned long long
         x = block_sum(x, s_red);
         if (threadIdx.x == 0) *dst[k] = x + (k == kStFlagged ? ctr->root_flagged : 0ull);
     }
-    const uint64_t lo = t * wpb, hi = std::min<uint64_t>(words, lo + wpb);
     unsigned long long c = 0;
-    for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x) c += (unsigned long long)__popcll(inv64[w]);
-    c = block_sum(c, s_red);
+    if (f.xbm) {
+        __shared__ unsigned long long s_w[kFoldWords];
+        __shared__ uint32_t s_a[kMaxHotClasses + 1], s_o[kMaxHotClasses + 1];
+        if ((uint64_t)t * kFoldWords < words) c = fold_tile(f, inv64, words, t, s_w, s_a, s_o, s_red);
+    } else {
+        const uint64_t lo = t * wpb, hi = std::min<uint64_t>(words, lo + wpb);
+        for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x) c += (unsigned long long)__popcll(inv64[w]);
+        c = block_sum(c, s_red);
+    }
     if (!total) {
         if (threadIdx.x == 0) status[t] = c;
         return;
@@ -1628,9 +1736,12 @@ __global__ __launch_bounds__(kBlock) void k_final_count(const unsigned long long
     if (threadIdx.x == 0) ctr->inv = all;
 }
 
+// The list: block t writes the set bits of its words [t * wpb, + wpb) of inv64 (the boundary's bitmap:
+// the labels' own, or xbm) in ascending order, after the sum of the counts of the status entries
+// before its own (spb entries per block: 1, or its fold tiles).
 __global__ __launch_bounds__(kBlock) void k_final_write(const unsigned long long* __restrict__ inv64, uint64_t words,
                                                         uint64_t wpb, const unsigned long long* __restrict__ status,
-                                                        WaveCtr* ctr, uint32_t* out, int need_done) {
+                                                        WaveCtr* ctr, uint32_t* out, int need_done, uint32_t spb) {
     if (need_done && ctr->phase != kPhaseDone) return;   // a fused wave whose tail stopped early: not yet
     __shared__ unsigned long long s_red[kBlock / 64];
     __shared__ unsigned long long s_wbase[kBlock / 64];
@@ -1644,7 +1755,7 @@ __global__ __launch_bounds__(kBlock) void k_final_write(const unsigned long long
     const uint64_t ww = (wpb + W - 1) / W;
     const uint64_t wlo = std::min<uint64_t>(hi, lo + wid * ww), whi = std::min<uint64_t>(hi, wlo + ww);
     unsigned long long part = 0;
-    for (uint32_t k = threadIdx.x; k < t; k += blockDim.x) part += status[k];
+    for (uint64_t k = threadIdx.x; k < (uint64_t)t * spb; k += blockDim.x) part += status[k];
     uint32_t wc = 0;
     for (uint64_t x = wlo + lane; x < whi; x += 64) wc += (uint32_t)__popcll(inv64[x]);
 #pragma unroll
@@ -1714,6 +1825,8 @@ struct CoopArgs {
     int bar_mode;                      // soft_grid_sync's memory ordering (FGI_BAR_MODE)
     unsigned long long* gbar;          // plain launch: the grid barrier's arrival counter (monotonic)
     int one_round;                     // chunk size by level_mult_one_round (FGI_COOP_CHUNKS=0: level_mult)
+    FoldArgs fold;                     // hot labels: the ids come from the folded bitmap (fold_tile)
+    uint64_t ext_words;                // words of the bitmap over boundary handles
 };
 
 // Grid barrier of a plain (non-cooperative) launch of k_wave_coop. A cooperative launch goes to the
@@ -1872,12 +1985,25 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
         }
     }
     unsigned long long c = 0;
-    for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x) {
-        const unsigned long long v = inv64[w];
-        if (w - lo < kFinalStage) s_words[w - lo] = v;
-        c += (unsigned long long)__popcll(v);
+    // hot labels: this block's fold tiles (the list is written from their bitmap over boundary handles)
+    const bool folded = a.fold.xbm != nullptr;
+    const uint64_t tiles = folded ? (a.ext_words + kFoldWords - 1) / kFoldWords : 0;
+    const uint64_t tpb = folded ? (tiles + gridDim.x - 1) / gridDim.x : 0;
+    const uint64_t f_lo = std::min<uint64_t>(a.ext_words, blockIdx.x * tpb * kFoldWords);
+    const uint64_t f_hi = std::min<uint64_t>(a.ext_words, f_lo + tpb * kFoldWords);
+    if (folded) {
+        unsigned long long* s_fw = reinterpret_cast<unsigned long long*>(s_x);   // kFoldWords words
+        __shared__ uint32_t s_fa[kMaxHotClasses + 1], s_fo[kMaxHotClasses + 1];
+        for (uint64_t t = blockIdx.x * tpb; t < std::min<uint64_t>(tiles, (blockIdx.x + 1) * tpb); ++t)
+            c += fold_tile(a.fold, inv64, a.ext_words, (uint32_t)t, s_fw, s_fa, s_fo, s_red);
+    } else {
+        for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x) {
+            const unsigned long long v = inv64[w];
+            if (w - lo < kFinalStage) s_words[w - lo] = v;
+            c += (unsigned long long)__popcll(v);
+        }
+        c = block_sum(c, s_red);
     }
-    c = block_sum(c, s_red);
     if (threadIdx.x == 0) coh_xchg(a.cnt + blockIdx.x, c);
     CPROBE(6);
     if (!grid_sync()) return;
@@ -1895,15 +2021,16 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
         a.acc[kAccFTotal] += f_total;
     }
     const uint32_t lane = lane_id(), wid = threadIdx.x >> 6;
-    const uint16_t* bits16 = reinterpret_cast<const uint16_t*>(inv64);
+    const uint16_t* bits16 = reinterpret_cast<const uint16_t*>(folded ? a.fold.xbm : inv64);
     uint64_t run = s_base_out + excl;
-    for (uint64_t w0 = lo; w0 < hi; w0 += (uint64_t)(blockDim.x >> 6) * kTileWords) {   // block-uniform
+    const uint64_t o_lo = folded ? f_lo : lo, o_hi = folded ? f_hi : hi;   // the words listed
+    for (uint64_t w0 = o_lo; w0 < o_hi; w0 += (uint64_t)(blockDim.x >> 6) * kTileWords) {   // block-uniform
         const uint64_t tw = w0 + (uint64_t)wid * kTileWords;
         const uint64_t q = tw * 4 + lane;
-        const uint64_t wl = tw - lo + lane / 4;
-        const uint32_t m = (tw + lane / 4 >= hi) ? 0u
-                           : wl < kFinalStage ? (uint32_t)(s_words[wl] >> (16 * (lane & 3))) & 0xFFFFu
-                                              : (uint32_t)bits16[q];
+        const uint64_t wl = tw - o_lo + lane / 4;
+        const uint32_t m = (tw + lane / 4 >= o_hi) ? 0u
+                           : (!folded && wl < kFinalStage) ? (uint32_t)(s_words[wl] >> (16 * (lane & 3))) & 0xFFFFu
+                                                           : (uint32_t)bits16[q];
         uint32_t tot;
         const uint32_t ex = wave_excl_scan((uint32_t)__popc(m), tot);
         __syncthreads();
@@ -1962,7 +2089,7 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
         }
     }
     for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x)
-        if (w - lo >= kFinalStage || s_words[w - lo]) invw[w] = 0ull;
+        if (folded || w - lo >= kFinalStage || s_words[w - lo]) invw[w] = 0ull;
     if (threadIdx.x < (uint32_t)kStats) a.blk[(uint64_t)threadIdx.x * kStatBlocks + blockIdx.x] = 0ull;
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) {
@@ -1976,6 +2103,77 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
     CPROBE(9);
 }
 
+// ---- the wave's tail: its last, small push levels in one persistent launch -------------------------
+// After a level group's k_collect + k_level launches, k_wave_tail (kTailBlocks blocks, software grid
+// barriers between levels, one wave per block fencing: 1.3 us per barrier at 32 blocks,
+// profiles/r7i_grid_barrier.txt) runs the levels that follow while they are small push levels: the
+// collect after a pull level, then one push level after the other, until the frontier is empty or a
+// level pulls or has more than max_edges edges (that level is left to the host's next group). It
+// records where it stopped in ctr->cur. A level group thus ends with one launch however many small push
+// levels the wave's tail has (configs[1]: levels 4 and 5, four launches before), and a wave whose pull
+// levels fit the group never needs a second group (the asynchronous waves rely on that: max_edges = ~0).
+constexpr uint32_t kTailBlocks = 32;
+constexpr int kGbarTail = 8;   // g->gbar word of the tail's barrier (its own grid size)
+
+struct TailArgs {
+    int L0;                            // the first level the group did not launch
+    WaveParams wp;
+    CollectArgs col[2];                // frontier buffers by level parity (collect after a pull level)
+    ExpandArgs x[2];
+    Out o[2];
+    const unsigned long long* node;
+    uint32_t* vis;
+    WaveCtr* ctr;
+    unsigned long long* blk;
+    unsigned long long* gbar;
+    uint64_t bar_timeout;
+    uint64_t max_edges;                // a level with more edges is left to the host's next group
+};
+
+__global__ __launch_bounds__(kBlock) void k_wave_tail(TailArgs a) {
+    __shared__ __align__(16) uint32_t s_x[kChunkEmitCap + 8];
+    uint32_t* s_rel = s_x;
+    uint32_t* s_base = s_x + kChunk + 4;
+    __shared__ Emit em;
+    __shared__ MsgEmit<false> me;
+    __shared__ unsigned long long s_st[kBlock / 64][kStats];
+    __shared__ unsigned long long s_ft;
+    WaveCtr* ctr = a.ctr;
+    auto grid_sync = [&]() -> bool { return soft_grid_sync(a.gbar, &ctr->broken, nullptr, a.bar_timeout, false, 1); };
+    int L = a.L0;
+    for (bool first = true;; ++L, first = false) {
+        LevelCtr& lc = ctr->lvl[L % kRing];
+        if (threadIdx.x == 0) s_ft = coh_read(&lc.ft);   // a push producer's packed counter (or the pull's F / T)
+        __syncthreads();
+        const uint64_t F = lc.F ? lc.F : (s_ft >> 32), T = lc.F ? lc.T : (s_ft & 0xFFFFFFFFull);
+        if (F == 0 || level_pulls(ctr, L, a.wp, F, T) || T > a.max_edges) break;
+        if (first && L > 0 && ctr->lvl[(L + kRing - 1) % kRing].pull) {   // after a pull level: its frontier list
+            collect_front(lc, a.wp.grid, a.col[L & 1], (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6),
+                          (uint64_t)gridDim.x * (blockDim.x >> 6));
+            if (!grid_sync()) return;
+        }
+        if (blockIdx.x == 0) {
+            if (threadIdx.x == 0) {
+                lc.pull = 0ull;
+                lc.mult = level_mult_one_round(T, gridDim.x);
+                ctr->lvl[(L + 1) % kRing].npull = lc.npull;
+            }
+            // level L + 1's counter accumulates during this level; L + 2's is cleared for the next one
+            if (threadIdx.x < sizeof(LevelCtr) / 8)
+                reinterpret_cast<unsigned long long*>(&ctr->lvl[(L + 2) % kRing])[threadIdx.x] = 0ull;
+        }
+        const int buf = L & 1;
+        Out o = a.o[buf ^ 1];
+        o.ln = &ctr->lvl[(L + 1) % kRing];
+        emit_init(em);
+        expand_level<false>(kProbeLevelsOff, F, T, level_mult_one_round(T, gridDim.x), a.x[buf], a.node, a.vis, o, em, s_x,
+                            me, s_rel, s_base, a.blk, s_st, RemoteArgs{});
+        if (!grid_sync()) return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) ctr->cur = (unsigned long long)L;
+}
+
+#if FGI_VARIANTS   // measured slower than the level groups: variant builds only
 // ---- fused waves: the small push levels of a wave inside two persistent launches -----------------
 // run_wave's launch sequence is: k_wave_fused<false> (head) — the wave's counters, bitmaps and
 // statistics cleared, the roots, then push levels while they are small; k_collect + k_level pairs
@@ -2158,6 +2356,8 @@ __global__ __launch_bounds__(kBlock) void k_wave_fused(FusedArgs a) {
         ctr->phase = kPhaseDone;
     }
 }
+
+#endif  // FGI_VARIANTS
 
 __global__ __launch_bounds__(kBlock) void k_wave_init(WaveCtr* ctr, unsigned long long* blk, uint32_t* inv_bm,
                                                       uint32_t* vis_bm, uint64_t bm_words) {
@@ -2365,17 +2565,32 @@ ExpandArgs expand_args(fgi_graph* g, int buf) {
 
 // the invalidated bitmap -> V_inv (ctr->inv) and, with ids, the invalidated list
 hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true) {
+    const auto* inv64 = reinterpret_cast<const unsigned long long*>(g->inv_bm);
+    const FoldArgs f = fold_args(g);
+    if (f.xbm) {   // hot labels: one fold tile per counting block, the list from the folded bitmap
+        const uint64_t words = ((uint64_t)g->ext_handles + 63) / 64;
+        const uint32_t tiles = (uint32_t)((words + kFoldWords - 1) / kFoldWords);
+        unsigned long long* st = g->fold_status;
+        hipLaunchKernelGGL(k_final_count, dim3(std::max<uint32_t>(tiles, kStats)), dim3(kBlock), 0, g->stream, inv64, words,
+                           (uint64_t)kFoldWords, st, g->ctr, (const unsigned long long*)g->blk_stats, ids ? 0 : 1, g->done, f);
+        if (ids) {
+            const uint32_t G = std::min<uint32_t>(kFinalBlocks, tiles), spb = (tiles + G - 1) / G;
+            const uint32_t G2 = (tiles + spb - 1) / spb;
+            hipLaunchKernelGGL(k_final_write, dim3(G2), dim3(kBlock), 0, g->stream, (const unsigned long long*)g->xbm, words,
+                               (uint64_t)spb * kFoldWords, (const unsigned long long*)st, g->ctr, g->inv, 0, spb);
+        }
+        return hipGetLastError();
+    }
     const uint64_t words = ((uint64_t)n_handles + 63) / 64;
     uint32_t G = (uint32_t)std::min<uint64_t>(kFinalBlocks, std::max<uint64_t>(kStats, (words + kFinalWpb - 1) / kFinalWpb));
     const uint64_t wpb = (words + G - 1) / G;
-    const auto* inv64 = reinterpret_cast<const unsigned long long*>(g->inv_bm);
     // per-block counts apart from the pull prefixes a collect may still read
     unsigned long long* st = g->bsum + 6ull * kStatBlocks;
     hipLaunchKernelGGL(k_final_count, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb, st, g->ctr,
-                       (const unsigned long long*)g->blk_stats, ids ? 0 : 1, g->done);
+                       (const unsigned long long*)g->blk_stats, ids ? 0 : 1, g->done, FoldArgs{});
     if (ids)
         hipLaunchKernelGGL(k_final_write, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb,
-                           (const unsigned long long*)st, g->ctr, g->inv, 0);
+                           (const unsigned long long*)st, g->ctr, g->inv, 0, 1u);
     return hipGetLastError();
 }
 
@@ -2383,7 +2598,8 @@ hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true) {
 #define FGI_ROOT_BLOCK 256   // measurement builds: make variant-rootblk RB=<threads> (a multiple of 64)
 #endif
 void launch_roots(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev, uint32_t base,
-                  uint32_t n_range, int publish) {
+                  uint32_t n_range, int publish, bool ext_roots = false) {
+    const RootMap rm{g->lbl_hot ? g->s2l : nullptr, g->ext_slots, g->ext_handles, g->lbl_K, ext_roots && g->lbl_K ? 1 : 0};
     constexpr uint32_t kRootBlock = FGI_ROOT_BLOCK;
     static_assert(kRootBlock % 64 == 0 && kRootBlock <= kBlock, "root block");
     const uint32_t nb = (n_roots + kRootBlock - 1) / kRootBlock;
@@ -2392,9 +2608,9 @@ void launch_roots(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, con
     // the immediate roots' launch never publishes: the second launch adds to the same counter
     if (imm_dev)
         hipLaunchKernelGGL(k_roots<1>, dim3(nb), dim3(kRootBlock), 0, g->stream, roots_dev, imm_dev, n_roots, base, n_range,
-                           node, g->vis_bm, o, g->ctr, g->done, 0);
+                           node, g->vis_bm, o, g->ctr, g->done, 0, rm);
     hipLaunchKernelGGL(k_roots<0>, dim3(nb), dim3(kRootBlock), 0, g->stream, roots_dev, imm_dev, n_roots, base, n_range, node,
-                       g->vis_bm, o, g->ctr, g->done, publish);
+                       g->vis_bm, o, g->ctr, g->done, publish, rm);
 }
 
 }  // namespace
@@ -2430,11 +2646,15 @@ static int bar_mode() {
 // FGI_COOP_LAUNCH=1: k_wave_coop as a cooperative launch (grid barriers by the device library)
 // instead of a plain launch with soft_grid_sync. Nothing else launches cooperatively.
 bool coop_launch_mode() {
+#if FGI_VARIANTS
     static const bool coop = [] {
         const char* e = getenv("FGI_COOP_LAUNCH");
         return e && e[0] == '1';
     }();
     return coop;
+#else
+    return false;   // the cooperative launch of round 3 (and its exit-time fault under rocprofv3): variant builds only
+#endif
 }
 
 // One push-only wave in a single launch of k_wave_coop (one block per CU, grid barriers between its
@@ -2453,7 +2673,7 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
     // fails the batch cleanly (soft_grid_sync) instead of hanging.
     int& per_cu = g->coop_per_cu;
     if (per_cu == 0 &&
-        (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, coop ? k_wave_coop<false> : k_wave_coop<true>, kBlock, 0) !=
+        (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_wave_coop<true>, kBlock, 0) !=
              hipSuccess ||
          per_cu < 1))
         per_cu = 1;
@@ -2519,9 +2739,13 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
         return e && e[0] == '0' ? 0 : 1;
     }();
     a.one_round = one_round;
+    a.fold = fold_args(g);
+    a.ext_words = ((uint64_t)g->ext_handles + 63) / 64;
     if (coop) {
+#if FGI_VARIANTS
         void* args[] = {&a};
         FGI_HIP(g, hipLaunchCooperativeKernel(reinterpret_cast<const void*>(k_wave_coop<false>), dim3(G), dim3(kBlock), args, 0, s));
+#endif
     } else {
         hipLaunchKernelGGL(k_wave_coop<true>, dim3(G), dim3(kBlock), 0, s, a);
         FGI_HIP(g, hipGetLastError());
@@ -2573,6 +2797,7 @@ void print_probe(fgi_graph* g, int L0, int L1) {
 
 namespace {
 
+#if FGI_VARIANTS
 // FGI_FUSED_BLOCKS: the fused kernels' grid (default one block per CU; measurement)
 
 bool fused_init_in_head() {
@@ -2591,6 +2816,8 @@ uint32_t fused_grid(const fgi_graph* g) {
     return std::max<uint32_t>((uint32_t)kStats, env ? env : (uint32_t)std::max(g->n_cu, 1));
 }
 
+#endif  // FGI_VARIANTS
+
 hipError_t ensure_events(fgi_graph* g, size_t n) {
     while (g->ev.size() < n) {
         hipEvent_t e;
@@ -2603,6 +2830,7 @@ hipError_t ensure_events(fgi_graph* g, size_t n) {
 
 }  // namespace
 
+#if FGI_VARIANTS
 // A wave as fused launches (k_wave_fused head, k_collect + k_level mid pairs, k_wave_fused tail; see
 // above): one host synchronisation when the predicted number of mid pairs suffices. Returns
 // FGI_ENOTSUP (nothing launched) if the fused grid cannot be resident on this device.
@@ -2697,7 +2925,7 @@ static fgi_status run_wave_fused(fgi_graph* g, uint32_t n_roots, const uint32_t*
         if (g->want_ids) {
             const auto* inv64 = reinterpret_cast<const unsigned long long*>(g->inv_bm);
             hipLaunchKernelGGL(k_final_write, dim3(a.fin_G), dim3(kBlock), 0, s, inv64, words, a.fin_wpb,
-                               (const unsigned long long*)a.status, g->ctr, g->inv, 1);
+                               (const unsigned long long*)a.status, g->ctr, g->inv, 1, 1u);
         }
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
@@ -2783,6 +3011,8 @@ static fgi_status run_wave_fused(fgi_graph* g, uint32_t n_roots, const uint32_t*
     return FGI_OK;
 }
 
+#endif  // FGI_VARIANTS
+
 // The end of a level group: the counters to the host and the host's wait for them. With
 // FGI_SPIN_WAIT a one-block kernel writes the counters into fine-grained host memory, then (after a
 // system-scope fence) a sequence word the host spins on: the wait ends when that word lands instead of
@@ -2806,21 +3036,45 @@ __global__ __launch_bounds__(256) void k_publish(const unsigned long long* __res
 
 // src[0, words) into the fine-grained host buffer dst (words + 2 long), waiting for the sequence word
 // dst[words]; dst[words + 1] is the publish kernel's start on the device wall clock
-fgi_status publish_wait(fgi_graph* g, hipStream_t s, const unsigned long long* src, uint32_t words, unsigned long long* dst) {
-    const unsigned long long seq = ++g->pub_seq;
-    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, src, words, dst, seq);
-    FGI_HIP(g, hipGetLastError());
-    unsigned long long* word = dst + words;
+// The host's wait for a published sequence word: x86 `pause` while the device works (the common case
+// ends within a wave's few hundred us), a hipStreamQuery every 1,024 pauses so a fault or a lost write
+// still ends the wait, then sched_yield between polls once the wait has lasted ~10 ms (a rank spinning
+// on a peer leaves its core to the collective's proxy threads), and FGI_EDEVICE after
+// FGI_WAIT_TIMEOUT_S (default 300) seconds: a collective whose peer never arrives fails the call
+// instead of spinning forever.
+static fgi_status wait_word(fgi_graph* g, hipStream_t s, const unsigned long long* word, unsigned long long seq) {
+    static const double limit_s = [] {
+        const char* e = getenv("FGI_WAIT_TIMEOUT_S");
+        return e && *e ? atof(e) : 300.0;
+    }();
+    const auto t0 = std::chrono::steady_clock::now();
     for (uint64_t k = 1; __atomic_load_n(word, __ATOMIC_ACQUIRE) != seq; ++k) {
-        __builtin_ia32_pause();
+        if (k < (1u << 15)) {
+            __builtin_ia32_pause();
+        } else {
+            sched_yield();
+        }
         if ((k & 1023) == 0) {
             const hipError_t e = hipStreamQuery(s);
-            if (e == hipErrorNotReady) continue;
+            if (e == hipErrorNotReady) {
+                if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s)
+                    return set_err(g, FGI_EDEVICE, "wait: the device did not publish within %.0f s (a collective's peer missing?)",
+                                   limit_s);
+                continue;
+            }
             if (e != hipSuccess) FGI_HIP(g, e);
             if (__atomic_load_n(word, __ATOMIC_ACQUIRE) != seq)
                 return set_err(g, FGI_EDEVICE, "publish: the stream completed without the sequence word");
         }
     }
+    return FGI_OK;
+}
+
+fgi_status publish_wait(fgi_graph* g, hipStream_t s, const unsigned long long* src, uint32_t words, unsigned long long* dst) {
+    const unsigned long long seq = ++g->pub_seq;
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, src, words, dst, seq);
+    FGI_HIP(g, hipGetLastError());
+    FGI_TRY(wait_word(g, s, dst + words, seq));
     g->last_pub_t = dst[words + 1];
     return FGI_OK;
 }
@@ -2859,7 +3113,7 @@ static fgi_status counters_to_host(fgi_graph* g, hipStream_t s, bool mark) {
 }  // namespace
 
 fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
-                    fgi_wave_stats* stats) {
+                    fgi_wave_stats* stats, bool ext_roots) {
     const auto t0 = std::chrono::steady_clock::now();
     hipStream_t s = g->stream;
     static const bool trace = getenv("FGI_TRACE") != nullptr;
@@ -2877,12 +3131,14 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     static_assert(sizeof(WaveCtr) % 8 == 0, "WaveCtr is cleared as 64-bit words");
     // fused launches when the wave's directions are settled (lists ready, or push only); a wave that
     // may still have to build the dependency lists part-way runs as level groups below
-    if ((g->opt_fused & kFusedOn) && (allow_pull || wp0.direction == 1)) {
+#if FGI_VARIANTS
+    if ((g->opt_fused & kFusedOn) && !g->lbl_K && (allow_pull || wp0.direction == 1)) {   // labels: level groups
         WaveParams wp = wp0;
         if (!allow_pull) wp.direction = 1;
         const fgi_status r = run_wave_fused(g, n_roots, roots_dev, imm_dev, stats, wp, timing, t0);
         if (r != FGI_ENOTSUP) return r;
     }
+#endif
     hipLaunchKernelGGL(k_wave_init, dim3(kInitBlocks), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
                        g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
     g->vis_stale = false;
@@ -2898,18 +3154,28 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     if (events) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
     if (n_roots) {
         g->v_dirty = true;
-        launch_roots(g, n_roots, roots_dev, imm_dev, 0u, g->n_handles, 0);
+        launch_roots(g, n_roots, roots_dev, imm_dev, 0u, g->n_handles, 0, ext_roots);
     }
     const auto* node = reinterpret_cast<const unsigned long long*>(g->node);
     // Levels run in groups between host synchronisations (one ~30 us round trip each); the first
     // group is sized by the previous wave's depth, so a repeated workload syncs once per wave and an
     // overshoot costs only empty levels (two ~2 us launches each). Every group ends with the final
     // collect, so the group that ends the wave needs no further round trip.
-    int group = std::min(8, std::max(2, g->last_levels));
-    int L = 0;
+    // With the tail (k_wave_tail, default on; FGI_TAIL=0 off for measurement) a group launches the
+    // levels up to the previous wave's last pull or large push level and the tail runs the rest.
+    static const uint64_t tail_edges = [] {
+        const char* e = getenv("FGI_TAIL");
+        if (e && e[0] == '0') return 0ull;
+        const char* m = getenv("FGI_TAIL_EDGES");
+        return m && *m ? (unsigned long long)strtoull(m, nullptr, 10) : (unsigned long long)kTailBlocks * kChunk;
+    }();
+    const bool use_tail = tail_edges != 0;
+    int group = use_tail ? std::min(8, std::max(1, g->last_head)) : std::min(8, std::max(2, g->last_levels));
+    int L = 0, head = 1;
     uint64_t levels = 0, e_trav = 0, f_total = 0, pull_levels = 0;
-    double expand_ms = 0, pull_ms = 0;
+    double expand_ms = 0, pull_ms = 0, tail_ms = 0;
     uint64_t expand_launches = 0, expand_edges = 0, expand_f = 0, pull_launches = 0, syncs = 0;
+    uint64_t tail_launches = 0, tail_edges_run = 0, tail_f = 0;
     bool done = (n_roots == 0);
     bool final_done = false;
     while (!done) {
@@ -2934,6 +3200,33 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                                g->done, RemoteArgs{}, ~0ull);
             if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L + 1], s));
         }
+        if (use_tail) {   // the wave's small push levels after the group: one persistent launch
+            TailArgs ta{};
+            ta.L0 = L;
+            ta.wp = wp;
+            for (int b = 0; b < 2; ++b) {
+                ta.col[b] = collect_args(g, g->n_slots, wp, b);
+                ta.x[b] = expand_args(g, b);
+                ta.o[b] = out_for(g, b, nullptr);
+            }
+            ta.node = node;
+            ta.vis = g->vis_bm;
+            ta.ctr = g->ctr;
+            ta.blk = g->blk_stats;
+            ta.gbar = g->gbar + kGbarTail;
+            ta.bar_timeout = kGridBarTimeout;
+            ta.max_edges = tail_edges;
+            if (timing) {
+                while (g->ev.size() < 2 * (size_t)(L + 1) + 4) {
+                    hipEvent_t e;
+                    FGI_HIP(g, hipEventCreateWithFlags(&e, event_flags()));
+                    g->ev.push_back(e);
+                }
+                FGI_HIP(g, hipEventRecord(g->ev[2 * L], s));
+            }
+            hipLaunchKernelGGL(k_wave_tail, dim3(kTailBlocks), dim3(kBlock), 0, s, ta);
+            if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L + 1], s));
+        }
         FGI_HIP(g, launch_final(g, g->n_handles, g->want_ids));   // idempotent: repeated if the wave goes on
         final_done = true;
         FGI_HIP(g, hipGetLastError());
@@ -2941,8 +3234,33 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         // recording it after the wait would cost the call a further device round trip
         FGI_TRY(counters_to_host(g, s, events));
         ++syncs;
+        if (use_tail && g->ctr_host->broken) {   // half a wave is applied: poisoned until fgi_restore (fgi.h)
+            FGI_HIP(g, hipMemsetAsync(g->gbar + kGbarTail, 0, sizeof(unsigned long long), s));
+            FGI_HIP(g, hipStreamSynchronize(s));
+            g->failed = true;
+            return set_err(g, FGI_EDEVICE, "the wave tail's grid barrier timed out (its blocks were not resident together)");
+        }
+        // the tail ran levels [L, stop)
+        const int stop = use_tail ? std::max<int>(L, (int)g->ctr_host->cur) : L;
+        if (use_tail) {
+            float ms = 0;
+            if (timing && hipEventElapsedTime(&ms, g->ev[2 * L], g->ev[2 * L + 1]) == hipSuccess) tail_ms += ms;
+            ++tail_launches;
+            for (int l = L; l < stop; ++l) {
+                const LevelCtr& lc = g->ctr_host->lvl[l % kRing];
+                ++levels;
+                e_trav += lvl_T(lc);
+                f_total += lvl_F(lc);
+                tail_edges_run += lvl_T(lc);
+                tail_f += lvl_F(lc);
+                if (trace)
+                    fprintf(stderr, "[fgi] level %d push (tail): frontier %llu edges %llu chunk x%llu\n", l,
+                            (unsigned long long)lvl_F(lc), (unsigned long long)lvl_T(lc), (unsigned long long)lc.mult);
+            }
+        }
         for (int l = L0; l < L; ++l) {
             const LevelCtr& lc = g->ctr_host->lvl[l % kRing];
+            if (lvl_F(lc) && (lc.pull || lvl_T(lc) > tail_edges)) head = l + 1;
             float ms = 0;
             if (timing) {
                 // every k_level launch counts (empty levels too), so the average launch duration
@@ -2976,6 +3294,9 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
 #if FGI_PROBE
         if (trace) print_probe(g, L0, L);
 #endif
+        if (use_tail && trace && stop > L)
+            fprintf(stderr, "[fgi] tail: levels %d..%d in one launch\n", L, stop - 1);
+        L = stop;
         done = lvl_F(g->ctr_host->lvl[L % kRing]) == 0;
         group = 4;
         // also when the wave is already done (its level groups are sized from the previous wave's
@@ -3000,7 +3321,10 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     // entries this wave made stale: the invalidated nodes' rows and the matched entries pointing at
     // them (fgi_prune_step's trigger)
     g->stale_est += e_trav + g->ctr_host->e_match;
-    if (n_roots) g->last_levels = (int)std::max<uint64_t>(levels, 1);
+    if (n_roots) {
+        g->last_levels = (int)std::max<uint64_t>(levels, 1);
+        g->last_head = head;
+    }
     const WaveCtr& c = *g->ctr_host;
     if (trace)
         fprintf(stderr,
@@ -3022,7 +3346,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         // node-word gather 8; per frontier entry: fr_off 4 + escan 8 read, fr_off 4 + fr_len 4 +
         // escan 8 written by the producer, its row length and offset 12 gathered. Final collect:
         // 4 B per invalidated node. Per root 5.
-        const uint64_t push_b = 20 * expand_edges + 40 * expand_f;
+        const uint64_t push_b = 20 * (expand_edges + tail_edges_run) + 40 * (expand_f + tail_f);
         const uint64_t pull_b = pull_level_bytes(c);
         stats->alg_bytes += push_b + pull_b + 4 * v + 5ull * n_roots;
         float wave_ms = 0;
@@ -3036,6 +3360,9 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         stats->pull_ms += pull_ms;
         stats->expand_launches += expand_launches;
         stats->expand_bytes += 20 * expand_edges + 40 * expand_f;
+        stats->fused_launches += tail_launches;
+        stats->fused_ms += tail_ms;
+        stats->fused_push_bytes += 20 * tail_edges_run + 40 * tail_f;
         stats->pull_bytes += pull_b;
         stats->pull_launches += pull_launches;
         stats->f_total += f_total;

@@ -48,7 +48,7 @@ class FgiError(RuntimeError):
 class Config(C.Structure):
     _fields_ = [("struct_size", C.c_uint32), ("device", C.c_int32), ("n_slots", C.c_uint32),
                 ("n_detached", C.c_uint32), ("edge_capacity", C.c_uint64), ("rank", C.c_int32),
-                ("world", C.c_int32)]
+                ("world", C.c_int32), ("labels", C.c_int32), ("reserved", C.c_int32)]
 
 
 class WaveStats(C.Structure):
@@ -247,9 +247,10 @@ class Graph:
     """One engine instance (one ComputedRegistry worth of nodes) on one device."""
 
     def __init__(self, n_slots: int, n_detached: int = 0, edge_capacity: int = 0, device: int = 0,
-                 rank: int = 0, world: int = 1):
+                 rank: int = 0, world: int = 1, labels: int = 0):
+        """labels: internal hub-first labels (fgi_config.labels): 0 auto, 1 always, -1 never."""
         self.lib = load_library()
-        cfg = Config(C.sizeof(Config), device, n_slots, n_detached, edge_capacity, rank, world)
+        cfg = Config(C.sizeof(Config), device, n_slots, n_detached, edge_capacity, rank, world, labels, 0)
         h = C.c_void_p()
         st = self.lib.fgi_create(C.byref(cfg), C.byref(h))
         if st != OK:

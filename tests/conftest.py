@@ -34,3 +34,21 @@ def gpu_available():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return True
+
+
+@pytest.fixture(scope="session")
+def variants(pkg, gpu_available):
+    """The measurement variants (fused waves, probe summary) are in libfgi_variants.so only
+    (make -C stl.fusion_amd/csrc variant-all; FGI_LIBRARY selects it): skip their tests otherwise."""
+    g = pkg.Graph(64)
+    try:
+        g.set_option(pkg.fgi.OPT_FUSED, 0)
+        try:
+            g.set_option(pkg.fgi.OPT_FUSED, 1)
+        except pkg.FgiError as e:
+            if e.status == pkg.fgi.ENOTSUP:
+                pytest.skip("measurement variant: run with FGI_LIBRARY=stl.fusion_amd/lib/libfgi_variants.so")
+            raise
+    finally:
+        g.close()
+    return True

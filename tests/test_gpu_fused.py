@@ -22,7 +22,7 @@ import fgo as O
 from harness import assert_states_equal, build_pair, random_states
 from test_gpu_parity import _edges_from_live
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("variants")]
 
 MODES = [0, 1, 1 | 2, 1 | 4, 1 | 8, 1 | 2 | 4]
 

@@ -9,7 +9,7 @@ import pytest
 
 import fgo as O
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.usefixtures("variants")]
 
 
 def _pair(pkg, scale, ef, seed, stale, sseed=0x5EED00C0):
