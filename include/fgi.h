@@ -216,6 +216,23 @@ fgi_status fgi_invalidate_dev(fgi_graph* g, uint32_t n_roots, const uint32_t* ro
  * stays available through fgi_last_wave_ids / fgi_wave_ids_dev (made on demand). out_bits may be NULL. */
 fgi_status fgi_invalidate_bits(fgi_graph* g, uint32_t n_roots, const uint32_t* roots, const uint8_t* immediately,
                                uint64_t* out_bits, uint64_t words, uint64_t* out_n, fgi_wave_stats* stats);
+/* Asynchronous waves (ComputedExt.WhenInvalidated, ComputedExt.cs:99-125, which the RPC server awaits
+ * at Client/Internal/RpcInboundComputeCall.cs:53): fgi_invalidate_async queues the wave
+ * fgi_invalidate_dev would run (device-resident roots, boundary handles) on the graph's stream and
+ * returns without waiting; *ticket names it (1, 2, ...). At most two waves are in flight: a third call
+ * first waits for the oldest. The next call's host work (fgi_restore, root uploads, its launches)
+ * overlaps the device's previous wave. fgi_wave_wait waits for the ticket's wave (and every earlier
+ * one) and returns its V_inv, its statistics and a device pointer to its invalidated ids (ascending;
+ * valid until the wave two tickets later is queued, or any synchronous wave runs); waiting again for a
+ * completed ticket returns its results again until the wave two tickets later is queued (FGI_EINVAL
+ * after that). Every other entry point except fgi_restore and
+ * fgi_set_option first waits for the waves in flight. A wave queued this way runs all its levels in
+ * one queue (no second level group): its later pull levels, if the previous wave's shape predicted
+ * fewer, run as push levels — same result, slower. */
+fgi_status fgi_invalidate_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
+                                uint64_t* ticket);
+fgi_status fgi_wave_wait(fgi_graph* g, uint64_t ticket, uint64_t* out_n, const uint32_t** ids_dev,
+                         fgi_wave_stats* stats);
 /* Page-locked host memory for the calls' host arrays (roots in, ids / bitmaps out): copies from and
  * to it run at full PCIe rate without a staging copy (SURVEY.md §8(b) "Ownership"). */
 fgi_status fgi_alloc_pinned(uint64_t bytes, void** out);

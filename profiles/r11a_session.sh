@@ -5,7 +5,7 @@
 set -u
 out=gpurun_out/r11a; mkdir -p $out
 T="timeout -k 10"
-$T 300 python -u -m pytest tests/test_gpu_labels.py -x -v --timeout 120 --timeout-method thread > $out/labels_tests.log 2>&1 || { echo "labels tests rc=$?"; tail -30 $out/labels_tests.log; exit 1; }
+$T 300 python -u -m pytest tests/test_gpu_labels.py tests/test_gpu_async.py tests/test_gpu_part_host.py -x -v --timeout 120 --timeout-method thread > $out/labels_tests.log 2>&1 || { echo "labels tests rc=$?"; tail -30 $out/labels_tests.log; exit 1; }
 tail -2 $out/labels_tests.log
 $T 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $out/gpu_tests.log 2>&1 || { echo "gpu tests rc=$?"; tail -30 $out/gpu_tests.log; exit 1; }
 tail -2 $out/gpu_tests.log

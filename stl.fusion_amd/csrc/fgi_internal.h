@@ -372,6 +372,24 @@ struct fgi_graph {
     uint8_t* imm_buf = nullptr;
     uint64_t roots_cap = 0;
     uint64_t last_wave_n = 0;
+    // asynchronous waves (fgi_invalidate_async / fgi_wave_wait): at most two in flight (tickets t and
+    // t + 1), each with its own published counters (apub[t % 2]) and id buffer (inv for even tickets,
+    // inv_alt for odd ones); inv_cur is the id list of the last wave a caller waited for
+    struct AsyncWave {
+        uint64_t ticket = 0, seq = 0;
+        uint64_t n_inv = 0;            // V_inv, once waited for
+        uint32_t n_roots = 0;
+        bool busy = false, imm = false, timing = false;
+        int group = 0;
+        std::chrono::steady_clock::time_point t0;
+    };
+    AsyncWave aw[2];
+    unsigned long long* apub[2] = {nullptr, nullptr};
+    uint64_t apub_seq = 0;
+    uint64_t next_ticket = 1;
+    uint32_t* inv_alt = nullptr;
+    uint32_t* inv_cur = nullptr;
+    bool lists_wanted = false;         // a wave met a frontier heavy enough to pull (async waves build lists first)
     bool want_ids = true;              // run_wave writes the invalidated list (false: bitmap and count only)
     bool ids_valid = false;            // inv holds the last wave's list (else ensure_ids rebuilds it)
     int last_levels = 4;               // non-empty levels of the last wave (sizes the first level group)
@@ -609,6 +627,13 @@ void print_coop_probe();
 fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev, const uint8_t* imm_dev,
                          const unsigned long long* n_dev, uint32_t* out, unsigned long long* out_n,
                          unsigned long long* acc, unsigned long long* abort);
+// Asynchronous waves (wave.hip): queue a wave and return (ticket), wait for one (and every earlier
+// one), wait for all in flight. Every entry point but fgi_restore, fgi_set_option and the async calls
+// themselves drains first (usable()).
+fgi_status run_wave_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
+                          uint64_t* ticket);
+fgi_status wave_wait(fgi_graph* g, uint64_t ticket, uint64_t* out_n, const uint32_t** ids_dev, fgi_wave_stats* stats);
+fgi_status drain_async(fgi_graph* g);
 // Rebuild the expandable-class bitmap if node words changed (wave.hip).
 fgi_status ensure_cls(fgi_graph* g);
 // Pull tiles of a level over n slots with `grid` blocks.

@@ -1830,10 +1830,20 @@ static fgi_status label_of(fgi_graph* g, uint32_t x, uint32_t* out) {
     return FGI_OK;
 }
 
-static fgi_status usable(fgi_graph* g) {
+static fgi_status usable_now(fgi_graph* g) {
     return g->failed ? set_err(g, FGI_ESTATE, "a streaming batch failed on the device (%s); fgi_restore or fgi_destroy",
                                "grid barrier timeout")
                      : FGI_OK;
+}
+// every call but fgi_restore, fgi_set_option and the asynchronous wave calls first waits for the
+// asynchronous waves in flight (their results are the graph's state the call sees)
+static fgi_status usable(fgi_graph* g) {
+    FGI_TRY(usable_now(g));
+    if (g->aw[0].busy || g->aw[1].busy) {
+        hipSetDevice(g->device);
+        FGI_TRY(drain_async(g));
+    }
+    return FGI_OK;
 }
 
 extern "C" {
@@ -1937,6 +1947,9 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->pool_tag);
     dfree(g->pool_top_dev);
     dfree(g->inv);
+    dfree(g->inv_alt);
+    for (int k = 0; k < 2; ++k)
+        if (g->apub[k]) hipHostFree(g->apub[k]);
     for (int i = 0; i < 2; ++i) {
         dfree(g->fr_off[i]);
         dfree(g->fr_len[i]);
@@ -2440,7 +2453,7 @@ static fgi_status copy_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, uint64
     if (!out_ids) return FGI_OK;
     if (n > cap) return FGI_ECAPACITY;
     FGI_TRY(ensure_ids(g));
-    return d2h(g, out_ids, g->inv, n);
+    return d2h(g, out_ids, g->inv_cur ? g->inv_cur : g->inv, n);
 }
 
 fgi_status fgi_invalidate(fgi_graph* g, uint32_t n_roots, const uint32_t* roots, const uint8_t* immediately,
@@ -2494,6 +2507,22 @@ fgi_status fgi_invalidate_bits(fgi_graph* g, uint32_t n_roots, const uint32_t* r
                need);
 }
 
+fgi_status fgi_invalidate_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
+                                uint64_t* ticket) {
+    if (!g || (n_roots && !roots_dev) || !ticket) return FGI_EINVAL;
+    FGI_TRY(usable_now(g));
+    if (g->part) return set_err(g, FGI_ESTATE, "fgi_invalidate_async: partitioned graph, use fgi_part_invalidate");
+    hipSetDevice(g->device);
+    return run_wave_async(g, n_roots, roots_dev, imm_dev, ticket);
+}
+
+fgi_status fgi_wave_wait(fgi_graph* g, uint64_t ticket, uint64_t* out_n, const uint32_t** ids_dev, fgi_wave_stats* stats) {
+    if (!g) return FGI_EINVAL;
+    FGI_TRY(usable_now(g));
+    hipSetDevice(g->device);
+    return wave_wait(g, ticket, out_n, ids_dev, stats);
+}
+
 fgi_status fgi_alloc_pinned(uint64_t bytes, void** out) {
     if (!out) return FGI_EINVAL;
     *out = nullptr;
@@ -2511,7 +2540,7 @@ fgi_status fgi_wave_ids_dev(fgi_graph* g, const uint32_t** ids_dev, uint64_t* n)
     FGI_TRY(usable(g));
     hipSetDevice(g->device);
     if (!g->part) FGI_TRY(ensure_ids(g));
-    *ids_dev = g->inv;
+    *ids_dev = (!g->part && g->inv_cur) ? g->inv_cur : g->inv;
     if (n) *n = g->last_wave_n;
     return FGI_OK;
 }

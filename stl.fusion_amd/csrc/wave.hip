@@ -2128,6 +2128,7 @@ struct TailArgs {
     unsigned long long* gbar;
     uint64_t bar_timeout;
     uint64_t max_edges;                // a level with more edges is left to the host's next group
+    int all;                           // run every remaining level (asynchronous waves: no second group)
 };
 
 __global__ __launch_bounds__(kBlock) void k_wave_tail(TailArgs a) {
@@ -2146,7 +2147,7 @@ __global__ __launch_bounds__(kBlock) void k_wave_tail(TailArgs a) {
         if (threadIdx.x == 0) s_ft = coh_read(&lc.ft);   // a push producer's packed counter (or the pull's F / T)
         __syncthreads();
         const uint64_t F = lc.F ? lc.F : (s_ft >> 32), T = lc.F ? lc.T : (s_ft & 0xFFFFFFFFull);
-        if (F == 0 || level_pulls(ctr, L, a.wp, F, T) || T > a.max_edges) break;
+        if (F == 0 || (!a.all && (level_pulls(ctr, L, a.wp, F, T) || T > a.max_edges))) break;
         if (first && L > 0 && ctr->lvl[(L + kRing - 1) % kRing].pull) {   // after a pull level: its frontier list
             collect_front(lc, a.wp.grid, a.col[L & 1], (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6),
                           (uint64_t)gridDim.x * (blockDim.x >> 6));
@@ -2564,7 +2565,8 @@ ExpandArgs expand_args(fgi_graph* g, int buf) {
 }
 
 // the invalidated bitmap -> V_inv (ctr->inv) and, with ids, the invalidated list
-hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true) {
+hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true, uint32_t* out = nullptr) {
+    if (!out) out = g->inv;
     const auto* inv64 = reinterpret_cast<const unsigned long long*>(g->inv_bm);
     const FoldArgs f = fold_args(g);
     if (f.xbm) {   // hot labels: one fold tile per counting block, the list from the folded bitmap
@@ -2577,7 +2579,7 @@ hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true) {
             const uint32_t G = std::min<uint32_t>(kFinalBlocks, tiles), spb = (tiles + G - 1) / G;
             const uint32_t G2 = (tiles + spb - 1) / spb;
             hipLaunchKernelGGL(k_final_write, dim3(G2), dim3(kBlock), 0, g->stream, (const unsigned long long*)g->xbm, words,
-                               (uint64_t)spb * kFoldWords, (const unsigned long long*)st, g->ctr, g->inv, 0, spb);
+                               (uint64_t)spb * kFoldWords, (const unsigned long long*)st, g->ctr, out, 0, spb);
         }
         return hipGetLastError();
     }
@@ -2590,8 +2592,27 @@ hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true) {
                        (const unsigned long long*)g->blk_stats, ids ? 0 : 1, g->done, FoldArgs{});
     if (ids)
         hipLaunchKernelGGL(k_final_write, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb,
-                           (const unsigned long long*)st, g->ctr, g->inv, 0, 1u);
+                           (const unsigned long long*)st, g->ctr, out, 0, 1u);
     return hipGetLastError();
+}
+
+TailArgs tail_args(fgi_graph* g, int L0, const WaveParams& wp, uint64_t max_edges) {
+    TailArgs ta{};
+    ta.L0 = L0;
+    ta.wp = wp;
+    for (int b = 0; b < 2; ++b) {
+        ta.col[b] = collect_args(g, g->n_slots, wp, b);
+        ta.x[b] = expand_args(g, b);
+        ta.o[b] = out_for(g, b, nullptr);
+    }
+    ta.node = reinterpret_cast<const unsigned long long*>(g->node);
+    ta.vis = g->vis_bm;
+    ta.ctr = g->ctr;
+    ta.blk = g->blk_stats;
+    ta.gbar = g->gbar + kGbarTail;
+    ta.bar_timeout = kGridBarTimeout;
+    ta.max_edges = max_edges;
+    return ta;
 }
 
 #ifndef FGI_ROOT_BLOCK
@@ -3201,21 +3222,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
             if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L + 1], s));
         }
         if (use_tail) {   // the wave's small push levels after the group: one persistent launch
-            TailArgs ta{};
-            ta.L0 = L;
-            ta.wp = wp;
-            for (int b = 0; b < 2; ++b) {
-                ta.col[b] = collect_args(g, g->n_slots, wp, b);
-                ta.x[b] = expand_args(g, b);
-                ta.o[b] = out_for(g, b, nullptr);
-            }
-            ta.node = node;
-            ta.vis = g->vis_bm;
-            ta.ctr = g->ctr;
-            ta.blk = g->blk_stats;
-            ta.gbar = g->gbar + kGbarTail;
-            ta.bar_timeout = kGridBarTimeout;
-            ta.max_edges = tail_edges;
+            const TailArgs ta = tail_args(g, L, wp, tail_edges);
             if (timing) {
                 while (g->ev.size() < 2 * (size_t)(L + 1) + 4) {
                     hipEvent_t e;
@@ -3305,6 +3312,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
             bool heavy = false;
             for (int l = L0; l <= L; ++l) heavy |= lvl_T(g->ctr_host->lvl[l % kRing]) > wp.pull_threshold;
             if (heavy) {
+                g->lists_wanted = true;
                 FGI_TRY(ensure_in_lists(g));
                 allow_pull = pull_ready(g, wp0);
             }
@@ -3318,6 +3326,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     if (imm_dev && n_roots) note_words(g);   // immediate roots changed node words
     g->last_wave_n = g->ctr_host->inv;
     g->ids_valid = g->want_ids;
+    g->inv_cur = g->inv;
     // entries this wave made stale: the invalidated nodes' rows and the matched entries pointing at
     // them (fgi_prune_step's trigger)
     g->stale_est += e_trav + g->ctr_host->e_match;
@@ -3372,10 +3381,164 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     return FGI_OK;
 }
 
+// ---- asynchronous waves -------------------------------------------------------------------------------
+// fgi_invalidate_async queues one whole wave — init, roots, a level group sized by the previous wave
+// (its pull levels and large push levels), the tail with every remaining level (all = 1: no level is
+// left to a second group, so the wave is complete in its queue), the final collect into the ticket's
+// id buffer and a publish of the counters into the ticket's host buffer — and returns. A wave whose
+// pull levels outnumber the group runs its later pull levels as push levels inside the tail: the
+// result is the same, only slower, and the next wave's group is sized from this one. The next call's
+// host work (restore, root upload, the launches) thus overlaps the device's previous wave
+// (ComputedExt.WhenInvalidated: the caller awaits the wave instead of blocking on it).
+fgi_status run_wave_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
+                          uint64_t* ticket) {
+    const uint64_t t = g->next_ticket;
+    fgi_graph::AsyncWave& a = g->aw[t & 1];
+    if (a.busy) FGI_TRY(wave_wait(g, a.ticket, nullptr, nullptr, nullptr));   // at most two in flight
+    const auto t0 = std::chrono::steady_clock::now();
+    hipStream_t s = g->stream;
+    if (!g->apub[0]) {
+        for (int k = 0; k < 2; ++k)
+            if (hipHostMalloc(reinterpret_cast<void**>(&g->apub[k]), sizeof(WaveCtr) + 128, hipHostMallocCoherent) != hipSuccess)
+                return set_err(g, FGI_ENOMEM, "async wave: published counters");
+        for (int k = 0; k < 2; ++k) memset(g->apub[k], 0, sizeof(WaveCtr) + 128);
+    }
+    if (!g->inv_alt) FGI_HIP(g, hipMalloc(reinterpret_cast<void**>(&g->inv_alt), (size_t)g->n_handles * 4));
+    FGI_TRY(ensure_cstart(g, g->pool_top));
+    FGI_TRY(ensure_cls(g));
+    const WaveParams wp0 = wave_params(g, 0, g->opt_direction, g->pool_top, g->n_slots);
+    // the dependency lists a pull level needs are built here, before anything is queued, once a wave
+    // has shown a frontier heavy enough to pull (as run_wave builds them after such a group)
+    if (n_roots && wp0.direction != 1 && (g->lists_wanted || wp0.direction == 2)) FGI_TRY(ensure_in_lists(g));
+    WaveParams wp = wp0;
+    if (!(wp0.direction != 1 && pull_ready(g, wp0))) wp.direction = 1;
+    hipLaunchKernelGGL(k_wave_init, dim3(kInitBlocks), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
+                       g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
+    g->vis_stale = false;
+    g->coop_clean = false;
+    const auto* node = reinterpret_cast<const unsigned long long*>(g->node);
+    int group = std::min(8, std::max(1, g->last_head));
+    if (n_roots) {
+        g->v_dirty = true;
+        launch_roots(g, n_roots, roots_dev, imm_dev, 0u, g->n_handles, 0, true);
+        for (int L = 0; L < group; ++L) {
+            const int buf = L & 1;
+            hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp,
+                               collect_args(g, g->n_slots, wp, buf), collect_args(g, g->n_slots, wp, buf), ~0ull);
+            hipLaunchKernelGGL(k_level<false>, dim3(wp.grid), dim3(kBlock), 0, s, L, wp, expand_args(g, buf),
+                               expand_args(g, buf), pull_args(g, g->n_slots, g->inv_bm), node, g->vis_bm,
+                               out_for(g, buf ^ 1, nullptr), out_for(g, buf ^ 1, nullptr), g->ctr, g->blk_stats,
+                               g->done, RemoteArgs{}, ~0ull);
+        }
+        TailArgs ta = tail_args(g, group, wp, ~0ull);
+        ta.all = 1;
+        hipLaunchKernelGGL(k_wave_tail, dim3(kTailBlocks), dim3(kBlock), 0, s, ta);
+    } else {
+        group = 0;
+    }
+    uint32_t* out = (t & 1) ? g->inv_alt : g->inv;
+    FGI_HIP(g, launch_final(g, g->n_handles, true, out));
+    const unsigned long long seq = ++g->apub_seq;
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, reinterpret_cast<const unsigned long long*>(g->ctr),
+                       (uint32_t)kPubWords, g->apub[t & 1], seq);
+    FGI_HIP(g, hipGetLastError());
+    if (imm_dev && n_roots) note_words(g);   // immediate roots change node words (fgi_restore copies them back)
+    a.ticket = t;
+    a.seq = seq;
+    a.n_roots = n_roots;
+    a.imm = imm_dev != nullptr;
+    a.group = group;
+    a.t0 = t0;
+    a.busy = true;
+    g->ids_valid = false;
+    g->next_ticket = t + 1;
+    if (ticket) *ticket = t;
+    return FGI_OK;
+}
+
+fgi_status wave_wait(fgi_graph* g, uint64_t ticket, uint64_t* out_n, const uint32_t** ids_dev, fgi_wave_stats* stats) {
+    if (ticket == 0 || ticket >= g->next_ticket) return set_err(g, FGI_EINVAL, "no wave with ticket %llu", (unsigned long long)ticket);
+    // the older one first: waves complete in ticket order
+    fgi_graph::AsyncWave& o = g->aw[(ticket + 1) & 1];
+    if (o.busy && o.ticket < ticket) FGI_TRY(wave_wait(g, o.ticket, nullptr, nullptr, nullptr));
+    fgi_graph::AsyncWave& a = g->aw[ticket & 1];
+    if (!a.busy || a.ticket != ticket) {   // already waited for: its count, its buffer (if still its own)
+        if (a.ticket != ticket)
+            return set_err(g, FGI_EINVAL, "the results of wave %llu are gone (a later wave took its buffers)",
+                           (unsigned long long)ticket);
+        if (out_n) *out_n = a.n_inv;
+        if (ids_dev) *ids_dev = (ticket & 1) ? g->inv_alt : g->inv;
+        return FGI_OK;
+    }
+    unsigned long long* pub = g->apub[ticket & 1];
+    const fgi_status ws = wait_word(g, g->stream, pub + kPubWords, a.seq);
+    a.busy = false;
+    FGI_TRY(ws);
+    const WaveCtr& c = *reinterpret_cast<const WaveCtr*>(pub);
+    uint64_t levels = 0, e_trav = 0, f_total = 0, pull_levels = 0, push_e = 0, push_f = 0, head = 1;
+    const uint64_t stop = a.group ? std::max<uint64_t>((uint64_t)a.group, c.cur) : 0;
+    for (uint64_t l = 0; l < stop; ++l) {
+        const LevelCtr& lc = c.lvl[l % kRing];
+        const uint64_t F = lvl_F(lc), T = lvl_T(lc);
+        if (!F) continue;
+        ++levels;
+        e_trav += T;
+        f_total += F;
+        if (lc.pull) {
+            ++pull_levels;
+        } else {
+            push_e += T;
+            push_f += F;
+        }
+        if (l < (uint64_t)a.group && (lc.pull || T > (uint64_t)kTailBlocks * kChunk)) head = l + 1;
+    }
+    a.n_inv = c.inv;
+    g->last_wave_n = c.inv;
+    g->inv_cur = (ticket & 1) ? g->inv_alt : g->inv;
+    g->ids_valid = true;
+    g->stale_est += e_trav + c.e_match;
+    if (a.n_roots) {
+        g->last_levels = (int)std::max<uint64_t>(levels, 1);
+        g->last_head = (int)head;
+        for (uint64_t l = 0; l < stop && !g->lists_wanted; ++l)
+            if (lvl_T(c.lvl[l % kRing]) > (g->pool_top / (uint64_t)std::max(1, g->opt_pull_alpha))) g->lists_wanted = true;
+    }
+    if (out_n) *out_n = c.inv;
+    if (ids_dev) *ids_dev = g->inv_cur;
+    if (stats) {
+        stats->roots += a.n_roots;
+        stats->levels += levels;
+        stats->v_inv += c.inv;
+        stats->e_trav += e_trav;
+        stats->e_match += c.e_match;
+        stats->n_flagged += c.n_flagged;
+        stats->pull_levels += pull_levels;
+        stats->pull_edges += c.pull_edges;
+        stats->alg_bytes += 20 * push_e + 40 * push_f + pull_level_bytes(c) + 4 * c.inv + 5ull * a.n_roots;
+        stats->kernel_ms += wall_ms(g, c.t0, pub[kPubWords + 1]);
+        stats->f_total += f_total;
+        stats->host_syncs += 1;
+        stats->total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a.t0).count();
+    }
+    return FGI_OK;
+}
+
+fgi_status drain_async(fgi_graph* g) {
+    for (int k = 0; k < 2; ++k) {
+        fgi_graph::AsyncWave& x = g->aw[k];
+        fgi_graph::AsyncWave& y = g->aw[k ^ 1];
+        if (x.busy && (!y.busy || x.ticket < y.ticket)) FGI_TRY(wave_wait(g, x.ticket, nullptr, nullptr, nullptr));
+    }
+    for (int k = 0; k < 2; ++k)
+        if (g->aw[k].busy) FGI_TRY(wave_wait(g, g->aw[k].ticket, nullptr, nullptr, nullptr));
+    return FGI_OK;
+}
+
 fgi_status ensure_ids(fgi_graph* g) {
     if (g->ids_valid) return FGI_OK;
     // the bitmap of the last wave is intact until the next wave starts: list it now
-    FGI_HIP(g, launch_final(g, g->n_handles, true));
+    if (!g->inv_cur) g->inv_cur = g->inv;
+    FGI_HIP(g, launch_final(g, g->n_handles, true, g->inv_cur));
     FGI_HIP(g, hipStreamSynchronize(g->stream));
     g->ids_valid = true;
     return FGI_OK;

@@ -151,6 +151,8 @@ SIGNATURES = {
     "fgi_part_run_batch": [_G, C.c_uint32, C.POINTER(Step), _u32p, C.c_uint64, _u64p, C.POINTER(BatchStats)],
     "fgi_part_prune": [_G, C.POINTER(PruneStats)],
     "fgi_part_init_host": [_G, C.c_uint32, C.c_void_p, C.c_void_p],
+    "fgi_invalidate_async": [_G, C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)],
+    "fgi_wave_wait": [_G, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(WaveStats)],
     "fgi_part_local_run_batch": [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32, C.POINTER(Step), _u32p, C.c_uint64,
                                  _u64p, C.POINTER(BatchStats)],
     "fgi_part_local_prune": [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(PruneStats)],
@@ -441,6 +443,22 @@ class Graph:
                                                 C.c_void_p(imm_ptr) if imm_ptr else None, None, C.byref(n),
                                                 C.byref(stats) if stats is not None else None), "invalidate_dev")
         return n.value
+
+    def invalidate_async(self, n_roots: int, roots_ptr: int, imm_ptr: int = 0) -> int:
+        """fgi_invalidate_async: queue a wave from device-resident roots; returns its ticket."""
+        t = C.c_uint64()
+        self._check(self.lib.fgi_invalidate_async(self.h, n_roots, C.c_void_p(roots_ptr),
+                                                  C.c_void_p(imm_ptr) if imm_ptr else None, C.byref(t)),
+                    "invalidate_async")
+        return t.value
+
+    def wave_wait(self, ticket: int, stats: Optional[WaveStats] = None) -> Tuple[int, int]:
+        """fgi_wave_wait: (V_inv, device pointer to the wave's ids) of the ticket's wave."""
+        n = C.c_uint64()
+        p = C.c_void_p()
+        self._check(self.lib.fgi_wave_wait(self.h, ticket, C.byref(n), C.byref(p),
+                                           C.byref(stats) if stats is not None else None), "wave_wait")
+        return n.value, p.value or 0
 
     def last_wave_ids(self) -> np.ndarray:
         """Handles invalidated by the last wave (e.g. begin_compute's displacement cascade)."""

@@ -1,0 +1,123 @@
+"""Asynchronous waves (fgi_invalidate_async / fgi_wave_wait; ComputedExt.WhenInvalidated,
+/root/reference/src/Stl.Fusion/ComputedExt.cs:99-125, awaited at Client/Internal/RpcInboundComputeCall.cs:53).
+
+Waves are pipelined the way bench.py's pipelined leg runs them — the next wave queued before the
+previous one is waited for, with fgi_restore between them — and every wave's invalidated ids (read
+from its own device buffer while the next wave runs) and V_inv are checked against the oracle
+(Computed.cs:162-230). Also: waves on an evolving graph (no restore, each wave sees the previous one's
+effects), a synchronous call after queued waves (it waits for them first), immediate roots, and
+labelled graphs (their ids fold back to slot order in each ticket's buffer)."""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+import fgo as O
+from harness import assert_states_equal
+
+pytestmark = pytest.mark.gpu
+
+_hip = None
+
+
+def _d2h(ptr, n):
+    """n uint32 from device memory (a completed wave's id buffer; another wave may still be running)."""
+    global _hip
+    if _hip is None:
+        _hip = ctypes.CDLL("libamdhip64.so")
+        _hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    out = np.zeros(n, np.uint32)
+    if n:
+        assert _hip.hipMemcpy(out.ctypes.data, ctypes.c_void_p(ptr), 4 * n, 2) == 0   # hipMemcpyDeviceToHost
+    return out
+
+
+def _pair(pkg, scale, ef, seed, labels):
+    n = 1 << scale
+    g = pkg.Graph(n, labels=labels)
+    g.synth_rmat(scale, ef, seed)
+    s, d = O.gen_rmat(scale, ef, seed)
+    o = O.Oracle(n)
+    o.load_graph(O.version_of(seed, np.arange(n)), None, s, d, O.gen_tags(s, d, seed))
+    return g, o, np.bincount(s, minlength=n)
+
+
+@pytest.mark.parametrize("labels", [-1, 1])
+def test_pipelined_waves_with_restore(pkg, gpu_available, labels):
+    scale, ef, seed = 16, 16, 0x5EED0024
+    n = 1 << scale
+    g, o, deg = _pair(pkg, scale, ef, seed, labels)
+    g.snapshot()
+    o.snapshot()
+    sets = [O.gen_roots(k, n, 0x5EED1024 + k, deg) for k in (256, 16, 1024)]
+    want = []
+    for r in sets:
+        o.restore()
+        o.clear_log()
+        o.invalidate_slots(r)
+        want.append(np.sort(o.inv_log()))
+    d_sets = [torch.from_numpy(r.astype(np.int32)).cuda() for r in sets]
+    torch.cuda.synchronize()
+    prev = None
+    seen = 0
+    for k in range(9):
+        g.restore()
+        t = g.invalidate_async(len(sets[k % 3]), d_sets[k % 3].data_ptr())
+        assert t == k + 1
+        if prev is not None:
+            st = pkg.WaveStats()
+            nv, ptr = g.wave_wait(prev, st)
+            w = want[(prev - 1) % 3]
+            assert nv == len(w) == st.v_inv, (prev, nv, len(w))
+            assert np.array_equal(_d2h(ptr, nv), w), prev
+            seen += 1
+        prev = t
+    nv, ptr = g.wave_wait(prev)
+    assert np.array_equal(_d2h(ptr, nv), want[(prev - 1) % 3])
+    assert seen == 8
+    # waiting again for a completed ticket returns its results again
+    assert g.wave_wait(prev)[0] == nv
+    g.close()
+    o.close()
+
+
+def test_async_waves_on_an_evolving_graph(pkg, gpu_available):
+    """No restore: each wave runs on the state the previous ones left (the queue keeps their order);
+    immediate roots; a synchronous wave and a state query after queued waves wait for them first."""
+    scale, ef, seed = 15, 8, 0x5EED0027
+    n = 1 << scale
+    g, o, deg = _pair(pkg, scale, ef, seed, 1)
+    tickets, want = [], []
+    rng = np.random.default_rng(3)
+    d_keep = []
+    for k in range(4):
+        r = O.gen_roots(8 + 8 * k, n, 77 + k, deg)
+        imm = (rng.random(len(r)) < 0.3).astype(np.uint8)
+        o.clear_log()
+        st = o.invalidate_slots(r, imm)
+        want.append((np.sort(o.inv_log()), st.v_inv))
+        dr, di = torch.from_numpy(r.astype(np.int32)).cuda(), torch.from_numpy(imm).cuda()
+        d_keep += [dr, di]
+        torch.cuda.synchronize()
+        tickets.append(g.invalidate_async(len(r), dr.data_ptr(), di.data_ptr()))
+    for t, (w, v) in zip(tickets[:2], want[:2]):
+        nv, ptr = g.wave_wait(t)
+        assert nv == v and np.array_equal(_d2h(ptr, nv), w), t
+    # two waves still in flight: the state query waits for them
+    assert_states_equal(g, o, n)
+    nv, ptr = g.wave_wait(tickets[3])
+    assert nv == want[3][1]
+    r = O.gen_roots(64, n, 999, deg)
+    o.clear_log()
+    o.invalidate_slots(r)
+    t = g.invalidate_async(len(r), torch.from_numpy(r.astype(np.int32)).cuda().data_ptr())
+    ids = g.invalidate(O.gen_roots(4, n, 5, deg))   # synchronous: waits for ticket t first
+    o_ids = np.sort(o.inv_log())
+    o.clear_log()
+    o.invalidate_slots(O.gen_roots(4, n, 5, deg))
+    assert np.array_equal(ids, np.sort(o.inv_log()))
+    assert g.wave_wait(t)[0] == len(o_ids)
+    assert_states_equal(g, o, n)
+    g.close()
+    o.close()
