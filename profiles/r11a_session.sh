@@ -17,11 +17,12 @@ bench() {  # tag config setting
   env "${envs[@]}" $T 240 python bench.py --no-cpu --no-e2e --steps 30 --warmup 5 --config $cfg > $out/$tag.json 2> $out/$tag.err || { echo "bench rc=$?"; tail -5 $out/$tag.err; exit 1; }
   python -c "
 import json; d = json.load(open('$out/$tag.json')); r = d['roofline']
-print('$cfg', '$setting', round(d['ms_per_step'], 4), 'pull', round(r['pull_levels']['ms_per_step'], 4), 'push', round(r['push_levels']['ms_per_step'], 4), 'tail', round(r.get('fused', {}).get('ms_per_step', 0), 4), 'kern', round(d['wave_kernel_ms'], 4), 'vinv', d['v_inv_per_step'], 'lv', d['levels_per_step'], 'syncs', d['host_syncs_per_step'], 'first', round(d['first_wave_s'], 3), 'build', round(d['build_s'], 2), flush=True)"
+print('$cfg', '$setting', round(d['ms_per_step'], 4), 'pull', round(r['pull_levels']['ms_per_step'], 4), 'push', round(r['push_levels']['ms_per_step'], 4), 'tail', round(r.get('fused', {}).get('ms_per_step', 0), 4), 'kern', round(d['wave_kernel_ms'], 4), 'vinv', d['v_inv_per_step'], 'lv', d['levels_per_step'], 'syncs', d['host_syncs_per_step'], 'pipe', round(d.get('pipelined_ms_per_step', 0), 4), d.get('pipelined', {}).get('same_counts_as_sync'), 'first', round(d['first_wave_s'], 3), 'build', round(d['build_s'], 2), flush=True)"
 }
 for r in 1 2; do
   bench c2_on_$r rmat27 "-"
   bench c2_off_$r rmat27 "FGI_LABELS=-1"
   bench c1_tail_$r rmat24 "-"
   bench c1_notail_$r rmat24 "FGI_TAIL=0"
+  bench c1_lbl_$r rmat24 "FGI_LABELS=1"
 done

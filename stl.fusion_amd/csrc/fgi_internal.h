@@ -129,7 +129,7 @@ constexpr int kEPT = 8;                 // edges per thread per chunk (largest c
 constexpr int kChunk = kBlock * kEPT;   // edges per expand chunk (largest chunk)
 constexpr int kFine = 256;              // edges per fine chunk of the chunk map (cstart granularity);
                                         // a push level expands chunks of 1..kEPT fine chunks
-constexpr uint32_t kStatBlocks = 4096;  // per-block statistics rows (grid limit of the hot kernels)
+constexpr uint32_t kStatBlocks = 8192;  // per-block statistics rows (grid limit of the hot kernels: 268M slots pull)
 constexpr int kStatCols = 8;
 constexpr int kPullTile = 1024;         // slots per pull tile (one block iteration of a pull level)
 constexpr int kDoneGroups = 16;         // two-level completion counters (last-block epilogues)
@@ -223,7 +223,8 @@ struct WaveCtr {
     unsigned long long mid_push_edges;  // edges / entries of the push levels run by k_level launches
     unsigned long long mid_push_f;
     unsigned long long t0;          // device wall clock at k_wave_init (a wave's kernel span without events)
-    unsigned long long pad2[2];
+    unsigned long long t_max;       // the wave's largest level, in edges (level-group waves: tail_account)
+    unsigned long long pad2;
     LevelCtr lvl[kRing];
 };
 constexpr unsigned long long kPhaseDone = 1;

@@ -1586,6 +1586,9 @@ fgi_status build_candidates(fgi_graph* g) {
     unsigned long long too_long = 0;
     FGI_TRY(d2h(g, &too_long, g->misc_dev + 15, 1));
     if (too_long == 0) g->cand_grid = G;
+    if (getenv("FGI_TRACE"))
+        fprintf(stderr, "[fgi] candidates: %u of %u slots, pull grid %u x %u tiles, %u hot heads, %llu rows too long\n", total,
+                N, G, tpb, g->n_hot, (unsigned long long)too_long);
     return FGI_OK;
 }
 

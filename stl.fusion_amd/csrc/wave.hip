@@ -2116,6 +2116,7 @@ constexpr uint32_t kTailBlocks = 32;
 constexpr int kGbarTail = 8;   // g->gbar word of the tail's barrier (its own grid size)
 
 struct TailArgs {
+    int grp0;                          // the group's first level (its levels' counters are summed here)
     int L0;                            // the first level the group did not launch
     WaveParams wp;
     CollectArgs col[2];                // frontier buffers by level parity (collect after a pull level)
@@ -2131,6 +2132,28 @@ struct TailArgs {
     int all;                           // run every remaining level (asynchronous waves: no second group)
 };
 
+// A level-group wave's totals on the device (one writer: block 0's first thread of the tail), so that
+// the host need not read them from the level ring, which a tail of more than kRing levels rolls over:
+// WaveCtr n_levels / e_trav / f_total / n_pull over the non-empty levels, push_edges / push_f over
+// the push levels, mid_push_edges / mid_push_f over those the tail ran, t_max the largest level's edges.
+__device__ __forceinline__ void tail_account(WaveCtr* c, uint64_t F, uint64_t T, bool pull, bool in_tail) {
+    if (!F) return;
+    c->n_levels += 1;
+    c->e_trav += T;
+    c->f_total += F;
+    if (pull) {
+        c->n_pull += 1;
+    } else {
+        c->push_edges += T;
+        c->push_f += F;
+    }
+    if (in_tail) {
+        c->mid_push_edges += T;
+        c->mid_push_f += F;
+    }
+    if (T > c->t_max) c->t_max = T;
+}
+
 __global__ __launch_bounds__(kBlock) void k_wave_tail(TailArgs a) {
     __shared__ __align__(16) uint32_t s_x[kChunkEmitCap + 8];
     uint32_t* s_rel = s_x;
@@ -2141,6 +2164,12 @@ __global__ __launch_bounds__(kBlock) void k_wave_tail(TailArgs a) {
     __shared__ unsigned long long s_ft;
     WaveCtr* ctr = a.ctr;
     auto grid_sync = [&]() -> bool { return soft_grid_sync(a.gbar, &ctr->broken, nullptr, a.bar_timeout, false, 1); };
+    // the wave's totals (WaveCtr n_levels ..): the group's levels, read before the ring rolls over
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        for (int l = a.grp0; l < a.L0; ++l) {
+            const LevelCtr& g = ctr->lvl[l % kRing];
+            tail_account(ctr, lvl_F(g), lvl_T(g), g.pull != 0, false);
+        }
     int L = a.L0;
     for (bool first = true;; ++L, first = false) {
         LevelCtr& lc = ctr->lvl[L % kRing];
@@ -2148,6 +2177,7 @@ __global__ __launch_bounds__(kBlock) void k_wave_tail(TailArgs a) {
         __syncthreads();
         const uint64_t F = lc.F ? lc.F : (s_ft >> 32), T = lc.F ? lc.T : (s_ft & 0xFFFFFFFFull);
         if (F == 0 || (!a.all && (level_pulls(ctr, L, a.wp, F, T) || T > a.max_edges))) break;
+        if (blockIdx.x == 0 && threadIdx.x == 0) tail_account(ctr, F, T, false, true);
         if (first && L > 0 && ctr->lvl[(L + kRing - 1) % kRing].pull) {   // after a pull level: its frontier list
             collect_front(lc, a.wp.grid, a.col[L & 1], (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6),
                           (uint64_t)gridDim.x * (blockDim.x >> 6));
@@ -2461,7 +2491,7 @@ static_assert(kFinalBlocks <= kLevelGridMax, "epilogue geometry");
 }  // namespace
 
 // kLevelOcc resident blocks per CU (k_level launch bounds); a pull block owns at most kMaxIter tiles, so a
-// larger graph gets more blocks, up to kLevelGridMax (134M slots per device); beyond that, no pull.
+// larger graph gets more blocks, up to kLevelGridMax (268M slots per device, hub-first labels included); beyond that, no pull.
 // FGI_OPT_PULL_TPB fixes the tiles per block instead (tests: every grid takes the same results).
 void pull_geometry(const fgi_graph* g, uint32_t* grid, uint32_t* tpb) {
     const uint64_t n_tiles = ((uint64_t)g->n_slots + kPullTile - 1) / kPullTile;
@@ -2596,8 +2626,9 @@ hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true, uint3
     return hipGetLastError();
 }
 
-TailArgs tail_args(fgi_graph* g, int L0, const WaveParams& wp, uint64_t max_edges) {
+TailArgs tail_args(fgi_graph* g, int grp0, int L0, const WaveParams& wp, uint64_t max_edges) {
     TailArgs ta{};
+    ta.grp0 = grp0;
     ta.L0 = L0;
     ta.wp = wp;
     for (int b = 0; b < 2; ++b) {
@@ -3146,7 +3177,8 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     // run push-only; once a level group shows a frontier heavy enough to pull, the cache is
     // (re)built and later groups may pull. Small waves (streaming mixes) never pay for it.
     const int direction = g->opt_direction;
-    const WaveParams wp0 = wave_params(g, 0, direction, g->pool_top, g->n_slots);
+    // Beamer's beta rule counts the graph's nodes: the boundary's slots (hub-first labels add K empty ones)
+    const WaveParams wp0 = wave_params(g, 0, direction, g->pool_top, g->ext_slots);
     if (wp0.direction == 2 && n_roots) FGI_TRY(ensure_in_lists(g));
     bool allow_pull = wp0.direction != 1 && pull_ready(g, wp0);
     static_assert(sizeof(WaveCtr) % 8 == 0, "WaveCtr is cleared as 64-bit words");
@@ -3190,7 +3222,10 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         const char* m = getenv("FGI_TAIL_EDGES");
         return m && *m ? (unsigned long long)strtoull(m, nullptr, 10) : (unsigned long long)kTailBlocks * kChunk;
     }();
-    const bool use_tail = tail_edges != 0;
+    // the tail only where the previous wave had at least two levels past its head (a pull level and the
+    // push level after it stay in the group: that level's collect scans the pull's winners, a full-grid
+    // job; one small level costs less as a k_level launch than as the tail: profiles/r11_tail_ab.txt)
+    const bool use_tail = tail_edges != 0 && g->last_levels >= g->last_head + 2;
     int group = use_tail ? std::min(8, std::max(1, g->last_head)) : std::min(8, std::max(2, g->last_levels));
     int L = 0, head = 1;
     uint64_t levels = 0, e_trav = 0, f_total = 0, pull_levels = 0;
@@ -3222,7 +3257,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
             if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L + 1], s));
         }
         if (use_tail) {   // the wave's small push levels after the group: one persistent launch
-            const TailArgs ta = tail_args(g, L, wp, tail_edges);
+            const TailArgs ta = tail_args(g, L0, L, wp, tail_edges);
             if (timing) {
                 while (g->ev.size() < 2 * (size_t)(L + 1) + 4) {
                     hipEvent_t e;
@@ -3247,27 +3282,24 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
             g->failed = true;
             return set_err(g, FGI_EDEVICE, "the wave tail's grid barrier timed out (its blocks were not resident together)");
         }
-        // the tail ran levels [L, stop)
+        // the tail ran levels [L, stop); the ring holds the last kRing levels' counters only (the wave's
+        // totals come from the device, tail_account), so a tail that ran more leaves the group's
+        // per-level figures (timing, trace, head) unread
         const int stop = use_tail ? std::max<int>(L, (int)g->ctr_host->cur) : L;
+        const bool ring_ok = stop - L0 < kRing - 4;
         if (use_tail) {
             float ms = 0;
             if (timing && hipEventElapsedTime(&ms, g->ev[2 * L], g->ev[2 * L + 1]) == hipSuccess) tail_ms += ms;
             ++tail_launches;
-            for (int l = L; l < stop; ++l) {
+            for (int l = std::max(L, stop - (kRing - 4)); trace && l < stop; ++l) {
                 const LevelCtr& lc = g->ctr_host->lvl[l % kRing];
-                ++levels;
-                e_trav += lvl_T(lc);
-                f_total += lvl_F(lc);
-                tail_edges_run += lvl_T(lc);
-                tail_f += lvl_F(lc);
-                if (trace)
-                    fprintf(stderr, "[fgi] level %d push (tail): frontier %llu edges %llu chunk x%llu\n", l,
-                            (unsigned long long)lvl_F(lc), (unsigned long long)lvl_T(lc), (unsigned long long)lc.mult);
+                fprintf(stderr, "[fgi] level %d push (tail): frontier %llu edges %llu chunk x%llu\n", l,
+                        (unsigned long long)lvl_F(lc), (unsigned long long)lvl_T(lc), (unsigned long long)lc.mult);
             }
         }
-        for (int l = L0; l < L; ++l) {
+        for (int l = L0; l < L && ring_ok; ++l) {
             const LevelCtr& lc = g->ctr_host->lvl[l % kRing];
-            if (lvl_F(lc) && (lc.pull || lvl_T(lc) > tail_edges)) head = l + 1;
+            if (lvl_F(lc) && (lc.pull || lvl_T(lc) > tail_edges)) head = l + 1 + (lc.pull ? 1 : 0);
             float ms = 0;
             if (timing) {
                 // every k_level launch counts (empty levels too), so the average launch duration
@@ -3282,7 +3314,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                 }
             }
             const uint64_t lF = lvl_F(lc), lT = lvl_T(lc);
-            if (lF) {
+            if (lF && !use_tail) {
                 ++levels;
                 e_trav += lT;
                 f_total += lF;
@@ -3309,8 +3341,8 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         // also when the wave is already done (its level groups are sized from the previous wave's
         // depth, so a repeated wave after a mutation finishes in one group): the next wave pulls
         if (!allow_pull && wp0.direction == 0) {
-            bool heavy = false;
-            for (int l = L0; l <= L; ++l) heavy |= lvl_T(g->ctr_host->lvl[l % kRing]) > wp.pull_threshold;
+            bool heavy = use_tail && g->ctr_host->t_max > wp.pull_threshold;
+            for (int l = L0; l <= L && ring_ok; ++l) heavy |= lvl_T(g->ctr_host->lvl[l % kRing]) > wp.pull_threshold;
             if (heavy) {
                 g->lists_wanted = true;
                 FGI_TRY(ensure_in_lists(g));
@@ -3322,6 +3354,17 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         FGI_HIP(g, launch_final(g, g->n_handles, g->want_ids));
         FGI_HIP(g, hipGetLastError());
         FGI_TRY(counters_to_host(g, s, events));
+    }
+    if (use_tail && final_done) {   // the device's totals (tail_account)
+        const WaveCtr& c = *g->ctr_host;
+        levels = c.n_levels;
+        e_trav = c.e_trav;
+        f_total = c.f_total;
+        pull_levels = c.n_pull;
+        tail_edges_run = c.mid_push_edges;
+        tail_f = c.mid_push_f;
+        expand_edges = c.push_edges - c.mid_push_edges;
+        expand_f = c.push_f - c.mid_push_f;
     }
     if (imm_dev && n_roots) note_words(g);   // immediate roots changed node words
     g->last_wave_n = g->ctr_host->inv;
@@ -3406,7 +3449,7 @@ fgi_status run_wave_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_
     if (!g->inv_alt) FGI_HIP(g, hipMalloc(reinterpret_cast<void**>(&g->inv_alt), (size_t)g->n_handles * 4));
     FGI_TRY(ensure_cstart(g, g->pool_top));
     FGI_TRY(ensure_cls(g));
-    const WaveParams wp0 = wave_params(g, 0, g->opt_direction, g->pool_top, g->n_slots);
+    const WaveParams wp0 = wave_params(g, 0, g->opt_direction, g->pool_top, g->ext_slots);
     // the dependency lists a pull level needs are built here, before anything is queued, once a wave
     // has shown a frontier heavy enough to pull (as run_wave builds them after such a group)
     if (n_roots && wp0.direction != 1 && (g->lists_wanted || wp0.direction == 2)) FGI_TRY(ensure_in_lists(g));
@@ -3417,7 +3460,8 @@ fgi_status run_wave_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_
     g->vis_stale = false;
     g->coop_clean = false;
     const auto* node = reinterpret_cast<const unsigned long long*>(g->node);
-    int group = std::min(8, std::max(1, g->last_head));
+    // the previous wave's levels in the group (up to 8), its head at least; the tail runs the rest
+    int group = std::min(8, std::max(std::max(1, g->last_head), g->last_levels));
     if (n_roots) {
         g->v_dirty = true;
         launch_roots(g, n_roots, roots_dev, imm_dev, 0u, g->n_handles, 0, true);
@@ -3430,7 +3474,7 @@ fgi_status run_wave_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_
                                out_for(g, buf ^ 1, nullptr), out_for(g, buf ^ 1, nullptr), g->ctr, g->blk_stats,
                                g->done, RemoteArgs{}, ~0ull);
         }
-        TailArgs ta = tail_args(g, group, wp, ~0ull);
+        TailArgs ta = tail_args(g, 0, group, wp, ~0ull);
         ta.all = 1;
         hipLaunchKernelGGL(k_wave_tail, dim3(kTailBlocks), dim3(kBlock), 0, s, ta);
     } else {
@@ -3475,22 +3519,18 @@ fgi_status wave_wait(fgi_graph* g, uint64_t ticket, uint64_t* out_n, const uint3
     a.busy = false;
     FGI_TRY(ws);
     const WaveCtr& c = *reinterpret_cast<const WaveCtr*>(pub);
-    uint64_t levels = 0, e_trav = 0, f_total = 0, pull_levels = 0, push_e = 0, push_f = 0, head = 1;
+    // the wave's totals from the device (tail_account); the group's levels from the ring while it has not
+    // rolled over (the next wave's group size)
+    const uint64_t levels = c.n_levels, e_trav = c.e_trav, f_total = c.f_total, pull_levels = c.n_pull;
+    const uint64_t push_e = c.push_edges, push_f = c.push_f;
+    uint64_t head = (uint64_t)std::max(1, g->last_head);
     const uint64_t stop = a.group ? std::max<uint64_t>((uint64_t)a.group, c.cur) : 0;
-    for (uint64_t l = 0; l < stop; ++l) {
-        const LevelCtr& lc = c.lvl[l % kRing];
-        const uint64_t F = lvl_F(lc), T = lvl_T(lc);
-        if (!F) continue;
-        ++levels;
-        e_trav += T;
-        f_total += F;
-        if (lc.pull) {
-            ++pull_levels;
-        } else {
-            push_e += T;
-            push_f += F;
+    if (stop < (uint64_t)kRing - 4) {
+        head = 1;
+        for (uint64_t l = 0; l < (uint64_t)a.group; ++l) {
+            const LevelCtr& lc = c.lvl[l % kRing];
+            if (lvl_F(lc) && (lc.pull || lvl_T(lc) > (uint64_t)kTailBlocks * kChunk)) head = l + 1 + (lc.pull ? 1 : 0);
         }
-        if (l < (uint64_t)a.group && (lc.pull || T > (uint64_t)kTailBlocks * kChunk)) head = l + 1;
     }
     a.n_inv = c.inv;
     g->last_wave_n = c.inv;
@@ -3500,8 +3540,7 @@ fgi_status wave_wait(fgi_graph* g, uint64_t ticket, uint64_t* out_n, const uint3
     if (a.n_roots) {
         g->last_levels = (int)std::max<uint64_t>(levels, 1);
         g->last_head = (int)head;
-        for (uint64_t l = 0; l < stop && !g->lists_wanted; ++l)
-            if (lvl_T(c.lvl[l % kRing]) > (g->pool_top / (uint64_t)std::max(1, g->opt_pull_alpha))) g->lists_wanted = true;
+        if (c.t_max > g->pool_top / (uint64_t)std::max(1, g->opt_pull_alpha)) g->lists_wanted = true;
     }
     if (out_n) *out_n = c.inv;
     if (ids_dev) *ids_dev = g->inv_cur;

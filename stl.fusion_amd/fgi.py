@@ -531,7 +531,8 @@ class Graph:
                 out = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
                 dist.all_gather(out, src, group=group)
                 if nbytes:
-                    C.memmove(recv, torch.cat(out).numpy().ctypes.data, nbytes * world)
+                    got = torch.cat(out).numpy()   # held: a temporary's buffer may be freed before the copy
+                    C.memmove(recv, got.ctypes.data, nbytes * world)
                 return 0
             except Exception as e:  # reported as FGI_EDEVICE by the engine
                 import sys

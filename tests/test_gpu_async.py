@@ -101,17 +101,20 @@ def test_async_waves_on_an_evolving_graph(pkg, gpu_available):
         d_keep += [dr, di]
         torch.cuda.synchronize()
         tickets.append(g.invalidate_async(len(r), dr.data_ptr(), di.data_ptr()))
-    for t, (w, v) in zip(tickets[:2], want[:2]):
-        nv, ptr = g.wave_wait(t)
-        assert nv == v and np.array_equal(_d2h(ptr, nv), w), t
-    # two waves still in flight: the state query waits for them
+        if 1 <= k <= 2:   # the previous wave, while this one is queued
+            nv, ptr = g.wave_wait(tickets[k - 1])
+            assert nv == want[k - 1][1] and np.array_equal(_d2h(ptr, nv), want[k - 1][0]), k
+    # waves 3 and 4 still in flight: the state query waits for them
     assert_states_equal(g, o, n)
-    nv, ptr = g.wave_wait(tickets[3])
-    assert nv == want[3][1]
+    for t in tickets[2:]:   # waited for by the query; their results stay until two later waves
+        nv, ptr = g.wave_wait(t)
+        assert nv == want[t - 1][1] and np.array_equal(_d2h(ptr, nv), want[t - 1][0]), t
     r = O.gen_roots(64, n, 999, deg)
     o.clear_log()
     o.invalidate_slots(r)
-    t = g.invalidate_async(len(r), torch.from_numpy(r.astype(np.int32)).cuda().data_ptr())
+    d_r = torch.from_numpy(r.astype(np.int32)).cuda()
+    torch.cuda.synchronize()
+    t = g.invalidate_async(len(r), d_r.data_ptr())
     ids = g.invalidate(O.gen_roots(4, n, 5, deg))   # synchronous: waits for ticket t first
     o_ids = np.sort(o.inv_log())
     o.clear_log()

@@ -20,6 +20,18 @@ pytestmark = pytest.mark.gpu
 SSEED = 0x5EED00C0
 
 
+def _alive_pairs(o):
+    """(slot, version) of every oracle node that is not Invalidated (current or displaced)."""
+    import ctypes as C
+    out, h = set(), 0
+    sl, v, f = C.c_uint32(), C.c_uint64(), C.c_uint32()
+    while o.l.fgo_node_info(o.o, h, C.byref(sl), C.byref(v), C.byref(f)) == 0:
+        if v.value and (f.value & 3) != 2:
+            out.add((sl.value, v.value))
+        h += 1
+    return out
+
+
 def _rmat(pkg, scale, ef, seed, stale, labels):
     n = 1 << scale
     g = pkg.Graph(n, n_detached=64, labels=labels)
@@ -167,11 +179,16 @@ def test_labelled_mutations_batches_and_prune(pkg, gpu_available, labels):
                 assert int(outs[k].sum()) == o.set_output_slots(sp[1]), b
         assert np.array_equal(np.sort(ids), np.sort(o.inv_log())), b
         assert_states_equal(g, o, n)
-    # `_usedBy` of single nodes, as the reference would hold them
+    # `_usedBy` of single nodes: fgi_get_used_by lists the live entries (fgi.h: a dependant d@t that
+    # is still alive and not Invalidated; the rows keep the others until a prune, as the reference's
+    # sets keep entries of collected nodes until PruneUsedBy, Computed.cs:400-419)
+    live = _alive_pairs(o)
     for x in rng.choice(n, 64, replace=False):
         gd, gt = g.used_by(int(x))
         oh = o.current(int(x))
         od, ot = o.used_by(oh) if oh != O.NONE else (np.zeros(0, np.uint32), np.zeros(0, np.uint64))
+        keep = np.array([(int(a), int(b)) in live for a, b in zip(od, ot)], bool)
+        od, ot = od[keep] if len(od) else od, ot[keep] if len(ot) else ot
         assert np.array_equal(canon_edges(np.full(len(gd), x), gd, gt), canon_edges(np.full(len(od), x), od, ot)), x
     # the pruner's walk over handle ranges, then a full prune
     batch = 1000

@@ -179,6 +179,51 @@ def test_cycles_and_self_loops(pkg, gpu_available, path):
     assert len(ids) == n and ws.levels == n
 
 
+@pytest.mark.parametrize("labels", [-1, 1])
+def test_deep_waves_through_the_tail(pkg, gpu_available, labels):
+    """A 1,000-level wave (one cycle with self loops), repeated from a snapshot: the first wave runs as
+    level groups; the repeats know the wave is deeper than its head and run its levels in the
+    persistent tail (k_wave_tail), far past the 64-entry level ring, with one host synchronisation.
+    Every wave equals the oracle: the set, V_inv, E_trav, the level count and every node word; the
+    asynchronous entry point (the tail with every level) too."""
+    import torch
+    n = 1000
+    versions = O.version_of(5, np.arange(n))
+    flags = np.full(n, CONSISTENT, np.uint32)
+    src = np.arange(n, dtype=np.uint32)
+    dst = ((src + 1) % n).astype(np.uint32)
+    src = np.concatenate([src, np.arange(0, n, 10, dtype=np.uint32)])
+    dst = np.concatenate([dst, np.arange(0, n, 10, dtype=np.uint32)])
+    tags = versions[dst]
+    g = pkg.Graph(n, labels=labels)
+    g.register_nodes(np.arange(n, dtype=np.uint32), versions, flags)
+    g.load_edges(src, dst, tags)
+    o = O.Oracle(n)
+    o.load_graph(versions, flags, src, dst, tags)
+    g.snapshot()
+    o.snapshot()
+    roots = np.array([17], np.uint32)
+    for rep in range(3):
+        g.restore()
+        o.restore()
+        ids, ws = _compare_wave(g, o, n, roots)
+        assert len(ids) == n and ws.levels == n, (rep, ws.levels)
+        if rep:
+            assert ws.host_syncs == 1, (rep, ws.host_syncs)
+    d_roots = torch.from_numpy(roots.astype(np.int32)).cuda()
+    torch.cuda.synchronize()
+    for rep in range(2):
+        g.restore()
+        ws = pkg.WaveStats()
+        nv, _ = g.wave_wait(g.invalidate_async(1, d_roots.data_ptr()), ws)
+        assert nv == n and ws.v_inv == n and ws.e_trav == 1100 and ws.levels == n, (ws.v_inv, ws.e_trav, ws.levels)
+    o.restore()
+    o.invalidate_slots(roots)
+    assert_states_equal(g, o, n)
+    g.close()
+    o.close()
+
+
 def test_empty_and_noop_waves(pkg, gpu_available):
     n = 100
     versions = O.version_of(9, np.arange(n))

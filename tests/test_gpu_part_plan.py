@@ -74,12 +74,13 @@ def test_planned_waves_match_oracle(pkg, gpu_available, P, stale, direction):
     o.close()
 
 
-@pytest.mark.parametrize("bucket", [3, 17, 1000])
-def test_planned_waves_with_small_buckets(pkg, gpu_available, bucket):
-    """Buckets of `bucket` words per peer: most forwarded ids wait for later push levels (which the
-    planned wave appends while any are left); the wave is still exactly the oracle's."""
+@pytest.mark.parametrize("bucket,scale", [(2, 13), (2, 15), (3, 13), (17, 13), (1000, 13)])
+def test_planned_waves_with_small_buckets(pkg, gpu_available, bucket, scale):
+    """Buckets of `bucket` words per peer (2, the smallest the clamp accepts: a count and one id):
+    most forwarded ids wait for later push levels (which the planned wave appends while any are
+    left); the wave is still exactly the oracle's."""
     P = 4
-    gs, o, s, n, block = _build(pkg, P, 13, 16, 0x5EED0027, 30)
+    gs, o, s, n, block = _build(pkg, P, scale, 16, 0x5EED0027, 30)
     for g in gs:
         g.snapshot()
     o.snapshot()
