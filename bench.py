@@ -125,7 +125,12 @@ def profiled_traffic(kname, config_scale, live_avg_ms):
     WRITE_SIZE per MI355X_MICROARCH.md). Used only if that run's average launch time is within 25%
     of the live one (same kernel build); otherwise (None, reason)."""
     here = os.path.dirname(os.path.abspath(__file__))
-    cands = sorted(glob.glob(os.path.join(here, "profiles", "r*_summary.json")))
+    import re
+
+    def order(path):   # r9a < r10b < r11c1: by round number, then the rest of the tag
+        m = re.match(r"r(\d+)(.*)_summary\.json$", os.path.basename(path))
+        return (int(m.group(1)), m.group(2)) if m else (-1, path)
+    cands = sorted(glob.glob(os.path.join(here, "profiles", "r*_summary.json")), key=order)
     for path in reversed(cands):
         try:
             doc = json.load(open(path))
@@ -189,6 +194,8 @@ def main():
     ap.add_argument("--cpu-scale", type=int, default=0,
                     help="R-MAT scale of the CPU baseline (default: the workload's own, i.e. the identical graph)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host roots -> host ids) leg")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the secondary workloads (configs2_single_gpu / weak_scaling; profiling runs)")
     ap.add_argument("--partition", action="store_true",
                     help="use the partitioned RCCL engine even at N=1 (it is always used for N>1)")
     ap.add_argument("--cpu-runs", type=int, default=5, help="timed CPU waves after one warm-up (median reported)")
@@ -385,7 +392,21 @@ def main():
                 "pull_ms_per_step": st_k.pull_ms / K, "push_ms_per_step": st_k.expand_ms / K,
                 "first_wave_s": m["first_wave_s"], "build_s": build_s,
                 "pipelined": m["pipelined"],
+                "roofline": kernel_roofline(st_k, K, cfg),
                 "parallelism": parallelism(), "n_gpus": world}
+
+    def kernel_roofline(st_k, K, cfg):
+        """k_level's achieved GB/s (algorithmic bytes / measured launch time, the instrumented pass) against
+        the HBM peak, and the PMC traffic of the matching committed profile (profiled_traffic)."""
+        k_ms = st_k.pull_ms + st_k.expand_ms
+        k_bytes = st_k.pull_bytes + st_k.expand_bytes
+        k_launches = st_k.pull_launches + st_k.expand_launches
+        gbs = (k_bytes / (k_ms * 1e-3) / 1e9) if k_ms > 0 else 0.0
+        traffic, src = profiled_traffic("k_level", cfg.get("scale"), k_ms / max(1, k_launches))
+        return {"bound": "hbm", "kernel": "k_level", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": gbs / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": src,
+                "launches_per_step": k_launches / K, "avg_launch_ms": k_ms / max(1, k_launches),
+                "alg_bytes_per_launch": k_bytes / max(1, k_launches)}
 
     def parallelism():
         if not partitioned:
@@ -573,7 +594,7 @@ def main():
         result["e2e"] = e2e
 
     # secondary workloads: configs[2] on this one GPU (N = 1), the weak-scaling point (N > 1)
-    for key, name, scale in sel["secondary"]:
+    for key, name, scale in ([] if args.no_secondary else sel["secondary"]):
         g2, cfg2, n2, roots2, e2, b2 = build(name, scale)
         m2 = measure(g2, roots2)
         g2.close()

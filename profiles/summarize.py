@@ -17,7 +17,7 @@ import shutil
 
 WAVE_KERNELS = ("k_roots", "k_level_begin", "k_scan_reduce", "k_scan_apply", "k_mark", "k_expand", "k_pull",
                 "k_pull_long", "k_clear_front", "k_level", "k_collect", "k_wave_init",
-                "k_final_count", "k_final_write", "k_final")
+                "k_final_count", "k_final_write", "k_final", "k_wave_tail", "k_publish")
 
 
 def base_name(n):

@@ -320,7 +320,9 @@ struct fgi_graph {
     bool lbl_done = false;             // the hot set has been chosen (first bulk edge load)
     uint32_t* s2l = nullptr;           // [ext_slots] hot label of a slot, FGI_NONE if cold
     uint32_t* l2s = nullptr;           // [lbl_K] slot of a hot label
-    uint32_t* fold_start = nullptr;    // [lbl_ncls][fold_tiles + 1] first hot label of class c at slots >= t * kFoldTile
+    uint32_t* fold_start = nullptr;    // [fold_tiles + 1][lbl_ncls] first hot label of class c at slots >= t * kFoldTile
+    uint16_t* fold_off = nullptr;      // [lbl_hot] per tile, its hot labels in (class, slot) order: slot - tile base
+    uint32_t* fold_base = nullptr;     // [fold_tiles + 1] each tile's first entry in fold_off
     uint32_t lbl_ncls = 0, fold_tiles = 0;
     unsigned long long* xbm = nullptr; // [ext words] the wave's invalidated set over the boundary's handles
     unsigned long long* fold_status = nullptr;   // [fold tiles, >= kStats] per-tile counts of the final collect
@@ -536,7 +538,7 @@ struct fgi_graph {
 // ---- internal entry points shared between translation units ----------------------------------
 namespace fgi {
 // ---- hub-first labels (labels.hip) ----
-constexpr uint32_t kFoldTile = 16384;            // slots per fold tile (256 bitmap words)
+constexpr uint32_t kFoldTile = 65536;            // slots per fold tile (1,024 bitmap words; offsets fit 16 bits)
 constexpr uint32_t kFoldWords = kFoldTile / 64;
 constexpr uint32_t kLabelAutoSlots = 1u << 25;   // auto: graphs whose bitmap outgrows one XCD's L2 (4 MB)
 constexpr uint32_t kClassPerOctave = 8;          // weight classes per octave of (dependencies + 1)
@@ -558,15 +560,22 @@ fgi_status labels_choose(fgi_graph* g, const uint64_t* keys, uint64_t m);
 struct FoldArgs {
     const uint32_t* l2s;           // null: no hot labels (the bitmap of handles is the labels' own)
     const uint32_t* fold_start;
-    uint32_t ncls, tiles;          // fold_start is [ncls][tiles + 1]
+    const uint16_t* off;           // fold_off / fold_base (fgi_graph)
+    const uint32_t* base;
+    uint32_t ncls, tiles;          // fold_start is [tiles + 1][ncls]
     uint32_t K;                    // cold label of handle x: K + x
     unsigned long long* xbm;       // out: the invalidated set over boundary handles
+    uint32_t exp;                  // measurement only (FGI_FOLD_EXP, results wrong): 1 no hot labels, 2 no cold copy, 4 no chunks, 8 no staging
 };
 // active (xbm set) iff the graph has a hot-label prefix (K > 0): the boundary's bitmap is then the
 // labels' one shifted by K, ORed with the hot labels' bits at their slots
 inline FoldArgs fold_args(const fgi_graph* g) {
-    return FoldArgs{g->lbl_hot ? g->l2s : nullptr, g->fold_start, g->lbl_hot ? g->lbl_ncls : 0u, g->fold_tiles, g->lbl_K,
-                    g->lbl_K ? g->xbm : nullptr};
+    static const uint32_t exp = [] {
+        const char* e = getenv("FGI_FOLD_EXP");
+        return e && *e ? (uint32_t)atoi(e) : 0u;
+    }();
+    return FoldArgs{g->lbl_hot ? g->l2s : nullptr, g->fold_start, g->fold_off, g->fold_base, g->lbl_hot ? g->lbl_ncls : 0u,
+                    g->fold_tiles, g->lbl_K, g->lbl_K ? g->xbm : nullptr, exp};
 }
 
 fgi_status set_err(fgi_graph* g, fgi_status st, const char* fmt, ...);

@@ -1996,6 +1996,8 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->s2l);
     dfree(g->l2s);
     dfree(g->fold_start);
+    dfree(g->fold_off);
+    dfree(g->fold_base);
     dfree(g->xbm);
     dfree(g->fold_status);
     if (g->scratch) hipFree(g->scratch);

@@ -105,13 +105,14 @@ __global__ void k_lbl_assign(uint32_t H, const uint64_t* __restrict__ sorted, ui
     s2l[s] = r;
 }
 
-// fold_start[j][t]: the first hot label of hot class j (labels [cb[j], cb[j + 1]), slots ascending) whose
-// slot is >= t * kFoldTile; t = tiles gives the class's end
+// fold_start[t][j] (tile-major: a fold tile reads its row and the next, two contiguous runs): the first
+// hot label of hot class j (labels [cb[j], cb[j + 1]), slots ascending) whose slot is >= t * kFoldTile;
+// t = tiles gives the class's end
 __global__ void k_lbl_fold_start(uint32_t ncls, uint32_t tiles, const uint32_t* __restrict__ cb,
                                  const uint32_t* __restrict__ l2s, uint32_t* fs) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= (uint64_t)ncls * (tiles + 1)) return;
-    const uint32_t j = (uint32_t)(i / (tiles + 1)), t = (uint32_t)(i % (tiles + 1));
+    const uint32_t t = (uint32_t)(i / ncls), j = (uint32_t)(i % ncls);
     uint32_t lo = cb[j], hi = cb[j + 1];
     const uint64_t x = (uint64_t)t * kFoldTile;
     while (lo < hi) {
@@ -120,6 +121,47 @@ __global__ void k_lbl_fold_start(uint32_t ncls, uint32_t tiles, const uint32_t* 
         else hi = mid;
     }
     fs[i] = lo;
+}
+
+// each fold tile's hot-label count (its runs over the classes)
+__global__ void k_lbl_tile_tot(uint32_t ncls, uint32_t tiles, const uint32_t* __restrict__ fs, uint32_t* tot) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= tiles) return;
+    uint32_t c = 0;
+    for (uint32_t j = 0; j < ncls; ++j) c += fs[(uint64_t)(t + 1) * ncls + j] - fs[(uint64_t)t * ncls + j];
+    tot[t] = c;
+}
+
+// fold_off: block t lists its tile's hot labels in the fold's order (class by class, each class's run in
+// slot order) as their slots' offsets in the tile, at base[t]: the fold then reads one contiguous run
+// of 2-byte offsets per tile instead of a label-map entry per hot label (a cache line per class run)
+__global__ __launch_bounds__(256) void k_lbl_fold_off(uint32_t ncls, const uint32_t* __restrict__ fs,
+                                                      const uint32_t* __restrict__ base, const uint32_t* __restrict__ l2s,
+                                                      uint16_t* off) {
+    __shared__ uint32_t s_a[kMaxHotClasses + 1], s_o[kMaxHotClasses + 1];
+    const uint32_t t = blockIdx.x;
+    if (threadIdx.x == 0) {
+        uint32_t o = 0;
+        for (uint32_t j = 0; j < ncls; ++j) {
+            const uint32_t a = fs[(uint64_t)t * ncls + j];
+            s_a[j] = a;
+            s_o[j] = o;
+            o += fs[(uint64_t)(t + 1) * ncls + j] - a;
+        }
+        s_o[ncls] = o;
+    }
+    __syncthreads();
+    const uint32_t total = s_o[ncls], b = base[t];
+    const uint64_t tile0 = (uint64_t)t * kFoldTile;
+    for (uint32_t k = threadIdx.x; k < total; k += blockDim.x) {
+        uint32_t lo = 0, hi = ncls;   // the last class j with s_o[j] <= k
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (s_o[mid] <= k) lo = mid;
+            else hi = mid;
+        }
+        off[b + k] = (uint16_t)(l2s[s_a[lo] + (k - s_o[lo])] - tile0);
+    }
 }
 
 // the registered node words of hot slots move from their cold label K + s to their hot label; a
@@ -247,6 +289,40 @@ fgi_status labels_choose(fgi_graph* g, const uint64_t* keys, uint64_t m) {
             return fail(e, "labels: class bases");
         hipLaunchKernelGGL(k_lbl_fold_start, dim3(nblk((uint64_t)ncls * (tiles + 1))), dim3(256), 0, s, ncls, tiles, cb,
                            g->l2s, g->fold_start);
+        // the fold's per-tile offset runs: tile counts, their prefix (host: tiles words), the offsets
+        for (void* p : {(void*)g->fold_off, (void*)g->fold_base})
+            if (p) hipFree(p);
+        g->fold_off = nullptr;
+        g->fold_base = nullptr;
+        if ((e = hipMalloc(&g->fold_off, ((size_t)H + 8ull * tiles + 8) * 2)) != hipSuccess ||
+            (e = hipMalloc(&g->fold_base, (size_t)(tiles + 1) * 4)) != hipSuccess)
+            return fail(e, "labels: fold offsets");
+        hipLaunchKernelGGL(k_lbl_tile_tot, dim3(nblk(tiles)), dim3(256), 0, s, ncls, tiles, g->fold_start, g->fold_base);
+        std::vector<uint32_t> tb_host(tiles + 1, 0);
+        if ((e = hipMemcpyAsync(tb_host.data(), g->fold_base, (size_t)tiles * 4, hipMemcpyDeviceToHost, s)) != hipSuccess ||
+            (e = hipStreamSynchronize(s)) != hipSuccess)
+            return fail(e, "labels: fold tile counts");
+        // each tile's run starts 16-byte aligned (8 entries): the fold stages it with 16-byte loads
+        uint64_t run = 0, covered = 0;
+        for (uint32_t t = 0; t <= tiles; ++t) {
+            const uint32_t c = t < tiles ? tb_host[t] : 0u;
+            tb_host[t] = (uint32_t)run;
+            run += (c + 7u) & ~7u;
+            covered += c;
+        }
+        if (covered != H) {
+            cleanup();
+            return set_err(g, FGI_EDEVICE, "labels: fold runs cover %llu of %llu hot labels", (unsigned long long)covered,
+                           (unsigned long long)H);
+        }
+        if (run > (1ull << 32)) {
+            cleanup();
+            return set_err(g, FGI_ENOTSUP, "labels: fold offsets exceed 2^32 entries");
+        }
+        if ((e = hipMemcpyAsync(g->fold_base, tb_host.data(), (size_t)(tiles + 1) * 4, hipMemcpyHostToDevice, s)) != hipSuccess)
+            return fail(e, "labels: fold bases");
+        hipLaunchKernelGGL(k_lbl_fold_off, dim3(tiles), dim3(256), 0, s, ncls, g->fold_start, g->fold_base, g->l2s,
+                           g->fold_off);
         hipLaunchKernelGGL(k_lbl_move_words, dim3(nblk(H)), dim3(256), 0, s, (uint32_t)H, g->l2s, g->lbl_K,
                            reinterpret_cast<unsigned long long*>(g->node));
         if (g->n_detached)

@@ -1616,69 +1616,147 @@ __global__ void k_part_tail(const WaveCtr* ctr, int L0, int L, uint32_t W, const
 // Hub-first labels (labels.hip): the bitmap over boundary handles of fold tile t
 // (handles [t * kFoldTile, + kFoldTile), kFoldWords 64-bit words) is the labels' bitmap shifted by K
 // (K + x is the label of every handle x that has no hot label; K is a multiple of kFoldTile), ORed with
-// the tile's hot labels' bits at their slots: per hot class j, the labels [fold_start[j][t],
-// fold_start[j][t + 1]), which keep slot order. Written to f.xbm; returns the tile's set bits (every
+// the tile's hot labels' bits at their slots: per hot class j, the labels [fold_start[t][j],
+// fold_start[t + 1][j]), which keep slot order. Written to f.xbm; returns the tile's set bits (every
 // thread). Block-uniform call; s_w: kFoldWords words, s_a / s_o: kMaxHotClasses + 1 words of LDS.
+constexpr uint32_t kFoldStage = 12288;   // a fold tile's slot offsets staged in LDS (24 KB; ~8,200 per tile at configs[2])
+
 __device__ unsigned long long fold_tile(const FoldArgs& f, const unsigned long long* __restrict__ inv64, uint64_t ext_words,
                                         uint32_t t, unsigned long long* s_w, uint32_t* s_a, uint32_t* s_o,
                                         unsigned long long* s_red) {
     const uint64_t w0 = (uint64_t)t * kFoldWords;
     const uint32_t nw = (uint32_t)std::min<uint64_t>(kFoldWords, ext_words > w0 ? ext_words - w0 : 0);
     const uint64_t kw = f.K / 64;
-    for (uint32_t i = threadIdx.x; i < kFoldWords; i += blockDim.x) s_w[i] = i < nw ? inv64[kw + w0 + i] : 0ull;
-    if (f.l2s && f.ncls) {
-        // this tile's run of each hot class: offsets by one block scan over the classes
-        uint32_t len = 0, a = 0;
-        if (threadIdx.x < f.ncls) {
-            const uint32_t* fs = f.fold_start + (uint64_t)threadIdx.x * (f.tiles + 1) + t;
-            a = fs[0];
-            len = fs[1] - a;
-        }
-        uint32_t tot;
-        const uint32_t ex = wave_excl_scan(len, tot);
+    __shared__ uint32_t s_wt[2][kBlock / 64];
+    __shared__ uint32_t s_i[kMaxHotClasses + 1];
+    __shared__ __align__(16) uint16_t s_off[kFoldStage];
+    __shared__ uint32_t s_eb[kFoldStage / 32 + 2];   // the staged entries' bits, in entry order
+    const bool hot = f.l2s && f.ncls && !(f.exp & 1);
+    for (uint32_t i = threadIdx.x; i < kFoldStage / 32 + 2; i += blockDim.x) s_eb[i] = 0u;
+    // every independent load first — the tile's run bounds, its classes' runs, the cold words, the slot
+    // offsets — then the LDS stores: a block's fold is a chain of round trips, so fewer links
+    const uint32_t b0 = hot ? f.base[t] : 0u, b1 = hot ? f.base[t + 1] : 0u;
+    uint32_t len = 0, a = 0;
+    if (hot && threadIdx.x < f.ncls) {
+        const uint32_t* fs = f.fold_start + (uint64_t)t * f.ncls + threadIdx.x;   // rows t and t + 1
+        a = fs[0];
+        len = fs[f.ncls] - a;
+    }
+    constexpr uint32_t kU = kFoldWords / kBlock;
+    static_assert(kFoldWords % kBlock == 0, "fold tile words per thread");
+    unsigned long long cw[kU];
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) {
+        const uint32_t i = u * kBlock + threadIdx.x;
+        cw[u] = i < nw && !(f.exp & 2) ? inv64[kw + w0 + i] : 0ull;
+    }
+    // the tile's slot offsets (fold_off: labels.hip k_lbl_fold_off, the same order, 2 bytes each; a tile's
+    // run starts 16-byte aligned and is padded to 8 entries) staged in LDS by 16-byte loads; a tile with
+    // more than kFoldStage reads the rest from memory
+    const uint16_t* toff = f.off + b0;
+    constexpr uint32_t kV = (kFoldStage / 8 + kBlock - 1) / kBlock;
+    const uint32_t n16 = (f.exp & 8) ? 0u : min(b1 - b0, kFoldStage) / 8;
+    uint4 v[kV];
+#pragma unroll
+    for (uint32_t u = 0; u < kV; ++u) {
+        const uint32_t i = u * kBlock + threadIdx.x;
+        if (i < n16) v[u] = reinterpret_cast<const uint4*>(toff)[i];
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kU; ++u) s_w[u * kBlock + threadIdx.x] = cw[u];
+#pragma unroll
+    for (uint32_t u = 0; u < kV; ++u) {
+        const uint32_t i = u * kBlock + threadIdx.x;
+        if (i < n16) reinterpret_cast<uint4*>(s_off)[i] = v[u];
+    }
+    if (hot) {
+        // this tile's run of each hot class, cut into chunks of up to 64 labels (one 64-bit window of the
+        // hot bitmap each): per class its first label (s_a), its first entry in the tile's fold_off run
+        // (s_o) and its first chunk (s_i), by one block scan over the classes
+        const uint32_t nch = (len + 63) >> 6;
+        uint32_t tot_l, tot_c;
+        const uint32_t ex_l = wave_excl_scan(len, tot_l);
+        const uint32_t ex_c = wave_excl_scan(nch, tot_c);
         const uint32_t wid = threadIdx.x >> 6;
-        __shared__ uint32_t s_wt[kBlock / 64];
-        if (lane_id() == 0) s_wt[wid] = tot;
+        if (lane_id() == 0) {
+            s_wt[0][wid] = tot_l;
+            s_wt[1][wid] = tot_c;
+        }
         __syncthreads();
-        uint32_t before = 0, total = 0;
+        uint32_t before_l = 0, before_c = 0, labels = 0, chunks = 0;
         for (uint32_t k = 0; k < blockDim.x / 64; ++k) {
-            before += k < wid ? s_wt[k] : 0u;
-            total += s_wt[k];
+            before_l += k < wid ? s_wt[0][k] : 0u;
+            before_c += k < wid ? s_wt[1][k] : 0u;
+            labels += s_wt[0][k];
+            chunks += s_wt[1][k];
         }
         if (threadIdx.x < f.ncls) {
             s_a[threadIdx.x] = a;
-            s_o[threadIdx.x] = before + ex;
+            s_o[threadIdx.x] = before_l + ex_l;
+            s_i[threadIdx.x] = before_c + ex_c;
         }
-        if (threadIdx.x == 0) s_o[f.ncls] = total;
+        if (threadIdx.x == 0) {
+            s_o[f.ncls] = labels;
+            s_i[f.ncls] = chunks;
+        }
         __syncthreads();
-        // one hot label per lane, four in flight per thread: its class by a binary search over the
-        // offsets, its bit, then (set bits only) its slot
-        constexpr int kPer = 4;
-        for (uint32_t k0 = 0; k0 < total; k0 += kPer * blockDim.x) {   // block-uniform
-            uint32_t lab[kPer];
-            bool hit[kPer];
+        // one chunk per thread: its class by a search over the chunk offsets, its labels' bits as one
+        // 64-bit window of the hot bitmap (two words at most), then per set bit its slot's offset (LDS)
+        // and the bit in the tile's words (LDS)
+        const uint32_t staged = n16 * 8;   // entries [0, staged) are in LDS
+        // per chunk (one per thread): its class by a search over the chunk offsets, its labels' bits as
+        // one 64-bit window of the hot bitmap (two words at most), copied into the tile's entry-order
+        // bitmap s_eb at its first entry (LDS); a chunk past the staged entries folds its bits itself
+        uint32_t* s_w32 = reinterpret_cast<uint32_t*>(s_w);   // 32-bit LDS atomics (little endian)
+        for (uint32_t q = threadIdx.x; q < ((f.exp & 4) ? 0u : chunks); q += blockDim.x) {
+            uint32_t lo = 0;   // the last class j with s_i[j] <= q
 #pragma unroll
-            for (int q = 0; q < kPer; ++q) {
-                const uint32_t k = k0 + q * blockDim.x + threadIdx.x;
-                lab[q] = FGI_NONE;
-                if (k < total) {
-                    uint32_t lo = 0, hi = f.ncls;   // the last class j with s_o[j] <= k
-                    while (hi - lo > 1) {
-                        const uint32_t mid = (lo + hi) >> 1;
-                        if (s_o[mid] <= k) lo = mid;
-                        else hi = mid;
-                    }
-                    lab[q] = s_a[lo] + (k - s_o[lo]);
+            for (uint32_t step = kMaxHotClasses / 2; step; step >>= 1) {
+                const uint32_t j = lo + step;
+                if (j < f.ncls && s_i[j] <= q) lo = j;
+            }
+            const uint32_t c0 = (q - s_i[lo]) << 6;      // the chunk's first label in its class's run
+            const uint32_t lab0 = s_a[lo] + c0;
+            const uint32_t e0 = s_o[lo] + c0;            // its first entry in the tile's offsets
+            const uint32_t m = min(64u, s_o[lo + 1] - s_o[lo] - c0);
+            const uint32_t wq = lab0 >> 6, sh = lab0 & 63;
+            unsigned long long bits = inv64[wq] >> sh;
+            if (sh && sh + m > 64) bits |= inv64[wq + 1] << (64 - sh);
+            if (m < 64) bits &= (1ull << m) - 1ull;
+            if (!bits) continue;
+            if (e0 + m <= staged) {
+                const uint32_t w = e0 >> 5, b = e0 & 31;
+                const uint32_t v0 = (uint32_t)bits, v1 = (uint32_t)(bits >> 32);
+                if (v0) {
+                    atomicOr(&s_eb[w], v0 << b);
+                    if (b) atomicOr(&s_eb[w + 1], v0 >> (32 - b));
                 }
+                if (v1) {
+                    atomicOr(&s_eb[w + 1], v1 << b);
+                    if (b) atomicOr(&s_eb[w + 2], v1 >> (32 - b));
+                }
+                continue;
+            }
+            for (; bits; bits &= bits - 1) {   // past the LDS stage (rare: > kFoldStage hot labels in a tile)
+                const uint32_t e = e0 + (uint32_t)(__ffsll((long long)bits) - 1);
+                const uint32_t x = e < staged ? s_off[e] : toff[e];   // < kFoldTile
+                atomicOr(&s_w32[x >> 5], 1u << (x & 31));
+            }
+        }
+        __syncthreads();
+        // one staged entry per lane: its bit from s_eb, its slot's offset from s_off, the bit in the tile's
+        // words — no search, no divergence
+        const uint32_t ne = min(labels, staged);
+        for (uint32_t k0 = 0; k0 < ne; k0 += 4 * blockDim.x) {   // block-uniform
+            uint32_t x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t k = k0 + u * blockDim.x + threadIdx.x;
+                x[u] = (k < ne && ((s_eb[k >> 5] >> (k & 31)) & 1u)) ? (uint32_t)s_off[k] : FGI_NONE;
             }
 #pragma unroll
-            for (int q = 0; q < kPer; ++q) hit[q] = lab[q] != FGI_NONE && ((inv64[lab[q] >> 6] >> (lab[q] & 63)) & 1ull);
-#pragma unroll
-            for (int q = 0; q < kPer; ++q)
-                if (hit[q]) {
-                    const uint32_t x = f.l2s[lab[q]] - (uint32_t)(w0 * 64);
-                    if (x < kFoldTile) atomicOr(&s_w[x >> 6], 1ull << (x & 63));   // always: the run is this tile's
-                }
+            for (int u = 0; u < 4; ++u)
+                if (x[u] != FGI_NONE) atomicOr(&s_w32[x[u] >> 5], 1u << (x[u] & 31));
         }
     }
     __syncthreads();
@@ -1692,6 +1770,8 @@ __device__ unsigned long long fold_tile(const FoldArgs& f, const unsigned long l
     __syncthreads();   // s_w, s_a, s_o are reused by the block's next tile
     return c;
 }
+
+constexpr uint32_t kFoldBlocks = 4096;   // k_final_count's grid with hot labels: one fold tile per block up to 2^28 handles
 
 // The final count: tickets 0..kStats-1 fold the per-block statistics into the wave counters; every
 // block counts the set bits of its 64-bit words [t * wpb, (t + 1) * wpb) into status[t]. With hot labels
@@ -1716,9 +1796,19 @@ __global__ __launch_bounds__(kBlock) void k_final_count(const unsigned long long
     }
     unsigned long long c = 0;
     if (f.xbm) {
+        // fold tiles t, t + G, ...: one status word per tile (k_final_write's spb groups); one tile per
+        // block up to kFoldBlocks tiles
         __shared__ unsigned long long s_w[kFoldWords];
         __shared__ uint32_t s_a[kMaxHotClasses + 1], s_o[kMaxHotClasses + 1];
-        if ((uint64_t)t * kFoldWords < words) c = fold_tile(f, inv64, words, t, s_w, s_a, s_o, s_red);
+        for (uint32_t tt = t; (uint64_t)tt * kFoldWords < words; tt += gridDim.x) {   // block-uniform
+            const unsigned long long ct = fold_tile(f, inv64, words, tt, s_w, s_a, s_o, s_red);
+            if (!total) {
+                if (threadIdx.x == 0) status[tt] = ct;
+            } else {
+                c += ct;
+            }
+        }
+        if (!total) return;
     } else {
         const uint64_t lo = t * wpb, hi = std::min<uint64_t>(words, lo + wpb);
         for (uint64_t w = lo + threadIdx.x; w < hi; w += blockDim.x) c += (unsigned long long)__popcll(inv64[w]);
@@ -1992,6 +2082,7 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
     const uint64_t f_lo = std::min<uint64_t>(a.ext_words, blockIdx.x * tpb * kFoldWords);
     const uint64_t f_hi = std::min<uint64_t>(a.ext_words, f_lo + tpb * kFoldWords);
     if (folded) {
+        static_assert((kChunkEmitCap + 8) * 4 >= kFoldWords * 8, "a fold tile's words fit the coop wave's LDS");
         unsigned long long* s_fw = reinterpret_cast<unsigned long long*>(s_x);   // kFoldWords words
         __shared__ uint32_t s_fa[kMaxHotClasses + 1], s_fo[kMaxHotClasses + 1];
         for (uint64_t t = blockIdx.x * tpb; t < std::min<uint64_t>(tiles, (blockIdx.x + 1) * tpb); ++t)
@@ -2603,7 +2694,8 @@ hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true, uint3
         const uint64_t words = ((uint64_t)g->ext_handles + 63) / 64;
         const uint32_t tiles = (uint32_t)((words + kFoldWords - 1) / kFoldWords);
         unsigned long long* st = g->fold_status;
-        hipLaunchKernelGGL(k_final_count, dim3(std::max<uint32_t>(tiles, kStats)), dim3(kBlock), 0, g->stream, inv64, words,
+        const uint32_t Gc = std::max<uint32_t>(std::min<uint32_t>(tiles, kFoldBlocks), kStats);
+        hipLaunchKernelGGL(k_final_count, dim3(Gc), dim3(kBlock), 0, g->stream, inv64, words,
                            (uint64_t)kFoldWords, st, g->ctr, (const unsigned long long*)g->blk_stats, ids ? 0 : 1, g->done, f);
         if (ids) {
             const uint32_t G = std::min<uint32_t>(kFinalBlocks, tiles), spb = (tiles + G - 1) / G;
