@@ -397,6 +397,7 @@ struct fgi_graph {
     bool ids_valid = false;            // inv holds the last wave's list (else ensure_ids rebuilds it)
     int last_levels = 4;               // non-empty levels of the last wave (sizes the first level group)
     int last_head = 4;                 // levels up to the last one the tail cannot run (pull, or large push)
+    std::vector<uint8_t> last_dirs;    // the last synchronous wave's levels: 1 pull, 0 push (k_collect grids)
     int last_mid = 3;                  // k_level launches the last fused wave needed (its mid pairs)
     int fused_per_cu = 0;              // resident k_wave_fused blocks per CU (0: not queried yet)
     bool coop_warm = false;            // a cooperative launch has run (coop_warm)

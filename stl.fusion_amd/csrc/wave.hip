@@ -122,8 +122,13 @@ __device__ __forceinline__ unsigned long long imm_word(unsigned long long w) {
 }
 
 // One visit of node h (word w, version already matched): a single atomicOr on the visit bitmap.
+// A plain read first: a bit already set (an earlier level's visit, or another block's in this one that
+// has reached L2) needs no atomic. Within a launch the bits only go from 0 to 1, so a stale read can only
+// show 0, and then the atomic decides; hub slots that many edges of a level reach stop contending on one
+// word (level 0 of configs[1]: 4,096 degree-weighted roots, 125 k edges onto a few thousand hubs).
 __device__ __forceinline__ int visit_bit(uint32_t* vis, uint32_t h, unsigned long long w) {
     const uint32_t b = 1u << (h & 31);
+    if (vis[h >> 5] & b) return 0;
     if (atomicOr(vis + (h >> 5), b) & b) return 0;
     return first_visit(w);
 }
@@ -1829,9 +1834,21 @@ __global__ __launch_bounds__(kBlock) void k_final_count(const unsigned long long
 // The list: block t writes the set bits of its words [t * wpb, + wpb) of inv64 (the boundary's bitmap:
 // the labels' own, or xbm) in ascending order, after the sum of the counts of the status entries
 // before its own (spb entries per block: 1, or its fold tiles).
+// With pub (a synchronous wave's list, run_wave): the last block to finish also publishes the wave's
+// counters to fine-grained host memory and then the sequence word (k_publish's protocol, one launch
+// fewer). The asynchronous waves keep k_publish: their ids are read by other streams after the wait, so
+// the word must follow the whole kernel.
+struct ListPub {
+    unsigned long long* dst;   // null: no publish
+    unsigned long long seq;
+    unsigned long long* done;
+    uint32_t words;
+};
+
 __global__ __launch_bounds__(kBlock) void k_final_write(const unsigned long long* __restrict__ inv64, uint64_t words,
                                                         uint64_t wpb, const unsigned long long* __restrict__ status,
-                                                        WaveCtr* ctr, uint32_t* out, int need_done, uint32_t spb) {
+                                                        WaveCtr* ctr, uint32_t* out, int need_done, uint32_t spb,
+                                                        ListPub pub) {
     if (need_done && ctr->phase != kPhaseDone) return;   // a fused wave whose tail stopped early: not yet
     __shared__ unsigned long long s_red[kBlock / 64];
     __shared__ unsigned long long s_wbase[kBlock / 64];
@@ -1869,6 +1886,14 @@ __global__ __launch_bounds__(kBlock) void k_final_write(const unsigned long long
         for (uint32_t i = lane; i < tot; i += 64) out[run + i] = s_stage[wid][i];
         __builtin_amdgcn_wave_barrier();
         run += tot;
+    }
+    if (pub.dst && last_block_arrive<true>(pub.done, gridDim.x)) {
+        if (threadIdx.x == 0) pub.dst[pub.words + 1] = wall_clock64();
+        unsigned long long* src = reinterpret_cast<unsigned long long*>(ctr);
+        for (uint32_t i = threadIdx.x; i < pub.words; i += blockDim.x) pub.dst[i] = coh_read(src + i);
+        __threadfence_system();
+        __syncthreads();
+        if (threadIdx.x == 0) __hip_atomic_store(pub.dst + pub.words, pub.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -2655,6 +2680,18 @@ uint32_t collect_grid(const fgi_graph* g, const WaveParams& wp) {
     return std::max<uint32_t>(1, (wp.grid + W - 1) / W);
 }
 
+// Level L's collect grid: the full one unless the previous wave's directions say the collect has nothing
+// to do (level L pushes and level L - 1 did not pull); a small grid then still does everything if the
+// prediction is wrong (k_collect's loops stride over any grid), only slower. An empty launch of the full
+// grid costs ~3.8 us on configs[1] (profiles/r12c1).
+uint32_t collect_grid_at(const fgi_graph* g, const WaveParams& wp, int L) {
+    const uint32_t full = collect_grid(g, wp);
+    const std::vector<uint8_t>& d = g->last_dirs;
+    if (L < 0 || (size_t)L >= d.size()) return full;
+    const bool needed = d[L] || (L > 0 && d[L - 1]);
+    return needed ? full : std::min<uint32_t>(full, 4u);
+}
+
 PullArgs pull_args(fgi_graph* g, uint32_t n_slots, const uint32_t* front_rd) {
     PullArgs p;
     p.n_slots = n_slots;
@@ -2686,7 +2723,8 @@ ExpandArgs expand_args(fgi_graph* g, int buf) {
 }
 
 // the invalidated bitmap -> V_inv (ctr->inv) and, with ids, the invalidated list
-hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true, uint32_t* out = nullptr) {
+hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true, uint32_t* out = nullptr, ListPub pub = ListPub{}) {
+    if (!ids) pub.dst = nullptr;   // no list kernel: the caller publishes
     if (!out) out = g->inv;
     const auto* inv64 = reinterpret_cast<const unsigned long long*>(g->inv_bm);
     const FoldArgs f = fold_args(g);
@@ -2701,7 +2739,7 @@ hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true, uint3
             const uint32_t G = std::min<uint32_t>(kFinalBlocks, tiles), spb = (tiles + G - 1) / G;
             const uint32_t G2 = (tiles + spb - 1) / spb;
             hipLaunchKernelGGL(k_final_write, dim3(G2), dim3(kBlock), 0, g->stream, (const unsigned long long*)g->xbm, words,
-                               (uint64_t)spb * kFoldWords, (const unsigned long long*)st, g->ctr, out, 0, spb);
+                               (uint64_t)spb * kFoldWords, (const unsigned long long*)st, g->ctr, out, 0, spb, pub);
         }
         return hipGetLastError();
     }
@@ -2714,7 +2752,7 @@ hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true, uint3
                        (const unsigned long long*)g->blk_stats, ids ? 0 : 1, g->done, FoldArgs{});
     if (ids)
         hipLaunchKernelGGL(k_final_write, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb,
-                           (const unsigned long long*)st, g->ctr, out, 0, 1u);
+                           (const unsigned long long*)st, g->ctr, out, 0, 1u, pub);
     return hipGetLastError();
 }
 
@@ -3069,7 +3107,7 @@ static fgi_status run_wave_fused(fgi_graph* g, uint32_t n_roots, const uint32_t*
         if (g->want_ids) {
             const auto* inv64 = reinterpret_cast<const unsigned long long*>(g->inv_bm);
             hipLaunchKernelGGL(k_final_write, dim3(a.fin_G), dim3(kBlock), 0, s, inv64, words, a.fin_wpb,
-                               (const unsigned long long*)a.status, g->ctr, g->inv, 1, 1u);
+                               (const unsigned long long*)a.status, g->ctr, g->inv, 1, 1u, ListPub{});
         }
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
@@ -3240,6 +3278,17 @@ float wall_ms(fgi_graph* g, uint64_t t0, uint64_t t1) {
 
 namespace {
 
+// The same wait when the wave's list kernel published the counters itself (launch_final with a ListPub of
+// sequence `seq`): the end marker is recorded behind that kernel.
+static fgi_status counters_published(fgi_graph* g, hipStream_t s, bool mark, unsigned long long seq) {
+    if (mark) FGI_HIP(g, hipEventRecord(g->ev_w1, s));
+    FGI_TRY(wait_word(g, s, g->ctr_pub + kPubWords, seq));
+    g->last_pub_t = g->ctr_pub[kPubWords + 1];
+    memcpy(g->ctr_host, g->ctr_pub, sizeof(WaveCtr));
+    if (mark) FGI_HIP(g, hipEventSynchronize(g->ev_w1));
+    return FGI_OK;
+}
+
 static fgi_status counters_to_host(fgi_graph* g, hipStream_t s, bool mark) {
 #if FGI_SPIN_WAIT
     if (mark) FGI_HIP(g, hipEventRecord(g->ev_w1, s));
@@ -3320,6 +3369,8 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     const bool use_tail = tail_edges != 0 && g->last_levels >= g->last_head + 2;
     int group = use_tail ? std::min(8, std::max(1, g->last_head)) : std::min(8, std::max(2, g->last_levels));
     int L = 0, head = 1;
+    std::vector<uint8_t> dirs;   // this wave's directions (the next wave's collect grids)
+    bool dirs_ok = true;
     uint64_t levels = 0, e_trav = 0, f_total = 0, pull_levels = 0;
     double expand_ms = 0, pull_ms = 0, tail_ms = 0;
     uint64_t expand_launches = 0, expand_edges = 0, expand_f = 0, pull_launches = 0, syncs = 0;
@@ -3332,7 +3383,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         if (!allow_pull) wp.direction = 1;
         for (int k = 0; k < group; ++k, ++L) {
             const int buf = L & 1;
-            hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp,
+            hipLaunchKernelGGL(k_collect, dim3(collect_grid_at(g, wp, L)), dim3(kCollectThreads), 0, s, L, g->ctr, wp,
                                collect_args(g, g->n_slots, wp, buf), collect_args(g, g->n_slots, wp, buf), ~0ull);
             if (timing) {
                 while (g->ev.size() < 2 * (size_t)(L + 1) + 2) {
@@ -3361,12 +3412,20 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
             hipLaunchKernelGGL(k_wave_tail, dim3(kTailBlocks), dim3(kBlock), 0, s, ta);
             if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L + 1], s));
         }
-        FGI_HIP(g, launch_final(g, g->n_handles, g->want_ids));   // idempotent: repeated if the wave goes on
+        // the list kernel may publish the counters itself (one launch fewer), but its last block's
+        // system-scope release then writes back the whole list first: 11.6 -> 33.7 us for configs[1]'s
+        // k_final_write, 0.231 -> 0.262 ms/step (profiles/r12c); measurement only (FGI_LIST_PUBLISH=1)
+        static const bool list_pub = getenv("FGI_LIST_PUBLISH") && getenv("FGI_LIST_PUBLISH")[0] == '1';
+        const bool merged = FGI_SPIN_WAIT && g->want_ids && list_pub;
+        ListPub lp{};
+        if (merged) lp = ListPub{g->ctr_pub, ++g->pub_seq, g->done, (uint32_t)kPubWords};
+        FGI_HIP(g, launch_final(g, g->n_handles, g->want_ids, nullptr, lp));   // idempotent: repeated if the wave goes on
         final_done = true;
         FGI_HIP(g, hipGetLastError());
         // the wave's end marker rides on the group's synchronisation (re-recorded if the wave goes on):
         // recording it after the wait would cost the call a further device round trip
-        FGI_TRY(counters_to_host(g, s, events));
+        if (merged) FGI_TRY(counters_published(g, s, events, lp.seq));
+        else FGI_TRY(counters_to_host(g, s, events));
         ++syncs;
         if (use_tail && g->ctr_host->broken) {   // half a wave is applied: poisoned until fgi_restore (fgi.h)
             FGI_HIP(g, hipMemsetAsync(g->gbar + kGbarTail, 0, sizeof(unsigned long long), s));
@@ -3388,6 +3447,12 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                 fprintf(stderr, "[fgi] level %d push (tail): frontier %llu edges %llu chunk x%llu\n", l,
                         (unsigned long long)lvl_F(lc), (unsigned long long)lvl_T(lc), (unsigned long long)lc.mult);
             }
+        }
+        if (ring_ok) {
+            dirs.resize(std::max<size_t>(dirs.size(), (size_t)stop), 0);
+            for (int l = L0; l < L; ++l) dirs[l] = g->ctr_host->lvl[l % kRing].pull ? 1 : 0;
+        } else {
+            dirs_ok = false;
         }
         for (int l = L0; l < L && ring_ok; ++l) {
             const LevelCtr& lc = g->ctr_host->lvl[l % kRing];
@@ -3468,6 +3533,8 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     if (n_roots) {
         g->last_levels = (int)std::max<uint64_t>(levels, 1);
         g->last_head = head;
+        if (dirs_ok) g->last_dirs.swap(dirs);
+        else g->last_dirs.clear();
     }
     const WaveCtr& c = *g->ctr_host;
     if (trace)
@@ -3559,7 +3626,7 @@ fgi_status run_wave_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_
         launch_roots(g, n_roots, roots_dev, imm_dev, 0u, g->n_handles, 0, true);
         for (int L = 0; L < group; ++L) {
             const int buf = L & 1;
-            hipLaunchKernelGGL(k_collect, dim3(collect_grid(g, wp)), dim3(kCollectThreads), 0, s, L, g->ctr, wp,
+            hipLaunchKernelGGL(k_collect, dim3(collect_grid_at(g, wp, L)), dim3(kCollectThreads), 0, s, L, g->ctr, wp,
                                collect_args(g, g->n_slots, wp, buf), collect_args(g, g->n_slots, wp, buf), ~0ull);
             hipLaunchKernelGGL(k_level<false>, dim3(wp.grid), dim3(kBlock), 0, s, L, wp, expand_args(g, buf),
                                expand_args(g, buf), pull_args(g, g->n_slots, g->inv_bm), node, g->vis_bm,
