@@ -116,7 +116,7 @@ typedef struct fgi_wave_stats {
     uint64_t pull_launches;    /* k_pull launches (every level of a wave that may pull) */
     /* fused waves: the head and tail launches that run the roots, the small push levels,
        the collect after a pull level and the final count inside one persistent grid each */
-    uint64_t fused_launches;   /* head / tail launches */
+    uint64_t fused_launches;   /* persistent launches: the wave tail (k_wave_tail), or a fused wave's head / tail */
     double fused_ms;           /* their summed device time (HIP events, FGI_OPT_LEVEL_TIMING) */
     uint64_t fused_push_bytes; /* algorithmic bytes of the push levels they ran (20 B per edge + 40 B
                                   per frontier entry, as a k_level push) */

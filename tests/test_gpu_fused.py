@@ -69,7 +69,9 @@ def test_fused_modes_rmat(pkg, gpu_available, stale):
                     if mode == 1 and rep == 1:
                         assert ws.host_syncs == 1, (key, ws.host_syncs)
                 else:
-                    assert ws.fused_launches == 0, key
+                    # level groups: fused_launches counts the wave tail's persistent launches (k_wave_tail,
+                    # at most one per group), never more than the host synchronisations
+                    assert ws.fused_launches <= ws.host_syncs, key
                 v, f = g.dump_states()
                 assert np.array_equal(v[:n], ov) and np.array_equal(f[:n], of), key
     g.close()
