@@ -834,6 +834,10 @@ __device__ __forceinline__ uint32_t lds_upper_bound(const uint32_t* s, uint32_t 
     return lo;
 }
 
+// measured slower on configs[1] (0.2354-0.2362 against 0.2333-0.2340 ms/step off, one box,
+// profiles/r11_tail_ab.txt r12f): off by default, FGI_PUSH_SMALL=<edges> for measurement
+constexpr uint64_t kPushSmallMax = 0;
+
 struct ExpandArgs {
     const uint32_t* __restrict__ fr_off;
     const uint64_t* __restrict__ escan;
@@ -841,6 +845,10 @@ struct ExpandArgs {
     const uint32_t* __restrict__ pool_col;
     const uint64_t* __restrict__ pool_tag;
     int dead_filter;
+    // levels of fewer edges (a measurement knob, FGI_PUSH_SMALL): no separate dead-edge filter trip
+    // (visited targets are caught by the visit's plain read) and the winners' rows gathered with the
+    // tags, speculatively (12 B per matched edge). 0: never (the default)
+    uint64_t small_max = kPushSmallMax;
 };
 
 // PART: multi-GPU rank — dependant slots outside [ra.base, ra.base + ra.n_local) are remote: their
@@ -922,7 +930,8 @@ __device__ __forceinline__ void expand_level(int L, uint64_t F, uint64_t T, uint
         // edges to nodes visited earlier need neither the tag nor the gather (the bitmap is read
         // without synchronisation: a stale 0 only costs the gather and an atomic that finds the bit).
         // Kept on small levels too (make variant-filtermin measures the alternative)
-        if (x.dead_filter && T >= (uint64_t)FGI_FILTER_MIN) {
+        const bool small = T < x.small_max;   // level-uniform
+        if (x.dead_filter && T >= (uint64_t)FGI_FILTER_MIN && !small) {
 #pragma unroll
             for (int j = 0; j < kEPT; ++j)
                 if (dst[j] != 0xFFFFFFFFu && bit_of(vis, dst[j])) dst[j] = 0xFFFFFFFFu;
@@ -933,13 +942,20 @@ __device__ __forceinline__ void expand_level(int L, uint64_t F, uint64_t T, uint
         PROBE(L, 5);
         uint64_t tag[kEPT];
         unsigned long long w[kEPT];
+        uint32_t rl[kEPT], ro[kEPT];
 #pragma unroll
         for (int j = 0; j < kEPT; ++j) {
             tag[j] = 0;
             w[j] = 0;
+            rl[j] = 0;
+            ro[j] = 0;
             if (dst[j] != 0xFFFFFFFFu) {
                 tag[j] = __builtin_nontemporal_load(x.pool_tag + pos[j]);
                 w[j] = node[dst[j]];
+                if (small) {
+                    rl[j] = o.row_len[dst[j]];
+                    ro[j] = (uint32_t)o.row_off[dst[j]];   // pool positions are < 2^32
+                }
             }
         }
         uint32_t win_mask = 0;
@@ -953,16 +969,18 @@ __device__ __forceinline__ void expand_level(int L, uint64_t F, uint64_t T, uint
             }
         }
         // a winner's invalidated bit and its row, requested as soon as its visit has returned (the
-        // flush then needs no gather round trip)
-        uint32_t rl[kEPT], ro[kEPT];
+        // flush then needs no gather round trip); a small level has its rows already
 #pragma unroll
         for (int j = 0; j < kEPT; ++j) {
-            rl[j] = 0;
-            ro[j] = 0;
             if ((win_mask >> j) & 1u) {
                 mark_invalidated(o.inv_bm, dst[j]);
-                rl[j] = o.row_len[dst[j]];
-                ro[j] = (uint32_t)o.row_off[dst[j]];   // pool positions are < 2^32
+                if (!small) {
+                    rl[j] = o.row_len[dst[j]];
+                    ro[j] = (uint32_t)o.row_off[dst[j]];   // pool positions are < 2^32
+                }
+            } else {
+                rl[j] = 0;
+                ro[j] = 0;
             }
         }
         // the chunk's winners (at most cedges) are staged over the chunk map, flushed before the
@@ -2252,23 +2270,38 @@ struct TailArgs {
 // the host need not read them from the level ring, which a tail of more than kRing levels rolls over:
 // WaveCtr n_levels / e_trav / f_total / n_pull over the non-empty levels, push_edges / push_f over
 // the push levels, mid_push_edges / mid_push_f over those the tail ran, t_max the largest level's edges.
-__device__ __forceinline__ void tail_account(WaveCtr* c, uint64_t F, uint64_t T, bool pull, bool in_tail) {
-    if (!F) return;
-    c->n_levels += 1;
-    c->e_trav += T;
-    c->f_total += F;
-    if (pull) {
-        c->n_pull += 1;
-    } else {
-        c->push_edges += T;
-        c->push_f += F;
+// Summed in registers over the launch and added to the counters once at its end.
+struct TailSums {
+    unsigned long long n = 0, e = 0, f = 0, np = 0, pe = 0, pf = 0, te = 0, tf = 0, tmax = 0;
+    __device__ void add(uint64_t F, uint64_t T, bool pull, bool in_tail) {
+        if (!F) return;
+        n += 1;
+        e += T;
+        f += F;
+        if (pull) {
+            np += 1;
+        } else {
+            pe += T;
+            pf += F;
+        }
+        if (in_tail) {
+            te += T;
+            tf += F;
+        }
+        if (T > tmax) tmax = T;
     }
-    if (in_tail) {
-        c->mid_push_edges += T;
-        c->mid_push_f += F;
+    __device__ void commit(WaveCtr* c) const {
+        c->n_levels += n;
+        c->e_trav += e;
+        c->f_total += f;
+        c->n_pull += np;
+        c->push_edges += pe;
+        c->push_f += pf;
+        c->mid_push_edges += te;
+        c->mid_push_f += tf;
+        if (tmax > c->t_max) c->t_max = tmax;
     }
-    if (T > c->t_max) c->t_max = T;
-}
+};
 
 __global__ __launch_bounds__(kBlock) void k_wave_tail(TailArgs a) {
     __shared__ __align__(16) uint32_t s_x[kChunkEmitCap + 8];
@@ -2280,12 +2313,27 @@ __global__ __launch_bounds__(kBlock) void k_wave_tail(TailArgs a) {
     __shared__ unsigned long long s_ft;
     WaveCtr* ctr = a.ctr;
     auto grid_sync = [&]() -> bool { return soft_grid_sync(a.gbar, &ctr->broken, nullptr, a.bar_timeout, false, 1); };
-    // the wave's totals (WaveCtr n_levels ..): the group's levels, read before the ring rolls over
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-        for (int l = a.grp0; l < a.L0; ++l) {
-            const LevelCtr& g = ctr->lvl[l % kRing];
-            tail_account(ctr, lvl_F(g), lvl_T(g), g.pull != 0, false);
+    // the wave's totals (WaveCtr n_levels ..): the group's levels, read before the ring rolls over — one
+    // level per lane of block 0's first wave, every load in flight together, then lane 0 adds them up
+    TailSums acc;
+    if (blockIdx.x == 0 && threadIdx.x < 64) {
+        const int n = a.L0 - a.grp0;
+        for (int l0 = 0; l0 < n; l0 += 64) {
+            const int l = a.grp0 + l0 + (int)threadIdx.x;
+            uint64_t F = 0, T = 0, P = 0;
+            if (l < a.L0) {
+                const LevelCtr& g = ctr->lvl[l % kRing];
+                F = lvl_F(g);
+                T = lvl_T(g);
+                P = g.pull;
+            }
+            const int m = min(64, n - l0);
+            for (int k = 0; k < m; ++k) {   // lane 0 accounts for lane k's level (in level order)
+                const uint64_t Fk = __shfl(F, k, 64), Tk = __shfl(T, k, 64), Pk = __shfl(P, k, 64);
+                if (threadIdx.x == 0) acc.add(Fk, Tk, Pk != 0, false);
+            }
         }
+    }
     int L = a.L0;
     for (bool first = true;; ++L, first = false) {
         LevelCtr& lc = ctr->lvl[L % kRing];
@@ -2293,7 +2341,7 @@ __global__ __launch_bounds__(kBlock) void k_wave_tail(TailArgs a) {
         __syncthreads();
         const uint64_t F = lc.F ? lc.F : (s_ft >> 32), T = lc.F ? lc.T : (s_ft & 0xFFFFFFFFull);
         if (F == 0 || (!a.all && (level_pulls(ctr, L, a.wp, F, T) || T > a.max_edges))) break;
-        if (blockIdx.x == 0 && threadIdx.x == 0) tail_account(ctr, F, T, false, true);
+        if (blockIdx.x == 0 && threadIdx.x == 0) acc.add(F, T, false, true);
         if (first && L > 0 && ctr->lvl[(L + kRing - 1) % kRing].pull) {   // after a pull level: its frontier list
             collect_front(lc, a.wp.grid, a.col[L & 1], (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6),
                           (uint64_t)gridDim.x * (blockDim.x >> 6));
@@ -2315,9 +2363,15 @@ __global__ __launch_bounds__(kBlock) void k_wave_tail(TailArgs a) {
         emit_init(em);
         expand_level<false>(kProbeLevelsOff, F, T, level_mult_one_round(T, gridDim.x), a.x[buf], a.node, a.vis, o, em, s_x,
                             me, s_rel, s_base, a.blk, s_st, RemoteArgs{});
-        if (!grid_sync()) return;
+        if (!grid_sync()) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) acc.commit(ctr);
+            return;
+        }
     }
-    if (blockIdx.x == 0 && threadIdx.x == 0) ctr->cur = (unsigned long long)L;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        acc.commit(ctr);
+        ctr->cur = (unsigned long long)L;
+    }
 }
 
 #if FGI_VARIANTS   // measured slower than the level groups: variant builds only
@@ -2719,7 +2773,13 @@ PullArgs pull_args(fgi_graph* g, uint32_t n_slots, const uint32_t* front_rd) {
 }
 
 ExpandArgs expand_args(fgi_graph* g, int buf) {
-    return ExpandArgs{g->fr_off[buf], g->escan[buf], g->cstart[buf], g->pool_col, g->pool_tag, g->opt_dead_filter};
+    static const uint64_t small_max = [] {
+        const char* e = getenv("FGI_PUSH_SMALL");   // measurement: the small-level threshold (0 off)
+        return e && *e ? (uint64_t)strtoull(e, nullptr, 10) : kPushSmallMax;
+    }();
+    ExpandArgs x{g->fr_off[buf], g->escan[buf], g->cstart[buf], g->pool_col, g->pool_tag, g->opt_dead_filter};
+    x.small_max = small_max;
+    return x;
 }
 
 // the invalidated bitmap -> V_inv (ctr->inv) and, with ids, the invalidated list
