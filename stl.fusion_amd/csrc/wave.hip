@@ -2247,6 +2247,25 @@ __global__ __launch_bounds__(kBlock) void k_wave_coop(CoopArgs a) {
 // levels the wave's tail has (configs[1]: levels 4 and 5, four launches before), and a wave whose pull
 // levels fit the group never needs a second group (the asynchronous waves rely on that: max_edges = ~0).
 constexpr uint32_t kTailBlocks = 32;
+
+// measurement knobs: the tail's grid (FGI_TAIL_BLOCKS, default kTailBlocks; its blocks must be resident
+// together) and whether the push level after a pull stays in the group (FGI_TAIL_HEAD=1: the tail runs it,
+// with the collect of the pull's winners)
+static uint32_t tail_blocks(const fgi_graph* g) {
+    static const uint32_t env = [] {
+        const char* e = getenv("FGI_TAIL_BLOCKS");
+        return e && *e ? (uint32_t)atoi(e) : 0u;
+    }();
+    const uint32_t b = env ? env : kTailBlocks;
+    return std::max<uint32_t>(1, std::min<uint32_t>(b, (uint32_t)std::max(1, g->n_cu)));
+}
+static int tail_head_after_pull() {
+    static const int v = [] {
+        const char* e = getenv("FGI_TAIL_HEAD");
+        return e && e[0] == '1' ? 1 : 2;
+    }();
+    return v;
+}
 constexpr int kGbarTail = 8;   // g->gbar word of the tail's barrier (its own grid size)
 
 struct TailArgs {
@@ -3421,7 +3440,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         const char* e = getenv("FGI_TAIL");
         if (e && e[0] == '0') return 0ull;
         const char* m = getenv("FGI_TAIL_EDGES");
-        return m && *m ? (unsigned long long)strtoull(m, nullptr, 10) : (unsigned long long)kTailBlocks * kChunk;
+        return m && *m ? (unsigned long long)strtoull(m, nullptr, 10) : (unsigned long long)kTailBlocks * kChunk;   // by the default grid
     }();
     // the tail only where the previous wave had at least two levels past its head (a pull level and the
     // push level after it stay in the group: that level's collect scans the pull's winners, a full-grid
@@ -3469,7 +3488,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                 }
                 FGI_HIP(g, hipEventRecord(g->ev[2 * L], s));
             }
-            hipLaunchKernelGGL(k_wave_tail, dim3(kTailBlocks), dim3(kBlock), 0, s, ta);
+            hipLaunchKernelGGL(k_wave_tail, dim3(tail_blocks(g)), dim3(kBlock), 0, s, ta);
             if (timing) FGI_HIP(g, hipEventRecord(g->ev[2 * L + 1], s));
         }
         // the list kernel may publish the counters itself (one launch fewer), but its last block's
@@ -3516,7 +3535,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         }
         for (int l = L0; l < L && ring_ok; ++l) {
             const LevelCtr& lc = g->ctr_host->lvl[l % kRing];
-            if (lvl_F(lc) && (lc.pull || lvl_T(lc) > tail_edges)) head = l + 1 + (lc.pull ? 1 : 0);
+            if (lvl_F(lc) && (lc.pull || lvl_T(lc) > tail_edges)) head = l + (lc.pull ? tail_head_after_pull() : 1);
             float ms = 0;
             if (timing) {
                 // every k_level launch counts (empty levels too), so the average launch duration
@@ -3695,7 +3714,7 @@ fgi_status run_wave_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_
         }
         TailArgs ta = tail_args(g, 0, group, wp, ~0ull);
         ta.all = 1;
-        hipLaunchKernelGGL(k_wave_tail, dim3(kTailBlocks), dim3(kBlock), 0, s, ta);
+        hipLaunchKernelGGL(k_wave_tail, dim3(tail_blocks(g)), dim3(kBlock), 0, s, ta);
     } else {
         group = 0;
     }
@@ -3748,7 +3767,8 @@ fgi_status wave_wait(fgi_graph* g, uint64_t ticket, uint64_t* out_n, const uint3
         head = 1;
         for (uint64_t l = 0; l < (uint64_t)a.group; ++l) {
             const LevelCtr& lc = c.lvl[l % kRing];
-            if (lvl_F(lc) && (lc.pull || lvl_T(lc) > (uint64_t)kTailBlocks * kChunk)) head = l + 1 + (lc.pull ? 1 : 0);
+            if (lvl_F(lc) && (lc.pull || lvl_T(lc) > (uint64_t)tail_blocks(g) * kChunk))
+                head = l + (lc.pull ? tail_head_after_pull() : 1);
         }
     }
     a.n_inv = c.inv;
