@@ -154,9 +154,12 @@ constexpr uint32_t kInitBlocks = FGI_INIT_BLOCKS;   // grid of k_wave_init
 #endif
 constexpr uint32_t kHot = FGI_HOT;      // most hot list heads (pull probes through a snapshot of kHot / 8 B)
 #ifndef FGI_LDS_HOT
-#define FGI_LDS_HOT 2048                // measurement builds: make variant-ldshot LDSHOT=<words>
+#define FGI_LDS_HOT 4096                // measurement builds: make variant-ldshot LDSHOT=<words>
 #endif
-constexpr uint32_t kLdsHot = FGI_LDS_HOT;   // hot snapshot words a pull block keeps in LDS (8 KB)
+// hot snapshot words a pull block keeps in LDS (16 KB): 4,096 against 2,048 measured -1% on configs[1]
+// and -2% on configs[2] with hub-first labels; 8,192 pulls faster still but its lower occupancy makes
+// the push levels 4x slower (round 5, profiles/r12i_ldshot_ab.txt)
+constexpr uint32_t kLdsHot = FGI_LDS_HOT;
 // fewest hot heads: 8 KB, or what the LDS copy holds (a graph's count: build_candidates, hot_count)
 constexpr uint32_t kHotMin = kLdsHot * 32 > 65536 ? kLdsHot * 32 : 65536;
 // resident k_level blocks per CU: LDS-bound once the LDS snapshot passes 8 KB (160 KB per CU)
