@@ -6,8 +6,8 @@ Per wave kernel, over the timed steps only (the last `--steps` waves, each wave 
 k_roots dispatch): launches per wave, average launch duration (kernel trace), and per-launch PMC
 values from the separate counter passes. HBM traffic follows MI355X_MICROARCH.md §HBM:
 FETCH_SIZE (KiB) is doubled (gfx950 tallies 128-B requests at 64 B), WRITE_SIZE taken as is; the
-doubling is calibrated for 16-B/lane streams only, so for narrow gathers the figure is an upper
-bound. Usage: python profiles/summarize.py gpurun_out/prof_r02 r02 [--steps 5]
+doubling holds for the engine's narrow gathers too (profiles/r13e_fetch_calib.txt: one 128-B line
+request per miss for 4-B and 8-B gathers, 16-B streams and 256-B runs alike). Usage: python profiles/summarize.py gpurun_out/prof_r02 r02 [--steps 5]
 """
 import argparse
 import csv
