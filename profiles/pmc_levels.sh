@@ -10,9 +10,11 @@ OUT=$R/gpurun_out/pmcl_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 i=0
-for pmc in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
+# PMC_PASSES="A B;C D" replaces the default counter groups (one pass per ';'-separated group)
+if [ -n "${PMC_PASSES:-}" ]; then IFS=';' read -r -a passes <<< "$PMC_PASSES"; else passes=("SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SMEM" \
-           "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_ATOMIC_sum"; do
+           "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum" "TCC_EA0_ATOMIC_sum"); fi
+for pmc in "${passes[@]}"; do
     i=$((i+1))
     timeout -s KILL 150 rocprofv3 --pmc $pmc -T -d "$OUT/p$i" -o run --output-format csv -- \
         python3 "$R/profiles/wave_levels.py" "$CFG" > "$OUT/p$i.out" 2> "$OUT/p$i.err" || exit 30

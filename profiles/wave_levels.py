@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Per-level trace of the configs[1] wave (measurement only): builds R-MAT 24, runs a few waves with
 FGI_TRACE=1 (the engine prints each level's direction, frontier, edges, chunking and k_level time,
-and the wave's pull statistics to stderr).  Usage: FGI_TRACE=1 python profiles/wave_levels.py"""
+and the wave's pull statistics to stderr).  Usage: FGI_TRACE=1 [WL_OPTS=1=0,...] python profiles/wave_levels.py [config]"""
 import os
 import sys
 
@@ -20,6 +20,9 @@ g = pkg.Graph(W.n_slots(cfg))
 W.build(g, cfg)
 roots = W.roots_for(g, cfg)
 d_roots = torch.from_numpy(roots.astype(np.int32)).cuda()
+for kv in filter(None, os.environ.get("WL_OPTS", "").split(",")):   # option=value pairs (fgi.h FGI_OPT_*)
+    k, v = kv.split("=")
+    g.set_option(int(k), int(v))
 g.snapshot()
 for k in range(3):
     g.restore()
