@@ -163,7 +163,11 @@ constexpr uint32_t kLdsHot = FGI_LDS_HOT;
 // fewest hot heads: 8 KB, or what the LDS copy holds (a graph's count: build_candidates, hot_count)
 constexpr uint32_t kHotMin = kLdsHot * 32 > 65536 ? kLdsHot * 32 : 65536;
 // resident k_level blocks per CU: LDS-bound once the LDS snapshot passes 8 KB (160 KB per CU)
+#ifdef FGI_LEVEL_OCC
+constexpr uint32_t kLevelOcc = FGI_LEVEL_OCC;   // measurement builds (variant-cpl)
+#else
 constexpr uint32_t kLevelOcc = kLdsHot <= 2048 ? 5 : kLdsHot <= 4096 ? 4 : 3;
+#endif
 constexpr int kAccCount = 8;            // batch accumulators (fgi_run_batch; run_wave_coop's acc)
 // A batch's abort word (fgi_run_batch): reason << 32 | (step + 1). kAbortBarrier: a cascade's grid
 // barrier timed out (no step index; the graph is poisoned until fgi_restore).

@@ -1036,11 +1036,18 @@ struct PullArgs {
 // queued in LDS and scanned at the wave's flush (pull_tails). Candidates neither hit nor queued,
 // and queued ones whose scan found nothing, are this level's survivors.
 constexpr uint32_t kMaxIter = 32;           // tiles per pull block (kMaxIter * kPullTile slots)
-constexpr uint32_t kTailCap = kChunk;       // queued candidates
+#ifndef FGI_CPL
+#define FGI_CPL 4          // measurement builds: make variant-cpl CPL=<candidates per lane> TCAP=<queue words>
+#endif
+#ifndef FGI_TAIL_CAP
+#define FGI_TAIL_CAP kChunk
+#endif
+constexpr uint32_t kCPL = FGI_CPL;          // candidates per lane per step
+constexpr uint32_t kTailCap = FGI_TAIL_CAP; // queued candidates
 constexpr uint32_t kTileWords = kPullTile / 64;
 constexpr uint32_t kOwnWords = 2 * kMaxIter * kTileWords;   // owned 32-bit bitmap words
-constexpr uint32_t kCandBatch = 4 * kBlock; // candidates per block step (4 per lane)
-constexpr uint32_t kWaveBatch = 4 * 64;     // a wave's run per step
+constexpr uint32_t kCandBatch = kCPL * kBlock; // candidates per block step (kCPL per lane)
+constexpr uint32_t kWaveBatch = kCPL * 64;     // a wave's run per step
 constexpr uint32_t kWaveTailCap = kTailCap / (kBlock / 64);   // queued candidates per wave
 constexpr uint32_t kLaneTail = 12;          // lists a lane scans alone in a tail pass (entries 4..11)
 
@@ -1056,11 +1063,12 @@ struct PullLds {
 };
 
 // k_level's LDS (32-bit words): push — the chunk map, then the chunk's winners; pull — the tail queue
-// (kTailCap) and PullLds at kChunk + 4
+// (kTailCap) and PullLds at kTailCap + 4
 // the multi-GPU push's per-owner staging (MsgEmit<true>) follows the push region
 constexpr uint32_t kPushLds = kChunkEmitCap + 8;
 constexpr uint32_t kLevelLds =
-    std::max<uint32_t>(kPushLds + (sizeof(MsgEmit<true>) + 7) / 8 * 2, kChunk + 4 + (sizeof(PullLds) + 3) / 4);
+    std::max<uint32_t>(kPushLds + (sizeof(MsgEmit<true>) + 7) / 8 * 2, kTailCap + 4 + (sizeof(PullLds) + 3) / 4);
+static_assert(kTailCap % 4 == 0 && kWaveBatch <= kTailCap / (kBlock / 64), "pull tail queue");
 
 // a thread's winners: count, those with a non-empty row, their row lengths
 struct WinSum {
@@ -1268,9 +1276,9 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
     uint32_t* const wl_out = p.wl + seg;       // this level's expandable winners
     // the first batch's entries are requested before the owned words are staged
     // (FGI_PULL_PREFETCH=0 builds the variant without the look-ahead, for measurement)
-    uint4 c[4];
+    uint4 c[kCPL];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
+    for (int j = 0; j < (int)kCPL; ++j) {
         const uint32_t i = (threadIdx.x >> 6) * kWaveBatch + j * 64 + lane;
         c[j] = load_cand(src + seg + i, i < cnt, (uint32_t)s_lo);
     }
@@ -1320,10 +1328,10 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
     uint32_t* wq = lds_q + wid * kWaveTailCap;
     uint32_t qn = 0;
     for (uint32_t base = wid * kWaveBatch; base < cnt; base += kCandBatch) {   // wave-uniform
-        bool lv[4];
-        uint32_t f0[4], f1[4];
+        bool lv[kCPL];
+        uint32_t f0[kCPL], f1[kCPL];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < (int)kCPL; ++j) {
             const bool in = base + j * 64 + lane < cnt;
             const uint32_t rel = c[j].x - (uint32_t)s_lo;
 #if FGI_EXP & 8
@@ -1339,9 +1347,9 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
             f1[j] = (lv[j] && c[j].w != FGI_NONE) ? head_bits(p, s, c[j].w, sum) : 0u;
 #endif
         }
-        uint4 cn[4];
+        uint4 cn[kCPL];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < (int)kCPL; ++j) {
 #if FGI_PULL_PREFETCH
             const uint32_t i = base + kCandBatch + j * 64 + lane;
 #else
@@ -1350,7 +1358,7 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
             cn[j] = load_cand(src + seg + i, i < cnt, (uint32_t)s_lo);
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < (int)kCPL; ++j) {
             const uint32_t i = base + j * 64 + lane;
             const uint32_t d = c[j].x, h0 = c[j].z, h1 = c[j].w, aux = c[j].y;
             const bool b0 = lv[j] && ((f0[j] >> (h0 & 31)) & 1u);
@@ -1407,7 +1415,7 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
             qn = 0;
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < (int)kCPL; ++j) {
 #if FGI_PULL_PREFETCH
             c[j] = cn[j];
 #else
@@ -1489,7 +1497,7 @@ __global__ __launch_bounds__(kBlock, kLevelOcc) void k_level(int Larg, WaveParam
     MsgEmit<PART>& me = *reinterpret_cast<MsgEmit<PART>*>(s_x + kPushLds);   // push levels only
     __shared__ unsigned long long s_st[kBlock / 64][kStats];
     __shared__ unsigned long long s_red[kBlock / 64];
-    static_assert(sizeof(PullLds) <= (kLevelLds - kChunk - 4) * 4 && kTailCap <= kChunk, "pull LDS");
+    static_assert(sizeof(PullLds) <= (kLevelLds - kTailCap - 4) * 4, "pull LDS");
     static_assert(kPushLds % 2 == 0 && (kPushLds + sizeof(MsgEmit<true>) / 4) <= kLevelLds, "push LDS");
     const bool fused = FGI_VARIANTS && !PART && Larg < 0;
     const int L = mid_level(ctr, Larg);
@@ -1527,7 +1535,7 @@ __global__ __launch_bounds__(kBlock, kLevelOcc) void k_level(int Larg, WaveParam
     if (pull) {
         unsigned long long bs[3] = {0, 0, 0};
         const bool sum = FGI_VARIANTS && p.sum != nullptr && lc.sum != 0;
-        pull_level(L, p, wp, npull, sum, node, vis, s_rel, *reinterpret_cast<PullLds*>(s_base), blk, s_st, bs);
+        pull_level(L, p, wp, npull, sum, node, vis, s_rel, *reinterpret_cast<PullLds*>(s_x + kTailCap + 4), blk, s_st, bs);
         PROBE(L, 4);
         pull_epilogue(L, p, o.ln, done, bs, s_red, fused ? &ctr->cur : nullptr);
         return;
