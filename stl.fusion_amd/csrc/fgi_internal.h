@@ -161,7 +161,11 @@ constexpr uint32_t kHot = FGI_HOT;      // most hot list heads (pull probes thro
 // the push levels 4x slower (round 5, profiles/r12i_ldshot_ab.txt)
 constexpr uint32_t kLdsHot = FGI_LDS_HOT;
 // fewest hot heads: 8 KB, or what the LDS copy holds (a graph's count: build_candidates, hot_count)
+#ifdef FGI_HOT_MIN
+constexpr uint32_t kHotMin = FGI_HOT_MIN;   // measurement builds (variant-cpl HOTMIN=)
+#else
 constexpr uint32_t kHotMin = kLdsHot * 32 > 65536 ? kLdsHot * 32 : 65536;
+#endif
 // resident k_level blocks per CU: LDS-bound once the LDS snapshot passes 8 KB (160 KB per CU)
 #ifdef FGI_LEVEL_OCC
 constexpr uint32_t kLevelOcc = FGI_LEVEL_OCC;   // measurement builds (variant-cpl)
