@@ -349,7 +349,7 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *                            a per-wave bitmap (E_match then counts examined edges only)
  *   FGI_OPT_DIRECTION   [0]  0 auto (push/pull per level), 1 push only, 2 pull only
  *   FGI_OPT_PULL_ALPHA  [28] auto: pull when frontier edges > total edges / alpha
- *   FGI_OPT_PULL_BETA   [24] auto: after a pull level, pull again while the frontier holds more
+ *   FGI_OPT_PULL_BETA   [32] auto: after a pull level, pull again while the frontier holds more
  *                            than n_slots / beta nodes (0: the alpha rule only)
  *   FGI_OPT_LEVEL_TIMING [1] with a stats argument, time every level's traversal launch with HIP
  *                            events (per-kernel figures for the roofline); 0 keeps only the

@@ -494,7 +494,7 @@ struct fgi_graph {
     uint32_t* sum_bm = nullptr;
     int64_t opt_sum_min = -1;         // fewest 64-bit bitmap words for a summary (-1: never; measured
                                       // slower on configs[2])
-    int opt_pull_beta = 24;           // after a pull, pull again while the frontier exceeds n / beta
+    int opt_pull_beta = 32;           // after a pull, pull again while the frontier exceeds n / beta
     int opt_level_timing = 1;         // HIP events around each level's k_level launch (statistics)
     int opt_fused = fgi::fused_default();  // FGI_OPT_FUSED (kFused* bits)
 
