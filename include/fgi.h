@@ -380,7 +380,11 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
  *                            cascade launched from now (fgi_run_batch), block b - 1 leaves at its first
  *                            grid barrier without arriving, and that cascade's barrier times out after
  *                            20 ms: the failure path runs deterministically (FGI_EDEVICE, then the
- *                            poisoned graph) */
+ *                            poisoned graph)
+ *   FGI_OPT_FAULT_INJECT_TAIL [0] tests only: the same for the (k+1)-th wave tail (the persistent
+ *                            launch that runs a wave's last small push levels, synchronous or
+ *                            asynchronous waves): fgi_invalidate* / fgi_wave_wait return FGI_EDEVICE and
+ *                            the graph is poisoned until fgi_restore */
 #define FGI_OPT_DEAD_FILTER 1
 #define FGI_OPT_DIRECTION 2
 #define FGI_OPT_PULL_ALPHA 3
@@ -394,6 +398,7 @@ fgi_status fgi_stream(fgi_graph* g, void** stream);
 #define FGI_OPT_FAULT_INJECT 11
 #define FGI_OPT_PART_PLAN 13
 #define FGI_OPT_PART_BUCKET 14
+#define FGI_OPT_FAULT_INJECT_TAIL 16
 /* 12 and 15: the measurement variants' options (include/fgi_variants.h); FGI_ENOTSUP here */
 fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value);
 

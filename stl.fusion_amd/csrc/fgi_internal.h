@@ -329,6 +329,7 @@ struct fgi_graph {
     uint32_t lbl_hot = 0;              // hot labels in use (<= lbl_K), set at the first bulk edge load
     int opt_labels = 0;                // fgi_config.labels: 0 auto, 1 always, -1 never
     bool lbl_done = false;             // the hot set has been chosen (first bulk edge load)
+    bool nodes_written = false;        // node words were written since create (note_words): at labels, if any
     uint32_t* s2l = nullptr;           // [ext_slots] hot label of a slot, FGI_NONE if cold
     uint32_t* l2s = nullptr;           // [lbl_K] slot of a hot label
     uint32_t* fold_start = nullptr;    // [fold_tiles + 1][lbl_ncls] first hot label of class c at slots >= t * kFoldTile
@@ -521,6 +522,8 @@ struct fgi_graph {
     int coop_per_cu = 0;                     // resident k_wave_coop blocks per CU on this graph's device
     uint32_t fault_block = 0;                // FGI_OPT_FAULT_INJECT: block + 1 of a cascade that skips a barrier
     uint32_t fault_skip = 0;                 // ... after this many more cascade launches
+    uint32_t fault_tail_block = 0;           // FGI_OPT_FAULT_INJECT_TAIL: the same for a wave tail (k_wave_tail)
+    uint32_t fault_tail_skip = 0;
 
     // timing
     std::vector<hipEvent_t> ev;        // pairs around expand launches
@@ -631,6 +634,7 @@ inline void touch(fgi_graph* g) { g->mut_epoch = ++g->epoch_counter; }
 inline void note_words(fgi_graph* g) {
     g->cls_valid = false;
     g->words_dirty = true;
+    g->nodes_written = true;
 }
 // Apply the visit bitmap to the node words and clear it (wave.hip). Every entry point that reads or
 // mutates node words outside a wave calls it first.

@@ -684,39 +684,19 @@ __device__ __forceinline__ int prune_mode(uint32_t h, uint32_t n_slots, unsigned
     return 2;                                          // Computing, or detached (not in the registry)
 }
 
-// measurement variants of the prune kernels (make variant-pexp PEXP=mask; wrong results): 1 = skip long
-// rows, 2 / 8 = non-temporal pool loads / stores, 4 = no liveness gathers
-#ifndef FGI_PEXP
-#define FGI_PEXP 0
-#endif
 #ifndef FGI_SHORT_PER
 #define FGI_SHORT_PER 4   // 64-entry slices a wave loads per step of the short-row prune
 #endif
 
 __device__ __forceinline__ bool edge_live(const unsigned long long* node, uint32_t dst, uint64_t tag) {
-#if FGI_PEXP & 4
-    return (tag ^ dst) & 1;
-#endif
     const unsigned long long w = node[dst];              // Computed.cs:412-413
     return word_is_current(w) && (w & kVMask) == tag;
 }
 
-// pool accesses of a prune (non-temporal loads in the PEXP & 2 variant, stores in PEXP & 8:
-// measured slower together, 6.6 against 5.5 ms on configs[3])
-template <class T> __device__ __forceinline__ T pr_ld(const T* p) {
-#if FGI_PEXP & 2
-    return __builtin_nontemporal_load(p);
-#else
-    return *p;
-#endif
-}
-template <class T> __device__ __forceinline__ void pr_st(T* p, T v) {
-#if FGI_PEXP & 8
-    __builtin_nontemporal_store(v, p);
-#else
-    *p = v;
-#endif
-}
+// pool accesses of a prune (plain: non-temporal loads and stores measured slower together, 6.6 against
+// 5.5 ms on configs[3], round 2)
+template <class T> __device__ __forceinline__ T pr_ld(const T* p) { return *p; }
+template <class T> __device__ __forceinline__ void pr_st(T* p, T v) { *p = v; }
 
 __device__ __forceinline__ uint32_t wave_excl_scan32(uint32_t v, uint32_t& total) {
     const uint32_t lane = threadIdx.x & 63;
@@ -822,7 +802,6 @@ __device__ void prune_short_rows(const PruneArgs& a, uint32_t* s_lh, uint32_t* s
         } else if (len && mode == 2) {
             acc[3] += len;
         } else if (len > kPruneLong) {
-#if !(FGI_PEXP & 1)
             const uint32_t nch = (len + kChunk - 1) / kChunk;
             const uint32_t q = atomicAdd(&s_nl, 1u);
             if (q < kBlockLong) {
@@ -832,7 +811,6 @@ __device__ void prune_short_rows(const PruneArgs& a, uint32_t* s_lh, uint32_t* s
                 const uint32_t cb = (uint32_t)atomicAdd(&a.st[kPrChunks], (unsigned long long)nch);
                 prune_map_row(a.chunk_map, (uint32_t)h, cb, nch, 0, 1);
             }
-#endif
         } else if (len) {
             eff = len;
         }
@@ -1834,8 +1812,8 @@ static fgi_status label_of(fgi_graph* g, uint32_t x, uint32_t* out) {
 }
 
 static fgi_status usable_now(fgi_graph* g) {
-    return g->failed ? set_err(g, FGI_ESTATE, "a streaming batch failed on the device (%s); fgi_restore or fgi_destroy",
-                               "grid barrier timeout")
+    return g->failed ? set_err(g, FGI_ESTATE, "a batch or wave failed on the device (%s); fgi_restore or fgi_destroy",
+                               "grid barrier timeout or device wait")
                      : FGI_OK;
 }
 // every call but fgi_restore, fgi_set_option and the asynchronous wave calls first waits for the
@@ -2320,8 +2298,11 @@ fgi_status fgi_restore(fgi_graph* g) {
     const size_t H = g->n_handles;
     hipStream_t s = g->stream;
     if (g->failed) {
-        // a failed batch: words, visit / invalidated bits and the wave counters are undefined. Every
-        // saved table is copied back and the wave state cleared before the graph is usable again.
+        // a failed batch or wave: words, visit / invalidated bits and the wave counters are undefined. Every
+        // saved table is copied back and the wave state cleared before the graph is usable again (the
+        // copies are stream-ordered after any wave still in flight; its results are forgotten).
+        g->aw[0] = fgi_graph::AsyncWave{};
+        g->aw[1] = fgi_graph::AsyncWave{};
         FGI_HIP(g, hipMemcpyAsync(g->node, g->snap_node, H * 8, hipMemcpyDeviceToDevice, s));
         FGI_HIP(g, hipMemsetAsync(g->vis_bm, 0, g->bm_words * 4, s));
         FGI_HIP(g, hipMemsetAsync(g->inv_bm, 0, g->bm_words * 4, s));
@@ -2429,6 +2410,12 @@ fgi_status fgi_set_option(fgi_graph* g, int option, int64_t value) {
             return set_err(g, FGI_EINVAL, "fault injection: (launches to skip << 16) | (block + 1), block + 1 > 0");
         g->fault_block = (uint32_t)(value & 0xFFFF);
         g->fault_skip = (uint32_t)(value >> 16);
+        return FGI_OK;
+    case FGI_OPT_FAULT_INJECT_TAIL:
+        if (value < 0 || ((value & 0xFFFF) == 0 && value != 0) || value >= (1ll << 32))
+            return set_err(g, FGI_EINVAL, "fault injection: (tail launches to skip << 16) | (block + 1), block + 1 > 0");
+        g->fault_tail_block = (uint32_t)(value & 0xFFFF);
+        g->fault_tail_skip = (uint32_t)(value >> 16);
         return FGI_OK;
     default: return set_err(g, FGI_EINVAL, "unknown option %d", option);
     }

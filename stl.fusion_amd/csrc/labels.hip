@@ -238,8 +238,14 @@ fgi_status labels_choose(fgi_graph* g, const uint64_t* keys, uint64_t m) {
         for (void* p : {(void*)cnt, (void*)hist, (void*)cb, (void*)k0, (void*)k1, tmp})
             if (p) hipFree(p);
     };
+    // a failure leaves no hot set (lbl_hot stays 0, lbl_done false) and no half-built fold tables: a retry
+    // starts from the same state
     auto fail = [&](hipError_t e, const char* what) {
         cleanup();
+        for (void** p : {(void**)&g->fold_start, (void**)&g->fold_off, (void**)&g->fold_base}) {
+            if (*p) hipFree(*p);
+            *p = nullptr;
+        }
         return hip_check(g, e, what);
     };
     hipError_t e;
@@ -273,9 +279,14 @@ fgi_status labels_choose(fgi_graph* g, const uint64_t* keys, uint64_t m) {
     const uint32_t ncls = (uint32_t)bases.size();
     bases.push_back((uint32_t)H);
     const uint32_t tiles = (uint32_t)(((uint64_t)g->ext_handles + kFoldTile - 1) / kFoldTile);
-    if (!g->s2l) {
-        if ((e = hipMalloc(&g->s2l, (size_t)n * 4)) != hipSuccess) return fail(e, "labels: slot map");
-        if ((e = hipMalloc(&g->l2s, (size_t)g->lbl_K * 4)) != hipSuccess) return fail(e, "labels: label map");
+    // each map on its own: a retry after a failed allocation finds the one that exists and makes the other
+    if (!g->s2l && (e = hipMalloc(&g->s2l, (size_t)n * 4)) != hipSuccess) {
+        g->s2l = nullptr;
+        return fail(e, "labels: slot map");
+    }
+    if (!g->l2s && (e = hipMalloc(&g->l2s, (size_t)g->lbl_K * 4)) != hipSuccess) {
+        g->l2s = nullptr;
+        return fail(e, "labels: label map");
     }
     (void)hipMemsetAsync(g->s2l, 0xFF, (size_t)n * 4, s);
     (void)hipMemsetAsync(g->l2s, 0xFF, (size_t)g->lbl_K * 4, s);

@@ -1236,7 +1236,10 @@ fgi_status fgi_part_init_host(fgi_graph* g, uint32_t n_global, fgi_allgather_fn 
 static fgi_status part_alloc(fgi_graph* g, uint32_t n_global) {
     if (!g || g->world < 1 || g->rank < 0 || g->rank >= g->world) return FGI_EINVAL;
     if (g->lbl_K) {   // a partition numbers its slots by rank ranges: no hub-first labels (a fresh graph drops them)
-        if (g->lbl_done || g->pool_top) return set_err(g, FGI_ESTATE, "a graph with loaded edges cannot join a partition");
+        // node words already written sit at labels K + x (and detached homes hold K + slot): dropping K
+        // would lose them, so only a graph with nothing in it yet may join
+        if (g->lbl_done || g->pool_top || g->nodes_written)
+            return set_err(g, FGI_ESTATE, "a graph with registered nodes or loaded edges cannot join a partition");
         g->lbl_K = 0;
         g->n_slots = g->ext_slots;
         g->n_handles = g->ext_handles;

@@ -41,18 +41,6 @@
 
 #include "fgi_internal.h"
 
-#ifndef FGI_PULL_PREFETCH
-#define FGI_PULL_PREFETCH 1
-#endif
-// measurement builds: the dead-edge filter only on push levels of at least this many edges
-#ifndef FGI_FILTER_MIN
-#define FGI_FILTER_MIN 0
-#endif
-// measurement-only builds (make variant-exp EXP=<mask>): parts of a pull level skipped to attribute
-// its time (results are wrong): 1 tail scans, 2 survivor writes, 4 head probes, 8 visit/class gathers
-#ifndef FGI_EXP
-#define FGI_EXP 0
-#endif
 // measurement-only build (make variant-probe): k_level stamps per-block phase times (100 MHz wall
 // clock) into d_probe; run_wave prints per-level medians with FGI_TRACE=1
 #ifndef FGI_PROBE
@@ -929,16 +917,13 @@ __device__ __forceinline__ void expand_level(int L, uint64_t F, uint64_t T, uint
         }
         // edges to nodes visited earlier need neither the tag nor the gather (the bitmap is read
         // without synchronisation: a stale 0 only costs the gather and an atomic that finds the bit).
-        // Kept on small levels too (make variant-filtermin measures the alternative)
+        // Kept on small levels too (round 3 measured the alternative: no gain)
         const bool small = T < x.small_max;   // level-uniform
-        if (x.dead_filter && T >= (uint64_t)FGI_FILTER_MIN && !small) {
+        if (x.dead_filter && !small) {
 #pragma unroll
             for (int j = 0; j < kEPT; ++j)
                 if (dst[j] != 0xFFFFFFFFu && bit_of(vis, dst[j])) dst[j] = 0xFFFFFFFFu;
         }
-#if FGI_PROBE
-        if (dst[0] == 0xFFFFFFFEu) __builtin_trap();   // never: orders the probe after the loads
-#endif
         PROBE(L, 5);
         uint64_t tag[kEPT];
         unsigned long long w[kEPT];
@@ -1275,7 +1260,6 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
     uint4* const sv_out = p.sv[dst] + seg;     // this level's survivors (the block's segment)
     uint32_t* const wl_out = p.wl + seg;       // this level's expandable winners
     // the first batch's entries are requested before the owned words are staged
-    // (FGI_PULL_PREFETCH=0 builds the variant without the look-ahead, for measurement)
     uint4 c[kCPL];
 #pragma unroll
     for (int j = 0; j < (int)kCPL; ++j) {
@@ -1334,27 +1318,15 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
         for (int j = 0; j < (int)kCPL; ++j) {
             const bool in = base + j * 64 + lane < cnt;
             const uint32_t rel = c[j].x - (uint32_t)s_lo;
-#if FGI_EXP & 8
-            lv[j] = in;
-#else
             lv[j] = in && !((s.vm[rel >> 5] >> (c[j].x & 31)) & 1u);
-#endif
-#if FGI_EXP & 4
-            f0[j] = (lv[j] && (c[j].z & 1)) ? ~0u : 0u;
-            f1[j] = 0u;
-#else
             f0[j] = lv[j] ? head_bits(p, s, c[j].z, sum) : 0u;
             f1[j] = (lv[j] && c[j].w != FGI_NONE) ? head_bits(p, s, c[j].w, sum) : 0u;
-#endif
         }
+        // the next run's entries are requested before this run's probes are consumed
         uint4 cn[kCPL];
 #pragma unroll
         for (int j = 0; j < (int)kCPL; ++j) {
-#if FGI_PULL_PREFETCH
             const uint32_t i = base + kCandBatch + j * 64 + lane;
-#else
-            const uint32_t i = cnt;
-#endif
             cn[j] = load_cand(src + seg + i, i < cnt, (uint32_t)s_lo);
         }
 #pragma unroll
@@ -1400,29 +1372,20 @@ __device__ __forceinline__ void pull_level(int L, const PullArgs& p, const WaveP
                 uint32_t sb = 0;
                 if (lane == 0) sb = atomicAdd(&s.sn, (uint32_t)__popcll(sm));
                 sb = from_lane0(sb);
-#if !(FGI_EXP & 2)
                 if (surv) sv_out[sb + rank_in(sm)] = c[j];
-#endif
             }
         }
         // scan the queued tails when the queue could overflow next batch, or at the wave's end
         if (base + kCandBatch >= cnt) PROBE(L, 7);
         if (qn > kWaveTailCap - kWaveBatch || base + kCandBatch >= cnt) {
             __builtin_amdgcn_wave_barrier();
-            pull_tails(p, src, sv_out, node, s_lo, seg, wq, (FGI_EXP & 1) ? 0u : qn, s, flagged, examined_tail, tails, ws,
+            pull_tails(p, src, sv_out, node, s_lo, seg, wq, qn, s, flagged, examined_tail, tails, ws,
                        sum);
             __builtin_amdgcn_wave_barrier();
             qn = 0;
         }
 #pragma unroll
-        for (int j = 0; j < (int)kCPL; ++j) {
-#if FGI_PULL_PREFETCH
-            c[j] = cn[j];
-#else
-            const uint32_t i = base + kCandBatch + j * 64 + lane;
-            c[j] = load_cand(src + seg + i, i < cnt, (uint32_t)s_lo);
-#endif
-        }
+        for (int j = 0; j < (int)kCPL; ++j) c[j] = cn[j];
     }
     PROBE(L, 2);
     __syncthreads();
@@ -2291,6 +2254,8 @@ struct TailArgs {
     uint64_t bar_timeout;
     uint64_t max_edges;                // a level with more edges is left to the host's next group
     int all;                           // run every remaining level (asynchronous waves: no second group)
+    uint32_t fault_block;              // fault injection (FGI_OPT_FAULT_INJECT_TAIL): block fault_block - 1
+                                       // leaves at its first grid barrier without arriving
 };
 
 // A level-group wave's totals on the device (one writer: block 0's first thread of the tail), so that
@@ -2339,7 +2304,12 @@ __global__ __launch_bounds__(kBlock) void k_wave_tail(TailArgs a) {
     __shared__ unsigned long long s_st[kBlock / 64][kStats];
     __shared__ unsigned long long s_ft;
     WaveCtr* ctr = a.ctr;
-    auto grid_sync = [&]() -> bool { return soft_grid_sync(a.gbar, &ctr->broken, nullptr, a.bar_timeout, false, 1); };
+    bool first_sync = true;
+    auto grid_sync = [&]() -> bool {
+        const bool skip = a.fault_block != 0 && first_sync && blockIdx.x + 1 == a.fault_block;
+        first_sync = false;
+        return soft_grid_sync(a.gbar, &ctr->broken, nullptr, a.bar_timeout, skip, 1);
+    };
     // the wave's totals (WaveCtr n_levels ..): the group's levels, read before the ring rolls over — one
     // level per lane of block 0's first wave, every load in flight together, then lane 0 adds them up
     TailSums acc;
@@ -2860,6 +2830,17 @@ TailArgs tail_args(fgi_graph* g, int grp0, int L0, const WaveParams& wp, uint64_
     ta.gbar = g->gbar + kGbarTail;
     ta.bar_timeout = kGridBarTimeout;
     ta.max_edges = max_edges;
+    // fault injection (tests): the (k+1)-th tail launched from the option on loses a block at its first
+    // barrier, which then times out after 20 ms (the failure path of run_wave / wave_wait)
+    if (g->fault_tail_block) {
+        if (g->fault_tail_skip == 0) {
+            ta.fault_block = g->fault_tail_block;
+            ta.bar_timeout = 2000000ull;
+            g->fault_tail_block = 0;
+        } else {
+            --g->fault_tail_skip;
+        }
+    }
     return ta;
 }
 
@@ -3392,9 +3373,17 @@ static fgi_status counters_to_host(fgi_graph* g, hipStream_t s, bool mark) {
 
 }  // namespace
 
+// A completed asynchronous wave's ids stay readable (fgi_wave_wait again) only while its buffer is its own:
+// a synchronous wave or a list made on demand that writes the buffer forgets the ticket's results
+static void forget_async_results(fgi_graph* g, const uint32_t* buf) {
+    for (fgi_graph::AsyncWave& a : g->aw)
+        if (!a.busy && a.ticket && ((a.ticket & 1) ? g->inv_alt : g->inv) == buf) a.ticket = 0;
+}
+
 fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                     fgi_wave_stats* stats, bool ext_roots) {
     const auto t0 = std::chrono::steady_clock::now();
+    forget_async_results(g, g->inv);   // the list goes to g->inv (now, or on demand: ensure_ids)
     hipStream_t s = g->stream;
     static const bool trace = getenv("FGI_TRACE") != nullptr;
     static const bool no_level_events = getenv("FGI_NO_LEVEL_EVENTS") != nullptr;   // measurement only
@@ -3762,9 +3751,26 @@ fgi_status wave_wait(fgi_graph* g, uint64_t ticket, uint64_t* out_n, const uint3
     }
     unsigned long long* pub = g->apub[ticket & 1];
     const fgi_status ws = wait_word(g, g->stream, pub + kPubWords, a.seq);
+    if (ws != FGI_OK) {
+        // the wave may still be running (a timeout) or the stream failed: its buffers stay its own and the
+        // graph is poisoned until fgi_restore (which orders its copies after the wave on the stream)
+        g->failed = true;
+        return ws;
+    }
     a.busy = false;
-    FGI_TRY(ws);
     const WaveCtr& c = *reinterpret_cast<const WaveCtr*>(pub);
+    if (c.broken) {
+        // the wave's tail left at a timed-out grid barrier: the wave is half applied (as run_wave's level
+        // groups, fgi.h). The other wave in flight, queued behind it, is drained first (its tail starts from
+        // the misaligned barrier counter and times out too), then the barrier word is reset.
+        g->aw[0].busy = g->aw[1].busy = false;
+        FGI_HIP(g, hipStreamSynchronize(g->stream));
+        FGI_HIP(g, hipMemsetAsync(g->gbar + kGbarTail, 0, sizeof(unsigned long long), g->stream));
+        FGI_HIP(g, hipStreamSynchronize(g->stream));
+        g->failed = true;
+        return set_err(g, FGI_EDEVICE, "wave %llu: the wave tail's grid barrier timed out (its blocks were not resident "
+                                       "together); the graph is unusable until fgi_restore", (unsigned long long)ticket);
+    }
     // the wave's totals from the device (tail_account); the group's levels from the ring while it has not
     // rolled over (the next wave's group size)
     const uint64_t levels = c.n_levels, e_trav = c.e_trav, f_total = c.f_total, pull_levels = c.n_pull;
@@ -3824,6 +3830,7 @@ fgi_status ensure_ids(fgi_graph* g) {
     if (g->ids_valid) return FGI_OK;
     // the bitmap of the last wave is intact until the next wave starts: list it now
     if (!g->inv_cur) g->inv_cur = g->inv;
+    forget_async_results(g, g->inv_cur);
     FGI_HIP(g, launch_final(g, g->n_handles, true, g->inv_cur));
     FGI_HIP(g, hipStreamSynchronize(g->stream));
     g->ids_valid = true;

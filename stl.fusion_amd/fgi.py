@@ -28,6 +28,7 @@ OPT_FAULT_INJECT = 11
 OPT_FUSED = 12
 OPT_PART_PLAN = 13
 OPT_PART_BUCKET = 14
+OPT_FAULT_INJECT_TAIL = 16
 OPT_PROBE_SUMMARY = 15
 DIR_AUTO, DIR_PUSH, DIR_PULL = 0, 1, 2
 NONE = 0xFFFFFFFF

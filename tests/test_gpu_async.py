@@ -124,3 +124,86 @@ def test_async_waves_on_an_evolving_graph(pkg, gpu_available):
     assert_states_equal(g, o, n)
     g.close()
     o.close()
+
+
+def _layered_pair(pkg, levels, width, fanout, seed):
+    n = levels * width
+    g = pkg.Graph(n)
+    g.synth_layered(levels, width, fanout, seed)
+    s, d = O.gen_layered(levels, width, fanout, seed)
+    o = O.Oracle(n)
+    o.load_graph(O.version_of(seed, np.arange(n)), None, s, d, O.gen_tags(s, d, seed))
+    return g, o, n
+
+
+@pytest.mark.parametrize("mode", ["async", "sync"])
+def test_wave_tail_timeout_poisons_until_restore(pkg, gpu_available, mode):
+    """A wave whose tail (the persistent launch running its last small push levels) loses a block at a grid
+    barrier (FGI_OPT_FAULT_INJECT_TAIL) is half applied: fgi_wave_wait (async) or fgi_invalidate (sync)
+    returns FGI_EDEVICE, every later call FGI_ESTATE until fgi_restore, and the graph then runs the same
+    waves as the oracle again — including a second tail, whose barrier word the failure path reset."""
+    fgi = pkg.fgi
+    levels, width, fanout, seed = 14, 64, 2, 0x5EED0031
+    g, o, n = _layered_pair(pkg, levels, width, fanout, seed)
+    g.snapshot()
+    o.snapshot()
+    roots = np.arange(8, dtype=np.uint32)   # level 0: the wave runs every one of the 14 levels
+    o.clear_log()
+    o.invalidate_slots(roots)
+    want = np.sort(o.inv_log())
+    assert len(want) > 12 * 8
+    d_r = torch.from_numpy(roots.astype(np.int32)).cuda()
+    torch.cuda.synchronize()
+
+    def wave():
+        if mode == "async":
+            t = g.invalidate_async(len(roots), d_r.data_ptr())
+            nv, ptr = g.wave_wait(t)
+            return _d2h(ptr, nv)
+        return g.invalidate(roots)
+
+    # a first wave teaches the engine the wave's depth: the next one runs its levels past the first
+    # group in the tail (the async queue runs every level past its group there anyway)
+    assert np.array_equal(wave(), want)
+    g.restore()
+    g.set_option(fgi.OPT_FAULT_INJECT_TAIL, 1)
+    with pytest.raises(fgi.FgiError) as e:
+        wave()
+    assert e.value.status == fgi.EDEVICE, e.value
+    for call in (lambda: g.get_state([0]), lambda: g.invalidate(roots), lambda: g.snapshot()):
+        with pytest.raises(fgi.FgiError) as e2:
+            call()
+        assert e2.value.status == fgi.ESTATE
+    g.restore()
+    assert_states_equal(g, o, n)
+    for _ in range(2):
+        assert np.array_equal(wave(), want)
+        g.restore()
+    g.close()
+    o.close()
+
+
+def test_ticket_results_forgotten_once_their_buffer_is_rewritten(pkg, gpu_available):
+    """A completed ticket's ids can be read again only while its buffer is its own: a synchronous wave (which
+    lists its ids into the even tickets' buffer) makes a later wait on an even ticket fail with FGI_EINVAL
+    instead of returning the other wave's ids."""
+    fgi = pkg.fgi
+    g, o, n = _layered_pair(pkg, 6, 256, 4, 0x5EED0032)
+    roots = np.arange(16, dtype=np.uint32)
+    d_r = torch.from_numpy(roots.astype(np.int32)).cuda()
+    torch.cuda.synchronize()
+    g.snapshot()
+    t1 = g.invalidate_async(len(roots), d_r.data_ptr())
+    g.wave_wait(t1)
+    g.restore()
+    t2 = g.invalidate_async(len(roots), d_r.data_ptr())
+    n2 = g.wave_wait(t2)[0]
+    assert g.wave_wait(t2)[0] == n2           # repeated wait: same results
+    g.restore()
+    g.invalidate(roots[:1])                   # writes the even tickets' buffer
+    with pytest.raises(fgi.FgiError) as e:
+        g.wave_wait(t2)
+    assert e.value.status == fgi.EINVAL
+    assert g.wave_wait(t1)[0] > 0             # odd ticket: its buffer was not touched
+    g.close()
+    o.close()
