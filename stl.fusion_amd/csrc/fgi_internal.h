@@ -195,6 +195,9 @@ struct LevelCtr {
     unsigned long long mult;    // push: fine chunks per expand chunk
     unsigned long long npull;   // pull levels of the wave before this one (which candidate list to read)
     unsigned long long sum;     // pull level: 1 if k_collect built the nonzero-word summary for its probes
+    unsigned long long want;    // 1 if the automatic choice (Beamer's rules) is pull, whatever the level ran
+                                // as (a level the host pinned to push, push-only options): the next wave's
+                                // launch plan (run_wave's left-out collects) learns from it
 };
 
 // A level's frontier totals: a push producer leaves them packed in ft (the single engine does not
@@ -419,6 +422,13 @@ struct fgi_graph {
     // no-op, so the pair (node word, visit bit) is the node's state; one atomicOr decides the first
     // visitor. fold() applies the bits to the words before any mutation or state query.
     uint32_t* vis_bm = nullptr;
+    // fgi_restore swaps in a clean second visit bitmap instead of leaving the clear to the next wave's init
+    // kernel; the next wave's list kernel clears the swapped-out one (spare_dirty) as it goes
+    uint32_t* vis_spare = nullptr;
+    bool spare_dirty = false;
+    // the last level-group wave left its counters, statistics and invalidated bitmap zeroed (its final
+    // kernels and publish did, WaveEnd): the next wave runs without k_wave_init
+    bool wave_clean = false;
     bool v_dirty = false;              // vis_bm may hold set bits
     bool vis_stale = false;            // fgi_restore left vis_bm's clearing to the next wave (flush_vis)
     bool coop_clean = false;           // wave counters, statistics and bitmaps clear (a cooperative wave left them so)

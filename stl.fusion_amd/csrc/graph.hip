@@ -1879,7 +1879,8 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
     if (K && (dmalloc(g, &g->xbm, ((uint64_t)g->ext_handles + 63) / 64 + 2) ||
               dmalloc(g, &g->fold_status, ((uint64_t)g->ext_handles + kFoldTile - 1) / kFoldTile + kStatCols + 1)))
         return fail(FGI_ENOMEM);
-    if (dmalloc(g, &g->vis_bm, g->bm_words) || dmalloc(g, &g->inv_bm, g->bm_words + kHot / 32) ||
+    if (dmalloc(g, &g->vis_bm, g->bm_words) || dmalloc(g, &g->vis_spare, g->bm_words) ||
+        dmalloc(g, &g->inv_bm, g->bm_words + kHot / 32) ||
         dmalloc(g, &g->cls_bm, g->bm_words) || dmalloc(g, &g->uin_more, g->bm_words) ||
         dmalloc(g, &g->sum_bm, ((uint64_t)H + 4095) / 4096 * 2 + 2))
         return fail(FGI_ENOMEM);
@@ -1887,6 +1888,7 @@ fgi_status fgi_create(const fgi_config* cfg, fgi_graph** out) {
     hipMemset(g->bsum, 0, 8ull * kStatBlocks * sizeof(unsigned long long));
     hipMemset(g->gbar, 0, kGbarWords * sizeof(unsigned long long));
     hipMemset(g->vis_bm, 0, g->bm_words * 4);
+    hipMemset(g->vis_spare, 0, g->bm_words * 4);
     hipMemset(g->inv_bm, 0, g->bm_words * 4);
     hipMemset(g->uin_more, 0, g->bm_words * 4);
     if (hipHostMalloc(reinterpret_cast<void**>(&g->ctr_host), sizeof(WaveCtr)) != hipSuccess ||
@@ -1953,6 +1955,7 @@ fgi_status fgi_destroy(fgi_graph* g) {
         dfree(g->sv_cnt[k]);
     }
     dfree(g->vis_bm);
+    dfree(g->vis_spare);
     dfree(g->cls_bm);
     dfree(g->uin_more);
     dfree(g->sum_bm);
@@ -2305,8 +2308,11 @@ fgi_status fgi_restore(fgi_graph* g) {
         g->aw[1] = fgi_graph::AsyncWave{};
         FGI_HIP(g, hipMemcpyAsync(g->node, g->snap_node, H * 8, hipMemcpyDeviceToDevice, s));
         FGI_HIP(g, hipMemsetAsync(g->vis_bm, 0, g->bm_words * 4, s));
+        FGI_HIP(g, hipMemsetAsync(g->vis_spare, 0, g->bm_words * 4, s));
         FGI_HIP(g, hipMemsetAsync(g->inv_bm, 0, g->bm_words * 4, s));
         FGI_HIP(g, hipMemsetAsync(g->gbar, 0, kGbarWords * sizeof(unsigned long long), s));
+        g->spare_dirty = false;
+        g->wave_clean = false;
         g->words_dirty = false;
         g->cls_valid = false;
         g->v_dirty = false;
@@ -2320,8 +2326,17 @@ fgi_status fgi_restore(fgi_graph* g) {
         g->words_dirty = false;
         g->cls_valid = false;
     }
-    // the visit bits are cleared by the next wave's init kernel (or flush_vis before any other use)
-    if (g->v_dirty) g->vis_stale = true;
+    // the visit bits are forgotten: the clean spare bitmap takes the visit bitmap's place, and the next
+    // wave's list kernel clears the old one; without a clean spare, the next wave's init kernel clears it
+    // (or flush_vis before any other use)
+    if (g->v_dirty) {
+        if (!g->spare_dirty && !g->vis_stale) {
+            std::swap(g->vis_bm, g->vis_spare);
+            g->spare_dirty = true;
+        } else {
+            g->vis_stale = true;
+        }
+    }
     g->v_dirty = false;
     if (g->mut_epoch == g->snap_mut_epoch) {
         // nothing but waves ran since the snapshot: rows and |_used| counts are unchanged. The

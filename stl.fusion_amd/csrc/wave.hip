@@ -629,10 +629,13 @@ __device__ __forceinline__ void root_step(uint32_t i, const uint32_t* __restrict
 // publish: unpack level 0's totals into F / T (the partitioned wave all-reduces those words);
 // the single engine reads the packed counter (lvl_F / lvl_T) and skips the hand-off
 template <int IMM>
+// stamp: no k_wave_init ran before this wave (the previous one left the state clean): the wave's start on
+// the device wall clock is stamped here instead (WaveCtr::t0)
 __global__ __launch_bounds__(kBlock) void k_roots(const uint32_t* __restrict__ roots, const uint8_t* __restrict__ imm,
                                                   uint32_t n, uint32_t base, uint32_t n_range, unsigned long long* node,
                                                   uint32_t* vis, Out o, WaveCtr* ctr, unsigned long long* done,
-                                                  int publish, RootMap rm) {
+                                                  int publish, RootMap rm, int stamp) {
+    if (stamp && blockIdx.x == 0 && threadIdx.x == 0) ctr->t0 = wall_clock64();
     root_step<IMM>(blockIdx.x * blockDim.x + threadIdx.x, roots, imm, n, base, n_range, node, vis, o, ctr, rm);
     if (publish) publish_ft(o.ln, done, gridDim.x);
 }
@@ -659,6 +662,24 @@ __device__ __forceinline__ bool level_pulls(const WaveCtr* ctr, int L, const Wav
     const LevelCtr& lc = ctr->lvl[L % kRing];
     if (wp.multi) return lc.pull != 0;
     return level_pulls(ctr, L, wp, lvl_F(lc), lvl_T(lc));
+}
+
+// A level group's end (run_wave): the wave is over when the level after the group's last one — or after
+// the last one its tail ran (ctr->cur) — has no frontier. The host decides the same from the published
+// counters, so the final kernels and the publish can leave the wave state clean for the next wave
+// (WaveEnd) exactly when the host will not run another group.
+struct WaveEnd {
+    WaveCtr* ctr;            // null: the state is left as it is
+    int L;                   // the first level the group did not launch
+    int tail;                // the group ended with k_wave_tail
+    unsigned long long* blk; // per-block statistics, cleared with the invalidated bitmap
+    uint32_t* inv_bm;        // the labels' invalidated bitmap: ext words of it cleared (64-bit words)
+    uint64_t words;          // 64-bit words of inv_bm the wave can have set (n_handles / 64, rounded up)
+    uint32_t* spare;         // the other visit bitmap, cleared whether the wave is over or not (nullable)
+};
+__device__ __forceinline__ bool wave_over(const WaveEnd& e) {
+    const uint64_t stop = e.tail ? max((uint64_t)e.L, (uint64_t)e.ctr->cur) : (uint64_t)e.L;
+    return lvl_F(e.ctr->lvl[stop % kRing]) == 0;
 }
 
 // fine chunks per expand chunk: as large as kEPT allows while every block still gets two chunks
@@ -1479,7 +1500,12 @@ __global__ __launch_bounds__(kBlock, kLevelOcc) void k_level(int Larg, WaveParam
         reinterpret_cast<unsigned long long*>(&ctr->lvl[(L + 2) % kRing])[threadIdx.x] = 0ull;
     const uint64_t npull = lc.npull;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        if (!PART) lc.pull = pull ? 1ull : 0ull;
+        if (!PART) {
+            lc.pull = pull ? 1ull : 0ull;
+            WaveParams wr = wp;   // what the automatic choice would be (the next wave's launch plan)
+            wr.direction = 0;
+            lc.want = (wp.direction == 0 ? pull : level_pulls(ctr, L, wr)) ? 1ull : 0ull;
+        }
         o.ln->npull = npull + (pull ? 1 : 0);
         if (fused) {
             ctr->n_levels += 1;
@@ -1834,10 +1860,14 @@ struct ListPub {
     uint32_t words;
 };
 
+// With end.ctr (a level group's list, run_wave): once the wave is over (wave_over), every block also
+// zeroes its share of the invalidated bitmap (its own words, after reading them, when it lists that
+// bitmap; hot labels: k_final_count has read it) and of the statistics rows, and with end.spare its share
+// of the swapped-out visit bitmap, so that the next wave needs no init kernel.
 __global__ __launch_bounds__(kBlock) void k_final_write(const unsigned long long* __restrict__ inv64, uint64_t words,
                                                         uint64_t wpb, const unsigned long long* __restrict__ status,
                                                         WaveCtr* ctr, uint32_t* out, int need_done, uint32_t spb,
-                                                        ListPub pub) {
+                                                        ListPub pub, WaveEnd end) {
     if (need_done && ctr->phase != kPhaseDone) return;   // a fused wave whose tail stopped early: not yet
     __shared__ unsigned long long s_red[kBlock / 64];
     __shared__ unsigned long long s_wbase[kBlock / 64];
@@ -1875,6 +1905,26 @@ __global__ __launch_bounds__(kBlock) void k_final_write(const unsigned long long
         for (uint32_t i = lane; i < tot; i += 64) out[run + i] = s_stage[wid][i];
         __builtin_amdgcn_wave_barrier();
         run += tot;
+    }
+    if (end.ctr) {   // block-uniform
+        const bool over = wave_over(end);
+        __syncthreads();   // the block's waves have read their words
+        // the block's share of the labels' bitmap: its own read range when it lists that bitmap (the
+        // partition is the launch's: ceil(words / grid) per block)
+        const uint64_t P = (end.words + gridDim.x - 1) / gridDim.x;
+        const uint64_t z0 = min(end.words, (uint64_t)t * P), z1 = min(end.words, z0 + P);
+        unsigned long long* iw = reinterpret_cast<unsigned long long*>(end.inv_bm);
+        unsigned long long* sw = reinterpret_cast<unsigned long long*>(end.spare);
+        for (uint64_t x = z0 + threadIdx.x; x < z1; x += blockDim.x) {
+            if (over) iw[x] = 0ull;
+            if (sw) sw[x] = 0ull;
+        }
+        if (over) {
+            constexpr uint64_t kBlk = (uint64_t)kStatBlocks * kStatCols;
+            const uint64_t Q = (kBlk + gridDim.x - 1) / gridDim.x;
+            const uint64_t b0 = min(kBlk, (uint64_t)t * Q), b1 = min(kBlk, b0 + Q);
+            for (uint64_t x = b0 + threadIdx.x; x < b1; x += blockDim.x) end.blk[x] = 0ull;
+        }
     }
     if (pub.dst && last_block_arrive<true>(pub.done, gridDim.x)) {
         if (threadIdx.x == 0) pub.dst[pub.words + 1] = wall_clock64();
@@ -2780,8 +2830,10 @@ ExpandArgs expand_args(fgi_graph* g, int buf) {
 }
 
 // the invalidated bitmap -> V_inv (ctr->inv) and, with ids, the invalidated list
-hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true, uint32_t* out = nullptr, ListPub pub = ListPub{}) {
+hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true, uint32_t* out = nullptr, ListPub pub = ListPub{},
+                        WaveEnd end = WaveEnd{}) {
     if (!ids) pub.dst = nullptr;   // no list kernel: the caller publishes
+    if (!end.ctr) g->wave_clean = false;   // the counters (inv, ...) are written and nothing clears them
     if (!out) out = g->inv;
     const auto* inv64 = reinterpret_cast<const unsigned long long*>(g->inv_bm);
     const FoldArgs f = fold_args(g);
@@ -2796,7 +2848,7 @@ hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true, uint3
             const uint32_t G = std::min<uint32_t>(kFinalBlocks, tiles), spb = (tiles + G - 1) / G;
             const uint32_t G2 = (tiles + spb - 1) / spb;
             hipLaunchKernelGGL(k_final_write, dim3(G2), dim3(kBlock), 0, g->stream, (const unsigned long long*)g->xbm, words,
-                               (uint64_t)spb * kFoldWords, (const unsigned long long*)st, g->ctr, out, 0, spb, pub);
+                               (uint64_t)spb * kFoldWords, (const unsigned long long*)st, g->ctr, out, 0, spb, pub, end);
         }
         return hipGetLastError();
     }
@@ -2809,7 +2861,7 @@ hipError_t launch_final(fgi_graph* g, uint32_t n_handles, bool ids = true, uint3
                        (const unsigned long long*)g->blk_stats, ids ? 0 : 1, g->done, FoldArgs{});
     if (ids)
         hipLaunchKernelGGL(k_final_write, dim3(G), dim3(kBlock), 0, g->stream, inv64, words, wpb,
-                           (const unsigned long long*)st, g->ctr, out, 0, 1u, pub);
+                           (const unsigned long long*)st, g->ctr, out, 0, 1u, pub, end);
     return hipGetLastError();
 }
 
@@ -2848,7 +2900,7 @@ TailArgs tail_args(fgi_graph* g, int grp0, int L0, const WaveParams& wp, uint64_
 #define FGI_ROOT_BLOCK 256   // measurement builds: make variant-rootblk RB=<threads> (a multiple of 64)
 #endif
 void launch_roots(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev, uint32_t base,
-                  uint32_t n_range, int publish, bool ext_roots = false) {
+                  uint32_t n_range, int publish, bool ext_roots = false, int stamp = 0) {
     const RootMap rm{g->lbl_hot ? g->s2l : nullptr, g->ext_slots, g->ext_handles, g->lbl_K, ext_roots && g->lbl_K ? 1 : 0};
     constexpr uint32_t kRootBlock = FGI_ROOT_BLOCK;
     static_assert(kRootBlock % 64 == 0 && kRootBlock <= kBlock, "root block");
@@ -2858,9 +2910,9 @@ void launch_roots(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, con
     // the immediate roots' launch never publishes: the second launch adds to the same counter
     if (imm_dev)
         hipLaunchKernelGGL(k_roots<1>, dim3(nb), dim3(kRootBlock), 0, g->stream, roots_dev, imm_dev, n_roots, base, n_range,
-                           node, g->vis_bm, o, g->ctr, g->done, 0, rm);
+                           node, g->vis_bm, o, g->ctr, g->done, 0, rm, stamp);
     hipLaunchKernelGGL(k_roots<0>, dim3(nb), dim3(kRootBlock), 0, g->stream, roots_dev, imm_dev, n_roots, base, n_range, node,
-                       g->vis_bm, o, g->ctr, g->done, publish, rm);
+                       g->vis_bm, o, g->ctr, g->done, publish, rm, imm_dev ? 0 : stamp);
 }
 
 }  // namespace
@@ -2938,6 +2990,7 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
         return set_err(g, FGI_ENOTSUP, "cooperative wave: %u blocks cannot be resident", G);
     FGI_TRY(fold(g));   // visits of a level-launched wave
     if (coop) FGI_TRY(coop_warm(g));
+    g->wave_clean = false;   // this path dirties the wave state (run_wave re-inits)
     if (!g->coop_clean)
         hipLaunchKernelGGL(k_wave_init, dim3(kInitBlocks), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
                            (uint32_t*)nullptr, (uint64_t)g->bm_words);
@@ -3142,6 +3195,7 @@ static fgi_status run_wave_fused(fgi_graph* g, uint32_t n_roots, const uint32_t*
     hipEvent_t* ev = g->ev.data();
     const size_t eh = 2 * (size_t)kMidMax;   // the head's / tail's event pair
     if (timing || stats) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
+    g->wave_clean = false;   // this path dirties the wave state (run_wave re-inits)
     if (!a.do_init)   // the wave state cleared by its own launch: the head's first barrier has no dirty 4 MB
         hipLaunchKernelGGL(k_wave_init, dim3(kInitBlocks), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
                            a.clear_vis ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
@@ -3175,7 +3229,7 @@ static fgi_status run_wave_fused(fgi_graph* g, uint32_t n_roots, const uint32_t*
         if (g->want_ids) {
             const auto* inv64 = reinterpret_cast<const unsigned long long*>(g->inv_bm);
             hipLaunchKernelGGL(k_final_write, dim3(a.fin_G), dim3(kBlock), 0, s, inv64, words, a.fin_wpb,
-                               (const unsigned long long*)a.status, g->ctr, g->inv, 1, 1u, ListPub{});
+                               (const unsigned long long*)a.status, g->ctr, g->inv, 1, 1u, ListPub{}, WaveEnd{});
         }
         FGI_HIP(g, hipGetLastError());
         FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
@@ -3273,13 +3327,20 @@ static fgi_status run_wave_fused(fgi_graph* g, uint32_t n_roots, const uint32_t*
 // with WaveCtr::t0 times a wave without stream events (each event record costs the stream ~5 us).
 [[maybe_unused]] constexpr uint32_t kPubWords = sizeof(WaveCtr) / 8;
 namespace {
+// end.ctr (a level group's counters, run_wave): once the wave is over, the counters are zeroed after
+// the copy — the next wave starts from them without an init kernel (WaveEnd)
 __global__ __launch_bounds__(256) void k_publish(const unsigned long long* __restrict__ src, uint32_t words,
-                                                 unsigned long long* dst, unsigned long long seq) {
+                                                 unsigned long long* dst, unsigned long long seq, WaveEnd end) {
+    const bool over = end.ctr && wave_over(end);
     if (threadIdx.x == 0) dst[words + 1] = wall_clock64();
     for (uint32_t i = threadIdx.x; i < words; i += blockDim.x) dst[i] = src[i];
     __threadfence_system();
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(dst + words, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (over) {
+        unsigned long long* c = reinterpret_cast<unsigned long long*>(end.ctr);
+        for (uint32_t i = threadIdx.x; i < (uint32_t)(sizeof(WaveCtr) / 8); i += blockDim.x) c[i] = 0ull;
+    }
 }
 
 }  // namespace
@@ -3322,7 +3383,7 @@ static fgi_status wait_word(fgi_graph* g, hipStream_t s, const unsigned long lon
 
 fgi_status publish_wait(fgi_graph* g, hipStream_t s, const unsigned long long* src, uint32_t words, unsigned long long* dst) {
     const unsigned long long seq = ++g->pub_seq;
-    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, src, words, dst, seq);
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, src, words, dst, seq, WaveEnd{});
     FGI_HIP(g, hipGetLastError());
     FGI_TRY(wait_word(g, s, dst + words, seq));
     g->last_pub_t = dst[words + 1];
@@ -3332,7 +3393,7 @@ fgi_status publish_wait(fgi_graph* g, hipStream_t s, const unsigned long long* s
 // src[0, words) into dst (fine-grained host memory) without waiting: a later publish_wait on the same
 // stream covers it (its sequence word lands after this kernel's system-scope fence)
 static fgi_status publish_async(fgi_graph* g, hipStream_t s, const unsigned long long* src, uint32_t words, unsigned long long* dst) {
-    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, src, words, dst, 0ull);
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, src, words, dst, 0ull, WaveEnd{});
     FGI_HIP(g, hipGetLastError());
     return FGI_OK;
 }
@@ -3357,13 +3418,19 @@ static fgi_status counters_published(fgi_graph* g, hipStream_t s, bool mark, uns
     return FGI_OK;
 }
 
-static fgi_status counters_to_host(fgi_graph* g, hipStream_t s, bool mark) {
+static fgi_status counters_to_host(fgi_graph* g, hipStream_t s, bool mark, const WaveEnd& end = WaveEnd{}) {
 #if FGI_SPIN_WAIT
     if (mark) FGI_HIP(g, hipEventRecord(g->ev_w1, s));
-    FGI_TRY(publish_wait(g, s, reinterpret_cast<const unsigned long long*>(g->ctr), kPubWords, g->ctr_pub));
+    const unsigned long long seq = ++g->pub_seq;
+    hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, reinterpret_cast<const unsigned long long*>(g->ctr),
+                       (uint32_t)kPubWords, g->ctr_pub, seq, end);
+    FGI_HIP(g, hipGetLastError());
+    FGI_TRY(wait_word(g, s, g->ctr_pub + kPubWords, seq));
+    g->last_pub_t = g->ctr_pub[kPubWords + 1];
     memcpy(g->ctr_host, g->ctr_pub, sizeof(WaveCtr));
     if (mark) FGI_HIP(g, hipEventSynchronize(g->ev_w1));
 #else
+    (void)end;
     FGI_HIP(g, hipMemcpyAsync(g->ctr_host, g->ctr, sizeof(WaveCtr), hipMemcpyDeviceToHost, s));
     if (mark) FGI_HIP(g, hipEventRecord(g->ev_w1, s));
     FGI_HIP(g, hipStreamSynchronize(s));
@@ -3409,8 +3476,13 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         if (r != FGI_ENOTSUP) return r;
     }
 #endif
-    hipLaunchKernelGGL(k_wave_init, dim3(kInitBlocks), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
-                       g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
+    // the previous wave left the counters, statistics and invalidated bitmap zeroed (WaveEnd) and the visit
+    // bitmap is clean (fgi_restore swapped in the spare): no init kernel, the roots kernel stamps t0
+    const bool clean_start = g->wave_clean && !g->vis_stale && n_roots != 0;
+    g->wave_clean = false;
+    if (!clean_start)
+        hipLaunchKernelGGL(k_wave_init, dim3(kInitBlocks), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
+                           g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
     g->vis_stale = false;
     g->coop_clean = false;
 #if FGI_PROBE
@@ -3424,9 +3496,14 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
     if (events) FGI_HIP(g, hipEventRecord(g->ev_w0, s));
     if (n_roots) {
         g->v_dirty = true;
-        launch_roots(g, n_roots, roots_dev, imm_dev, 0u, g->n_handles, 0, ext_roots);
+        launch_roots(g, n_roots, roots_dev, imm_dev, 0u, g->n_handles, 0, ext_roots, clean_start ? 1 : 0);
     }
     const auto* node = reinterpret_cast<const unsigned long long*>(g->node);
+    // the list kernel and the publish of a group leave the state clean once the wave is over (WaveEnd):
+    // only when the list kernel runs (ids wanted, not the measurement-only merged publish)
+    static const bool list_pub = getenv("FGI_LIST_PUBLISH") && getenv("FGI_LIST_PUBLISH")[0] == '1';
+    const bool merged = FGI_SPIN_WAIT && g->want_ids && list_pub;
+    const bool leave_clean = g->want_ids && !merged && FGI_SPIN_WAIT;
     // Levels run in groups between host synchronisations (one ~30 us round trip each); the first
     // group is sized by the previous wave's depth, so a repeated workload syncs once per wave and an
     // overshoot costs only empty levels (two ~2 us launches each). Every group ends with the final
@@ -3457,10 +3534,35 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         const int L0 = L;
         WaveParams wp = wp0;
         if (!allow_pull) wp.direction = 1;
+        // k_collect has nothing to do before a push level that follows a push level (no hot snapshot, no
+        // pull winners to list). Where the previous wave's directions (their Beamer rule: LevelCtr::want)
+        // say so, the launch is left out and both levels are pinned to push — a cost choice, the result
+        // does not depend on it; a wave whose shape changed pushes there once, records what the rule
+        // wanted, and the next wave's plan follows.
+        uint32_t skip = 0, pin = 0;   // per level of the group (bit k: level L0 + k)
+        {
+            const std::vector<uint8_t>& d = g->last_dirs;
+            auto pushes = [&](int l) -> int {   // 1 push, 0 pull or unknown
+                if (wp.direction != 0) return wp.direction == 1;
+                if (l < L0) return l == L0 - 1 ? !g->ctr_host->lvl[l % kRing].pull : 0;   // the last group's (ran)
+                return (size_t)l < d.size() ? !d[l] : 0;
+            };
+            for (int k = 0; k < group && k < 32; ++k) {
+                const int l = L0 + k;
+                if (pushes(l) && (l == 0 || pushes(l - 1))) {
+                    skip |= 1u << k;
+                    pin |= 1u << k;
+                    if (k > 0) pin |= 1u << (k - 1);
+                }
+            }
+        }
         for (int k = 0; k < group; ++k, ++L) {
             const int buf = L & 1;
-            hipLaunchKernelGGL(k_collect, dim3(collect_grid_at(g, wp, L)), dim3(kCollectThreads), 0, s, L, g->ctr, wp,
-                               collect_args(g, g->n_slots, wp, buf), collect_args(g, g->n_slots, wp, buf), ~0ull);
+            WaveParams wl = wp;
+            if (k < 32 && ((pin >> k) & 1u)) wl.direction = 1;
+            if (!(k < 32 && ((skip >> k) & 1u)))
+                hipLaunchKernelGGL(k_collect, dim3(collect_grid_at(g, wl, L)), dim3(kCollectThreads), 0, s, L, g->ctr, wl,
+                                   collect_args(g, g->n_slots, wl, buf), collect_args(g, g->n_slots, wl, buf), ~0ull);
             if (timing) {
                 while (g->ev.size() < 2 * (size_t)(L + 1) + 2) {
                     hipEvent_t e;
@@ -3469,7 +3571,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
                 }
                 FGI_HIP(g, hipEventRecord(g->ev[2 * L], s));
             }
-            hipLaunchKernelGGL(k_level<false>, dim3(wp.grid), dim3(kBlock), 0, s, L, wp, expand_args(g, buf),
+            hipLaunchKernelGGL(k_level<false>, dim3(wl.grid), dim3(kBlock), 0, s, L, wl, expand_args(g, buf),
                                expand_args(g, buf), pull_args(g, g->n_slots, g->inv_bm), node, g->vis_bm,
                                out_for(g, buf ^ 1, nullptr), out_for(g, buf ^ 1, nullptr), g->ctr, g->blk_stats,
                                g->done, RemoteArgs{}, ~0ull);
@@ -3491,17 +3593,21 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         // the list kernel may publish the counters itself (one launch fewer), but its last block's
         // system-scope release then writes back the whole list first: 11.6 -> 33.7 us for configs[1]'s
         // k_final_write, 0.231 -> 0.262 ms/step (profiles/r12c); measurement only (FGI_LIST_PUBLISH=1)
-        static const bool list_pub = getenv("FGI_LIST_PUBLISH") && getenv("FGI_LIST_PUBLISH")[0] == '1';
-        const bool merged = FGI_SPIN_WAIT && g->want_ids && list_pub;
         ListPub lp{};
         if (merged) lp = ListPub{g->ctr_pub, ++g->pub_seq, g->done, (uint32_t)kPubWords};
-        FGI_HIP(g, launch_final(g, g->n_handles, g->want_ids, nullptr, lp));   // idempotent: repeated if the wave goes on
+        WaveEnd we{};
+        if (leave_clean) {
+            we = WaveEnd{g->ctr, L, use_tail ? 1 : 0, g->blk_stats, g->inv_bm, ((uint64_t)g->n_handles + 63) / 64,
+                         g->spare_dirty ? g->vis_spare : nullptr};
+            g->spare_dirty = false;   // the list kernel clears it whether the wave goes on or not
+        }
+        FGI_HIP(g, launch_final(g, g->n_handles, g->want_ids, nullptr, lp, we));   // idempotent: repeated if the wave goes on
         final_done = true;
         FGI_HIP(g, hipGetLastError());
         // the wave's end marker rides on the group's synchronisation (re-recorded if the wave goes on):
         // recording it after the wait would cost the call a further device round trip
         if (merged) FGI_TRY(counters_published(g, s, events, lp.seq));
-        else FGI_TRY(counters_to_host(g, s, events));
+        else FGI_TRY(counters_to_host(g, s, events, we));
         ++syncs;
         if (use_tail && g->ctr_host->broken) {   // half a wave is applied: poisoned until fgi_restore (fgi.h)
             FGI_HIP(g, hipMemsetAsync(g->gbar + kGbarTail, 0, sizeof(unsigned long long), s));
@@ -3526,7 +3632,7 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         }
         if (ring_ok) {
             dirs.resize(std::max<size_t>(dirs.size(), (size_t)stop), 0);
-            for (int l = L0; l < L; ++l) dirs[l] = g->ctr_host->lvl[l % kRing].pull ? 1 : 0;
+            for (int l = L0; l < L; ++l) dirs[l] = g->ctr_host->lvl[l % kRing].want ? 1 : 0;
         } else {
             dirs_ok = false;
         }
@@ -3600,6 +3706,8 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         expand_f = c.push_f - c.mid_push_f;
     }
     if (imm_dev && n_roots) note_words(g);   // immediate roots changed node words
+    // the last group's list kernel and publish saw the wave over (the host's loop ends on the same test)
+    g->wave_clean = leave_clean && final_done;
     g->last_wave_n = g->ctr_host->inv;
     g->ids_valid = g->want_ids;
     g->inv_cur = g->inv;
@@ -3689,6 +3797,7 @@ fgi_status run_wave_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_
     // has shown a frontier heavy enough to pull (as run_wave builds them after such a group)
     if (n_roots && wp0.direction != 1 && (g->lists_wanted || wp0.direction == 2)) FGI_TRY(ensure_in_lists(g));
     WaveParams wp = wp0;
+    g->wave_clean = false;   // this path dirties the wave state (run_wave re-inits)
     if (!(wp0.direction != 1 && pull_ready(g, wp0))) wp.direction = 1;
     hipLaunchKernelGGL(k_wave_init, dim3(kInitBlocks), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
                        g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
@@ -3719,7 +3828,7 @@ fgi_status run_wave_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_
     FGI_HIP(g, launch_final(g, g->n_handles, true, out));
     const unsigned long long seq = ++g->apub_seq;
     hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, reinterpret_cast<const unsigned long long*>(g->ctr),
-                       (uint32_t)kPubWords, g->apub[t & 1], seq);
+                       (uint32_t)kPubWords, g->apub[t & 1], seq, WaveEnd{});
     FGI_HIP(g, hipGetLastError());
     if (imm_dev && n_roots) note_words(g);   // immediate roots change node words (fgi_restore copies them back)
     a.ticket = t;
@@ -4052,6 +4161,7 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     // one rank: nothing is remote, the collectives are identities (skipped unless FGI_OPT_PART_COLLECTIVES)
     const bool coll = pv.world > 1 || g->opt_part_coll;
     if (coll) FGI_HIP(g, hipMemsetAsync(pv.sent_bm, 0, pv.sent_words * 4, s));
+    g->wave_clean = false;   // this path dirties the wave state (run_wave re-inits)
     if (coll) FGI_TRY(part_front_reset(g));
     hipLaunchKernelGGL(k_wave_init, dim3(kInitBlocks), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
                        g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);

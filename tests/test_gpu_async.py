@@ -145,6 +145,9 @@ def test_wave_tail_timeout_poisons_until_restore(pkg, gpu_available, mode):
     fgi = pkg.fgi
     levels, width, fanout, seed = 14, 64, 2, 0x5EED0031
     g, o, n = _layered_pair(pkg, levels, width, fanout, seed)
+    # push only: every level after the first group is a small push level, which the tail runs (a pull level
+    # would end a synchronous wave's tail before its first barrier)
+    g.set_option(fgi.OPT_DIRECTION, 1)
     g.snapshot()
     o.snapshot()
     roots = np.arange(8, dtype=np.uint32)   # level 0: the wave runs every one of the 14 levels
@@ -152,6 +155,7 @@ def test_wave_tail_timeout_poisons_until_restore(pkg, gpu_available, mode):
     o.invalidate_slots(roots)
     want = np.sort(o.inv_log())
     assert len(want) > 12 * 8
+    o.restore()   # the oracle back at the snapshot: the states a restored graph must show
     d_r = torch.from_numpy(roots.astype(np.int32)).cuda()
     torch.cuda.synchronize()
 
