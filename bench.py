@@ -180,6 +180,47 @@ def select_workloads(world: int, config: str, partition: bool) -> dict:
     return out
 
 
+def select_comm(world: int, n_gpus: int, partitioned: bool, forced: str = "") -> str:
+    """The partition's communicator (pinned by tests/test_bench_select.py): none for a single device; RCCL
+    with one process per GPU; host collectives (torch.distributed over gloo, fgi_part_init_host) when the
+    ranks outnumber the node's GPUs (RCCL refuses two ranks on one device); FGI_PART_COMM forces either."""
+    if not partitioned:
+        return ""
+    if forced:
+        return forced
+    if world <= 1:
+        return ""
+    return "host" if world > max(1, n_gpus) else "rccl"
+
+
+def line_head(world, steps, warmup, config, elapsed, v_inv, workload, n, n_edges, n_roots, parallelism, cfg) -> dict:
+    """The bench line's contract fields (pinned by tests/test_bench_select.py): value = the invalidated
+    nodes of all ranks over the max-over-ranks time of the K timed steps."""
+    return {
+        "metric": METRIC,
+        "value": v_inv / elapsed,
+        "unit": "invalidated nodes/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": elapsed / steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong" if config in ("rmat24", "rmat27") else "weak",
+        "scaling_note": ("N > 1 runs BASELINE.json configs[2] (R-MAT 27, edge factor 8) over the N GPUs: total work "
+                         "fixed. At N = 1 the headline is configs[1] (the metric's one-GPU configuration) and the "
+                         "curve's base is the `configs2_single_gpu` sub-record (configs[2]'s graph on this GPU)"),
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic",
+        "config": {
+            "workload": workload,
+            "nodes": n, "edges": int(n_edges), "roots": int(n_roots),
+            "parallelism": parallelism,
+            "scale": cfg.get("scale"), "edge_factor": cfg.get("edge_factor"),
+        },
+    }
+
+
 def main():
     # Libraries (RCCL prints a banner on communicator init) must not write to stdout: the driver
     # reads exactly one JSON line from it. Route fd 1 to stderr and keep a handle on the real one.
@@ -203,6 +244,8 @@ def main():
                     help="skip the single-threaded CPU wave (one wave at T = 1 on the identical graph, ~1 min)")
     ap.add_argument("--cpu-c2-scale", type=int, default=25,
                     help="R-MAT scale of the labelled configs[2] CPU sample (configs[2]'s generator; 0 skips it)")
+    ap.add_argument("--scale", type=int, default=0,
+                    help="rehearsals and tests only: the headline workload's generator at this R-MAT scale")
     args = ap.parse_args()
 
     import torch
@@ -215,7 +258,14 @@ def main():
     torch.cuda.set_device(gpu)
     dist = None
     if world > 1:
+        import datetime
         import torch.distributed as dist
+        # fail fast: every wait of a rank on its peers is bounded (the engine's RCCL init and collectives,
+        # its host waits, torch's bookkeeping group) and a failure exits non-zero naming the rank and the
+        # collective (main's caller), instead of the run hanging until the driver's limit
+        os.environ.setdefault("FGI_WAIT_TIMEOUT_S", "240")
+        os.environ.setdefault("FGI_RCCL_INIT_TIMEOUT_S", "180")
+        pg_timeout = datetime.timedelta(seconds=int(os.environ.get("FGI_BENCH_TIMEOUT_S", "600")))
         # The engine's collectives run over RCCL through libfgi's own communicator (fgi_part_init,
         # /opt/rocm's librccl). torch's group carries only the bench's bookkeeping — the communicator's
         # unique id, the barriers around the timed region, the max of the per-rank times, the root
@@ -223,9 +273,9 @@ def main():
         # (FGI_BENCH_TORCH_BACKEND=nccl selects torch's RCCL for it instead).
         backend = os.environ.get("FGI_BENCH_TORCH_BACKEND", "gloo")
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu), timeout=pg_timeout)
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=pg_timeout)
     tdev = "cpu" if (dist is not None and dist.get_backend() != "nccl") else f"cuda:{gpu}"
 
     pkg = _pkg.load()
@@ -235,9 +285,7 @@ def main():
     # one process per GPU; ranks beyond the node's GPUs (a rehearsal of N ranks on a smaller box) share
     # device local_rank % count, and then the engine's collectives go through the host (torch's gloo
     # group, fgi_part_init_host): RCCL refuses two ranks on one GPU
-    comm = os.environ.get("FGI_PART_COMM", "")
-    if partitioned and world > 1 and not comm:
-        comm = "host" if world > max(1, n_gpus_visible()) else "rccl"
+    comm = select_comm(world, n_gpus_visible(), partitioned, os.environ.get("FGI_PART_COMM", ""))
     knobs = (("FGI_PULL_ALPHA", "OPT_PULL_ALPHA"), ("FGI_PULL_BETA", "OPT_PULL_BETA"), ("FGI_PULL_TPB", "OPT_PULL_TPB"),
              ("FGI_PART_PLAN", "OPT_PART_PLAN"), ("FGI_PROBE_SUMMARY", "OPT_PROBE_SUMMARY"),
              ("FGI_HOT_HEADS", "OPT_HOT_HEADS"))
@@ -247,6 +295,8 @@ def main():
         cfg = dict(W.CONFIGS[name])
         if scale:
             cfg["scale"] = scale
+        elif args.scale and name == sel["headline"]:
+            cfg["scale"] = args.scale
         n = W.n_slots(cfg)
         t0 = time.time()
         if partitioned:
@@ -296,6 +346,11 @@ def main():
     def measure(g, roots):
         """W untimed warm-up steps, then K timed steps between barriers (max over ranks), then the
         same K steps again with per-level HIP events (the roofline figures)."""
+        if os.environ.get("FGI_BENCH_DROP_RANK") == str(rank):
+            # tests only: this rank leaves before its first wave, as a rank that died would; its peers'
+            # first collective must then fail within the bounded waits, naming itself
+            log(f"[rank {rank}] FGI_BENCH_DROP_RANK: leaving before the first wave")
+            os._exit(0)
         d_roots = torch.from_numpy(roots.astype(np.int32)).to(f"cuda:{gpu}")
 
         def step(stats):
@@ -515,28 +570,9 @@ def main():
     k_gbs = (k_bytes / (k_ms * 1e-3) / 1e9) if k_ms > 0 else 0.0
     traffic, traffic_src = profiled_traffic(kname, cfg.get("scale"), k_ms / max(1, k_launches))
     wave_gbs = (st.alg_bytes / (st.kernel_ms * 1e-3) / 1e9) if st.kernel_ms > 0 else 0.0
-    result = {
-        "metric": METRIC,
-        "value": value,
-        "unit": "invalidated nodes/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": elapsed / args.steps * 1e3,
-        "higher_is_better": True,
-        "scaling": "strong" if args.config in ("rmat24", "rmat27") else "weak",
-        "scaling_note": ("N > 1 runs BASELINE.json configs[2] (R-MAT 27, edge factor 8) over the N GPUs: total work "
-                         "fixed. At N = 1 the headline is configs[1] (the metric's one-GPU configuration) and the "
-                         "curve's base is the `configs2_single_gpu` sub-record (configs[2]'s graph on this GPU)"),
-        "vs_baseline": None,
-        "dtype": "u64",
-        "data": "synthetic",
-        "config": {
-            "workload": workload_name(cfg),
-            "nodes": n, "edges": int(n_edges), "roots": int(len(roots)),
-            "parallelism": parallelism(),
-            "scale": cfg.get("scale"), "edge_factor": cfg.get("edge_factor"),
-        },
+    result = line_head(world, args.steps, args.warmup, args.config, elapsed, v_inv, workload_name(cfg), n, n_edges,
+                       len(roots), parallelism(), cfg)
+    result.update({
         "gteps": gteps,
         "v_inv_per_step": v_inv // args.steps,
         "e_trav_per_step": e_trav // args.steps,
@@ -572,7 +608,7 @@ def main():
                             "gbs": (st_k.pull_bytes / (st_k.pull_ms * 1e-3) / 1e9) if st_k.pull_ms > 0 else 0.0},
         },
         "rccl": rccl,
-    }
+    })
     # SURVEY.md §8(d)'s layout-A formula B = 28 V_exp + 24 E_trav + 4 E_match + 4 R counts every
     # edge of every expanded node, as a push-only traversal would read them. Pull levels read
     # dependency-list heads instead of those edges, so B / t is a push-equivalent rate that can exceed
@@ -685,5 +721,10 @@ def n_gpus_visible() -> int:
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except Exception as e:  # a failed rank exits non-zero with its rank and the failing call named
+        log(f"[rank {os.environ.get('RANK', '0')} of {os.environ.get('WORLD_SIZE', '1')}] bench failed: "
+            f"{type(e).__name__}: {e}")
+        raise SystemExit(3)
     dump_maps()

@@ -121,6 +121,9 @@ typedef struct fgi_wave_stats {
     uint64_t fused_push_bytes; /* algorithmic bytes of the push levels they ran (20 B per edge + 40 B
                                   per frontier entry, as a k_level push) */
     uint64_t host_syncs;       /* times the wave waited for the device */
+    uint64_t pull_pushed;      /* asynchronous waves: levels past the queued group that the automatic
+                                  direction choice would pull and the wave ran as push (same result,
+                                  slower; the next queued wave's group covers them) */
 } fgi_wave_stats;
 
 typedef struct fgi_prune_stats {
@@ -228,11 +231,23 @@ fgi_status fgi_invalidate_bits(fgi_graph* g, uint32_t n_roots, const uint32_t* r
  * after that). Every other entry point except fgi_restore and
  * fgi_set_option first waits for the waves in flight. A wave queued this way runs all its levels in
  * one queue (no second level group): its later pull levels, if the previous wave's shape predicted
- * fewer, run as push levels — same result, slower. */
+ * fewer, run as push levels — same result, slower, and counted in fgi_wave_stats.pull_pushed. A wave
+ * whose tail's grid barrier times out fails its fgi_wave_wait with FGI_EDEVICE and poisons the graph
+ * until fgi_restore, as a synchronous wave does. */
 fgi_status fgi_invalidate_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                                 uint64_t* ticket);
 fgi_status fgi_wave_wait(fgi_graph* g, uint64_t ticket, uint64_t* out_n, const uint32_t** ids_dev,
                          fgi_wave_stats* stats);
+/* The same pair for a host layer that holds its roots and wants its ids in host memory (the scope-dispose
+ * flush of `using (Computed.Invalidate())` with ComputedExt.WhenInvalidated awaited later): the roots
+ * (boundary handles, as fgi_invalidate) are staged through a pinned buffer of the ticket's own and copied
+ * on the graph's stream, so the call returns without waiting; fgi_wave_wait_ids waits like fgi_wave_wait
+ * and copies the ticket's ids (ascending) into out_ids (FGI_ECAPACITY with *out_n set if cap is short;
+ * out_ids may be NULL for the count). A wave queued after the ticket keeps running during the copy. */
+fgi_status fgi_invalidate_async_host(fgi_graph* g, uint32_t n_roots, const uint32_t* roots, const uint8_t* immediately,
+                                     uint64_t* ticket);
+fgi_status fgi_wave_wait_ids(fgi_graph* g, uint64_t ticket, uint32_t* out_ids, uint64_t cap, uint64_t* out_n,
+                             fgi_wave_stats* stats);
 /* Page-locked host memory for the calls' host arrays (roots in, ids / bitmaps out): copies from and
  * to it run at full PCIe rate without a staging copy (SURVEY.md §8(b) "Ownership"). */
 fgi_status fgi_alloc_pinned(uint64_t bytes, void** out);

@@ -238,7 +238,7 @@ struct WaveCtr {
     unsigned long long mid_push_f;
     unsigned long long t0;          // device wall clock at k_wave_init (a wave's kernel span without events)
     unsigned long long t_max;       // the wave's largest level, in edges (level-group waves: tail_account)
-    unsigned long long pad2;
+    unsigned long long pull_pushed; // levels the automatic choice would pull that a tail ran as push (async `all`)
     LevelCtr lvl[kRing];
 };
 constexpr unsigned long long kPhaseDone = 1;
@@ -407,6 +407,10 @@ struct fgi_graph {
     uint64_t next_ticket = 1;
     uint32_t* inv_alt = nullptr;
     uint32_t* inv_cur = nullptr;
+    // fgi_invalidate_async_host: per ticket parity, the roots staged in pinned memory and their device copy
+    uint32_t* ar_h[2] = {nullptr, nullptr};
+    uint32_t* ar_d[2] = {nullptr, nullptr};
+    uint64_t ar_cap[2] = {0, 0};
     bool lists_wanted = false;         // a wave met a frontier heavy enough to pull (async waves build lists first)
     bool want_ids = true;              // run_wave writes the invalidated list (false: bitmap and count only)
     bool ids_valid = false;            // inv holds the last wave's list (else ensure_ids rebuilds it)
@@ -669,6 +673,8 @@ fgi_status run_wave_coop(fgi_graph* g, uint32_t n_max, const uint32_t* roots_dev
 fgi_status run_wave_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                           uint64_t* ticket);
 fgi_status wave_wait(fgi_graph* g, uint64_t ticket, uint64_t* out_n, const uint32_t** ids_dev, fgi_wave_stats* stats);
+// the same wave from roots in host memory: staged through the ticket parity's pinned buffer
+fgi_status run_wave_async_host(fgi_graph* g, uint32_t n_roots, const uint32_t* roots, const uint8_t* imm, uint64_t* ticket);
 fgi_status drain_async(fgi_graph* g);
 // Rebuild the expandable-class bitmap if node words changed (wave.hip).
 fgi_status ensure_cls(fgi_graph* g);

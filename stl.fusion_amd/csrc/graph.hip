@@ -1931,6 +1931,10 @@ fgi_status fgi_destroy(fgi_graph* g) {
     dfree(g->pool_top_dev);
     dfree(g->inv);
     dfree(g->inv_alt);
+    for (int k = 0; k < 2; ++k) {
+        if (g->ar_h[k]) (void)hipHostFree(g->ar_h[k]);
+        dfree(g->ar_d[k]);
+    }
     for (int k = 0; k < 2; ++k)
         if (g->apub[k]) hipHostFree(g->apub[k]);
     for (int i = 0; i < 2; ++i) {
@@ -2528,6 +2532,33 @@ fgi_status fgi_wave_wait(fgi_graph* g, uint64_t ticket, uint64_t* out_n, const u
     FGI_TRY(usable_now(g));
     hipSetDevice(g->device);
     return wave_wait(g, ticket, out_n, ids_dev, stats);
+}
+
+fgi_status fgi_invalidate_async_host(fgi_graph* g, uint32_t n_roots, const uint32_t* roots, const uint8_t* immediately,
+                                     uint64_t* ticket) {
+    if (!g || (n_roots && !roots) || !ticket) return FGI_EINVAL;
+    FGI_TRY(usable_now(g));
+    if (g->part) return set_err(g, FGI_ESTATE, "fgi_invalidate_async_host: partitioned graph, use fgi_part_invalidate");
+    hipSetDevice(g->device);
+    return run_wave_async_host(g, n_roots, roots, immediately, ticket);
+}
+
+fgi_status fgi_wave_wait_ids(fgi_graph* g, uint64_t ticket, uint32_t* out_ids, uint64_t cap, uint64_t* out_n,
+                             fgi_wave_stats* stats) {
+    if (!g) return FGI_EINVAL;
+    FGI_TRY(usable_now(g));
+    hipSetDevice(g->device);
+    uint64_t n = 0;
+    const uint32_t* ids = nullptr;
+    FGI_TRY(wave_wait(g, ticket, &n, &ids, stats));
+    if (out_n) *out_n = n;
+    if (!out_ids || n == 0) return FGI_OK;
+    if (n > cap) return set_err(g, FGI_ECAPACITY, "wave %llu invalidated %llu handles, the buffer holds %llu",
+                                (unsigned long long)ticket, (unsigned long long)n, (unsigned long long)cap);
+    // a blocking copy on the null stream: the graph's stream is non-blocking, so a wave queued after this
+    // ticket's keeps running (the ticket's buffer is its own until the wave two tickets later is queued)
+    FGI_HIP(g, hipMemcpy(out_ids, ids, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return FGI_OK;
 }
 
 fgi_status fgi_alloc_pinned(uint64_t bytes, void** out) {

@@ -21,6 +21,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <dlfcn.h>
+#include <sched.h>
 
 #include <algorithm>
 #include <condition_variable>
@@ -124,6 +125,9 @@ struct RcclApi {
     decltype(&ncclGetVersion) GetVersion = nullptr;
     decltype(&ncclGetUniqueId) GetUniqueId = nullptr;
     decltype(&ncclCommInitRank) CommInitRank = nullptr;
+    decltype(&ncclCommInitRankConfig) CommInitRankConfig = nullptr;
+    decltype(&ncclCommGetAsyncError) CommGetAsyncError = nullptr;
+    decltype(&ncclCommAbort) CommAbort = nullptr;
     decltype(&ncclCommDestroy) CommDestroy = nullptr;
     decltype(&ncclGetErrorString) GetErrorString = nullptr;
     decltype(&ncclAllReduce) AllReduce = nullptr;
@@ -158,6 +162,9 @@ static const RcclApi& rccl() {
         sym(a.GetVersion, "ncclGetVersion");
         sym(a.GetUniqueId, "ncclGetUniqueId");
         sym(a.CommInitRank, "ncclCommInitRank");
+        sym(a.CommInitRankConfig, "ncclCommInitRankConfig");
+        sym(a.CommGetAsyncError, "ncclCommGetAsyncError");
+        sym(a.CommAbort, "ncclCommAbort");
         sym(a.CommDestroy, "ncclCommDestroy");
         sym(a.GetErrorString, "ncclGetErrorString");
         sym(a.AllReduce, "ncclAllReduce");
@@ -232,15 +239,69 @@ bool part_view(fgi_graph* g, PartView* v) {
     return true;
 }
 
-static fgi_status nccl_check(fgi_graph* g, ncclResult_t r, const char* what) {
-    if (r == ncclSuccess) return FGI_OK;
-    return set_err(g, FGI_EDEVICE, "%s: %s", what, rccl().GetErrorString(r));
+// ---- bounded waits on the RCCL path (fail fast, never hang) ------------------------------------------
+// A rank whose peer never joins a collective would otherwise wait forever: in ncclCommInitRank, in a
+// grouped send/recv's connection setup, or on its stream behind a collective kernel. The communicator
+// is non-blocking (ncclConfig_t.blocking = 0): every RCCL call that reports ncclInProgress is polled
+// through ncclCommGetAsyncError, and every host wait behind a collective polls the stream, each for at
+// most FGI_WAIT_TIMEOUT_S seconds (default 300; FGI_RCCL_INIT_TIMEOUT_S, default 120, for the
+// communicator's creation). On timeout the communicator is aborted (its kernels leave), the graph is
+// marked failed and the call returns FGI_EDEVICE naming the rank and the collective.
+static double wait_limit_s(const char* var, double dflt) {
+    const char* e = getenv(var);
+    return e && *e ? atof(e) : dflt;
 }
-#define FGI_NCCL(g, call)                                                  \
-    do {                                                                   \
-        ncclResult_t _r = (call);                                          \
-        if (_r != ncclSuccess) return nccl_check((g), _r, #call);          \
+
+static fgi_status comm_fail(fgi_graph* g, const char* what, double limit_s) {
+    PartState* p = ps(g);
+    if (p && p->comm && rccl().CommAbort) {
+        rccl().CommAbort(p->comm);
+        p->comm = nullptr;
+    }
+    g->failed = true;
+    return set_err(g, FGI_EDEVICE, "rank %d of %d: %s did not complete within %.0f s (a peer missing or stuck); "
+                                   "the communicator was aborted", g->rank, g->world, what, limit_s);
+}
+
+// an RCCL call's result: ncclInProgress (non-blocking communicator) is waited out, bounded
+static fgi_status nccl_settle(fgi_graph* g, ncclComm_t comm, ncclResult_t r, const char* what, double limit_s) {
+    if (r == ncclInProgress && comm && rccl().CommGetAsyncError) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint64_t k = 0; r == ncclInProgress; ++k) {
+            if (rccl().CommGetAsyncError(comm, &r) != ncclSuccess) break;
+            if (r != ncclInProgress) break;
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s)
+                return comm_fail(g, what, limit_s);
+            if (k > 1024) sched_yield();
+        }
+    }
+    if (r == ncclSuccess) return FGI_OK;
+    g->failed = true;
+    return set_err(g, FGI_EDEVICE, "rank %d of %d: %s: %s", g->rank, g->world, what, rccl().GetErrorString(r));
+}
+#define FGI_NCCL(g, call)                                                                                  \
+    do {                                                                                                   \
+        ncclResult_t _r = (call);                                                                          \
+        if (_r != ncclSuccess)                                                                             \
+            FGI_TRY(nccl_settle((g), ps(g) ? ps(g)->comm : nullptr, _r, #call,                             \
+                                wait_limit_s("FGI_WAIT_TIMEOUT_S", 300.0)));                                \
     } while (0)
+
+// the host's wait behind this rank's collectives: the stream polled, bounded
+static fgi_status comm_sync(fgi_graph* g, hipStream_t s, const char* what) {
+    const double limit_s = wait_limit_s("FGI_WAIT_TIMEOUT_S", 300.0);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint64_t k = 0;; ++k) {
+        const hipError_t e = hipStreamQuery(s);
+        if (e == hipSuccess) return FGI_OK;
+        if (e != hipErrorNotReady) return hip_check(g, e, what);
+        if ((k & 255) == 0 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit_s)
+            return comm_fail(g, what, limit_s);
+        if (k < 4096) __builtin_ia32_pause();
+        else sched_yield();
+    }
+}
 
 // ---- RCCL (one process per GPU) ----------------------------------------------------------------
 struct RcclComm final : PartComm {
@@ -257,11 +318,13 @@ struct RcclComm final : PartComm {
         }
 #if FGI_SPIN_WAIT
         (void)host;
-        FGI_TRY(publish_wait(g, s, src, count, g->red_pub));   // the host spins instead of a stream sync
+        // the host spins instead of a stream sync (publish_wait is bounded by FGI_WAIT_TIMEOUT_S too)
+        if (publish_wait(g, s, src, count, g->red_pub) != FGI_OK)
+            return comm_fail(g, "all-reduce (wave counters)", wait_limit_s("FGI_WAIT_TIMEOUT_S", 300.0));
         for (uint32_t i = 0; i < count; ++i) out[i] = g->red_pub[i];
 #else
         FGI_HIP(g, hipMemcpyAsync(host, src, 8 * count, hipMemcpyDeviceToHost, s));
-        FGI_HIP(g, hipStreamSynchronize(s));
+        FGI_TRY(comm_sync(g, s, "all-reduce (wave counters)"));
         for (uint32_t i = 0; i < count; ++i) out[i] = host[i];
 #endif
         return FGI_OK;
@@ -276,8 +339,7 @@ struct RcclComm final : PartComm {
         PartState* p = ps(g);
         if (n && (p->v.world > 1 || g->opt_part_coll))
             FGI_NCCL(g, rccl().AllReduce(dev, dev, n, ncclUint32, ncclSum, p->comm, g->stream));
-        FGI_HIP(g, hipStreamSynchronize(g->stream));
-        return FGI_OK;
+        return comm_sync(g, g->stream, "all-reduce (u32)");
     }
     fgi_status allgather_cur_async(fgi_graph* g) override {
         PartState* p = ps(g);
@@ -293,7 +355,7 @@ struct RcclComm final : PartComm {
         hipStream_t s = g->stream;
         FGI_NCCL(g, rccl().AllGather(p->v.send_cnt, p->all_cnt, S, ncclUint64, p->comm, s));
         FGI_HIP(g, hipMemcpyAsync(p->all_cnt_host, p->all_cnt, (size_t)W * S * 8, hipMemcpyDeviceToHost, s));
-        FGI_HIP(g, hipStreamSynchronize(s));
+        FGI_TRY(comm_sync(g, s, "all-gather of the push level's counts"));
         const unsigned long long* c = p->all_cnt_host;   // c[q * S + r]: sent by q to r; c[q * S + W + i]: q's F, T
         sum_counts(c, W, glob);
         uint64_t recv = 0, sent = 0;
@@ -324,7 +386,7 @@ struct RcclComm final : PartComm {
         FGI_HIP(g, hipMemcpyAsync(p->scalar, p->scalar_host, 8, hipMemcpyHostToDevice, g->stream));
         FGI_NCCL(g, rccl().AllGather(p->scalar, p->all_cnt, 1, ncclUint64, p->comm, g->stream));
         FGI_HIP(g, hipMemcpyAsync(p->all_cnt_host, p->all_cnt, (size_t)W * 8, hipMemcpyDeviceToHost, g->stream));
-        FGI_HIP(g, hipStreamSynchronize(g->stream));
+        FGI_TRY(comm_sync(g, g->stream, "all-gather of a count"));
         for (uint32_t q = 0; q < W; ++q) all[q] = p->all_cnt_host[q];
         return FGI_OK;
     }
@@ -364,7 +426,10 @@ struct HostComm final : PartComm {
         rbuf.resize((size_t)W * bytes + 1);
         if (sbuf.size() < bytes) sbuf.resize(bytes);
         const int rc = fn(ctx, sbuf.data(), bytes, rbuf.data());
-        return rc == 0 ? FGI_OK : set_err(g, FGI_EDEVICE, "host all-gather failed (%d)", rc);
+        if (rc == 0) return FGI_OK;
+        g->failed = true;   // a collective of the wave's protocol is missing on this rank: its state is undefined
+        return set_err(g, FGI_EDEVICE, "rank %d of %d: host all-gather of %llu bytes failed (%d; a peer missing?)", g->rank,
+                       g->world, (unsigned long long)bytes, rc);
     }
     // device -> sbuf (synchronises the stream: the device words are final)
     fgi_status stage(fgi_graph* g, const void* dev, uint64_t bytes, uint64_t at = 0) {
@@ -1216,10 +1281,32 @@ fgi_status fgi_part_init(fgi_graph* g, uint32_t n_global, const uint8_t* id128) 
     PartState* p = ps(g);
     ncclUniqueId id;
     std::memcpy(id.internal, id128, NCCL_UNIQUE_ID_BYTES);
-    ncclResult_t r = rccl().CommInitRank(&p->comm, (int)p->v.world, id, g->rank);
+    // non-blocking communicator: its creation (every rank must join) and every later call that reports
+    // ncclInProgress are waited out with a bound (nccl_settle); FGI_RCCL_BLOCKING=1 makes the plain
+    // blocking communicator instead (no bounds)
+    const char* blk = getenv("FGI_RCCL_BLOCKING");
+    ncclResult_t r;
+    if (blk && blk[0] == '1') {
+        r = rccl().CommInitRank(&p->comm, (int)p->v.world, id, g->rank);
+    } else {
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        r = rccl().CommInitRankConfig(&p->comm, (int)p->v.world, id, g->rank, &cfg);
+        if (r == ncclInProgress) {
+            const fgi_status st = nccl_settle(g, p->comm, r, "ncclCommInitRankConfig (every rank must join)",
+                                              wait_limit_s("FGI_RCCL_INIT_TIMEOUT_S", 120.0));
+            if (st != FGI_OK) {
+                const std::string err = g->err;
+                part_destroy(g);
+                g->failed = false;   // the graph itself is intact: the partition was not created
+                return set_err(g, st, "%s", err.c_str());
+            }
+            r = ncclSuccess;
+        }
+    }
     if (r != ncclSuccess) {
         part_destroy(g);
-        return set_err(g, FGI_EDEVICE, "ncclCommInitRank: %s", rccl().GetErrorString(r));
+        return set_err(g, FGI_EDEVICE, "rank %d of %d: ncclCommInitRank: %s", g->rank, g->world, rccl().GetErrorString(r));
     }
     p->ops.reset(new RcclComm());
     return FGI_OK;

@@ -2387,8 +2387,12 @@ __global__ __launch_bounds__(kBlock) void k_wave_tail(TailArgs a) {
         if (threadIdx.x == 0) s_ft = coh_read(&lc.ft);   // a push producer's packed counter (or the pull's F / T)
         __syncthreads();
         const uint64_t F = lc.F ? lc.F : (s_ft >> 32), T = lc.F ? lc.T : (s_ft & 0xFFFFFFFFull);
-        if (F == 0 || (!a.all && (level_pulls(ctr, L, a.wp, F, T) || T > a.max_edges))) break;
-        if (blockIdx.x == 0 && threadIdx.x == 0) acc.add(F, T, false, true);
+        const bool wants_pull = F != 0 && level_pulls(ctr, L, a.wp, F, T);
+        if (F == 0 || (!a.all && (wants_pull || T > a.max_edges))) break;
+        if (blockIdx.x == 0 && threadIdx.x == 0) {
+            acc.add(F, T, false, true);
+            if (wants_pull) ctr->pull_pushed += 1;   // an asynchronous wave's level past its queued group
+        }
         if (first && L > 0 && ctr->lvl[(L + kRing - 1) % kRing].pull) {   // after a pull level: its frontier list
             collect_front(lc, a.wp.grid, a.col[L & 1], (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6),
                           (uint64_t)gridDim.x * (blockDim.x >> 6));
@@ -3447,6 +3451,31 @@ static void forget_async_results(fgi_graph* g, const uint32_t* buf) {
         if (!a.busy && a.ticket && ((a.ticket & 1) ? g->inv_alt : g->inv) == buf) a.ticket = 0;
 }
 
+// k_collect has nothing to do before a push level that follows a push level (no hot snapshot, no pull
+// winners to list). Where the previous wave's directions (what the automatic choice wanted:
+// LevelCtr::want) say so, a level group leaves the launch out and pins both levels to push — a cost
+// choice, the result does not depend on it; a wave whose shape changed pushes there once, records what
+// the rule wanted, and the next wave's plan follows. Bit k of *skip / *pin: level L0 + k. prev_pull: the
+// level before L0 pulled (-1: L0 is the wave's first level or the group follows nothing known).
+static void plan_collects(const fgi_graph* g, const WaveParams& wp, int L0, int group, int prev_pull, uint32_t* skip,
+                          uint32_t* pin) {
+    const std::vector<uint8_t>& d = g->last_dirs;
+    auto pushes = [&](int l) -> bool {
+        if (wp.direction != 0) return wp.direction == 1;
+        if (l < L0) return prev_pull == 0;   // only the level just before the group is known (it ran)
+        return (size_t)l < d.size() && !d[l];
+    };
+    *skip = *pin = 0;
+    for (int k = 0; k < group && k < 32; ++k) {
+        const int l = L0 + k;
+        if (pushes(l) && (l == 0 || pushes(l - 1))) {
+            *skip |= 1u << k;
+            *pin |= 1u << k;
+            if (k > 0) *pin |= 1u << (k - 1);
+        }
+    }
+}
+
 fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, const uint8_t* imm_dev,
                     fgi_wave_stats* stats, bool ext_roots) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -3534,28 +3563,8 @@ fgi_status run_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_dev, c
         const int L0 = L;
         WaveParams wp = wp0;
         if (!allow_pull) wp.direction = 1;
-        // k_collect has nothing to do before a push level that follows a push level (no hot snapshot, no
-        // pull winners to list). Where the previous wave's directions (their Beamer rule: LevelCtr::want)
-        // say so, the launch is left out and both levels are pinned to push — a cost choice, the result
-        // does not depend on it; a wave whose shape changed pushes there once, records what the rule
-        // wanted, and the next wave's plan follows.
-        uint32_t skip = 0, pin = 0;   // per level of the group (bit k: level L0 + k)
-        {
-            const std::vector<uint8_t>& d = g->last_dirs;
-            auto pushes = [&](int l) -> int {   // 1 push, 0 pull or unknown
-                if (wp.direction != 0) return wp.direction == 1;
-                if (l < L0) return l == L0 - 1 ? !g->ctr_host->lvl[l % kRing].pull : 0;   // the last group's (ran)
-                return (size_t)l < d.size() ? !d[l] : 0;
-            };
-            for (int k = 0; k < group && k < 32; ++k) {
-                const int l = L0 + k;
-                if (pushes(l) && (l == 0 || pushes(l - 1))) {
-                    skip |= 1u << k;
-                    pin |= 1u << k;
-                    if (k > 0) pin |= 1u << (k - 1);
-                }
-            }
-        }
+        uint32_t skip = 0, pin = 0;   // left-out collects, levels pinned to push (plan_collects)
+        plan_collects(g, wp, L0, group, L0 > 0 ? (g->ctr_host->lvl[(L0 - 1) % kRing].pull ? 1 : 0) : -1, &skip, &pin);
         for (int k = 0; k < group; ++k, ++L) {
             const int buf = L & 1;
             WaveParams wl = wp;
@@ -3797,10 +3806,13 @@ fgi_status run_wave_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_
     // has shown a frontier heavy enough to pull (as run_wave builds them after such a group)
     if (n_roots && wp0.direction != 1 && (g->lists_wanted || wp0.direction == 2)) FGI_TRY(ensure_in_lists(g));
     WaveParams wp = wp0;
-    g->wave_clean = false;   // this path dirties the wave state (run_wave re-inits)
     if (!(wp0.direction != 1 && pull_ready(g, wp0))) wp.direction = 1;
-    hipLaunchKernelGGL(k_wave_init, dim3(kInitBlocks), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
-                       g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
+    // as run_wave: no init kernel after a wave that left the state clean (the queue is stream-ordered)
+    const bool clean_start = g->wave_clean && !g->vis_stale && n_roots != 0;
+    g->wave_clean = false;
+    if (!clean_start)
+        hipLaunchKernelGGL(k_wave_init, dim3(kInitBlocks), dim3(kBlock), 0, s, g->ctr, g->blk_stats, g->inv_bm,
+                           g->vis_stale ? g->vis_bm : nullptr, (uint64_t)g->bm_words);
     g->vis_stale = false;
     g->coop_clean = false;
     const auto* node = reinterpret_cast<const unsigned long long*>(g->node);
@@ -3808,12 +3820,17 @@ fgi_status run_wave_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_
     int group = std::min(8, std::max(std::max(1, g->last_head), g->last_levels));
     if (n_roots) {
         g->v_dirty = true;
-        launch_roots(g, n_roots, roots_dev, imm_dev, 0u, g->n_handles, 0, true);
+        launch_roots(g, n_roots, roots_dev, imm_dev, 0u, g->n_handles, 0, true, clean_start ? 1 : 0);
+        uint32_t skip = 0, pin = 0;
+        plan_collects(g, wp, 0, group, -1, &skip, &pin);
         for (int L = 0; L < group; ++L) {
             const int buf = L & 1;
-            hipLaunchKernelGGL(k_collect, dim3(collect_grid_at(g, wp, L)), dim3(kCollectThreads), 0, s, L, g->ctr, wp,
-                               collect_args(g, g->n_slots, wp, buf), collect_args(g, g->n_slots, wp, buf), ~0ull);
-            hipLaunchKernelGGL(k_level<false>, dim3(wp.grid), dim3(kBlock), 0, s, L, wp, expand_args(g, buf),
+            WaveParams wl = wp;
+            if (L < 32 && ((pin >> L) & 1u)) wl.direction = 1;
+            if (!(L < 32 && ((skip >> L) & 1u)))
+                hipLaunchKernelGGL(k_collect, dim3(collect_grid_at(g, wl, L)), dim3(kCollectThreads), 0, s, L, g->ctr, wl,
+                                   collect_args(g, g->n_slots, wl, buf), collect_args(g, g->n_slots, wl, buf), ~0ull);
+            hipLaunchKernelGGL(k_level<false>, dim3(wl.grid), dim3(kBlock), 0, s, L, wl, expand_args(g, buf),
                                expand_args(g, buf), pull_args(g, g->n_slots, g->inv_bm), node, g->vis_bm,
                                out_for(g, buf ^ 1, nullptr), out_for(g, buf ^ 1, nullptr), g->ctr, g->blk_stats,
                                g->done, RemoteArgs{}, ~0ull);
@@ -3825,11 +3842,17 @@ fgi_status run_wave_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_
         group = 0;
     }
     uint32_t* out = (t & 1) ? g->inv_alt : g->inv;
-    FGI_HIP(g, launch_final(g, g->n_handles, true, out));
+    // the queue runs every level (the tail's `all`), so the wave is over after it: its list kernel and
+    // publish leave the state clean for the next wave (WaveEnd)
+    const WaveEnd we{g->ctr, group, 1, g->blk_stats, g->inv_bm, ((uint64_t)g->n_handles + 63) / 64,
+                     g->spare_dirty ? g->vis_spare : nullptr};
+    g->spare_dirty = false;
+    FGI_HIP(g, launch_final(g, g->n_handles, true, out, ListPub{}, we));
     const unsigned long long seq = ++g->apub_seq;
     hipLaunchKernelGGL(k_publish, dim3(1), dim3(256), 0, s, reinterpret_cast<const unsigned long long*>(g->ctr),
-                       (uint32_t)kPubWords, g->apub[t & 1], seq, WaveEnd{});
+                       (uint32_t)kPubWords, g->apub[t & 1], seq, we);
     FGI_HIP(g, hipGetLastError());
+    g->wave_clean = true;   // once the queue has run (every later launch is stream-ordered after it)
     if (imm_dev && n_roots) note_words(g);   // immediate roots change node words (fgi_restore copies them back)
     a.ticket = t;
     a.seq = seq;
@@ -3842,6 +3865,40 @@ fgi_status run_wave_async(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_
     g->next_ticket = t + 1;
     if (ticket) *ticket = t;
     return FGI_OK;
+}
+
+// fgi_invalidate_async with roots in host memory: the ticket parity's pinned buffer takes a copy (its
+// previous wave, two tickets back, has completed before its slot is reused: run_wave_async waits for it)
+// and a stream-ordered copy moves it to the device, so the call still returns without waiting.
+fgi_status run_wave_async_host(fgi_graph* g, uint32_t n_roots, const uint32_t* roots, const uint8_t* imm, uint64_t* ticket) {
+    const uint64_t t = g->next_ticket;
+    const int k = (int)(t & 1);
+    fgi_graph::AsyncWave& a = g->aw[k];
+    if (a.busy) FGI_TRY(wave_wait(g, a.ticket, nullptr, nullptr, nullptr));   // its staged roots are consumed
+    const uint64_t need = std::max<uint64_t>(n_roots, 1);
+    if (g->ar_cap[k] < need) {
+        if (g->ar_h[k]) (void)hipHostFree(g->ar_h[k]);
+        if (g->ar_d[k]) (void)hipFree(g->ar_d[k]);
+        g->ar_h[k] = g->ar_d[k] = nullptr;
+        g->ar_cap[k] = 0;
+        const uint64_t cap = std::max<uint64_t>(need, 4096);
+        // roots (4 B each) then the immediately flags (1 B each), in one pinned and one device buffer
+        if (hipHostMalloc(reinterpret_cast<void**>(&g->ar_h[k]), cap * 5, hipHostMallocDefault) != hipSuccess ||
+            hipMalloc(reinterpret_cast<void**>(&g->ar_d[k]), cap * 5) != hipSuccess)
+            return set_err(g, FGI_ENOMEM, "async wave: root staging");
+        g->ar_cap[k] = cap;
+    }
+    uint8_t* imm_h = reinterpret_cast<uint8_t*>(g->ar_h[k] + g->ar_cap[k]);
+    uint8_t* imm_d = reinterpret_cast<uint8_t*>(g->ar_d[k] + g->ar_cap[k]);
+    if (n_roots) {
+        memcpy(g->ar_h[k], roots, (size_t)n_roots * 4);
+        FGI_HIP(g, hipMemcpyAsync(g->ar_d[k], g->ar_h[k], (size_t)n_roots * 4, hipMemcpyHostToDevice, g->stream));
+        if (imm) {
+            memcpy(imm_h, imm, n_roots);
+            FGI_HIP(g, hipMemcpyAsync(imm_d, imm_h, n_roots, hipMemcpyHostToDevice, g->stream));
+        }
+    }
+    return run_wave_async(g, n_roots, g->ar_d[k], imm && n_roots ? imm_d : nullptr, ticket);
 }
 
 fgi_status wave_wait(fgi_graph* g, uint64_t ticket, uint64_t* out_n, const uint32_t** ids_dev, fgi_wave_stats* stats) {
@@ -3888,11 +3945,16 @@ fgi_status wave_wait(fgi_graph* g, uint64_t ticket, uint64_t* out_n, const uint3
     const uint64_t stop = a.group ? std::max<uint64_t>((uint64_t)a.group, c.cur) : 0;
     if (stop < (uint64_t)kRing - 4) {
         head = 1;
+        std::vector<uint8_t> dirs(stop, 0);   // the next waves' launch plans (plan_collects); the tail's levels push
         for (uint64_t l = 0; l < (uint64_t)a.group; ++l) {
             const LevelCtr& lc = c.lvl[l % kRing];
+            dirs[l] = lc.want ? 1 : 0;
             if (lvl_F(lc) && (lc.pull || lvl_T(lc) > (uint64_t)tail_blocks(g) * kChunk))
                 head = l + (lc.pull ? tail_head_after_pull() : 1);
         }
+        if (a.n_roots) g->last_dirs.swap(dirs);
+    } else if (a.n_roots) {
+        g->last_dirs.clear();
     }
     a.n_inv = c.inv;
     g->last_wave_n = c.inv;
@@ -3919,6 +3981,7 @@ fgi_status wave_wait(fgi_graph* g, uint64_t ticket, uint64_t* out_n, const uint3
         stats->kernel_ms += wall_ms(g, c.t0, pub[kPubWords + 1]);
         stats->f_total += f_total;
         stats->host_syncs += 1;
+        stats->pull_pushed += c.pull_pushed;
         stats->total_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a.t0).count();
     }
     return FGI_OK;

@@ -60,7 +60,7 @@ class WaveStats(C.Structure):
                 ("expand_ms", C.c_double), ("expand_bytes", C.c_uint64), ("pull_levels", C.c_uint64),
                 ("pull_edges", C.c_uint64), ("pull_ms", C.c_double), ("pull_bytes", C.c_uint64),
                 ("pull_launches", C.c_uint64), ("fused_launches", C.c_uint64), ("fused_ms", C.c_double),
-                ("fused_push_bytes", C.c_uint64), ("host_syncs", C.c_uint64)]
+                ("fused_push_bytes", C.c_uint64), ("host_syncs", C.c_uint64), ("pull_pushed", C.c_uint64)]
 
     def as_dict(self) -> dict:
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -154,6 +154,8 @@ SIGNATURES = {
     "fgi_part_init_host": [_G, C.c_uint32, C.c_void_p, C.c_void_p],
     "fgi_invalidate_async": [_G, C.c_uint32, C.c_void_p, C.c_void_p, C.POINTER(C.c_uint64)],
     "fgi_wave_wait": [_G, C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(C.c_void_p), C.POINTER(WaveStats)],
+    "fgi_invalidate_async_host": [_G, C.c_uint32, C.POINTER(C.c_uint32), C.POINTER(C.c_uint8), C.POINTER(C.c_uint64)],
+    "fgi_wave_wait_ids": [_G, C.c_uint64, C.POINTER(C.c_uint32), C.c_uint64, C.POINTER(C.c_uint64), C.POINTER(WaveStats)],
     "fgi_part_local_run_batch": [C.POINTER(C.c_void_p), C.c_uint32, C.c_uint32, C.POINTER(Step), _u32p, C.c_uint64,
                                  _u64p, C.POINTER(BatchStats)],
     "fgi_part_local_prune": [C.POINTER(C.c_void_p), C.c_uint32, C.POINTER(PruneStats)],
@@ -460,6 +462,25 @@ class Graph:
         self._check(self.lib.fgi_wave_wait(self.h, ticket, C.byref(n), C.byref(p),
                                            C.byref(stats) if stats is not None else None), "wave_wait")
         return n.value, p.value or 0
+
+    def invalidate_async_host(self, roots, immediately=None) -> int:
+        """fgi_invalidate_async_host: queue a wave from roots in host memory; returns its ticket."""
+        r = _u32(roots)
+        imm = _u8(immediately) if immediately is not None else None
+        t = C.c_uint64()
+        self._check(self.lib.fgi_invalidate_async_host(self.h, len(r), _ptr(r, C.c_uint32), _ptr(imm, C.c_uint8),
+                                                       C.byref(t)), "invalidate_async_host")
+        return t.value
+
+    def wave_wait_ids(self, ticket: int, stats: Optional[WaveStats] = None) -> np.ndarray:
+        """fgi_wave_wait_ids: wait for the ticket's wave, its invalidated handles (ascending) on the host."""
+        n = C.c_uint64()
+        self._check(self.lib.fgi_wave_wait_ids(self.h, ticket, None, 0, C.byref(n),
+                                               C.byref(stats) if stats is not None else None), "wave_wait_ids")
+        ids = np.zeros(n.value, np.uint32)
+        self._check(self.lib.fgi_wave_wait_ids(self.h, ticket, _ptr(ids, C.c_uint32), len(ids), C.byref(n), None),
+                    "wave_wait_ids")
+        return ids
 
     def last_wave_ids(self) -> np.ndarray:
         """Handles invalidated by the last wave (e.g. begin_compute's displacement cascade)."""

@@ -101,6 +101,7 @@ uint32_t* ComputedRegistry::IdsBuffer(uint64_t need) {
 }
 
 std::shared_ptr<Computed> ComputedRegistry::Get(const std::string& input) {
+    CompletePending();
     const uint32_t s = SlotOf(input, false);
     if (s == FGI_NONE || !current_[s]) return nullptr;
     const ConsistencyState st = current_[s]->State();
@@ -116,6 +117,7 @@ void ComputedRegistry::MoveSubs(uint32_t from, uint32_t to) {
 }
 
 std::shared_ptr<Computed> ComputedRegistry::BeginCompute(const std::string& input, bool has_delay) {
+    CompletePending();
     const uint32_t s = SlotOf(input, true);
     auto c = std::make_shared<Computed>();
     c->reg_ = this;
@@ -151,6 +153,7 @@ std::shared_ptr<Computed> ComputedRegistry::BeginCompute(const std::string& inpu
 }
 
 uint32_t ComputedRegistry::AddUsed(Computed& dependant, Computed& used) {
+    CompletePending();
     uint32_t out = 0;
     const uint32_t d = dependant.handle_, u = used.handle_;
     Check(fgi_add_used(g_, 1, &d, &u, &out), "fgi_add_used");
@@ -158,6 +161,7 @@ uint32_t ComputedRegistry::AddUsed(Computed& dependant, Computed& used) {
 }
 
 bool ComputedRegistry::SetOutput(Computed& c) {
+    CompletePending();
     uint8_t set = 0;
     const uint32_t h = c.handle_;
     uint64_t n = 0;
@@ -173,6 +177,7 @@ bool ComputedRegistry::SetOutput(Computed& c) {
 }
 
 void ComputedRegistry::RunWave(const uint32_t* roots, size_t n_roots, const uint8_t* imm) {
+    CompletePending();
     uint64_t n = 0;
     last_ = fgi_wave_stats{};
     // the bitmap (n_handles / 8 bytes) costs less to bring back than the id list (4 B per node) once a
@@ -420,15 +425,89 @@ void ComputedRegistry::InvalidateSlots(const std::vector<uint32_t>& slots) {
 }
 
 void ComputedRegistry::FlushScope() {
+    const bool async = async_scope_;
+    async_scope_ = false;
     if (scope_roots_.empty()) return;
     std::vector<uint32_t> roots;
     std::vector<uint8_t> imm;
     roots.swap(scope_roots_);
     imm.swap(scope_imm_);
+    if (async) {
+        InvalidateSlotsAsync(roots, &imm);
+        return;
+    }
     RunWave(roots.data(), roots.size(), imm.data());
 }
 
+// ---- asynchronous waves (ComputedExt.WhenInvalidated over fgi_invalidate_async_host) ------------------
+// The engine keeps at most two waves in flight (a third call waits for the oldest inside the library);
+// the mirror completes a wave — its ids brought back and fanned out exactly as a synchronous wave's —
+// when asked, or before any other registry call (whose view of the registry must include the wave).
+uint64_t ComputedRegistry::InvalidateSlotsAsync(const std::vector<uint32_t>& roots, const std::vector<uint8_t>* imm) {
+    // a third wave makes the library wait for the oldest: complete it here so its fan-out runs in order
+    while (pending_.size() >= 2) Complete(pending_.front());
+    uint64_t t = 0;
+    Check(fgi_invalidate_async_host(g_, (uint32_t)roots.size(), roots.data(),
+                                    imm && imm->size() == roots.size() ? imm->data() : nullptr, &t),
+          "fgi_invalidate_async_host");
+    pending_.push_back(t);
+    last_ticket_ = t;
+    return t;
+}
+
+void ComputedRegistry::Complete(uint64_t ticket) {
+    while (!pending_.empty() && pending_.front() <= ticket) {
+        const uint64_t t = pending_.front();
+        pending_.pop_front();   // before the fan-out: its handlers may call back into the registry
+        fgi_wave_stats ws{};
+        uint64_t n = 0;
+        uint32_t* ids = IdsBuffer(1024);
+        fgi_status s = fgi_wave_wait_ids(g_, t, ids, ids_cap_, &n, &ws);
+        if (s == FGI_ECAPACITY) {   // the wave completed; fetch its ids with the right size
+            ids = IdsBuffer(n);
+            s = fgi_wave_wait_ids(g_, t, ids, n, &n, nullptr);
+        }
+        Check(s, "fgi_wave_wait_ids");
+        last_ = ws;
+        pred_v_ = n;
+        Dispatch(ids, n);
+    }
+}
+
+void ComputedRegistry::CompletePending() {
+    if (!pending_.empty()) Complete(pending_.back());
+}
+
+// ---- access reports (ComputedRegistry.ReportAccess, Computed.RenewTimeouts) -----------------------
+void ComputedRegistry::ReportAccess(Computed& c, bool is_new) {
+    if (!OnAccess) return;
+    if (c.IsInvalidated()) return;   // RenewTimeouts returns early for an Invalidated node (Computed.cs:250-251)
+    OnAccess(c, is_new);
+}
+
+std::shared_ptr<Computed> ComputedRegistry::TryUseExisting(const std::string& input, Computed* usedBy) {
+    auto existing = Get(input);
+    if (!existing || !existing->IsConsistent()) return nullptr;
+    if (usedBy) AddUsed(*usedBy, *existing);
+    if (OnAccess) OnAccess(*existing, true);   // Consistent: RenewTimeouts(true) reports it
+    return existing;
+}
+
+std::shared_ptr<Computed> ComputedRegistry::GetExisting(const std::string& input) {
+    CompletePending();
+    const uint32_t s = SlotOf(input, false);
+    if (s == FGI_NONE || !current_[s]) return nullptr;
+    ReportAccess(*current_[s], false);
+    return current_[s];
+}
+
+void ComputedRegistry::UseNew(Computed& computed, Computed* usedBy) {
+    if (usedBy) AddUsed(*usedBy, computed);
+    ReportAccess(computed, true);
+}
+
 void ComputedRegistry::InvalidateEverything() {
+    CompletePending();
     uint64_t n = 0;
     last_ = fgi_wave_stats{};
     uint32_t* ids = IdsBuffer(1024);
@@ -442,6 +521,7 @@ void ComputedRegistry::InvalidateEverything() {
 }
 
 std::pair<uint64_t, uint64_t> ComputedRegistry::Prune() {
+    CompletePending();
     fgi_prune_stats ps{};
     Check(fgi_prune(g_, &ps), "fgi_prune");
     return {ps.old_edges, ps.new_edges};
@@ -451,6 +531,7 @@ std::pair<uint64_t, uint64_t> ComputedRegistry::Prune() {
 ConsistencyState Computed::State() const { return (ConsistencyState)(Flags() & FGI_STATE_MASK); }
 
 uint32_t Computed::Flags() const {
+    reg_->CompletePending();   // the state includes the waves in flight (their handlers run first)
     uint64_t v = 0;
     uint32_t f = 0;
     reg_->Check(fgi_get_state(reg_->g_, 1, &handle_, &v, &f), "fgi_get_state");
@@ -483,6 +564,22 @@ void Computed::OnInvalidated(const InvalidatedHandler& handler) {
 }
 
 void Computed::RemoveOnInvalidated(const InvalidatedHandler& handler) { handlers_.Remove(handler); }
+
+std::shared_future<void> Computed::WhenInvalidated() {
+    if (when_) return when_f_;
+    when_ = std::make_shared<std::promise<void>>();
+    when_f_ = when_->get_future().share();
+    // ComputedExt.cs:101-102: already Invalidated -> completed. Every invalidation of a node the mirror
+    // holds goes through its fan-out (fired_), so the test needs no device query — which would complete
+    // the asynchronous waves in flight, while the caller wants to await them.
+    if (fired_) {
+        when_->set_value();
+        return when_f_;
+    }
+    std::shared_ptr<std::promise<void>> p = when_;
+    handlers_.Add(std::make_shared<const std::function<void(Computed&)>>([p](Computed&) { p->set_value(); }));
+    return when_f_;
+}
 
 std::vector<std::pair<uint32_t, LTag>> Computed::UsedBy() const {
     uint64_t n = 0;

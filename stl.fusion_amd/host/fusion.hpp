@@ -1,8 +1,13 @@
 // fusion.hpp — host-layer mirror of Stl.Fusion's invalidation API over the fgi C-ABI.
 //
 // This is the layer a Fusion host keeps in front of the engine. It mirrors:
-//   ComputedRegistry.Get / Register / InvalidateEverything / OnRegister / OnUnregister
-//                                                   (src/Stl.Fusion/ComputedRegistry.cs:34-147)
+//   ComputedRegistry.Get / Register / InvalidateEverything / OnRegister / OnUnregister / OnAccess
+//                                                   (src/Stl.Fusion/ComputedRegistry.cs:34-147, 172-176)
+//   ComputedExt.TryUseExisting / UseNew -> RenewTimeouts -> ReportAccess
+//                                                   (Internal/ComputedExt.cs:10-76, Computed.cs:248-262)
+//   ComputedExt.WhenInvalidated                      (ComputedExt.cs:99-125): a future completed by the
+//                                                   node's Invalidated handler, also across asynchronous
+//                                                   (pipelined) waves (fgi_invalidate_async_host)
 //   Computed.Invalidate() scope, Computed.IsInvalidating()   (Computed.Static.cs:41-47)
 //   IComputed.Invalidate(immediately), ConsistencyState, Version, event Invalidated
 //                                                   (Computed.cs:11-26, 84-105, 162)
@@ -29,7 +34,9 @@
 #pragma once
 
 #include <cstdint>
+#include <deque>
 #include <functional>
+#include <future>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -98,6 +105,11 @@ class Computed {
     void RemoveOnInvalidated(const InvalidatedHandler& handler);
     std::vector<std::pair<uint32_t, LTag>> UsedBy() const;   // IComputedImpl.UsedBy
     uint32_t UsedCount() const;                               // IComputedImpl.Used.Length
+    // ComputedExt.WhenInvalidated (ComputedExt.cs:99-125): ready at once for an Invalidated node, else
+    // completed by the node's Invalidated event — after a synchronous wave's fan-out, or when the
+    // registry completes the asynchronous wave that invalidated it (Complete / CompletePending). Every call
+    // returns the same future.
+    std::shared_future<void> WhenInvalidated();
 
    private:
     friend class ComputedRegistry;
@@ -107,6 +119,8 @@ class Computed {
     LTag version_ = 0;
     bool fired_ = false;
     InvalidatedHandlerSet handlers_;
+    std::shared_ptr<std::promise<void>> when_;   // WhenInvalidated's promise, once asked for
+    std::shared_future<void> when_f_;
 };
 
 // Per-wave fan-out statistics (the last Dispatch).
@@ -143,6 +157,17 @@ class ComputedRegistry {
     // one ComputedGraphPruner pass; returns (old, new) `_usedBy` totals of the pruned nodes
     std::pair<uint64_t, uint64_t> Prune();
 
+    // ComputedExt.TryUseExisting with no call options (Internal/ComputedExt.cs:10-23): the input's
+    // Consistent current node, made a dependency of usedBy (nullable) and reported as accessed
+    // (RenewTimeouts(true) -> OnAccess); null if there is none (the caller computes it)
+    std::shared_ptr<Computed> TryUseExisting(const std::string& input, Computed* usedBy = nullptr);
+    // CallOptions.GetExisting (ComputedExt.cs:38-42): the current node in any state, reported as
+    // accessed with isNew = false unless it is Invalidated (RenewTimeouts returns early then)
+    std::shared_ptr<Computed> GetExisting(const std::string& input);
+    // ComputedExt.UseNew (ComputedExt.cs:70-76) after a computation: AddUsed from usedBy, then the access
+    // report with isNew = true
+    void UseNew(Computed& computed, Computed* usedBy = nullptr);
+
     // `using (Computed.Invalidate()) { ... }`: roots collected while the scope is open are
     // invalidated as one batched wave when the outermost scope closes.
     class InvalidationScope {
@@ -158,6 +183,21 @@ class ComputedRegistry {
     };
     InvalidationScope Invalidate() { return InvalidationScope(this); }
     bool IsInvalidating() const { return scope_depth_ > 0; }
+    // The same scope, flushed as an asynchronous wave (fgi_invalidate_async_host): closing the outermost
+    // scope queues the wave and returns; the nodes' Invalidated handlers (and WhenInvalidated futures) run
+    // when the registry completes the wave — Complete(ticket), CompletePending(), or any other registry
+    // call, which completes the waves in flight first. LastTicket() names the last queued wave.
+    InvalidationScope InvalidateAsync() {
+        async_scope_ = true;
+        return InvalidationScope(this);
+    }
+    uint64_t LastTicket() const { return last_ticket_; }
+    // Queue one wave from slot / handle roots without waiting (what an async scope's flush does)
+    uint64_t InvalidateSlotsAsync(const std::vector<uint32_t>& roots, const std::vector<uint8_t>* immediately = nullptr);
+    // Wait for the asynchronous waves up to `ticket` (in order) and fan their results out (Dispatch)
+    void Complete(uint64_t ticket);
+    void CompletePending();
+    size_t PendingWaves() const { return pending_.size(); }
     // `_ = svc.Get(input)` inside a scope: TryUseExisting's Invalidate branch (ComputedExt.cs:29-35)
     void InvalidateInput(const std::string& input);
     // Slot-level roots (inputs already resolved by the host, e.g. bulk-registered nodes)
@@ -178,6 +218,9 @@ class ComputedRegistry {
     int WaveOutput = 0;
 
     std::function<void(Computed&)> OnRegister, OnUnregister;
+    // event OnAccess (ComputedRegistry.cs:36, ReportAccess 172-176): a compute-method node was used —
+    // isNew is RenewTimeouts' argument (TryUseExisting / UseNew: true, GetExisting: false)
+    std::function<void(Computed&, bool)> OnAccess;
     // registry-level handler class: the wave's invalidated handles, BatchChunk at a time
     std::function<void(const uint32_t* ids, size_t n)> OnInvalidatedBatch;
     size_t BatchChunk = 65536;
@@ -201,6 +244,7 @@ class ComputedRegistry {
     void DispatchBits(const uint64_t* bits, uint64_t words, uint64_t n);
     void DispatchImpl(const uint32_t* ids, const uint64_t* bits, uint64_t words, uint64_t n);
     void FlushScope();
+    void ReportAccess(Computed& c, bool is_new);
     LTag NextVersion(LTag current);
     void MoveSubs(uint32_t from, uint32_t to);
 
@@ -213,6 +257,9 @@ class ComputedRegistry {
     std::vector<uint32_t> scope_roots_;
     std::vector<uint8_t> scope_imm_;
     int scope_depth_ = 0;
+    bool async_scope_ = false;               // the outermost open scope flushes asynchronously
+    std::deque<uint64_t> pending_;           // asynchronous waves queued, not yet completed (ticket order)
+    uint64_t last_ticket_ = 0;
     LTag ltag_ = 0x100000;
     fgi_wave_stats last_{};
     FanoutStats fan_;

@@ -347,6 +347,76 @@ static void fanout_10m() {
                 "\"runs\": [%s]}\n", runs.c_str());
 }
 
+// ComputedExt.WhenInvalidated (ComputedExt.cs:99-125) awaited across pipelined waves: two scopes flushed
+// as asynchronous waves (fgi_invalidate_async_host), both in flight before either is completed; the
+// futures and handlers complete with their own wave's fan-out, in ticket order. Then OnAccess
+// (ComputedRegistry.cs:36, 172-176) through TryUseExisting / GetExisting / UseNew (Internal/ComputedExt.cs).
+static void when_invalidated_async() {
+    using namespace std::chrono_literals;
+    ComputedRegistry r(256);
+    auto a = Compute(r, "a");
+    auto b = Compute(r, "b", {a});
+    auto c = Compute(r, "c", {b});
+    auto x = Compute(r, "x");
+    auto y = Compute(r, "y", {x});
+    auto fc = c->WhenInvalidated();
+    auto fy = y->WhenInvalidated();
+    CHECK(fc.wait_for(0s) == std::future_status::timeout);
+    int fired_c = 0, fired_y = 0;
+    c->OnInvalidated([&](Computed&) { ++fired_c; });
+    y->OnInvalidated([&](Computed&) {
+        CHECK(fired_c == 1);   // the first wave's fan-out ran first
+        ++fired_y;
+    });
+    {
+        auto scope = r.InvalidateAsync();
+        r.InvalidateInput("a");
+    }
+    const uint64_t t1 = r.LastTicket();
+    CHECK(t1 > 0 && r.PendingWaves() == 1);
+    {
+        auto scope = r.InvalidateAsync();   // queued while the first wave may still run
+        r.InvalidateInput("x");
+    }
+    const uint64_t t2 = r.LastTicket();
+    CHECK(t2 == t1 + 1 && r.PendingWaves() == 2);
+    CHECK(fired_c == 0 && fc.wait_for(0s) == std::future_status::timeout);   // nothing fans out before completion
+    r.Complete(t1);
+    CHECK(fc.wait_for(0s) == std::future_status::ready && fired_c == 1 && r.LastWave().v_inv == 3);
+    CHECK(fy.wait_for(0s) == std::future_status::timeout && fired_y == 0 && r.PendingWaves() == 1);
+    r.CompletePending();
+    CHECK(fy.wait_for(0s) == std::future_status::ready && fired_y == 1 && r.LastWave().v_inv == 2);
+    CHECK(b->IsInvalidated() && c->IsInvalidated() && y->IsInvalidated() && r.PendingWaves() == 0);
+    CHECK(b->WhenInvalidated().wait_for(0s) == std::future_status::ready);   // already invalidated
+    CHECK(fc.wait_for(0s) == std::future_status::ready && c->WhenInvalidated().valid());
+    // any other registry call completes the waves in flight first (its view includes them)
+    auto p = Compute(r, "p");
+    auto q = Compute(r, "q", {p});
+    auto fq = q->WhenInvalidated();
+    {
+        auto scope = r.InvalidateAsync();
+        r.InvalidateInput("p");
+    }
+    CHECK(r.PendingWaves() == 1);
+    CHECK(r.Get("q") == nullptr && r.PendingWaves() == 0);
+    CHECK(fq.wait_for(0s) == std::future_status::ready);
+    // OnAccess: TryUseExisting -> RenewTimeouts(true), GetExisting -> RenewTimeouts(false), UseNew -> true
+    std::vector<std::pair<std::string, bool>> acc;
+    r.OnAccess = [&](Computed& cc, bool is_new) { acc.emplace_back(cc.Input(), is_new); };
+    auto m = Compute(r, "m");
+    auto n = r.BeginCompute("n");
+    CHECK(r.TryUseExisting("m", n.get()) == m);   // n now depends on m
+    CHECK(acc.size() == 1 && acc[0].first == "m" && acc[0].second);
+    CHECK(r.SetOutput(*n));
+    r.UseNew(*n);
+    CHECK(acc.size() == 2 && acc[1].first == "n" && acc[1].second);
+    CHECK(r.GetExisting("m") == m && acc.size() == 3 && acc[2].first == "m" && !acc[2].second);
+    CHECK(n->UsedCount() == 1);
+    m->Invalidate();   // the edge TryUseExisting captured carries the cascade
+    CHECK(n->IsInvalidated());
+    CHECK(r.TryUseExisting("m") == nullptr && r.GetExisting("m") == m && acc.size() == 3);   // Invalidated: no report
+}
+
 int main(int argc, char** argv) {
     if (argc > 1 && std::strcmp(argv[1], "--fanout") == 0) {
         try {
@@ -370,6 +440,7 @@ int main(int argc, char** argv) {
         register_displacement();
         prune();
         reentrant_handlers();
+        when_invalidated_async();
     } catch (const FgiError& e) {
         std::fprintf(stderr, "FgiError %d: %s\n", (int)e.status, e.what());
         return 2;

@@ -211,3 +211,60 @@ def test_ticket_results_forgotten_once_their_buffer_is_rewritten(pkg, gpu_availa
     assert g.wave_wait(t1)[0] > 0             # odd ticket: its buffer was not touched
     g.close()
     o.close()
+
+
+@pytest.mark.parametrize("labels", [-1, 1])
+def test_async_host_roots_and_ids_match_oracle(pkg, gpu_available, labels):
+    """fgi_invalidate_async_host / fgi_wave_wait_ids (the host layer's scope flush awaited later): roots and
+    immediately flags from host memory, two waves in flight on an evolving graph, each wave's ids brought
+    back to the host against the oracle (Computed.cs:162-230), node states after them."""
+    scale, ef, seed = 14, 8, 0x5EED0033
+    n = 1 << scale
+    g, o, deg = _pair(pkg, scale, ef, seed, labels)
+    rng = np.random.default_rng(11)
+    tickets, want = [], []
+    for k in range(5):
+        r = O.gen_roots(4 + 12 * k, n, 300 + k, deg)
+        imm = (rng.random(len(r)) < 0.25).astype(np.uint8)
+        o.clear_log()
+        st = o.invalidate_slots(r, imm)
+        want.append((np.sort(o.inv_log()), st.v_inv))
+        tickets.append(g.invalidate_async_host(r, imm))
+        if k >= 1:   # the previous wave, while this one is in flight
+            t = tickets[k - 1]
+            ws = pkg.WaveStats()
+            ids = g.wave_wait_ids(t, ws)
+            assert ws.v_inv == want[k - 1][1] and np.array_equal(ids, want[k - 1][0]), k
+    ids = g.wave_wait_ids(tickets[-1])
+    assert np.array_equal(ids, want[-1][0])
+    assert_states_equal(g, o, n)
+    g.close()
+    o.close()
+
+
+def test_async_wave_reports_pull_levels_run_as_push(pkg, gpu_available):
+    """A queued wave runs every level past its group in the tail as push levels: with pull-only waves on a
+    14-level graph, the first queued wave's group (4 levels: nothing learnt yet) leaves 10 levels that would
+    pull to the tail — counted in pull_pushed — and still matches the oracle; the next wave's group is sized
+    from it (8 levels), so fewer are left.""" 
+    fgi = pkg.fgi
+    g, o, n = _layered_pair(pkg, 14, 256, 2, 0x5EED0034)
+    g.set_option(fgi.OPT_DIRECTION, 2)
+    g.snapshot()
+    o.snapshot()
+    roots = np.arange(32, dtype=np.uint32)
+    o.clear_log()
+    o.invalidate_slots(roots)
+    want = np.sort(o.inv_log())
+    pushed, levels = [], []
+    for _ in range(2):
+        g.restore()
+        ws = pkg.WaveStats()
+        ids = g.wave_wait_ids(g.invalidate_async_host(roots), ws)
+        assert np.array_equal(ids, want)
+        levels.append(ws.levels)   # levels with frontier entries (the last level's nodes have no rows)
+        pushed.append(ws.pull_pushed)
+    assert levels[0] == levels[1] >= 12, levels
+    assert pushed == [levels[0] - 4, levels[0] - 8], (pushed, levels)
+    g.close()
+    o.close()
