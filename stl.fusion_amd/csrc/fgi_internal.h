@@ -333,6 +333,14 @@ struct fgi_graph {
     int opt_labels = 0;                // fgi_config.labels: 0 auto, 1 always, -1 never
     bool lbl_done = false;             // the hot set has been chosen (first bulk edge load)
     bool nodes_written = false;        // node words were written since create (note_words): at labels, if any
+    // Partition codes: a partition renumbers the slots within each rank's range, heaviest
+    // first, so that the all-gathered invalidated bitmap the pull levels probe holds every rank's hubs in a
+    // compact run at the start of its range. Ownership is unchanged (a slot's code lies in its owner's
+    // range). Every fgi_part_* entry point and every query maps slots <-> codes; the engine runs on codes.
+    bool lbl_perm = false;
+    uint32_t* pg_gc = nullptr;         // [n_global] slot -> code (device)
+    uint32_t* pg_ig = nullptr;         // [n_global] code -> slot (device)
+    std::vector<uint32_t> pg_gc_h, pg_ig_h;   // host copies
     uint32_t* s2l = nullptr;           // [ext_slots] hot label of a slot, FGI_NONE if cold
     uint32_t* l2s = nullptr;           // [lbl_K] slot of a hot label
     uint32_t* fold_start = nullptr;    // [fold_tiles + 1][lbl_ncls] first hot label of class c at slots >= t * kFoldTile
@@ -585,6 +593,19 @@ fgi_status labels_unmap_keys(fgi_graph* g, uint64_t* keys, uint64_t m);
 // move the node words already registered to their labels. No-op unless the graph wants labels and has
 // not chosen them yet.
 fgi_status labels_choose(fgi_graph* g, const uint64_t* keys, uint64_t m);
+// ---- partition codes (part.hip) ----
+// whether a partition of n_global slots renumbers its slots (fgi_config.labels / FGI_LABELS, auto from 2^25)
+bool part_codes_wanted(const fgi_graph* g, uint32_t n_global);
+// global slots -> codes (host arrays, into out; returns the array to use: `in` itself without codes)
+const uint32_t* part_codes_in(const fgi_graph* g, uint64_t n, const uint32_t* in, std::vector<uint32_t>& out);
+// a partition's local handles (owned slots base + h, h < n_local; detached handles unchanged) <-> the
+// engine's local indices, in place on the device (out: engine -> boundary), or one on the host
+fgi_status part_codes_local(fgi_graph* g, uint32_t* dev, uint64_t n, bool out);
+uint32_t part_code_local_h(const fgi_graph* g, uint32_t h, bool out);
+// a global code -> its slot on the host (ids and dependants leaving the engine)
+inline uint32_t part_slot_of(const fgi_graph* g, uint32_t code) {
+    return (g->lbl_perm && code < g->pg_ig_h.size()) ? g->pg_ig_h[code] : code;
+}
 // the words of a fold tile's slots: per hot class, the hot labels of the tile's slots, or none
 struct FoldArgs {
     const uint32_t* l2s;           // null: no hot labels (the bitmap of handles is the labels' own)

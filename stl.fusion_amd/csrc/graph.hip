@@ -1795,6 +1795,10 @@ static fgi_status single_only(fgi_graph* g, const char* what);
 // fgi_destroy, fgi_last_error and fgi_set_option.
 // a boundary handle's label, on the host (one lookup for a hot slot)
 static fgi_status label_of(fgi_graph* g, uint32_t x, uint32_t* out) {
+    if (g->lbl_perm) {   // a partition's local handle -> its code's local index
+        *out = part_code_local_h(g, x, false);
+        return FGI_OK;
+    }
     if (!g->lbl_K) {
         *out = x;
         return FGI_OK;
@@ -2090,7 +2094,7 @@ fgi_status fgi_dump_states(fgi_graph* g, uint64_t* version, uint32_t* state_flag
     FGI_TRY(fold(g));
     const uint32_t H = g->ext_handles;
     std::vector<uint64_t> w(H);
-    if (g->lbl_K) {   // the words of boundary handles 0 .. H-1 at their labels
+    if (g->lbl_K || g->lbl_perm) {   // the words of boundary handles 0 .. H-1 at their labels (codes)
         Tmp th, tw;
         uint32_t* dh;
         unsigned long long* dw;
@@ -2161,7 +2165,10 @@ fgi_status fgi_get_used_by(fgi_graph* g, uint32_t handle, uint32_t* dep, uint64_
                            g->pool_tag + off, reinterpret_cast<const unsigned long long*>(g->node), g->n_slots,
                            g->n_detached, g->home, dkeep);
         FGI_HIP(g, hipGetLastError());
-        if (g->lbl_K) {   // the entries' dependants as boundary slots
+        if (g->lbl_perm) {   // a partition's entries hold global codes: their slots
+            FGI_TRY(d2h(g, d.data(), g->pool_col + off, len));
+            for (uint32_t i = 0; i < len; ++i) d[i] = part_slot_of(g, d[i]);
+        } else if (g->lbl_K) {   // the entries' dependants as boundary slots
             Tmp tc;
             uint32_t* dc;
             FGI_TRY(tmalloc(g, tc, &dc, len));
@@ -2256,6 +2263,22 @@ fgi_status fgi_export_edges(fgi_graph* g, uint32_t* used, uint32_t* dep, uint64_
     std::vector<uint64_t> hk(m);
     FGI_TRY(d2h(g, hk.data(), keys, m));
     if (tag) FGI_TRY(d2h(g, tag, tags, m));
+    if (g->lbl_perm && m) {   // partition codes: (local used handle, dependant slot), in that order again
+        std::vector<uint64_t> ht(m);
+        FGI_TRY(d2h(g, ht.data(), tags, m));
+        std::vector<uint64_t> idx(m);
+        for (uint64_t e = 0; e < m; ++e) {
+            hk[e] = ((uint64_t)part_code_local_h(g, (uint32_t)(hk[e] >> 32), true) << 32) | part_slot_of(g, (uint32_t)hk[e]);
+            idx[e] = e;
+        }
+        std::sort(idx.begin(), idx.end(), [&](uint64_t a, uint64_t b) { return hk[a] != hk[b] ? hk[a] < hk[b] : ht[a] < ht[b]; });
+        std::vector<uint64_t> k2(m);
+        for (uint64_t e = 0; e < m; ++e) {
+            k2[e] = hk[idx[e]];
+            if (tag) tag[e] = ht[idx[e]];
+        }
+        hk.swap(k2);
+    }
     for (uint64_t e = 0; e < m; ++e) {
         if (used) used[e] = (uint32_t)(hk[e] >> 32);
         if (dep) dep[e] = (uint32_t)hk[e];
@@ -3452,7 +3475,8 @@ fgi_status part_take_ids(fgi_graph* g, const PartView& pv, std::vector<uint32_t>
     const size_t at = ids->size();
     ids->resize(at + g->last_wave_n);
     FGI_TRY(d2h(g, ids->data() + at, g->inv, g->last_wave_n));
-    for (size_t i = at; i < ids->size(); ++i) (*ids)[i] += pv.base;
+    for (size_t i = at; i < ids->size(); ++i) (*ids)[i] = part_slot_of(g, (*ids)[i] + pv.base);
+    if (g->lbl_perm) std::sort(ids->begin() + (ptrdiff_t)at, ids->end());   // the cascade's slots, ascending
     return FGI_OK;
 }
 
@@ -3772,7 +3796,8 @@ fgi_status fgi_part_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot
                                   const uint8_t* has_delay, uint32_t* out_detached, uint32_t* out_ids, uint64_t cap,
                                   uint64_t* out_n, fgi_wave_stats* stats) {
     if (!g) return FGI_EINVAL;
-    std::vector<uint32_t> ids;
+    std::vector<uint32_t> ids, ms;
+    slot = part_codes_in(g, n, slot, ms);   // partition codes; outputs are slots again
     FGI_TRY(part_begin_compute(g, n, slot, version, has_delay, out_detached, stats, &ids));
     return part_copy_ids(g, ids, out_ids, cap, out_n);
 }
@@ -3780,13 +3805,15 @@ fgi_status fgi_part_begin_compute(fgi_graph* g, uint32_t n, const uint32_t* slot
 fgi_status fgi_part_add_used(fgi_graph* g, uint32_t n, const uint32_t* dependant, const uint32_t* used,
                              uint32_t* out_result) {
     if (!g) return FGI_EINVAL;
-    return part_add_used(g, n, dependant, used, out_result);
+    std::vector<uint32_t> md, mu;
+    return part_add_used(g, n, part_codes_in(g, n, dependant, md), part_codes_in(g, n, used, mu), out_result);
 }
 
 fgi_status fgi_part_set_output(fgi_graph* g, uint32_t n, const uint32_t* slot, uint8_t* out_set, uint32_t* out_ids,
                                uint64_t cap, uint64_t* out_n, fgi_wave_stats* stats) {
     if (!g) return FGI_EINVAL;
-    std::vector<uint32_t> ids;
+    std::vector<uint32_t> ids, ms;
+    slot = part_codes_in(g, n, slot, ms);
     FGI_TRY(part_set_output(g, n, slot, out_set, stats, &ids));
     return part_copy_ids(g, ids, out_ids, cap, out_n);
 }
@@ -3832,7 +3859,10 @@ fgi_status fgi_part_run_batch(fgi_graph* g, uint32_t n_steps, const fgi_step* st
     std::vector<uint32_t> ids;
     fgi_wave_stats ws{};
     for (uint32_t k = 0; k < n_steps; ++k) {
-        const fgi_step& sp = steps[k];
+        fgi_step sp = steps[k];   // its slots as codes (partition codes)
+        std::vector<uint32_t> mh, mu;
+        sp.handles = part_codes_in(g, sp.n, sp.handles, mh);
+        if (sp.kind == FGI_STEP_ADD_USED) sp.used = part_codes_in(g, sp.n, sp.used, mu);
         if (sp.n && !sp.handles) return set_err(g, FGI_EINVAL, "step %u: no handles", k);
         const uint64_t before = ws.v_inv;
         switch (sp.kind) {

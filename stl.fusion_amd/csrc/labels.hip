@@ -195,6 +195,7 @@ uint32_t labels_capacity(uint32_t n_slots, int opt) {
 }
 
 fgi_status labels_map_in(fgi_graph* g, uint32_t* dev, uint64_t n) {
+    if (g->lbl_perm) return part_codes_local(g, dev, n, false);
     if (!g->lbl_K || n == 0) return FGI_OK;
     hipLaunchKernelGGL(k_lbl_map_in, dim3(std::min<uint32_t>(nblk(n), 8192)), dim3(256), 0, g->stream, n, dev, g->ext_slots,
                        g->lbl_hot ? g->s2l : nullptr, g->lbl_K);
@@ -203,6 +204,7 @@ fgi_status labels_map_in(fgi_graph* g, uint32_t* dev, uint64_t n) {
 }
 
 fgi_status labels_map_out(fgi_graph* g, uint32_t* dev, uint64_t n) {
+    if (g->lbl_perm) return part_codes_local(g, dev, n, true);
     if (!g->lbl_K || n == 0) return FGI_OK;
     hipLaunchKernelGGL(k_lbl_map_out, dim3(std::min<uint32_t>(nblk(n), 8192)), dim3(256), 0, g->stream, n, dev, g->l2s,
                        g->lbl_K);

@@ -109,6 +109,8 @@ struct PartState {
     unsigned long long* cur_local = nullptr;
     unsigned long long* cur_all = nullptr;
     std::vector<uint32_t> u32_host;            // allreduce_u32's host copy (in-process groups)
+    uint32_t* roots_codes = nullptr;           // fgi_part_invalidate's roots as codes (partition codes)
+    uint32_t roots_cap = 0;
 };
 
 static PartState* ps(fgi_graph* g) { return reinterpret_cast<PartState*>(g->part); }
@@ -224,11 +226,18 @@ fgi_status part_destroy(fgi_graph* g) {
     hipFree(p->red);
     hipFree(p->cur_local);
     hipFree(p->cur_all);
+    hipFree(p->roots_codes);
     if (p->red_host) hipHostFree(p->red_host);
     if (p->all_cnt_host) hipHostFree(p->all_cnt_host);
     if (p->scalar_host) hipHostFree(p->scalar_host);
     delete p;
     g->part = nullptr;
+    hipFree(g->pg_gc);
+    hipFree(g->pg_ig);
+    g->pg_gc = g->pg_ig = nullptr;
+    g->pg_gc_h.clear();
+    g->pg_ig_h.clear();
+    g->lbl_perm = false;
     return FGI_OK;
 }
 
@@ -964,14 +973,16 @@ fgi_status part_allreduce_sum(fgi_graph* g, const unsigned long long* dev_val, u
 
 namespace {
 
-__global__ void k_versions_all(uint32_t n, uint64_t seed, uint64_t* ver) {
+// versions by slot; with partition codes (ig: code -> slot) entry c holds the version of slot ig[c]
+__global__ void k_versions_all(uint32_t n, uint64_t seed, uint64_t* ver, const uint32_t* __restrict__ ig) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) ver[i] = synth_version(seed, (uint32_t)i);
+    if (i < n) ver[i] = synth_version(seed, ig ? ig[i] : (uint32_t)i);
 }
 
-__global__ void k_versions_local(uint32_t n, uint32_t base, uint64_t seed, unsigned long long* node) {
+__global__ void k_versions_local(uint32_t n, uint32_t base, uint64_t seed, unsigned long long* node,
+                                 const uint32_t* __restrict__ ig) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) node[i] = synth_version(seed, base + i) | kW_Consistent;
+    if (i < n) node[i] = synth_version(seed, ig ? ig[base + i] : base + i) | kW_Consistent;
 }
 
 // Row-range R-MAT (fgi_part_synth_rmat): edge i is a pure function of i, so every rank walks the
@@ -982,10 +993,14 @@ __global__ void k_versions_local(uint32_t n, uint32_t base, uint64_t seed, unsig
 // edge to its dependant's weight (the list order: a slot's live dependencies over the whole graph);
 // pass 1 writes the shares at the blocks' exclusive offsets (wave ballots, LDS cursors).
 constexpr uint32_t kGenBlocks = 4096;
+// With partition codes (gc: slot -> code, fill pass only) the kept keys hold codes, and each row entry's tag
+// (computed from the slot ids, as build_rows_from_keys would: the dependant's version, + 1 if stale) goes to
+// rtags. A slot's code has the slot's owner, so the shares and counts are those of the slot ids.
 __global__ __launch_bounds__(256) void k_rmat_part(uint64_t m, uint64_t per, uint32_t scale, uint64_t seed, uint32_t base,
                                                    uint32_t n_local, uint32_t stale_pct, uint64_t stale_seed, int fill,
                                                    unsigned long long* blk_cnt, const unsigned long long* blk_off,
-                                                   uint64_t* rows, uint64_t* ins, uint32_t* weight) {
+                                                   uint64_t* rows, uint64_t* ins, uint32_t* weight,
+                                                   const uint32_t* __restrict__ gc, uint64_t* rtags) {
     __shared__ unsigned long long s_cur[2];
     __shared__ unsigned long long s_red[2][4];
     const uint64_t lo = (uint64_t)blockIdx.x * per, hi = lo + per < m ? lo + per : m;
@@ -1018,8 +1033,17 @@ __global__ __launch_bounds__(256) void k_rmat_part(uint64_t m, uint64_t per, uin
         br = __shfl(br, 0, 64);
         bi = __shfl(bi, 0, 64);
         const unsigned long long lt = (1ull << lane) - 1ull;
-        if (own_row) rows[br + __popcll(mr & lt)] = ((uint64_t)(s - base) << 32) | d;
-        if (own_in) ins[bi + __popcll(mi & lt)] = ((uint64_t)(d - base) << 32) | s;
+        uint32_t sc = s, dc = d;
+        if (gc && (own_row || own_in)) {
+            sc = gc[s];
+            dc = gc[d];
+        }
+        if (own_row) {
+            const uint64_t at = br + __popcll(mr & lt);
+            rows[at] = ((uint64_t)(sc - base) << 32) | dc;
+            if (rtags) rtags[at] = synth_version(seed, d) + (synth_stale(stale_pct, stale_seed, s, d) ? 1u : 0u);
+        }
+        if (own_in) ins[bi + __popcll(mi & lt)] = ((uint64_t)(dc - base) << 32) | sc;
     }
     if (fill) return;
     for (int dd = 32; dd >= 1; dd >>= 1) {
@@ -1039,9 +1063,11 @@ __global__ __launch_bounds__(256) void k_rmat_part(uint64_t m, uint64_t per, uin
 }
 
 __global__ void k_in_tags_synth(uint64_t m, const uint64_t* __restrict__ keys, uint32_t base, uint64_t seed,
-                                uint64_t* tags) {
+                                uint64_t* tags, const uint32_t* __restrict__ ig) {
     const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (e < m) tags[e] = synth_version(seed, (uint32_t)(keys[e] >> 32) + base);
+    if (e >= m) return;
+    const uint32_t c = (uint32_t)(keys[e] >> 32) + base;   // the dependant (its code, with partition codes)
+    tags[e] = synth_version(seed, ig ? ig[c] : c);
 }
 
 // the in-store's live entries (tag == version of the dependant's node): flag for the compaction
@@ -1108,6 +1134,83 @@ __global__ void k_part_weight(uint64_t m, const uint32_t* __restrict__ dep, cons
 
 inline uint32_t nblk(uint64_t n) { return (uint32_t)((n + 255) / 256); }
 
+// ---- partition codes ------------------------------------------------------------------
+// The code order: each rank's range sorted by weight class (8 classes per octave of weight + 1, the
+// heaviest first, as the single device's labels), ties in slot order. A slot's code comes from its position
+// in that order (pc_code), inside its owner's range ([q * block, q * block + n_local)), so a slot keeps its
+// owner and every rank computes the same tables from the same global weights.
+__device__ __forceinline__ uint32_t pc_class(uint32_t w) {
+    const uint32_t x = w + 1u;
+    const uint32_t l = 31u - (uint32_t)__builtin_clz(x);
+    const uint32_t frac = l >= 3 ? (x >> (l - 3)) & 7u : (x << (3 - l)) & 7u;
+    return l * kClassPerOctave + frac;
+}
+__global__ void k_pc_keys(uint32_t N, uint32_t B, const uint32_t* __restrict__ w, uint64_t* keys) {
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= N) return;
+    keys[x] = ((uint64_t)(x / B) << 48) | ((uint64_t)(kLabelClasses - 1u - pc_class(w[x])) << 32) | x;
+}
+// Position i of that order (rank q's range [q * B, q * B + n_q)) -> its code. Contiguous (T = 0), the heaviest
+// slots of a rank would all fall to its first pull blocks (a pull block owns a fixed run of T slots); so the
+// order is dealt round-robin over the runs of T slots instead: run j gets positions j, j + S, j + 2S, ... (S
+// runs, the last one short; once the short run is full the rest are dealt over the S - 1 full runs), and
+// every pull block starts with its share of the hubs, in weight order.
+__device__ __forceinline__ uint32_t pc_code(uint32_t i, uint32_t N, uint32_t B, uint32_t T) {
+    const uint32_t q = i / B, base = q * B, nq = min(B, N - base), r = i - base;
+    if (T == 0 || nq <= T) return i;
+    const uint32_t S = (nq + T - 1) / T, last = nq - (S - 1) * T, A = last * S;
+    uint32_t run, k;
+    if (r < A) {
+        run = r % S;
+        k = r / S;
+    } else {
+        run = (r - A) % (S - 1);
+        k = last + (r - A) / (S - 1);
+    }
+    return base + run * T + k;
+}
+__global__ void k_pc_tables(uint32_t N, uint32_t B, uint32_t T, const uint64_t* __restrict__ sorted, uint32_t* gc,
+                            uint32_t* ig) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    const uint32_t x = (uint32_t)sorted[i];
+    const uint32_t c = pc_code(i, N, B, T);
+    gc[x] = c;
+    ig[c] = x;
+}
+// what was installed before the codes (registered nodes, versions, weights), moved to the codes
+__global__ void k_pc_move_local(uint32_t nl, uint32_t base, const uint32_t* __restrict__ gc,
+                                const unsigned long long* __restrict__ node_old, unsigned long long* node,
+                                const uint32_t* __restrict__ used_old, uint32_t* used) {
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= nl) return;
+    const uint32_t c = gc[base + h] - base;
+    node[c] = node_old[h];
+    used[c] = used_old[h];
+}
+__global__ void k_pc_move_global(uint32_t N, const uint32_t* __restrict__ gc, const uint64_t* __restrict__ ver_old,
+                                 uint64_t* ver, const uint32_t* __restrict__ w_old, uint32_t* w) {
+    const uint32_t x = blockIdx.x * blockDim.x + threadIdx.x;
+    if (x >= N) return;
+    const uint32_t c = gc[x];
+    ver[c] = ver_old[x];
+    w[c] = w_old[x];
+}
+// local handles <-> local code indices (owned range only), in place
+__global__ void k_pc_local(uint64_t n, uint32_t* a, const uint32_t* __restrict__ table, uint32_t base, uint32_t nl) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t h = a[i];
+        if (h < nl) a[i] = table[base + h] - base;
+    }
+}
+// global slots -> codes, in place
+__global__ void k_pc_global(uint64_t n, uint32_t* a, const uint32_t* __restrict__ gc, uint32_t N) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t x = a[i];
+        if (x < N) a[i] = gc[x];
+    }
+}
+
 // exclusive scan of flag[0, m) into pos; returns the total (synchronises the stream)
 fgi_status scan_flags(fgi_graph* g, const uint32_t* flag, uint32_t* pos, uint64_t m, uint64_t* total) {
     hipStream_t s = g->stream;
@@ -1132,6 +1235,81 @@ fgi_status scan_flags(fgi_graph* g, const uint32_t* flag, uint32_t* pos, uint64_
 // owned dependant node's version: the reference's d._used, Computed.cs:365-366) sorted and
 // deduplicated into lists of global used ids, each ordered by the entries' weights (as the single
 // engine: most-depended-on first), then the heads and the pull candidates. Local to the rank.
+// Choose the codes from every slot's weight (weight_dev: [n_global], by slot; replaced by the weights in
+// code order) and move what is already installed: the owned node words and |_used| counts, the version
+// replica. Only before any row or dependency entry exists and while no detached handle is taken.
+static fgi_status part_codes_choose(fgi_graph* g, uint32_t* weight_dev) {
+    PartState* p = ps(g);
+    const uint32_t N = p->v.n_global, B = p->v.block, base = p->v.base, nl = p->v.n_local;
+    hipStream_t s = g->stream;
+    FGI_TRY(fold(g));
+    uint64_t *k0 = nullptr, *k1 = nullptr, *ver_old = nullptr;
+    uint32_t *w_old = nullptr, *used_old = nullptr;
+    unsigned long long* node_old = nullptr;
+    void* tmp = nullptr;
+    fgi_status st = FGI_OK;
+    do {
+        if (!g->pg_gc && (hipMalloc(&g->pg_gc, (size_t)N * 4) != hipSuccess || hipMalloc(&g->pg_ig, (size_t)N * 4) != hipSuccess)) {
+            st = set_err(g, FGI_ENOMEM, "partition codes");
+            break;
+        }
+        if (hipMalloc(&k0, (size_t)N * 8) != hipSuccess || hipMalloc(&k1, (size_t)N * 8) != hipSuccess) {
+            st = set_err(g, FGI_ENOMEM, "partition code keys");
+            break;
+        }
+        hipLaunchKernelGGL(k_pc_keys, dim3(nblk(N)), dim3(256), 0, s, N, B, weight_dev, k0);
+        size_t tb = 0;
+        rocprim::radix_sort_keys(nullptr, tb, k0, k1, (size_t)N, 0, 56, s);
+        if (hipMalloc(&tmp, std::max<size_t>(tb, 16)) != hipSuccess) {
+            st = set_err(g, FGI_ENOMEM, "partition code sort");
+            break;
+        }
+        rocprim::radix_sort_keys(tmp, tb, k0, k1, (size_t)N, 0, 56, s);
+        uint32_t pgrid = 0, ptpb = 0;
+        pull_geometry(g, &pgrid, &ptpb);
+        const uint32_t T = pgrid ? ptpb * kPullTile : 0u;   // the slots a pull block owns
+        hipLaunchKernelGGL(k_pc_tables, dim3(nblk(N)), dim3(256), 0, s, N, B, T, k1, g->pg_gc, g->pg_ig);
+        if (hipMalloc(&ver_old, (size_t)N * 8) != hipSuccess || hipMalloc(&w_old, (size_t)N * 4) != hipSuccess ||
+            hipMalloc(&node_old, (size_t)std::max<uint32_t>(nl, 1) * 8) != hipSuccess ||
+            hipMalloc(&used_old, (size_t)std::max<uint32_t>(nl, 1) * 4) != hipSuccess) {
+            st = set_err(g, FGI_ENOMEM, "partition code moves");
+            break;
+        }
+        hipMemcpyAsync(ver_old, p->v.ver_all, (size_t)N * 8, hipMemcpyDeviceToDevice, s);
+        hipMemcpyAsync(w_old, weight_dev, (size_t)N * 4, hipMemcpyDeviceToDevice, s);
+        hipMemcpyAsync(node_old, g->node, (size_t)nl * 8, hipMemcpyDeviceToDevice, s);
+        hipMemcpyAsync(used_old, g->used_cnt, (size_t)nl * 4, hipMemcpyDeviceToDevice, s);
+        hipLaunchKernelGGL(k_pc_move_global, dim3(nblk(N)), dim3(256), 0, s, N, g->pg_gc, ver_old, p->v.ver_all, w_old,
+                           weight_dev);
+        if (nl)
+            hipLaunchKernelGGL(k_pc_move_local, dim3(nblk(nl)), dim3(256), 0, s, nl, base, g->pg_gc, node_old,
+                               reinterpret_cast<unsigned long long*>(g->node), used_old, g->used_cnt);
+        g->pg_gc_h.resize(N);
+        g->pg_ig_h.resize(N);
+        if (hipMemcpyAsync(g->pg_gc_h.data(), g->pg_gc, (size_t)N * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipMemcpyAsync(g->pg_ig_h.data(), g->pg_ig, (size_t)N * 4, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess) {
+            st = set_err(g, FGI_EDEVICE, "partition codes");
+            break;
+        }
+    } while (0);
+    for (void* q : {(void*)k0, (void*)k1, (void*)ver_old, (void*)w_old, (void*)node_old, (void*)used_old, tmp})
+        if (q) hipFree(q);
+    if (st != FGI_OK) return st;
+    g->lbl_perm = true;
+    touch(g);
+    note_words(g);
+    if (getenv("FGI_TRACE")) fprintf(stderr, "[fgi] partition codes: rank %u of %u, %u slots\n", p->v.rank, p->v.world, N);
+    return FGI_OK;
+}
+
+// the first bulk load of a partition that wants codes (nothing loaded, no detached handle taken)
+static bool part_codes_now(fgi_graph* g) {
+    PartState* p = ps(g);
+    return !g->lbl_perm && part_codes_wanted(g, p->v.n_global) && g->pool_top == 0 && p->in_n == 0 &&
+           g->free_detached.size() == g->n_detached;
+}
+
 static fgi_status part_rebuild_lists(fgi_graph* g) {
     PartState* p = ps(g);
     hipStream_t s = g->stream;
@@ -1217,6 +1395,33 @@ fgi_status part_ensure_lists(fgi_graph* g) {
     PartState* p = ps(g);
     if (!p || g->uin_epoch == g->mut_epoch || p->in_n == 0) return FGI_OK;
     return part_rebuild_lists(g);
+}
+
+bool part_codes_wanted(const fgi_graph* g, uint32_t n_global) {
+    return labels_capacity(n_global, g->opt_labels) != 0;   // fgi_config.labels / FGI_LABELS, auto from 2^25
+}
+
+const uint32_t* part_codes_in(const fgi_graph* g, uint64_t n, const uint32_t* in, std::vector<uint32_t>& out) {
+    if (!g->lbl_perm || !in || n == 0) return in;
+    out.resize(n);
+    const uint64_t N = g->pg_gc_h.size();
+    for (uint64_t i = 0; i < n; ++i) out[i] = in[i] < N ? g->pg_gc_h[in[i]] : in[i];
+    return out.data();
+}
+
+fgi_status part_codes_local(fgi_graph* g, uint32_t* dev, uint64_t n, bool out) {
+    PartState* p = ps(g);
+    if (!g->lbl_perm || !p || n == 0) return FGI_OK;
+    hipLaunchKernelGGL(k_pc_local, dim3(std::min<uint32_t>(nblk(n), 8192)), dim3(256), 0, g->stream, n, dev,
+                       out ? g->pg_ig : g->pg_gc, p->v.base, p->v.n_local);
+    FGI_HIP(g, hipGetLastError());
+    return FGI_OK;
+}
+
+uint32_t part_code_local_h(const fgi_graph* g, uint32_t h, bool out) {
+    const PartState* p = reinterpret_cast<const PartState*>(g->part);
+    if (!g->lbl_perm || !p || h >= p->v.n_local) return h;
+    return (out ? g->pg_ig_h : g->pg_gc_h)[p->v.base + h] - p->v.base;
 }
 
 // append m device entries (keys: dependant local << 32 | used global, tags) to the in-store
@@ -1352,7 +1557,10 @@ static fgi_status part_alloc(fgi_graph* g, uint32_t n_global) {
         part_destroy(g);
         return set_err(g, FGI_ENOMEM, "partition allocation failed: %s", what);
     };
-    if (hipMalloc(&p->v.ver_all, (size_t)n_global * 8) != hipSuccess) return fail("versions");
+    // an empty slot's version is 0 in the replica (fgi_part_register_nodes writes only the present ones)
+    if (hipMalloc(&p->v.ver_all, (size_t)n_global * 8) != hipSuccess ||
+        hipMemset(p->v.ver_all, 0, (size_t)n_global * 8) != hipSuccess)
+        return fail("versions");
     if (hipMalloc(&p->v.sent_bm, p->v.sent_words * 4) != hipSuccess) return fail("sent bitmap");
     if (hipMalloc(&p->v.send_buf, (size_t)W * block * 4) != hipSuccess) return fail("send buffer");
     if (hipMalloc(&p->v.recv_buf, (size_t)W * block * 4) != hipSuccess) return fail("recv buffer");
@@ -1428,8 +1636,10 @@ fgi_status fgi_part_local_invalidate(fgi_graph* const* gs, uint32_t P, uint32_t 
             if (n_roots && (hipMalloc(&rd, n_roots * 4) != hipSuccess ||
                             (immediately && hipMalloc(&id, n_roots) != hipSuccess)))
                 s = set_err(g, FGI_ENOMEM, "root buffers");
+            std::vector<uint32_t> mapped;
+            const uint32_t* rr = part_codes_in(g, n_roots, roots, mapped);
             if (s == FGI_OK && n_roots) {
-                if (hipMemcpy(rd, roots, n_roots * 4, hipMemcpyHostToDevice) != hipSuccess ||
+                if (hipMemcpy(rd, rr, n_roots * 4, hipMemcpyHostToDevice) != hipSuccess ||
                     (immediately && hipMemcpy(id, immediately, n_roots, hipMemcpyHostToDevice) != hipSuccess))
                     s = set_err(g, FGI_EDEVICE, "root copy");
             }
@@ -1573,22 +1783,26 @@ fgi_status fgi_part_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_facto
     g->v_dirty = false;
     g->vis_stale = false;
     note_words(g);
+    // partition codes: chosen after the count pass (the weights); a graph that already has codes keeps them
+    const bool choose = !g->lbl_perm && part_codes_wanted(g, N) && g->free_detached.size() == g->n_detached;
     hipLaunchKernelGGL(k_versions_local, dim3((nl + 255) / 256), dim3(256), 0, s, nl, base, seed,
-                       reinterpret_cast<unsigned long long*>(g->node));
-    hipLaunchKernelGGL(k_versions_all, dim3((N + 255) / 256), dim3(256), 0, s, N, seed, p->v.ver_all);
+                       reinterpret_cast<unsigned long long*>(g->node), g->lbl_perm ? g->pg_ig : (const uint32_t*)nullptr);
+    hipLaunchKernelGGL(k_versions_all, dim3((N + 255) / 256), dim3(256), 0, s, N, seed, p->v.ver_all,
+                       g->lbl_perm ? g->pg_ig : (const uint32_t*)nullptr);
     part_clear_store(p);
     FGI_HIP(g, hipMemsetAsync(p->weight, 0, (size_t)N * 4, s));
     // the rank's rows and dependency entries, generated by edge-index range (k_rmat_part)
     const uint64_t m = (uint64_t)edge_factor << scale;
     const uint64_t per = (m + kGenBlocks - 1) / kGenBlocks;
     unsigned long long *cnt = nullptr, *off = nullptr;
-    uint64_t *rows = nullptr, *ins = nullptr, *tags = nullptr;
+    uint64_t *rows = nullptr, *ins = nullptr, *tags = nullptr, *rtags = nullptr;
     auto cleanup = [&]() {
         hipFree(cnt);
         hipFree(off);
         hipFree(rows);
         hipFree(ins);
         hipFree(tags);
+        hipFree(rtags);
     };
     fgi_status st = FGI_OK;
     do {
@@ -1598,7 +1812,30 @@ fgi_status fgi_part_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_facto
         }
         hipLaunchKernelGGL(k_rmat_part, dim3(kGenBlocks), dim3(256), 0, s, m, per, scale, seed, base, nl, stale_pct,
                            stale_seed, 0, cnt, (const unsigned long long*)nullptr, (uint64_t*)nullptr, (uint64_t*)nullptr,
-                           p->weight);
+                           p->weight, (const uint32_t*)nullptr, (uint64_t*)nullptr);
+        if (choose) {   // the weights by slot are complete: codes, then the versions at them
+            g->pool_top = 0;   // the rows are rebuilt below
+            st = part_codes_choose(g, p->weight);
+            if (st != FGI_OK) break;
+            hipLaunchKernelGGL(k_versions_local, dim3((nl + 255) / 256), dim3(256), 0, s, nl, base, seed,
+                               reinterpret_cast<unsigned long long*>(g->node), (const uint32_t*)g->pg_ig);
+            hipLaunchKernelGGL(k_versions_all, dim3((N + 255) / 256), dim3(256), 0, s, N, seed, p->v.ver_all,
+                               (const uint32_t*)g->pg_ig);
+        } else if (g->lbl_perm) {   // the weights by slot into code order
+            uint32_t* w2 = nullptr;
+            if (hipMalloc(&w2, (size_t)N * 4) != hipSuccess) {
+                st = set_err(g, FGI_ENOMEM, "weights");
+                break;
+            }
+            hipMemcpyAsync(w2, p->weight, (size_t)N * 4, hipMemcpyDeviceToDevice, s);
+            hipLaunchKernelGGL(k_pc_move_global, dim3(nblk(N)), dim3(256), 0, s, N, (const uint32_t*)g->pg_gc,
+                               (const uint64_t*)p->v.ver_all, p->v.ver_all, (const uint32_t*)w2, p->weight);
+            hipStreamSynchronize(s);
+            hipFree(w2);
+            // k_pc_move_global also moved ver_all: write it again at the codes
+            hipLaunchKernelGGL(k_versions_all, dim3((N + 255) / 256), dim3(256), 0, s, N, seed, p->v.ver_all,
+                               (const uint32_t*)g->pg_ig);
+        }
         std::vector<unsigned long long> hc(2 * kGenBlocks), ho(2 * kGenBlocks);
         if (hipMemcpyAsync(hc.data(), cnt, hc.size() * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
             hipStreamSynchronize(s) != hipSuccess) {
@@ -1614,14 +1851,18 @@ fgi_status fgi_part_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_facto
         const uint64_t mo = tot[0], mi = tot[1];
         if (hipMalloc(&rows, std::max<uint64_t>(mo, 1) * 8) != hipSuccess ||
             hipMalloc(&ins, std::max<uint64_t>(mi, 1) * 8) != hipSuccess ||
-            hipMalloc(&tags, std::max<uint64_t>(mi, 1) * 8) != hipSuccess) {
+            hipMalloc(&tags, std::max<uint64_t>(mi, 1) * 8) != hipSuccess ||
+            (g->lbl_perm && hipMalloc(&rtags, std::max<uint64_t>(mo, 1) * 8) != hipSuccess)) {
             st = set_err(g, FGI_ENOMEM, "owned edges");
             break;
         }
         FGI_HIP(g, hipMemcpyAsync(off, ho.data(), ho.size() * 8, hipMemcpyHostToDevice, s));
         hipLaunchKernelGGL(k_rmat_part, dim3(kGenBlocks), dim3(256), 0, s, m, per, scale, seed, base, nl, stale_pct,
-                           stale_seed, 1, cnt, (const unsigned long long*)off, rows, ins, (uint32_t*)nullptr);
-        if (mi) hipLaunchKernelGGL(k_in_tags_synth, dim3(nblk(mi)), dim3(256), 0, s, mi, ins, base, seed, tags);
+                           stale_seed, 1, cnt, (const unsigned long long*)off, rows, ins, (uint32_t*)nullptr,
+                           g->lbl_perm ? (const uint32_t*)g->pg_gc : (const uint32_t*)nullptr, rtags);
+        if (mi)
+            hipLaunchKernelGGL(k_in_tags_synth, dim3(nblk(mi)), dim3(256), 0, s, mi, ins, base, seed, tags,
+                               g->lbl_perm ? (const uint32_t*)g->pg_ig : (const uint32_t*)nullptr);
         if (hipStreamSynchronize(s) != hipSuccess) {
             st = set_err(g, FGI_EDEVICE, "generator fill pass");
             break;
@@ -1629,8 +1870,9 @@ fgi_status fgi_part_synth_rmat(fgi_graph* g, uint32_t scale, uint32_t edge_facto
         hipFree(cnt);
         hipFree(off);
         cnt = off = nullptr;
-        // rows: (owned used << 32 | global dependant), tags synthesised from global ids
-        st = build_rows_from_keys(g, mo, rows, nullptr, seed, stale_pct, stale_seed, base, base);
+        // rows: (owned used << 32 | global dependant), tags synthesised from global ids (with codes: from the
+        // slot ids, by the generator)
+        st = build_rows_from_keys(g, mo, rows, rtags, seed, stale_pct, stale_seed, base, base);
         if (st != FGI_OK) break;
         hipFree(rows);
         rows = nullptr;
@@ -1653,6 +1895,8 @@ fgi_status fgi_part_register_nodes(fgi_graph* g, uint32_t n, const uint32_t* slo
         if (state_flags && (state_flags[i] & 3u) == 3u) return set_err(g, FGI_EINVAL, "bad state for slot %u", slot[i]);
     }
     if (n == 0) return FGI_OK;
+    std::vector<uint32_t> mapped;
+    slot = part_codes_in(g, n, slot, mapped);   // partition codes
     hipSetDevice(g->device);
     hipStream_t s = g->stream;
     FGI_TRY(fold(g));
@@ -1688,25 +1932,22 @@ fgi_status fgi_part_load_edges(fgi_graph* g, uint64_t m, const uint32_t* used, c
     if (!g->part) return set_err(g, FGI_ESTATE, "fgi_part_load_edges: partition not initialised");
     PartState* p = ps(g);
     const uint32_t base = p->v.base, nl = p->v.n_local, N = p->v.n_global;
-    std::vector<uint64_t> rk, rt, ik, it;
     for (uint64_t e = 0; e < m; ++e) {
         if (used[e] >= N || dependant[e] >= N)
             return set_err(g, FGI_EINVAL, "edge %llu out of range", (unsigned long long)e);
         if (tag[e] == 0) return set_err(g, FGI_EINVAL, "edge %llu has tag 0 (LTags are positive)", (unsigned long long)e);
-        if (used[e] - base < nl) {   // a row this rank owns: (local used, global dependant)
-            rk.push_back(((uint64_t)(used[e] - base) << 32) | dependant[e]);
-            rt.push_back(tag[e]);
-        }
-        if (dependant[e] - base < nl) {   // a dependency entry of a slot this rank owns
-            ik.push_back(((uint64_t)(dependant[e] - base) << 32) | used[e]);
-            it.push_back(tag[e]);
-        }
     }
     hipSetDevice(g->device);
-    hipStream_t s = g->stream;
-    FGI_TRY(load_rows(g, rk.size(), rk.data(), rt.data(), base, base));
-    // list weights: every rank sees the whole batch (and every version, ver_all)
+    // list weights: every rank sees the whole batch (and every version, ver_all). At the first bulk load of a
+    // partition that wants codes they decide the codes (by slot), which then number the batch and all else.
+    const bool choose = m && part_codes_now(g);
+    std::vector<uint32_t> mu, md;
+    if (!choose) {
+        used = part_codes_in(g, m, used, mu);
+        dependant = part_codes_in(g, m, dependant, md);
+    }
     if (m) {
+        hipStream_t s = g->stream;
         uint32_t* dd = nullptr;
         uint64_t* dt = nullptr;
         fgi_status st = FGI_OK;
@@ -1722,6 +1963,23 @@ fgi_status fgi_part_load_edges(fgi_graph* g, uint64_t m, const uint32_t* used, c
         hipFree(dt);
         FGI_TRY(st);
     }
+    if (choose) {
+        FGI_TRY(part_codes_choose(g, p->weight));
+        used = part_codes_in(g, m, used, mu);
+        dependant = part_codes_in(g, m, dependant, md);
+    }
+    std::vector<uint64_t> rk, rt, ik, it;
+    for (uint64_t e = 0; e < m; ++e) {
+        if (used[e] - base < nl) {   // a row this rank owns: (local used, global dependant)
+            rk.push_back(((uint64_t)(used[e] - base) << 32) | dependant[e]);
+            rt.push_back(tag[e]);
+        }
+        if (dependant[e] - base < nl) {   // a dependency entry of a slot this rank owns
+            ik.push_back(((uint64_t)(dependant[e] - base) << 32) | used[e]);
+            it.push_back(tag[e]);
+        }
+    }
+    FGI_TRY(load_rows(g, rk.size(), rk.data(), rt.data(), base, base));
     FGI_TRY(part_store_in(g, ik.data(), it.data(), ik.size()));
     return part_rebuild_lists(g);
 }
@@ -1730,6 +1988,20 @@ fgi_status fgi_part_invalidate(fgi_graph* g, uint32_t n_roots, const uint32_t* r
                                uint64_t* out_n, fgi_wave_stats* stats) {
     if (!g || !g->part || (n_roots && !roots_dev)) return FGI_EINVAL;
     hipSetDevice(g->device);
+    if (g->lbl_perm && n_roots) {   // the roots' codes (the caller's buffer stays as it is)
+        PartState* p = ps(g);
+        if (p->roots_cap < n_roots) {
+            hipFree(p->roots_codes);
+            p->roots_codes = nullptr;
+            p->roots_cap = 0;
+            FGI_HIP(g, hipMalloc(&p->roots_codes, (size_t)n_roots * 4));
+            p->roots_cap = n_roots;
+        }
+        FGI_HIP(g, hipMemcpyAsync(p->roots_codes, roots_dev, (size_t)n_roots * 4, hipMemcpyDeviceToDevice, g->stream));
+        hipLaunchKernelGGL(k_pc_global, dim3(std::min<uint32_t>(nblk(n_roots), 4096)), dim3(256), 0, g->stream,
+                           (uint64_t)n_roots, p->roots_codes, (const uint32_t*)g->pg_gc, p->v.n_global);
+        roots_dev = p->roots_codes;
+    }
     FGI_TRY(run_part_wave(g, n_roots, roots_dev, imm_dev, stats));
     if (out_n) *out_n = g->last_wave_n;
     return FGI_OK;
@@ -1749,7 +2021,8 @@ fgi_status fgi_part_export_ids(fgi_graph* g, uint32_t* out_ids, uint64_t cap, ui
     hipSetDevice(g->device);
     FGI_HIP(g, hipMemcpy(out_ids, g->inv, n * 4, hipMemcpyDeviceToHost));
     const uint32_t base = ps(g)->v.base;
-    for (uint64_t i = 0; i < n; ++i) out_ids[i] += base;   // local handle -> global slot
+    for (uint64_t i = 0; i < n; ++i) out_ids[i] = part_slot_of(g, out_ids[i] + base);   // local -> global slot
+    if (g->lbl_perm) std::sort(out_ids, out_ids + n);   // ascending slots
     return FGI_OK;
 }
 

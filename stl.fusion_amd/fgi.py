@@ -723,7 +723,7 @@ def part_local_invalidate(graphs, roots, immediately=None):
     stats = (WaveStats * len(graphs))()
     st = lib.fgi_part_local_invalidate(arr, len(graphs), len(r), _ptr(r, C.c_uint32), _ptr(imm, C.c_uint8), stats)
     if st != OK:
-        raise FgiError(st, "fgi_part_local_invalidate")
+        _local_error(lib, graphs, st, "fgi_part_local_invalidate")
     return list(stats)
 
 

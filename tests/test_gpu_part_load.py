@@ -21,13 +21,15 @@ pytestmark = pytest.mark.gpu
 GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.json")))
 
 
-def _partitioned(pkg, n, P, versions, flags, used, dep, tags, direction):
+def _partitioned(pkg, n, P, versions, flags, used, dep, tags, direction, labels=0, tpb=0):
     block = -(-n // P)
-    gs = [pkg.Graph(block, rank=r, world=P) for r in range(P)]
+    gs = [pkg.Graph(block, rank=r, world=P, labels=labels) for r in range(P)]
     pkg.fgi.part_init_local(gs, n)
     present = np.nonzero(versions)[0].astype(np.uint32)
     for g in gs:
         g.set_option(pkg.fgi.OPT_DIRECTION, direction)
+        if tpb:
+            g.set_option(pkg.fgi.OPT_PULL_TPB, tpb)
         g.part_register_nodes(present, versions[present], flags[present])
         if len(used):
             g.part_load_edges(used, dep, tags)
@@ -80,7 +82,7 @@ def test_partition_loads_golden_fixture(pkg, gpu_available, path, P, direction):
 
 @pytest.mark.parametrize("direction", [1, 2, 0])
 @pytest.mark.parametrize("P", [2, 3, 8])
-def test_partition_loads_mixed_state_graph(pkg, gpu_available, P, direction):
+def test_partition_loads_mixed_state_graph(pkg, gpu_available, P, direction, labels=0, tpb=0):
     rng = np.random.default_rng(100 + 10 * P + direction)
     n = 4096
     versions, flags = random_states(n, rng)
@@ -90,7 +92,7 @@ def test_partition_loads_mixed_state_graph(pkg, gpu_available, P, direction):
     src2 = np.concatenate([src2, src[:500]])
     dst2 = np.concatenate([dst2, dst[:500]])
     tags2 = np.concatenate([tags2, tags[:500]])
-    gs, block = _partitioned(pkg, n, P, versions, flags, src, dst, tags, direction)
+    gs, block = _partitioned(pkg, n, P, versions, flags, src, dst, tags, direction, labels, tpb)
     for g in gs:
         g.part_load_edges(src2, dst2, tags2)
     o = O.Oracle(n)
@@ -119,6 +121,20 @@ def test_partition_loads_mixed_state_graph(pkg, gpu_available, P, direction):
     for g in gs:
         g.close()
     o.close()
+
+
+@pytest.mark.parametrize("tpb", [0, 1])
+@pytest.mark.parametrize("direction", [2, 0])
+@pytest.mark.parametrize("P", [2, 3, 8])
+def test_partition_codes_mixed_state_graph(pkg, gpu_available, P, direction, tpb):
+    """Partition codes (labels=1: hub-first numbering inside each rank's range, chosen at the first bulk
+    load, dealt over the runs of slots the pull blocks own: one tile per block with tpb=1, so P=2's
+    2,048-slot ranges become two runs) on the mixed-state graphs, twice in a row: the second set of
+    graphs gets the first one's freed device memory, whose version replica held every slot's version, so
+    an empty slot's replica entry must start at 0 (stale edges into empty slots carry exactly those
+    versions)."""
+    for _ in range(2):
+        test_partition_loads_mixed_state_graph(pkg, gpu_available, P, direction, labels=1, tpb=tpb)
 
 
 def test_part_load_refusals(pkg, gpu_available):
