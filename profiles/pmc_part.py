@@ -13,7 +13,7 @@ rows = defaultdict(dict)
 for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursive=True):
     for r in csv.DictReader(open(f)):
         key = int(r["Dispatch_Id"])
-        rows[key]["name"] = r["Kernel_Name"].split("(")[0]
+        rows[key]["name"] = r["Kernel_Name"]
         rows[key][r["Counter_Name"]] = rows[key].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
 lv = [v for _, v in sorted(rows.items()) if "k_level" in v["name"]]
 counters = sorted({k for v in lv for k in v if k != "name"})
