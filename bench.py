@@ -235,6 +235,8 @@ def main():
     ap.add_argument("--cpu-scale", type=int, default=0,
                     help="R-MAT scale of the CPU baseline (default: the workload's own, i.e. the identical graph)")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end (host roots -> host ids) leg")
+    ap.add_argument("--no-pipelined", action="store_true",
+                    help="skip the pipelined (asynchronous) leg (profiling runs: the last waves are then the timed ones)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the secondary workloads (configs2_single_gpu / weak_scaling; profiling runs)")
     ap.add_argument("--partition", action="store_true",
@@ -391,7 +393,7 @@ def main():
         instrumented_ms = (time.perf_counter() - t_k) / args.steps * 1e3
         v_inv, e_trav, e_match = st.v_inv, st.e_trav, st.e_match
         pipe = None
-        if not partitioned:
+        if not partitioned and not args.no_pipelined:
             # pipelined leg (fgi_invalidate_async / fgi_wave_wait, ComputedExt.WhenInvalidated): the next
             # wave is queued before the previous one is waited for, so the host's wait, the published
             # counters' read and the next wave's launches overlap the device's work
