@@ -341,6 +341,7 @@ struct fgi_graph {
     uint32_t* pg_gc = nullptr;         // [n_global] slot -> code (device)
     uint32_t* pg_ig = nullptr;         // [n_global] code -> slot (device)
     std::vector<uint32_t> pg_gc_h, pg_ig_h;   // host copies
+    uint64_t pg_hash = 0;               // of the slot -> code table (0: no codes); every rank's must agree
     uint32_t* s2l = nullptr;           // [ext_slots] hot label of a slot, FGI_NONE if cold
     uint32_t* l2s = nullptr;           // [lbl_K] slot of a hot label
     uint32_t* fold_start = nullptr;    // [fold_tiles + 1][lbl_ncls] first hot label of class c at slots >= t * kFoldTile

@@ -238,6 +238,7 @@ fgi_status part_destroy(fgi_graph* g) {
     g->pg_gc_h.clear();
     g->pg_ig_h.clear();
     g->lbl_perm = false;
+    g->pg_hash = 0;
     return FGI_OK;
 }
 
@@ -1296,6 +1297,11 @@ static fgi_status part_codes_choose(fgi_graph* g, uint32_t* weight_dev) {
     for (void* q : {(void*)k0, (void*)k1, (void*)ver_old, (void*)w_old, (void*)node_old, (void*)used_old, tmp})
         if (q) hipFree(q);
     if (st != FGI_OK) return st;
+    // the table's fingerprint: the wave's first all-reduce checks that every rank chose the same codes (each
+    // rank chooses them alone, from the same arrays; a rank given other arrays would number slots otherwise)
+    uint64_t hsh = 0xcbf29ce484222325ull;
+    for (uint32_t x = 0; x < N; ++x) hsh = (hsh ^ g->pg_gc_h[x]) * 0x100000001b3ull;
+    g->pg_hash = hsh ? hsh : 1;
     g->lbl_perm = true;
     touch(g);
     note_words(g);

@@ -4244,7 +4244,7 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     FGI_HIP(g, hipGetLastError());
     const auto* node = reinterpret_cast<const unsigned long long*>(g->node);
     // one all-reduce of {local edges, level-0 frontier, its edges, ranks without pull lists, ranks
-    // that can follow the previous wave's plan}
+    // that can follow the previous wave's plan, the partition codes' fingerprint and its square}
     const WaveParams wp0 = wave_params(g, 1, g->opt_direction, g->pool_top, pv.n_global);
     const bool can_pull = wp0.direction != 1 && pull_ready(g, wp0);
     const PartBuckets pb = part_buckets(g);
@@ -4253,17 +4253,26 @@ fgi_status run_part_wave(fgi_graph* g, uint32_t n_roots, const uint32_t* roots_d
     // a rank whose lists appeared since votes no, and the wave learns a new plan)
     const bool plan_ok = g->opt_part_plan && !g->part_plan.empty() && g->opt_front_exchange != 2 &&
                          g->part_plan_key == key && (can_pull || !g->part_plan_pull);
-    uint64_t sums[5] = {0, 0, 0, 0, 0};
+    uint64_t sums[7] = {0, 0, 0, 0, 0, 0, 0};
     if (!coll && plan_ok) {
         // one rank without collectives: nothing to agree on (the plan is this rank's own)
         sums[0] = g->pool_top;
         sums[4] = 1;
     } else {
-        const uint64_t head[1] = {g->pool_top}, tail[2] = {can_pull ? 0ull : 1ull, plan_ok ? 1ull : 0ull};
+        const uint64_t head[1] = {g->pool_top};
+        const uint64_t tail[4] = {can_pull ? 0ull : 1ull, plan_ok ? 1ull : 0ull, g->pg_hash, g->pg_hash * g->pg_hash};
         FGI_HIP(g, hipMemcpyAsync(pb.red, head, 8, hipMemcpyHostToDevice, s));
         FGI_HIP(g, hipMemcpyAsync(pb.red + 1, &g->ctr->lvl[0].F, 16, hipMemcpyDeviceToDevice, s));
-        FGI_HIP(g, hipMemcpyAsync(pb.red + 3, tail, 16, hipMemcpyHostToDevice, s));
-        FGI_TRY(part_allreduce_sum(g, pb.red, sums, 5));
+        FGI_HIP(g, hipMemcpyAsync(pb.red + 3, tail, 32, hipMemcpyHostToDevice, s));
+        FGI_TRY(part_allreduce_sum(g, pb.red, sums, 7));
+        // every rank sees the same sums, so every rank fails here together when the ranks' codes differ
+        // (sum h = W h and sum h^2 = W h^2 for every rank's h only when all are equal)
+        if (sums[5] != (uint64_t)pv.world * g->pg_hash || sums[6] != (uint64_t)pv.world * g->pg_hash * g->pg_hash) {
+            g->failed = true;
+            return set_err(g, FGI_ESTATE, "rank %u of %u: the ranks numbered their slots differently (partition codes "
+                                          "chosen from different arrays: every rank must be given the same "
+                                          "fgi_part_register_nodes / fgi_part_load_edges arrays)", pv.rank, pv.world);
+        }
     }
     const WaveParams wp = wave_params(g, 1, g->opt_direction, sums[0], pv.n_global);
     if (sums[4] == pv.world)   // every rank follows the plan: no host synchronisation until the wave's end

@@ -137,6 +137,33 @@ def test_partition_codes_mixed_state_graph(pkg, gpu_available, P, direction, tpb
         test_partition_loads_mixed_state_graph(pkg, gpu_available, P, direction, labels=1, tpb=tpb)
 
 
+def test_partition_codes_disagreement_fails_every_rank(pkg, gpu_available):
+    """Each rank chooses its partition codes alone, from the arrays it is given; the host contract is that
+    every rank gets the same ones. A rank given other arrays (here rank 0 misses one registration, so the
+    heavy slot 700 weighs nothing in its replica) numbers the slots differently, and the wave's first
+    all-reduce (the codes' fingerprint) fails the wave on every rank instead of returning wrong ids."""
+    n, P = 1024, 2
+    block = n // P
+    gs = [pkg.Graph(block, rank=r, world=P, labels=1) for r in range(P)]
+    pkg.fgi.part_init_local(gs, n)
+    versions = O.version_of(1, np.arange(n, dtype=np.uint64))
+    rng = np.random.default_rng(7)
+    src = rng.integers(0, n, 4000).astype(np.uint32)
+    dst = rng.integers(0, n, 4000).astype(np.uint32)
+    dst[:600] = 700                                  # slot 700 (rank 1's) is the heaviest dependant
+    tags = versions[dst]
+    allslots = np.arange(n, dtype=np.uint32)
+    for r, g in enumerate(gs):
+        reg = allslots if r == 1 else allslots[allslots != 700]
+        g.part_register_nodes(reg, versions[reg])
+        g.part_load_edges(src, dst, tags)
+    with pytest.raises(pkg.FgiError) as e:
+        pkg.fgi.part_local_invalidate(gs, np.array([1, 2, 3], np.uint32))
+    assert e.value.status == pkg.fgi.ESTATE and "numbered their slots differently" in str(e.value)
+    for g in gs:
+        g.close()
+
+
 def test_part_load_refusals(pkg, gpu_available):
     n, P = 1024, 2
     gs = [pkg.Graph(n // P, rank=r, world=P) for r in range(P)]
