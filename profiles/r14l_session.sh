@@ -1,14 +1,10 @@
 #!/bin/bash
-# Round 6: (1) the partition suites with codes forced on a build whose version replica is NOT zeroed
-# (libfgi_dbg.so: the round's original failure, in its original test order); (2) bench --partition at N = 1
-# (the partitioned engine on one device) with partition codes forced vs host numbering, configs[1] and [2]
+# Round 6: bench --partition at N = 1 (the partitioned engine on one device) with partition codes forced vs host
+# numbering, configs[1] and [2] (the run also held a debug step, profiles/r14_replica_debug.txt)
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 out=$R/gpurun_out/r14l; mkdir -p $out
 cd $R
-FGI_LABELS=1 FGI_LIBRARY=$R/stl.fusion_amd/lib/libfgi_dbg.so timeout -k 10 600 python -u -m pytest tests/test_gpu_part.py \
-    tests/test_gpu_part_plan.py tests/test_gpu_part_load.py -m gpu -q --timeout 300 --timeout-method thread > $out/dbg_seq.txt 2>&1
-echo "dbg sequence rc=$?"; tail -3 $out/dbg_seq.txt
 for cfg in rmat24 rmat27; do
   for lab in 1 -1; do
     FGI_LABELS=$lab timeout -k 10 300 python bench.py --partition --config $cfg --steps 20 --warmup 3 --no-cpu --no-e2e --no-secondary > $out/part_${cfg}_$lab.json 2> $out/part_${cfg}_$lab.err || { echo "bench rc=$?"; tail -5 $out/part_${cfg}_$lab.err; exit 1; }
