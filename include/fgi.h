@@ -447,7 +447,10 @@ fgi_status fgi_part_register_nodes(fgi_graph* g, uint32_t n, const uint32_t* slo
  * set semantics). Every rank is given the same batch: it keeps the rows of the `used` slots it owns
  * (entries keep global dependant ids) and the dependency entries of the dependants it owns, from
  * which it rebuilds its pull lists (the reference's `_used`, Computed.cs:36, 365-366). No collective
- * runs. */
+ * runs. The first bulk load of a partition that uses partition codes (labels: automatic from 2^25
+ * slots, fgi_config.labels = 1 forces them) also numbers every rank's slots by weight, each rank on
+ * its own from the arrays it was given; ranks given different arrays number them differently, and
+ * the next collective wave then fails on every rank with FGI_ESTATE. */
 fgi_status fgi_part_load_edges(fgi_graph* g, uint64_t m, const uint32_t* used, const uint32_t* dependant,
                                const uint64_t* tag);
 /* Collective wave: every rank passes the same global root list; each rank reports the
