@@ -2,7 +2,7 @@
 # Round 6 close: the whole GPU suite, smoke(), the default bench line (N = 1)
 set -u
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-out=$R/gpurun_out/r14z; mkdir -p $out
+out=$R/gpurun_out/r14zz; mkdir -p $out
 cd $R
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $out/gpu_tests.log 2>&1 || { echo "gpu tests rc=$?"; tail -30 $out/gpu_tests.log; exit 1; }
 tail -1 $out/gpu_tests.log
