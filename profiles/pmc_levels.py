@@ -19,8 +19,8 @@ for (d, i), v in sorted(rows.items()):
     by_pass[d].append(v)
 names = ("k_roots", "k_collect", "k_level", "k_final_count", "k_final_write", "k_final")
 for d, lst in sorted(by_pass.items()):
-    # the last wave: from the last k_wave_init on
-    starts = [i for i, v in enumerate(lst) if v["name"].startswith("k_wave_init")]
+    # the last wave: from its k_roots on (round 6: a steady-state wave has no k_wave_init)
+    starts = [i for i, v in enumerate(lst) if v["name"].startswith("k_roots")]
     tail = lst[starts[-1]:] if starts else lst
     print(f"== {os.path.relpath(d, root)}")
     for v in tail:
